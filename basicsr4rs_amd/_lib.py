@@ -1,0 +1,98 @@
+"""ctypes binding of the C ABI in include/sr_hip.h (libsr_hip.so, gfx950).
+
+The product path calls the HIP kernels only through this module.  There is no CPU or
+PyTorch fallback: if the shared library is missing or a tensor is not on the GPU the call
+raises, like the reference's extension ops (basicsr/ops/dcn/deform_conv.py:61-62 raises
+NotImplementedError for CPU tensors; TORCH_CHECK failures surface as RuntimeError).
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.environ.get('SR_HIP_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib',
+                                                         'libsr_hip.so')
+
+SR_F32, SR_BF16 = 0, 1
+ACT_NONE, ACT_RELU, ACT_LRELU = 0, 1, 2
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_i64 = ctypes.c_int64
+_sz = ctypes.c_size_t
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [('dtype', _i), ('N', _i), ('H', _i), ('W', _i), ('Cin', _i), ('ldx', _i), ('xcoff', _i),
+                ('in_ps', _i), ('Cout', _i), ('Cout_real', _i), ('ldw', _i), ('ldy', _i), ('ycoff', _i),
+                ('out_ps', _i), ('out_nchw', _i), ('act', _i), ('slope', _f), ('alpha', _f), ('ldg', _i),
+                ('gcoff', _i), ('gate_slope', _f), ('ldr', _i), ('rcoff', _i), ('beta', _f)]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [('dtype', _i), ('N', _i), ('H', _i), ('W', _i), ('Cin', _i), ('Cin_real', _i), ('ldx', _i),
+                ('xcoff', _i), ('Cout', _i), ('Cout_real', _i), ('ldy', _i), ('ycoff', _i), ('out_ps', _i),
+                ('scale', _f)]
+
+
+# name -> (restype, argtypes); must match include/sr_hip.h (checked by tests/test_abi.py)
+SIGNATURES = {
+    'sr_version': (ctypes.c_char_p, []),
+    'sr_last_error': (ctypes.c_char_p, []),
+    'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_conv3x3_wgrad_workspace': (_sz, [ctypes.POINTER(WgradDesc)]),
+    'sr_conv3x3_wgrad': (_i, [ctypes.POINTER(WgradDesc), _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    'sr_conv3x3_prep': (_i, [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    'sr_nchw_to_nhwc': (_i, [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    'sr_nhwc_to_nchw': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    'sr_pixel_shuffle_nchw': (_i, [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    'sr_l1_loss': (_i, [_vp, _vp, _i64, _f, _i, _vp, _vp, _vp, _sz, _vp]),
+    'sr_l1_loss_workspace': (_sz, [_i64]),
+    'sr_act_backward': (_i, [_i, _vp, _vp, _i64, _i, _f, _f, _vp, _vp]),
+    'sr_adam_ema': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _f, _f, _vp]),
+}
+
+_LIB = None
+
+
+def load():
+    """Load libsr_hip.so once; raise loudly if it was not built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f'libsr_hip.so not found at {LIB_PATH}; build it with '
+                              '`python -c "import __graft_entry__ as g; g.build()"` or `make -C basicsr4rs_amd/csrc`')
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = lib
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(f'libsr_hip: {load().sr_last_error().decode()} (status {rc})')
+
+
+def stream():
+    return _vp(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Refuses CPU tensors: no CPU path."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise NotImplementedError('basicsr4rs_amd HIP ops need tensors on the MI355X (cuda) device')
+    return _vp(t.data_ptr())
+
+
+def dtype_code(dt):
+    if dt == torch.bfloat16:
+        return SR_BF16
+    if dt == torch.float32:
+        return SR_F32
+    raise TypeError(f'unsupported feature dtype {dt}')

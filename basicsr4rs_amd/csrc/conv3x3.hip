@@ -1,0 +1,812 @@
+// 3x3 / stride 1 / pad 1 convolution as an im2col-free implicit GEMM on CDNA4 MFMA.
+//
+// Replaces the cuDNN nn.Conv2d(C, C', 3, 1, 1) calls of the reference SR nets
+// (basicsr/archs/arch_util.py:78-79, edsr_arch.py:44-48, rcan_arch.py:40-42,
+// rrdbnet_arch.py:21-25): forward, data gradient (same kernel, flipped weights) and
+// weight/bias gradient (split-K over pixels, deterministic slab reduction).
+//
+// GEMM view of the forward: rows m = output pixels (n, y, x) of the NHWC map, columns
+// n = output channels, K = (tap, ci) with tap = ky*3 + kx.  The A tile of a K-step is a
+// [BM pixels][128 B] slice of the input shifted by the tap (zeros outside the image come
+// from the buffer range check), the B tile is [BN][128 B] of the weight rows; both are
+// staged through registers into an XOR-swizzled LDS image (conflict-free ds_read_b128,
+// tools/lds_banks.py) with one barrier per K-step and a double-buffered image.
+// bf16 uses v_mfma_f32_16x16x32_bf16, fp32 (parity mode) v_mfma_f32_16x16x4_f32 on the
+// same 16-byte chunk image.  The epilogue stages the fp32 tile through LDS and applies
+// bias, activation, ReLU-mask gate, scale, residual, pixel-shuffle / NCHW store with
+// 16-byte coalesced stores.
+#include "sr_common.h"
+#include "sr_internal.h"
+
+namespace {
+
+struct FwdArgs {
+  const void* x;
+  const void* w;
+  const float* bias;
+  const void* gate;
+  const void* res;
+  const float* aff_scale;
+  const float* aff_shift;
+  void* y;
+  uint32_t x_bytes, w_bytes, g_bytes, r_bytes;
+  int N, H, W, M;
+  int Cin, ldx, xcoff, in_ps, cpt;  // cpt: 16-byte chunks per tap
+  int Cout, Cout_real, ldw, nkc;    // nkc: total K chunks (9*cpt)
+  int ldy, ycoff, out_ps, out_nchw;
+  int act;
+  float slope, alpha;
+  int ldg, gcoff;
+  float gate_slope;
+  int ldr, rcoff;
+  float beta;
+  int tiles_n, tiles;
+  FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
+};
+
+template <typename T>
+SR_DEV void mfma_chunk(const u32x4& a, const u32x4& b, f32x4& acc);
+
+template <>
+SR_DEV void mfma_chunk<bf16_t>(const u32x4& a, const u32x4& b, f32x4& acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, a),
+                                                __builtin_bit_cast(s16x8, b), acc, 0, 0, 0);
+}
+template <>
+SR_DEV void mfma_chunk<float>(const u32x4& a, const u32x4& b, f32x4& acc) {
+  // one 16-byte chunk = 4 consecutive K elements per lane: 4 f32 MFMAs (K=4 each); the
+  // lane->k assignment is the same for A and B so the permuted K order sums correctly.
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[s]), __uint_as_float(b[s]), acc,
+                                               0, 0, 0);
+}
+
+// Byte offset of chunk c of row r inside a [rows][128 B] swizzled image.
+SR_DEV uint32_t swz128(uint32_t r, uint32_t c) { return r * 128u + ((c ^ (r & 7u)) << 4); }
+
+template <typename T, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void conv3x3_fwd_kernel(FwdArgs a) {
+  constexpr int PER = Elt<T>::PER16;
+  constexpr int SZ = Elt<T>::SIZE;
+  constexpr int MI = BM / WM / 16;
+  constexpr int NI = BN / WN / 16;
+  constexpr int A_CH = BM * 8 / 256;                     // A chunks per thread
+  constexpr int B_CH = (BN * 8 >= 256) ? BN * 8 / 256 : 1;  // B chunks per thread
+  constexpr bool B_PART = BN * 8 < 256;                   // only some threads load B
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int CSTR = BN + 4;  // epilogue fp32 row stride (floats)
+  constexpr int SMEM = (2 * STAGE > BM * CSTR * 4) ? 2 * STAGE : BM * CSTR * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (int)(tile / a.tiles_n) * BM;
+  const int n0 = (int)(tile % a.tiles_n) * BN;
+
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  // ---- per-thread A rows: pixel coordinates, fixed for the whole K loop ----
+  const int cA = tid & 7;
+  int ay[A_CH], ax[A_CH], anh[A_CH];  // y, x, n*H (anh < 0: row beyond M)
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    int m = m0 + (tid >> 3) + 32 * i;
+    if (m < a.M) {
+      uint32_t q = fdiv((uint32_t)m, a.fd_W);
+      ax[i] = m - (int)q * a.W;
+      uint32_t n = fdiv(q, a.fd_H);
+      ay[i] = (int)q - (int)n * a.H;
+      anh[i] = (int)n * a.H;
+    } else {
+      ax[i] = 0; ay[i] = -100000; anh[i] = 0;
+    }
+  }
+  const int bRow = tid >> 3;  // B rows bRow + 32*i
+
+  u32x4 ra[A_CH], rb[B_CH];
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.nkc + 7) >> 3;
+
+  auto load = [&](int ks) {
+    const int q = ks * 8 + cA;  // this thread's K chunk
+    const int tap = (int)fdiv((uint32_t)q, a.fd_cpt);
+    const int cc = q - tap * a.cpt;
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    const bool kval = q < a.nkc;
+    const int ch = cc * PER;  // GEMM input channel of the chunk
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int yy = ay[i] + dy, xx = ax[i] + dx;
+      const bool v = kval && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      uint32_t off;
+      if (a.in_ps == 0) {
+        off = (uint32_t)((((anh[i] + yy) * a.W + xx) * a.ldx + a.xcoff + ch) * SZ);
+      } else {
+        const int r = a.in_ps;
+        const int s = (int)fdiv((uint32_t)ch, a.fd_cps);
+        const int c = ch - s * a.fd_cps.d;
+        const int si = s / r, sj = s - (s / r) * r;
+        const int Wr = a.W * r;
+        off = (uint32_t)((((anh[i] + yy) * r + si) * Wr + xx * r + sj) * a.ldx + a.xcoff + c) * SZ;
+      }
+      ra[i] = buf_load16(xr, v ? off : SR_OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = n0 + bRow + 32 * i;
+      const bool v = kval && row < a.Cout && (!B_PART || tid < BN * 8);
+      const uint32_t off = (uint32_t)((row * a.ldw + q * PER) * SZ);
+      rb[i] = buf_load16(wr, v ? off : SR_OOB);
+    }
+  };
+  auto store = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * 128;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) *(u32x4*)(As + swz128((tid >> 3) + 32 * i, cA)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i)
+      if (!B_PART || tid < BN * 8) *(u32x4*)(Bs + swz128(bRow + 32 * i, cA)) = rb[i];
+  };
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const uint32_t c = kk * 4 + (lane >> 4);
+      u32x4 fa[MI], fb[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        fa[i] = *(const u32x4*)(As + swz128(wm * (BM / WM) + i * 16 + (lane & 15), c));
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        fb[j] = *(const u32x4*)(Bs + swz128(wn * (BN / WN) + j * 16 + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) mfma_chunk<T>(fa[i], fb[j], acc[i][j]);
+    }
+  };
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const bool more = ks + 1 < nk;
+    if (more) load(ks + 1);
+    compute(ks & 1);
+    if (more) store((ks + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage fp32 tile in LDS, then coalesced fused stores ----
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * (BN / WN) + j * 16 + (lane & 15);
+        Cs[row * CSTR + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  if (a.out_nchw) {
+    // fp32 NCHW store with per-channel affine; consecutive threads -> consecutive pixels.
+    float* y = (float*)a.y;
+    const int HW = a.H * a.W;
+    for (int idx = tid; idx < BM * BN; idx += 256) {
+      const int row = idx % BM, col = idx / BM;
+      const int m = m0 + row, n = n0 + col;
+      if (m >= a.M || n >= a.Cout_real) continue;
+      float v = Cs[row * CSTR + col] + (a.bias ? a.bias[n] : 0.f);
+      v = act_apply(v, a.act, a.slope) * a.alpha;
+      v = v * (a.aff_scale ? a.aff_scale[n] : 1.f) + (a.aff_shift ? a.aff_shift[n] : 0.f);
+      const int img = m / HW, pix = m - img * HW;
+      y[((size_t)img * a.Cout_real + n) * HW + pix] = v;
+    }
+    return;
+  }
+
+  constexpr int CG = BN / 8;  // 8-channel groups per row
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  for (int idx = tid; idx < BM * CG; idx += 256) {
+    const int row = idx / CG, cg = idx % CG;
+    const int m = m0 + row, n = n0 + cg * 8;
+    if (m >= a.M || n >= a.Cout) continue;
+    float v[8];
+    const f32x4 c0 = *(const f32x4*)(Cs + row * CSTR + cg * 8);
+    const f32x4 c1 = *(const f32x4*)(Cs + row * CSTR + cg * 8 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = c0[j]; v[4 + j] = c1[j]; }
+    if (a.bias) {
+      const f32x4 b0 = *(const f32x4*)(a.bias + n);
+      const f32x4 b1 = *(const f32x4*)(a.bias + n + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+    if (a.gate) {
+      float g[8];
+      const uint32_t off = (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ);
+      if constexpr (SZ == 2) {
+        u32x4 gg = buf_load16(gr, off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          g[2 * j] = bf16_to_f32(gg[j] & 0xffff);
+          g[2 * j + 1] = bf16_to_f32(gg[j] >> 16);
+        }
+      } else {
+        u32x4 g0 = buf_load16(gr, off), g1 = buf_load16(gr, off + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { g[j] = __uint_as_float(g0[j]); g[4 + j] = __uint_as_float(g1[j]); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+    if (a.res) {
+      float rv[8];
+      const uint32_t off = (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ);
+      if constexpr (SZ == 2) {
+        u32x4 rr4 = buf_load16(rr, off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          rv[2 * j] = bf16_to_f32(rr4[j] & 0xffff);
+          rv[2 * j + 1] = bf16_to_f32(rr4[j] >> 16);
+        }
+      } else {
+        u32x4 r0 = buf_load16(rr, off), r1 = buf_load16(rr, off + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { rv[j] = __uint_as_float(r0[j]); rv[4 + j] = __uint_as_float(r1[j]); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = a.beta * rv[j] + v[j];
+    }
+    size_t dst;  // element offset of the 8-channel group
+    if (a.out_ps == 0) {
+      dst = (size_t)m * a.ldy + a.ycoff + n;
+    } else {
+      const int r = a.out_ps;
+      const int s = (int)fdiv((uint32_t)n, a.fd_cps);
+      const int c = n - s * a.fd_cps.d;
+      const int si = s / r, sj = s - (s / r) * r;
+      const int xq = (int)fdiv((uint32_t)m, a.fd_W);
+      const int xx = m - xq * a.W;  // xq = n*H + y
+      dst = ((size_t)(xq * r + si) * (a.W * r) + xx * r + sj) * a.ldy + a.ycoff + c;
+    }
+    if constexpr (SZ == 2) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      *(u32x4*)((bf16_t*)a.y + dst) = o;
+    } else {
+      *(f32x4*)((float*)a.y + dst) = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)((float*)a.y + dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient.  GEMM per tap: C[co][ci] = sum_p dy[p][co] * x[p + tap][ci] over a
+// K-range of pixels (split-K).  LDS images are [pixels][cols] (rows = K); MFMA operands
+// need 8 consecutive K per lane, read with ds_read_b64_tr_b16 (bf16) or ds_read_b32
+// (f32).  Partial tiles go to an fp32 slab ws[split][tap][co][ci]; blocks of the centre
+// tap and first ci tile also emit the bias-gradient partial sums.
+// ------------------------------------------------------------------------------------
+struct WgArgs {
+  const void* dy;
+  const void* x;
+  float* ws;    // [S][9][Cout][Cin]
+  float* wsb;   // [S][Cout]
+  uint32_t dy_bytes, x_bytes;
+  int N, H, W, M;
+  int Cin, ldx, xcoff;
+  int Cout, ldy, ycoff, out_ps;
+  int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
+  FastDiv fd_W, fd_H, fd_cps;
+};
+
+// 32-byte-block XOR swizzle for the [K rows][256 B] tr-read image (tools/lds_banks.py):
+// the 8 rows a 32-lane half reads ({0..3, 8..11} + base) land on 8 distinct blocks.
+SR_DEV uint32_t swz_tr(uint32_t row, uint32_t byte_in_row, uint32_t row_bytes) {
+  const uint32_t f = (row & 3u) | (((row >> 3) & 1u) << 2);
+  const uint32_t blk = (byte_in_row >> 5) ^ (f & ((row_bytes >> 5) - 1));
+  return row * row_bytes + (blk << 5) + (byte_in_row & 31u);
+}
+
+template <typename T, int BMW, int BNW, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_kernel(WgArgs a) {
+  constexpr int PER = Elt<T>::PER16;
+  constexpr int SZ = Elt<T>::SIZE;
+  constexpr bool BF = (SZ == 2);
+  constexpr int KSTEP = BF ? 64 : 32;  // pixels per K-step
+  constexpr int MI = BMW / WM / 16;
+  constexpr int NI = BNW / WN / 16;
+  constexpr int ARB = BMW * SZ;  // bytes per A row (one pixel's co tile)
+  constexpr int BRB = BNW * SZ;
+  constexpr int ACPR = ARB / 16, BCPR = BRB / 16;  // chunks per row
+  constexpr int ACH = KSTEP * ACPR, BCH = KSTEP * BCPR;  // chunks per tile
+  constexpr int A_PT = (ACH + 255) / 256, B_PT = (BCH + 255) / 256;
+  constexpr int STAGE = KSTEP * (ARB + BRB);
+  constexpr int SMEM = 2 * STAGE > 256 * 8 * 4 ? 2 * STAGE : 256 * 8 * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  // block -> (split, tap, co tile, ci tile); splits outermost so concurrent blocks share
+  // the same pixel range (dy / x rows re-read from L2).
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_split = 9 * a.tiles_co * a.tiles_ci;
+  const int split = (int)b / per_split;
+  int rem = (int)b - split * per_split;
+  const int tap = rem / (a.tiles_co * a.tiles_ci);
+  rem -= tap * a.tiles_co * a.tiles_ci;
+  const int co0 = (rem / a.tiles_ci) * BMW;
+  const int ci0 = (rem % a.tiles_ci) * BNW;
+  const int dy_ = tap / 3 - 1, dx_ = tap % 3 - 1;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const bool do_bias = (tap == 4) && (ci0 == 0) && a.wsb != nullptr;
+
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+
+  u32x4 ra[A_PT], rb[B_PT];
+  float bacc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto pix_decomp = [&](int p, int& nh, int& y, int& x) {
+    uint32_t q = fdiv((uint32_t)p, a.fd_W);
+    x = p - (int)q * a.W;
+    uint32_t n = fdiv(q, a.fd_H);
+    y = (int)q - (int)n * a.H;
+    nh = (int)n * a.H;
+  };
+
+  auto load = [&](int p0) {
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c / ACPR, cc = c % ACPR;
+      const int p = p0 + row;
+      const int co = co0 + cc * PER;
+      bool v = (c < ACH) && p < p_end && co < a.Cout;
+      uint32_t off = SR_OOB;
+      if (v) {
+        if (a.out_ps == 0) {
+          off = (uint32_t)(((size_t)p * a.ldy + a.ycoff + co) * SZ);
+        } else {
+          int nh, y, x;
+          pix_decomp(p, nh, y, x);
+          const int r = a.out_ps;
+          const int s = (int)fdiv((uint32_t)co, a.fd_cps);
+          const int cch = co - s * a.fd_cps.d;
+          const int si = s / r, sj = s - (s / r) * r;
+          off = (uint32_t)((((size_t)((nh + y) * r + si) * (a.W * r) + x * r + sj) * a.ldy + a.ycoff + cch) * SZ);
+        }
+      }
+      ra[i] = buf_load16(dyr, off);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c / BCPR, cc = c % BCPR;
+      const int p = p0 + row;
+      const int ci = ci0 + cc * PER;
+      bool v = (c < BCH) && p < p_end && ci < a.Cin;
+      uint32_t off = SR_OOB;
+      if (v) {
+        int nh, y, x;
+        pix_decomp(p, nh, y, x);
+        const int yy = y + dy_, xx = x + dx_;
+        if ((unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W)
+          off = (uint32_t)(((size_t)((nh + yy) * a.W + xx) * a.ldx + a.xcoff + ci) * SZ);
+      }
+      rb[i] = buf_load16(xr, off);
+    }
+  };
+  auto bias_accum = [&]() {
+    // every A chunk a thread loads covers the same 8 (or 4) channels across K-steps
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      if (BF) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bacc[2 * j] += bf16_to_f32(ra[i][j] & 0xffff);
+          bacc[2 * j + 1] += bf16_to_f32(ra[i][j] >> 16);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bacc[j] += __uint_as_float(ra[i][j]);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + KSTEP * ARB;
+#pragma unroll
+    for (int i = 0; i < A_PT; ++i) {
+      const int c = tid + 256 * i;
+      if (c < ACH) {
+        const int row = c / ACPR, cc = c % ACPR;
+        const uint32_t o = BF ? swz_tr(row, cc * 16, ARB) : (uint32_t)(row * ARB + cc * 16);
+        *(u32x4*)(As + o) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_PT; ++i) {
+      const int c = tid + 256 * i;
+      if (c < BCH) {
+        const int row = c / BCPR, cc = c % BCPR;
+        const uint32_t o = BF ? swz_tr(row, cc * 16, BRB) : (uint32_t)(row * BRB + cc * 16);
+        *(u32x4*)(Bs + o) = rb[i];
+      }
+    }
+  };
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + KSTEP * ARB;
+    if constexpr (BF) {
+      const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        s16x8 fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int col = wm * (BMW / WM) + i * 16 + 4 * p;  // co column of this lane's address
+          const int r0 = kk * 32 + 8 * g + q;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(As + swz_tr(r0, col * 2, ARB)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(As + swz_tr(r0 + 4, col * 2, ARB)));
+          fa[i] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = wn * (BNW / WN) + j * 16 + 4 * p;
+          const int r0 = kk * 32 + 8 * g + q;
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Bs + swz_tr(r0, col * 2, BRB)));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(Bs + swz_tr(r0 + 4, col * 2, BRB)));
+          fb[j] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const int k = lane >> 4, c16 = lane & 15;
+#pragma unroll 4
+      for (int ks = 0; ks < KSTEP; ks += 4) {
+        float fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          fa[i] = *(const float*)(As + (ks + k) * ARB + (wm * (BMW / WM) + i * 16 + c16) * 4);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          fb[j] = *(const float*)(Bs + (ks + k) * BRB + (wn * (BNW / WN) + j * 16 + c16) * 4);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nk = (p_end - p_begin + KSTEP - 1) / KSTEP;
+  if (nk > 0) {
+    load(p_begin);
+    if (do_bias) bias_accum();
+    store(0);
+  }
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const bool more = ks + 1 < nk;
+    if (more) load(p_begin + (ks + 1) * KSTEP);
+    compute(ks & 1);
+    if (more) {
+      if (do_bias) bias_accum();
+      store((ks + 1) & 1);
+    }
+    __syncthreads();
+  }
+
+  // partial tile -> slab ws[split][tap][co][ci]; C/D layout: row = co, col = ci
+  float* ws = a.ws + ((size_t)split * 9 + tap) * a.Cout * a.Cin;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * (BMW / WM) + i * 16 + (lane >> 4) * 4 + r;
+        const int ci = ci0 + wn * (BNW / WN) + j * 16 + (lane & 15);
+        if (co < a.Cout && ci < a.Cin) ws[(size_t)co * a.Cin + ci] = acc[i][j][r];
+      }
+
+  if (do_bias) {
+    float* red = (float*)smem;  // [256][8]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < BMW) {
+      const int cc = tid / PER, j = tid % PER;
+      float s = 0.f;
+      // threads whose A chunks are chunk cc of a row: tid' with (tid' + 256 i) % ACPR == cc
+      for (int t2 = 0; t2 < 256; ++t2)
+        if ((t2 % ACPR) == cc && t2 < ACH) s += red[t2 * 8 + j];
+      if (co0 + tid < a.Cout) a.wsb[(size_t)split * a.Cout + co0 + tid] = s;
+    }
+  }
+}
+
+// dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co = perm(co'); db likewise.
+__global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
+                                    int Cout, int Cin, int Cout_real, int Cin_real, int out_ps,
+                                    float scale) {
+  const int64_t total = (int64_t)Cout_real * Cin_real * 9;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
+  const int cps = Cout_real / r2;  // C' (channels after shuffle)
+  if (i < total) {
+    const int tap = (int)(i % 9);
+    const int ci = (int)((i / 9) % Cin_real);
+    const int co = (int)(i / (9 * (int64_t)Cin_real));
+    const int cop = out_ps > 0 ? (co % r2) * cps + co / r2 : co;  // GEMM column of co
+    const size_t stride = (size_t)9 * Cout * Cin;
+    const float* src = ws + ((size_t)tap * Cout + cop) * Cin + ci;
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += src[k * stride];
+    dw[i] = s * scale;
+  }
+  if (db && i < Cout_real) {
+    const int co = (int)i;
+    const int cop = out_ps > 0 ? (co % r2) * cps + co / r2 : co;
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += wsb[(size_t)k * Cout + cop];
+    db[co] = s * scale;
+  }
+}
+
+template <typename T>
+__global__ void prep_kernel(const float* w, const float* bias, int Cout_real, int Cin_real, int Cout,
+                            int Cin, int out_ps, T* wf, T* wd, float* bias_g) {
+  // one thread per (n, ci, tap) of the padded GEMM weight
+  const int64_t total = (int64_t)Cout * Cin * 9;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
+  const int cps = Cout_real / r2;
+  if (i < total) {
+    const int tap = (int)(i % 9);
+    const int ci = (int)((i / 9) % Cin);
+    const int n = (int)(i / (9 * (int64_t)Cin));
+    int co = -1;
+    if (n < Cout_real) co = out_ps > 0 ? (n % cps) * r2 + n / cps : n;
+    float v = 0.f;
+    if (co >= 0 && ci < Cin_real) v = w[((size_t)co * Cin_real + ci) * 9 + tap];
+    if (wf) wf[(size_t)n * 9 * Cin + (size_t)tap * Cin + ci] = Elt<T>::from_f(v);
+    if (wd) wd[(size_t)ci * 9 * Cout + (size_t)(8 - tap) * Cout + n] = Elt<T>::from_f(v);
+  }
+  if (bias_g && i < Cout) {
+    const int n = (int)i;
+    float v = 0.f;
+    if (n < Cout_real && bias) v = bias[out_ps > 0 ? (n % cps) * r2 + n / cps : n];
+    bias_g[n] = v;
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
+  FwdArgs a = a0;
+  const int tm = (a.M + BM - 1) / BM;
+  a.tiles_n = (a.Cout + BN - 1) / BN;
+  a.tiles = tm * a.tiles_n;
+  hipLaunchKernelGGL((conv3x3_fwd_kernel<T, BM, BN, WM, WN>), dim3(a.tiles), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
+  if (a.out_nchw || a.Cout <= 16) return launch_fwd<T, 256, 16, 4, 1>(a, s);
+  if (a.Cout <= 32) return launch_fwd<T, 256, 32, 4, 1>(a, s);
+  if (a.Cout <= 64) return launch_fwd<T, 128, 64, 2, 2>(a, s);
+  return launch_fwd<T, 128, 128, 2, 2>(a, s);
+}
+
+inline int tile_for(int c) { return c <= 16 ? 16 : c <= 32 ? 32 : c <= 64 ? 64 : 128; }
+// wgrad tile (co x ci): grow the larger side until 4 waves each own a 16x16 sub-tile.
+inline void wg_tiles(int cout, int cin, int* bm, int* bn) {
+  int m = tile_for(cout), n = tile_for(cin);
+  while ((m / 16) * (n / 16) < 4) {
+    if (m <= n) n *= 2; else m *= 2;
+  }
+  *bm = m;
+  *bn = n;
+}
+
+// Wave grid (WM x WN = 4) for a BMW x BNW wgrad tile: every wave needs >= one 16x16 tile.
+constexpr int wg_wm(int bm, int bn) {
+  return (bm >= 32 && bn >= 32) ? 2 : (bm >= 64 ? 4 : 1);
+}
+
+template <typename T, int BMW, int BNW>
+hipError_t launch_wg(WgArgs a, hipStream_t s) {
+  constexpr int WM = wg_wm(BMW, BNW);
+  constexpr int WN = 4 / WM;
+  static_assert(BMW / WM >= 16 && BNW / WN >= 16, "wgrad tile too small for 4 waves");
+  a.tiles_co = (a.Cout + BMW - 1) / BMW;
+  a.tiles_ci = (a.Cin + BNW - 1) / BNW;
+  const int blocks = a.splits * 9 * a.tiles_co * a.tiles_ci;
+  hipLaunchKernelGGL((conv3x3_wgrad_kernel<T, BMW, BNW, WM, WN>), dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t dispatch_wg(const WgArgs& a, hipStream_t s) {
+  int bm, bn;
+  wg_tiles(a.Cout, a.Cin, &bm, &bn);
+#define SR_WG(X, Y) \
+  if (bm == X && bn == Y) return launch_wg<T, X, Y>(a, s);
+  SR_WG(128, 128) SR_WG(128, 64) SR_WG(64, 128) SR_WG(64, 64) SR_WG(128, 32) SR_WG(32, 128)
+  SR_WG(128, 16) SR_WG(16, 128) SR_WG(64, 32) SR_WG(32, 64) SR_WG(64, 16) SR_WG(16, 64)
+  SR_WG(32, 32)
+#undef SR_WG
+  return hipErrorInvalidValue;
+}
+
+// Split-K factor: enough blocks to cover the chip ~2x, pixels per split a multiple of 64.
+void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
+  const int M = d->N * d->H * d->W;
+  int bm, bn;
+  wg_tiles(d->Cout, d->Cin, &bm, &bn);
+  const int tiles = 9 * ((d->Cout + bm - 1) / bm) * ((d->Cin + bn - 1) / bn);
+  int S = (1024 + tiles - 1) / tiles;
+  const int maxS = (M + 255) / 256;  // at least 256 pixels per split
+  if (S > maxS) S = maxS;
+  if (S < 1) S = 1;
+  int kp = (M + S - 1) / S;
+  kp = (kp + 63) / 64 * 64;
+  S = (M + kp - 1) / kp;
+  *splits = S;
+  *kper = kp;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
+                   const void* gate, const void* res, const float* aff_scale,
+                   const float* aff_shift, void* y, void* stream) {
+  if (!d || !x || !w || !y) return sr_fail(SR_EINVAL, "conv3x3_fwd: null pointer");
+  const int SZ = d->dtype == SR_BF16 ? 2 : 4;
+  const int PER = 16 / SZ;
+  if (d->Cin % 8 || d->ldx % PER || d->xcoff % PER || (!d->out_nchw && (d->Cout % 8)))
+    return sr_fail(SR_EINVAL, "conv3x3_fwd: Cin/Cout/ld/coff must be multiples of 8 (pad channels)");
+  if (d->ldw < 9 * d->Cin) return sr_fail(SR_EINVAL, "conv3x3_fwd: ldw < 9*Cin");
+  if ((gate || res) && d->out_ps) return sr_fail(SR_EINVAL, "conv3x3_fwd: gate/res need plain store");
+  const int M = d->N * d->H * d->W;
+  const int r_in = d->in_ps > 0 ? d->in_ps : 1;
+  const size_t xb = (size_t)M * r_in * r_in * (size_t)d->ldx * SZ;
+  const size_t wb = (size_t)d->Cout * d->ldw * SZ;
+  if (xb >= 0x80000000ull || wb >= 0x80000000ull)
+    return sr_fail(SR_ETOOBIG, "conv3x3_fwd: tensor >= 2 GiB (split the batch)");
+  FwdArgs a{};
+  a.x = x; a.w = w; a.bias = bias; a.gate = gate; a.res = res;
+  a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.y = y;
+  a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
+  a.g_bytes = gate ? (uint32_t)((size_t)M * d->ldg * SZ) : 0;
+  a.r_bytes = res ? (uint32_t)((size_t)M * d->ldr * SZ) : 0;
+  a.N = d->N; a.H = d->H; a.W = d->W; a.M = M;
+  a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff; a.in_ps = d->in_ps;
+  a.cpt = d->Cin / PER; a.nkc = 9 * a.cpt;
+  a.Cout = d->Cout; a.Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout; a.ldw = d->ldw;
+  a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps; a.out_nchw = d->out_nchw;
+  a.act = d->act; a.slope = d->slope; a.alpha = d->alpha;
+  a.ldg = d->ldg; a.gcoff = d->gcoff; a.gate_slope = d->gate_slope;
+  a.ldr = d->ldr; a.rcoff = d->rcoff; a.beta = d->beta;
+  a.fd_cpt = make_fastdiv(a.cpt);
+  a.fd_W = make_fastdiv(d->W);
+  a.fd_H = make_fastdiv(d->H);
+  int cps = 1;
+  if (d->in_ps > 0) cps = d->Cin / (d->in_ps * d->in_ps);
+  if (d->out_ps > 0) cps = d->Cout / (d->out_ps * d->out_ps);
+  if (d->in_ps > 0 && d->out_ps > 0) return sr_fail(SR_EINVAL, "conv3x3_fwd: in_ps and out_ps exclusive");
+  if ((d->in_ps > 0 || d->out_ps > 0) && cps % PER)
+    return sr_fail(SR_EINVAL, "conv3x3_fwd: shuffled channel count must be a multiple of 8");
+  a.fd_cps = make_fastdiv(cps);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = d->dtype == SR_BF16 ? dispatch_fwd<bf16_t>(a, s) : dispatch_fwd<float>(a, s);
+  return sr_check(e, "conv3x3_fwd launch");
+}
+
+size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d) {
+  int S, kp;
+  wgrad_plan(d, &S, &kp);
+  return ((size_t)S * 9 * d->Cout * d->Cin + (size_t)S * d->Cout) * sizeof(float) + 256;
+}
+
+int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void* x, void* workspace,
+                     size_t ws_bytes, float* dw, float* db, void* stream) {
+  if (!d || !dy || !x || !workspace || !dw) return sr_fail(SR_EINVAL, "conv3x3_wgrad: null pointer");
+  const int SZ = d->dtype == SR_BF16 ? 2 : 4;
+  const int PER = 16 / SZ;
+  if (d->Cin % 8 || d->Cout % 8 || d->ldx % PER || d->ldy % PER || d->xcoff % PER || d->ycoff % PER)
+    return sr_fail(SR_EINVAL, "conv3x3_wgrad: channel counts / strides must be multiples of 8");
+  if (ws_bytes < sr_conv3x3_wgrad_workspace(d)) return sr_fail(SR_EINVAL, "conv3x3_wgrad: workspace too small");
+  const int M = d->N * d->H * d->W;
+  const int r = d->out_ps > 0 ? d->out_ps : 1;
+  const size_t xb = (size_t)M * d->ldx * SZ;
+  const size_t dyb2 = (size_t)M * r * r * (size_t)d->ldy * SZ;
+  if (xb >= 0x80000000ull || dyb2 >= 0x80000000ull)
+    return sr_fail(SR_ETOOBIG, "conv3x3_wgrad: tensor >= 2 GiB (split the batch)");
+  WgArgs a{};
+  a.dy = dy; a.x = x;
+  int S, kp;
+  wgrad_plan(d, &S, &kp);
+  a.ws = (float*)workspace;
+  a.wsb = db ? a.ws + (size_t)S * 9 * d->Cout * d->Cin : nullptr;
+  a.dy_bytes = (uint32_t)dyb2; a.x_bytes = (uint32_t)xb;
+  a.N = d->N; a.H = d->H; a.W = d->W; a.M = M;
+  a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff;
+  a.Cout = d->Cout; a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps;
+  a.splits = S; a.kper = kp;
+  a.fd_W = make_fastdiv(d->W); a.fd_H = make_fastdiv(d->H);
+  int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 1;
+  if (d->out_ps > 0 && cps % PER)
+    return sr_fail(SR_EINVAL, "conv3x3_wgrad: shuffled channel count must be a multiple of 8");
+  a.fd_cps = make_fastdiv(cps);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = d->dtype == SR_BF16 ? dispatch_wg<bf16_t>(a, s) : dispatch_wg<float>(a, s);
+  if (e != hipSuccess) return sr_check(e, "conv3x3_wgrad launch");
+  const int Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout;
+  const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
+  const int64_t total = (int64_t)Cout_real * Cin_real * 9;
+  const int64_t work = total > Cout_real ? total : Cout_real;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                     (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
+                     Cin_real, d->out_ps, d->scale);
+  return sr_check(hipGetLastError(), "conv3x3_wgrad reduce launch");
+}
+
+int sr_conv3x3_prep(int dtype, const float* w, const float* bias, int Cout_real, int Cin_real, int Cout,
+                    int Cin, int out_ps, void* wf, void* wd, float* bias_g, void* stream) {
+  if (!w) return sr_fail(SR_EINVAL, "conv3x3_prep: null weight");
+  if (Cout < Cout_real || Cin < Cin_real) return sr_fail(SR_EINVAL, "conv3x3_prep: padded < real");
+  if (out_ps > 0 && (Cout_real % (out_ps * out_ps) || Cout != Cout_real))
+    return sr_fail(SR_EINVAL, "conv3x3_prep: shuffled conv needs Cout == Cout_real divisible by r^2");
+  const int64_t total = (int64_t)Cout * Cin * 9;
+  const int64_t work = total > Cout ? total : Cout;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(prep_kernel<bf16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w,
+                       bias, Cout_real, Cin_real, Cout, Cin, out_ps, (bf16_t*)wf, (bf16_t*)wd, bias_g);
+  else
+    hipLaunchKernelGGL(prep_kernel<float>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w,
+                       bias, Cout_real, Cin_real, Cout, Cin, out_ps, (float*)wf, (float*)wd, bias_g);
+  return sr_check(hipGetLastError(), "conv3x3_prep launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) super-resolution kernels.
+//
+// Conventions used by every kernel in this directory:
+//   * feature maps are NHWC, element type float (parity mode) or bf16 (train mode),
+//     with an explicit pixel stride (`ld`, in elements) so channel slices of a wider
+//     buffer (RRDB dense blocks) can be read and written in place;
+//   * every global load of activation/weight tiles goes through a buffer resource
+//     (V#) whose range check returns zeros for out-of-range offsets: that is how the
+//     3x3 zero padding and partial tiles are implemented (no branches in the loaders);
+//   * kernels take the caller's hipStream_t and never allocate or synchronise.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SR_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+// Offset that is guaranteed to fail the buffer range check (load returns 0).
+#define SR_OOB 0x80000000u
+
+SR_DEV float bf16_to_f32(unsigned short u) { return __uint_as_float(((unsigned)u) << 16); }
+SR_DEV unsigned short f32_to_bf16(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+SR_DEV unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+}
+
+// Element traits: the kernels are written once over "16-byte chunks"; T decides how
+// many channels a chunk carries (8 bf16 or 4 f32) and how it converts to f32.
+template <typename T> struct Elt;
+template <> struct Elt<float> {
+  static constexpr int PER16 = 4;  // elements per 16 B chunk
+  static constexpr int SIZE = 4;
+  SR_DEV static float to_f(float v) { return v; }
+  SR_DEV static float from_f(float v) { return v; }
+};
+template <> struct Elt<unsigned short> {
+  static constexpr int PER16 = 8;
+  static constexpr int SIZE = 2;
+  SR_DEV static float to_f(unsigned short v) { return bf16_to_f32(v); }
+  SR_DEV static unsigned short from_f(float v) { return f32_to_bf16(v); }
+};
+typedef unsigned short bf16_t;
+
+SR_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+SR_DEV u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// Fast unsigned division by a runtime constant (Hacker's Delight 10-9, round-up variant,
+// exact for every 32-bit numerator). d == 1 is handled by the caller-visible flag.
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d <= 1) { f.mul = 0; f.shr = 0; return f; }
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;  // l = ceil(log2 d)
+  f.mul = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1);
+  f.shr = l - 1;
+  return f;
+}
+SR_DEV uint32_t fdiv(uint32_t n, FastDiv f) {
+  if (f.d == 1) return n;
+  uint32_t t = __umulhi(n, f.mul);
+  return (t + ((n - t) >> 1)) >> f.shr;
+}
+
+// XCD-aware, bijective block-id remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): consecutive logical tiles land on the same XCD (shared L2).
+SR_DEV uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  if (nwg < 16) return bid;
+  uint32_t q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+SR_DEV float act_apply(float v, int act, float slope) {
+  // act: 0 none, 1 relu, 2 leaky relu(slope)
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return v > 0.f ? v : v * slope;
+  return v;
+}

@@ -1,0 +1,311 @@
+"""3x3 convolution ops on NHWC feature maps, backed by libsr_hip (csrc/conv3x3.hip).
+
+These replace the cuDNN ``nn.Conv2d(C, C', 3, 1, 1)`` calls of the reference SR nets
+(basicsr/archs/arch_util.py:78-79, 135-139; edsr_arch.py:44-48; rcan_arch.py:40-42;
+rrdbnet_arch.py:21-25).  Parameters stay the reference's ``nn.Conv2d`` parameters
+(``weight`` [Cout, Cin, 3, 3] fp32, ``bias`` [Cout]) so state_dict keys and init match;
+their GEMM images (forward rows, flipped dgrad rows, bias in GEMM order) are prepared by
+a HIP kernel once per parameter update and cached.
+
+Feature maps inside the nets are NHWC tensors ``[N, H, W, Cp]`` with Cp = channels padded
+to a multiple of 8 (padded channels are exactly zero).  Compute dtype: bf16 when CUDA
+autocast is enabled (the reference's AMP path, basicsr/models/srrs_model.py:28-31, uses
+fp16; bf16 is the documented divergence), fp32 otherwise.
+"""
+import math
+
+import torch
+
+from .. import _lib
+
+_PARAM_EPOCH = [0]  # bumped by optimizers that update parameters behind autograd's back
+
+
+def bump_param_epoch():
+    _PARAM_EPOCH[0] += 1
+
+
+def pad8(c):
+    return (c + 7) // 8 * 8
+
+
+def feature_dtype():
+    """Compute dtype of the HIP kernels for the current context."""
+    if torch.is_autocast_enabled('cuda'):
+        return torch.bfloat16
+    return torch.float32
+
+
+class ConvSpec:
+    """Static configuration of one conv call (epilogue fusion flags)."""
+    __slots__ = ('cin', 'cout', 'cin_p', 'cout_p', 'act', 'slope', 'alpha', 'beta', 'out_ps', 'out_nchw',
+                 'aff_scale', 'aff_shift')
+
+    def __init__(self, cin, cout, act=_lib.ACT_NONE, slope=0.0, alpha=1.0, beta=1.0, out_ps=0, out_nchw=False,
+                 aff_scale=None, aff_shift=None, cin_p=None, cout_p=None):
+        self.cin, self.cout = cin, cout
+        self.cin_p = cin_p or pad8(cin)
+        self.cout_p = cout_p or pad8(cout)
+        self.act, self.slope, self.alpha, self.beta = act, float(slope), float(alpha), float(beta)
+        self.out_ps, self.out_nchw = out_ps, out_nchw
+        self.aff_scale, self.aff_shift = aff_scale, aff_shift
+        if out_ps:
+            assert cout % (out_ps * out_ps) == 0 and (cout // (out_ps * out_ps)) % 8 == 0, \
+                'pixel-shuffled conv needs Cout/r^2 to be a multiple of 8'
+            self.cout_p = cout
+
+
+def prepared(weight, bias, spec, dtype):
+    """GEMM images of a conv parameter pair, cached until the parameter changes."""
+    key = (weight._version, _PARAM_EPOCH[0], dtype, spec.cin_p, spec.cout_p, spec.out_ps, weight.data_ptr())
+    cache = getattr(weight, '_sr_prep', None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    dev = weight.device
+    wf = torch.empty(spec.cout_p, 9 * spec.cin_p, device=dev, dtype=dtype)
+    wd = torch.empty(spec.cin_p, 9 * spec.cout_p, device=dev, dtype=dtype)
+    bg = torch.empty(spec.cout_p, device=dev, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_conv3x3_prep(_lib.dtype_code(dtype), _lib.ptr(weight.detach()),
+                            _lib.ptr(bias.detach() if bias is not None else None), spec.cout, spec.cin,
+                            spec.cout_p, spec.cin_p, spec.out_ps, _lib.ptr(wf), _lib.ptr(wd), _lib.ptr(bg),
+                            _lib.stream()))
+    val = (wf, wd, bg)
+    weight._sr_prep = (key, val)
+    return val
+
+
+def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
+    d = _lib.ConvDesc()
+    d.dtype = _lib.dtype_code(dtype)
+    d.N, d.H, d.W = N, H, W
+    d.Cin, d.ldx, d.xcoff, d.in_ps = cin, ldx, kw.get('xcoff', 0), kw.get('in_ps', 0)
+    d.Cout, d.Cout_real, d.ldw = cout, cout_real, 9 * cin
+    d.ldy, d.ycoff, d.out_ps, d.out_nchw = ldy, kw.get('ycoff', 0), kw.get('out_ps', 0), int(kw.get('out_nchw', 0))
+    d.act, d.slope, d.alpha = kw.get('act', 0), kw.get('slope', 0.0), kw.get('alpha', 1.0)
+    d.ldg, d.gcoff, d.gate_slope = kw.get('ldg', 0), kw.get('gcoff', 0), kw.get('gate_slope', 0.0)
+    d.ldr, d.rcoff, d.beta = kw.get('ldr', 0), kw.get('rcoff', 0), kw.get('beta', 1.0)
+    return d
+
+
+def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res=None, aff_scale=None,
+                 aff_shift=None, **kw):
+    """Launch sr_conv3x3_fwd on already-prepared GEMM weights (shapes checked here)."""
+    assert x.is_contiguous() and y.is_contiguous()
+    ldx = kw.pop('ldx', x.shape[-1])
+    ldy = kw.pop('ldy', y.shape[-1] if not kw.get('out_nchw') else 0)
+    if gate is not None:
+        kw.setdefault('ldg', gate.shape[-1])
+    if res is not None:
+        kw.setdefault('ldr', res.shape[-1])
+    d = _desc(x.dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw)
+    assert wf.shape[0] >= cout and wf.shape[1] == 9 * cin, (wf.shape, cout, cin)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_conv3x3_fwd(d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res),
+                           _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.stream()))
+    return y
+
+
+def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, out_ps=0, need_bias=True, **kw):
+    """Weight / bias gradient in the nn.Conv2d parameter layout (fp32)."""
+    d = _lib.WgradDesc()
+    d.dtype = _lib.dtype_code(x.dtype)
+    d.N, d.H, d.W = N, H, W
+    d.Cin, d.Cin_real, d.ldx, d.xcoff = cin, cin_real, kw.get('ldx', x.shape[-1]), kw.get('xcoff', 0)
+    d.Cout, d.Cout_real, d.ldy, d.ycoff, d.out_ps = cout, cout_real, kw.get('ldy', dy.shape[-1]), kw.get(
+        'ycoff', 0), out_ps
+    d.scale = scale
+    lib = _lib.load()
+    ws_bytes = lib.sr_conv3x3_wgrad_workspace(d)
+    ws = torch.empty(ws_bytes // 4 + 1, device=x.device, dtype=torch.float32)
+    dw = torch.empty(cout_real, cin_real, 3, 3, device=x.device, dtype=torch.float32)
+    db = torch.empty(cout_real, device=x.device, dtype=torch.float32) if need_bias else None
+    _lib.check(
+        lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(dw), _lib.ptr(db),
+                             _lib.stream()))
+    return dw, db
+
+
+def nchw_to_nhwc(x, cp, dtype, shift=None, scale=None):
+    N, C, H, W = x.shape
+    y = torch.empty(N, H, W, cp, device=x.device, dtype=dtype)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_nchw_to_nhwc(_lib.dtype_code(dtype), _lib.ptr(x.contiguous()), N, C, H, W, cp, _lib.ptr(shift),
+                            _lib.ptr(scale), _lib.ptr(y), _lib.stream()))
+    return y
+
+
+def nhwc_to_nchw(x, c, scale=None, shift=None, coff=0):
+    N, H, W, ld = x.shape
+    y = torch.empty(N, c, H, W, device=x.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_nhwc_to_nchw(_lib.dtype_code(x.dtype), _lib.ptr(x), N, H, W, ld, coff, c, _lib.ptr(scale),
+                            _lib.ptr(shift), _lib.ptr(y), _lib.stream()))
+    return y
+
+
+def _out_shape(spec, N, H, W):
+    if spec.out_nchw:
+        return (N, spec.cout, H, W)
+    if spec.out_ps:
+        r = spec.out_ps
+        return (N, H * r, W * r, spec.cout // (r * r))
+    return (N, H, W, spec.cout_p)
+
+
+class _Conv3x3(torch.autograd.Function):
+    """y = beta*res + alpha*act(conv3x3(x) + b), fused pixel-shuffle / NCHW-affine store."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, spec):
+        dtype = x.dtype
+        N, H, W, _ = x.shape
+        wf, wd, bg = prepared(weight, bias, spec, dtype)
+        out_dtype = torch.float32 if spec.out_nchw else dtype
+        y = torch.empty(_out_shape(spec, N, H, W), device=x.device, dtype=out_dtype)
+        conv_fwd_raw(x, wf, bg, y, N, H, W, spec.cin_p, spec.cout_p, spec.cout, res=res,
+                     aff_scale=spec.aff_scale, aff_shift=spec.aff_shift, act=spec.act, slope=spec.slope,
+                     alpha=spec.alpha, beta=spec.beta, out_ps=spec.out_ps, out_nchw=spec.out_nchw)
+        ctx.spec = spec
+        ctx.has_res = res is not None
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, bias, y if spec.act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        spec = ctx.spec
+        x, weight, bias, y = ctx.saved_tensors
+        N, H, W, _ = x.shape
+        dtype = x.dtype
+        alpha = spec.alpha
+        if spec.out_nchw:
+            assert not spec.act
+            scale = spec.aff_scale * alpha if spec.aff_scale is not None else None
+            if scale is None and alpha != 1.0:
+                scale = torch.full((spec.cout, ), alpha, device=dy.device)
+            dY = nchw_to_nhwc(dy, spec.cout_p, dtype, scale=scale)
+            alpha = 1.0
+        else:
+            dY = dy.to(dtype).contiguous()
+            if spec.act:
+                dY = act_backward(dY, y, spec.act, spec.slope, alpha)
+                alpha = 1.0
+        _, wd, _ = prepared(weight, bias, spec, dtype)
+        dx = dres = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(N, H, W, spec.cin_p, device=x.device, dtype=dtype)
+            conv_fwd_raw(dY, wd, None, dx, N, H, W, spec.cout_p, spec.cin_p, spec.cin_p, alpha=alpha,
+                         in_ps=spec.out_ps, ldx=dY.shape[-1])
+        if ctx.has_res and ctx.needs_input_grad[1]:
+            dres = dy if spec.beta == 1.0 else dy * spec.beta
+        if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
+            dw, db = conv_wgrad_raw(dY, x, N, H, W, spec.cin_p, spec.cin, spec.cout_p, spec.cout, scale=alpha,
+                                    out_ps=spec.out_ps, need_bias=ctx.has_bias)
+        return dx, dres, dw, db, None
+
+
+def conv3x3(x, conv, res=None, **kw):
+    """Apply an nn.Conv2d(., ., 3, 1, 1) parameter module to an NHWC feature map."""
+    spec = ConvSpec(conv.in_channels, conv.out_channels, **kw)
+    return _Conv3x3.apply(x, res, conv.weight, conv.bias, spec)
+
+
+class _ResBlock(torch.autograd.Function):
+    """ResidualBlockNoBN (basicsr/archs/arch_util.py:64-88): x + rs * conv2(relu(conv1(x))).
+
+    Forward = 2 fused convs; backward = 2 dgrads (ReLU mask and residual fused in the
+    epilogues) + 2 wgrads.  Saves x and t = relu(conv1(x)).
+    """
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, spec1, spec2, res_scale):
+        dtype = x.dtype
+        N, H, W, C = x.shape
+        wf1, _, bg1 = prepared(w1, b1, spec1, dtype)
+        wf2, _, bg2 = prepared(w2, b2, spec2, dtype)
+        t = torch.empty(N, H, W, spec1.cout_p, device=x.device, dtype=dtype)
+        conv_fwd_raw(x, wf1, bg1, t, N, H, W, spec1.cin_p, spec1.cout_p, spec1.cout, act=_lib.ACT_RELU)
+        y = torch.empty(N, H, W, spec2.cout_p, device=x.device, dtype=dtype)
+        conv_fwd_raw(t, wf2, bg2, y, N, H, W, spec2.cin_p, spec2.cout_p, spec2.cout, res=x, alpha=res_scale,
+                     beta=1.0)
+        ctx.specs = (spec1, spec2)
+        ctx.res_scale = res_scale
+        ctx.save_for_backward(x, t, w1, b1, w2, b2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, t, w1, b1, w2, b2 = ctx.saved_tensors
+        spec1, spec2 = ctx.specs
+        rs = ctx.res_scale
+        dtype = x.dtype
+        N, H, W, C = x.shape
+        dy = dy.to(dtype).contiguous()
+        _, wd1, _ = prepared(w1, b1, spec1, dtype)
+        _, wd2, _ = prepared(w2, b2, spec2, dtype)
+        dz1 = torch.empty_like(t)
+        conv_fwd_raw(dy, wd2, None, dz1, N, H, W, spec2.cout_p, spec2.cin_p, spec2.cin_p, alpha=rs, gate=t,
+                     gate_slope=0.0)
+        dw2, db2 = conv_wgrad_raw(dy, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout, scale=rs)
+        dx = torch.empty_like(x)
+        conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
+        dw1, db1 = conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, scale=1.0)
+        return dx, dw1, db1, dw2, db2, None, None, None
+
+
+def res_block(x, conv1, conv2, res_scale):
+    s1 = ConvSpec(conv1.in_channels, conv1.out_channels, act=_lib.ACT_RELU)
+    s2 = ConvSpec(conv2.in_channels, conv2.out_channels, alpha=res_scale)
+    return _ResBlock.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, s1, s2, float(res_scale))
+
+
+def act_backward(dy, y, act, slope, alpha):
+    """dz = alpha * dy * act'(.) using the sign of the activation output y (relu/lrelu)."""
+    lib = _lib.load()
+    out = torch.empty_like(dy)
+    _lib.check(
+        lib.sr_act_backward(_lib.dtype_code(dy.dtype), _lib.ptr(dy), _lib.ptr(y.contiguous()), dy.numel(), act,
+                            float(slope), float(alpha), _lib.ptr(out), _lib.stream()))
+    return out
+
+
+class _ToNHWC(torch.autograd.Function):
+    """Network head: NCHW fp32 image -> NHWC feature map, y = (x - shift) * scale."""
+
+    @staticmethod
+    def forward(ctx, x, cp, dtype, shift, scale):
+        ctx.c = x.shape[1]
+        ctx.scale = scale
+        return nchw_to_nhwc(x, cp, dtype, shift=shift, scale=scale)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return nhwc_to_nchw(dy.contiguous(), ctx.c, scale=ctx.scale), None, None, None, None
+
+
+def to_nhwc(x, cp, dtype, shift=None, scale=None):
+    if x.shape[1] > cp:
+        raise ValueError('channel padding smaller than the input channels')
+    return _ToNHWC.apply(x.contiguous().float(), cp, dtype, shift, scale)
+
+
+def vec(values, device):
+    """Small per-channel fp32 constant on the device (mean / scale vectors)."""
+    return torch.as_tensor(values, dtype=torch.float32).reshape(-1).to(device)
+
+
+def inv_range(img_range, c, device):
+    return torch.full((c, ), 1.0 / img_range, dtype=torch.float32, device=device)
+
+
+def upsample_specs(scale):
+    if (scale & (scale - 1)) == 0:
+        return [2] * int(math.log(scale, 2))
+    if scale == 3:
+        return [3]
+    raise ValueError(f'scale {scale} is not supported. Supported scales: 2^n and 3.')

@@ -1,0 +1,150 @@
+"""GPU parity of the HIP 3x3 conv path against the CPU oracle (torch fp32 restatement).
+
+Tolerances: fp32 mode runs exact-f32 MFMA (v_mfma_f32_16x16x4_f32) and differs from the
+CPU only by summation order -> |err| <= 1e-4 * max(1, |ref|max).  bf16 mode rounds inputs
+and weights to bf16 (8 significant bits) and accumulates in fp32 -> compared against the
+oracle evaluated on the same bf16-rounded operands, |err| <= 2e-2 * |ref|max.
+"""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from basicsr4rs_amd import _lib
+from basicsr4rs_amd.ops import conv as C
+from basicsr4rs_amd.ops.layout import pixel_shuffle, pixel_unshuffle
+from oracle import nets as O
+
+pytestmark = pytest.mark.gpu
+
+
+def nhwc_to_nchw_t(y, c):
+    return y[..., :c].permute(0, 3, 1, 2).float()
+
+
+def rel_err(a, b):
+    return (a - b).abs().max().item() / max(1.0, b.abs().max().item())
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+CASES = [
+    # (N, H, W, cin, cout, kwargs)
+    (2, 16, 16, 64, 64, {}),
+    (1, 12, 20, 3, 64, {}),
+    (2, 8, 8, 24, 40, {'act': _lib.ACT_RELU}),
+    (1, 16, 16, 64, 48, {'act': _lib.ACT_LRELU, 'slope': 0.2}),
+    (2, 8, 8, 64, 256, {'out_ps': 2}),
+    (1, 8, 8, 32, 288, {'out_ps': 3}),
+    (2, 16, 16, 64, 3, {'out_nchw': True}),
+    (1, 64, 64, 256, 256, {}),
+]
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('case', CASES)
+def test_conv3x3_fwd_bwd(cuda, case, dtype):
+    N, H, W, cin, cout, kw = case
+    torch.manual_seed(0)
+    conv = nn.Conv2d(cin, cout, 3, 1, 1)
+    x = torch.randn(N, cin, H, W)
+    w, b = conv.weight.detach(), conv.bias.detach()
+    if dtype == torch.bfloat16:
+        xr, wr = bf(x), bf(w)
+    else:
+        xr, wr = x.clone(), w
+    xr.requires_grad_(True)
+    wr = wr.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = F.conv2d(xr, wr, br, padding=1)
+    if kw.get('act') == _lib.ACT_RELU:
+        ref = F.relu(ref)
+    elif kw.get('act') == _lib.ACT_LRELU:
+        ref = F.leaky_relu(ref, kw['slope'])
+    if kw.get('out_ps'):
+        ref = O.pixel_shuffle(ref, kw['out_ps'])
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+
+    gconv = copy.deepcopy(conv).to(cuda)
+    xg = x.to(cuda).requires_grad_(True)
+    h = C.to_nhwc(xg, C.pad8(cin), dtype)
+    y = C.conv3x3(h, gconv, **kw)
+    if kw.get('out_nchw'):
+        yn = y
+    else:
+        yn = nhwc_to_nchw_t(y, ref.shape[1])
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert yn.shape == ref.shape
+    assert rel_err(yn.cpu(), ref.detach()) < tol
+    (yn * g.to(cuda)).sum().backward()
+    assert rel_err(gconv.weight.grad.cpu(), wr.grad) < tol * 2
+    assert rel_err(gconv.bias.grad.cpu(), br.grad) < tol * 2
+    assert rel_err(xg.grad.cpu(), xr.grad) < tol * 2
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_residual_block(cuda, dtype):
+    from basicsr4rs_amd.archs.arch_util import ResidualBlockNoBN
+    torch.manual_seed(1)
+    blk = ResidualBlockNoBN(64, res_scale=0.1)
+    x = torch.randn(2, 64, 16, 16)
+    sd = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    if dtype == torch.bfloat16:
+        sd = {k: (bf(v) if k.endswith('weight') else v) for k, v in sd.items()}
+        xr = bf(x)
+    else:
+        xr = x
+    sd = {k: v.requires_grad_(True) for k, v in sd.items()}
+    xr = xr.clone().requires_grad_(True)
+    sd2 = {f'blk.{k}': v for k, v in sd.items()}
+    ref = O.residual_block(xr, sd2, 'blk', 0.1)
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    gb = copy.deepcopy(blk).to(cuda)
+    xg = x.to(cuda).requires_grad_(True)
+    h = C.to_nhwc(xg, 64, dtype)
+    y = nhwc_to_nchw_t(gb(h), 64)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert rel_err(y.cpu(), ref.detach()) < tol
+    (y * g.to(cuda)).sum().backward()
+    assert rel_err(xg.grad.cpu(), xr.grad) < tol * 2
+    for n, p in gb.named_parameters():
+        assert rel_err(p.grad.cpu(), sd[n].grad) < tol * 4, n
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('r', [2, 3])
+def test_pixel_shuffle_bit_exact(cuda, dtype, r):
+    x = torch.randn(2, 4 * r * r, 5, 7, dtype=dtype)
+    y = pixel_shuffle(x.to(cuda), r).cpu()
+    assert torch.equal(y, O.pixel_shuffle(x, r))
+    assert torch.equal(y, nn.PixelShuffle(r)(x))
+    z = pixel_unshuffle(y.to(cuda), r).cpu()
+    assert torch.equal(z, x)
+    assert torch.equal(z, O.pixel_unshuffle(y, r))
+
+
+def test_edsr_m_parity_fp32(cuda):
+    from basicsr4rs_amd.archs import build_network
+    torch.manual_seed(42)
+    net = build_network(dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=4, upscale=4))
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in net.state_dict().items()}
+    x = torch.rand(1, 3, 64, 64, generator=torch.Generator().manual_seed(0))
+    gt = torch.rand(1, 3, 256, 256, generator=torch.Generator().manual_seed(1))
+    ref = O.edsr(sd, x, num_block=4, upscale=4)
+    O.l1_loss(ref, gt).backward()
+    gnet = copy.deepcopy(net).to(cuda)
+    out = gnet(x.to(cuda))
+    err = (out.cpu() - ref.detach()).abs().max().item()
+    assert err < 1e-3, err
+    mse = ((out.cpu() - ref.detach())**2).mean().item()
+    psnr = 10 * torch.log10(torch.tensor(1.0 / max(mse, 1e-20))).item()
+    assert psnr > 60, psnr
+    (out - gt.to(cuda)).abs().mean().backward()
+    for n, p in gnet.named_parameters():
+        assert rel_err(p.grad.cpu(), sd[n].grad) < 1e-3, n
