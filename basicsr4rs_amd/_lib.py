@@ -50,7 +50,7 @@ SIGNATURES = {
     'sr_l1_loss': (_i, [_vp, _vp, _i64, _f, _i, _vp, _vp, _vp, _sz, _vp]),
     'sr_l1_loss_workspace': (_sz, [_i64]),
     'sr_act_backward': (_i, [_i, _vp, _vp, _i64, _i, _f, _f, _vp, _vp]),
-    'sr_adam_ema': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _f, _f, _vp]),
+    'sr_adam_ema': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _f, _f, _f, _vp]),
 }
 
 _LIB = None

@@ -126,12 +126,13 @@ __global__ void l1_final_kernel(const float* __restrict__ partial, int nb, float
 
 __global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                 float* __restrict__ v, float* __restrict__ ema, int64_t n, float lr,
-                                float beta1, float beta2, float eps, float bc1, float bc2, float decay) {
+                                float beta1, float beta2, float eps, float bc1, float bc2, float decay,
+                                float gscale) {
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = g[i];
+    const float gi = g[i] * gscale;
     float mi = m[i], vi = v[i];
     mi = mi + (1.f - beta1) * (gi - mi);          // exp_avg.lerp_(grad, 1 - beta1)
     vi = vi * beta2 + (1.f - beta2) * gi * gi;    // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
@@ -254,11 +255,11 @@ int sr_l1_loss(const float* pred, const float* gt, int64_t n, float weight, int 
 }
 
 int sr_adam_ema(float* p, const float* g, float* m, float* v, float* ema, int64_t n, float lr, float beta1,
-                float beta2, float eps, float bc1, float bc2, float ema_decay, void* stream) {
+                float beta2, float eps, float bc1, float bc2, float ema_decay, float grad_scale, void* stream) {
   if (!p || !g || !m || !v || n <= 0) return sr_fail(SR_EINVAL, "adam_ema: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(adam_ema_kernel, dim3(grid_for(n, 8192)), dim3(256), 0, s, p, g, m, v, ema, n, lr,
-                     beta1, beta2, eps, bc1, bc2, ema_decay);
+                     beta1, beta2, eps, bc1, bc2, ema_decay, grad_scale);
   return sr_check(hipGetLastError(), "adam_ema launch");
 }
 

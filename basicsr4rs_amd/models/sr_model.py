@@ -1,0 +1,157 @@
+"""Single-image SR model (mirror of basicsr/models/sr_model.py:16-279 and the AMP variant
+basicsr/models/srrs_model.py:33-88).
+
+The train step ``optimize_parameters`` is the north-star hot path: zero_grad -> net_g
+forward on the HIP engine -> L1 (fused HIP reduction + gradient) -> backward (HIP conv
+dgrad/wgrad; bucketed RCCL all-reduce launched from backward hooks when distributed) ->
+one fused Adam + EMA kernel over the flat parameter vector.  No host synchronisation
+inside the step (the loss log is reduced when read).
+
+AMP: ``train.use_amp`` (SRRSModel's key) turns on autocast; the HIP kernels then compute
+in bf16 (the reference uses fp16 + GradScaler; bf16 needs no loss scaling).
+"""
+from collections import OrderedDict
+from os import path as osp
+
+import torch
+
+from ..archs import build_network
+from ..losses import build_loss
+from ..metrics import calculate_metric
+from ..utils.flat import FlatParams
+from ..utils.img_util import imwrite, tensor2img
+from ..utils.registry import MODEL_REGISTRY
+from .base_model import BaseModel
+
+
+@MODEL_REGISTRY.register()
+class SRModel(BaseModel):
+
+    def build_optional_loss(self, opt_dict, key):
+        if key not in opt_dict or opt_dict[key] is None:
+            return None
+        if key == 'perceptual_opt':
+            raise NotImplementedError('PerceptualLoss needs pretrained VGG weights; out of scope (SURVEY.md §2a)')
+        return build_loss(opt_dict[key]).to(self.device)
+
+    def __init__(self, opt):
+        super().__init__(opt)
+        self.net_g = build_network(opt['network_g'])
+        self.net_g = self.model_to_device(self.net_g)
+        self.print_network(self.net_g)
+        load_path = self.opt.get('path', {}).get('pretrain_network_g', None)
+        if load_path is not None:
+            param_key = self.opt['path'].get('param_key_g', 'params')
+            self.load_network(self.net_g, load_path, self.opt['path'].get('strict_load_g', True), param_key)
+        if self.is_train:
+            self.init_training_settings()
+
+    def init_training_settings(self):
+        self.net_g.train()
+        train_opt = self.opt['train']
+        self.use_amp = bool(train_opt.get('use_amp', False))
+        self.ema_decay = train_opt.get('ema_decay', 0)
+        if self.ema_decay > 0:
+            self.net_g_ema = build_network(self.opt['network_g']).to(self.device)
+            self.flat_ema = FlatParams(self.net_g_ema, with_grad=False)
+            load_path = self.opt.get('path', {}).get('pretrain_network_g', None)
+            if load_path is not None:
+                self.load_network(self.net_g_ema, load_path, self.opt['path'].get('strict_load_g', True), 'params_ema')
+            else:
+                self.model_ema(0)
+            self.net_g_ema.eval()
+        self.cri_pix = self.build_optional_loss(train_opt, 'pixel_opt')
+        self.cri_perceptual = self.build_optional_loss(train_opt, 'perceptual_opt')
+        if self.cri_pix is None and self.cri_perceptual is None:
+            raise ValueError('Both pixel and perceptual losses are None.')
+        self.setup_optimizers()
+        self.setup_schedulers()
+
+    def setup_optimizers(self):
+        train_opt = self.opt['train']
+        optim_opt = dict(train_opt['optim_g'])
+        optim_type = optim_opt.pop('type')
+        self.optimizer_g = self.get_optimizer(optim_type, self.flat_g.params, **optim_opt)
+        self.optimizers.append(self.optimizer_g)
+
+    def feed_data(self, data):
+        self.lq = data['lq'].to(self.device, non_blocking=True)
+        if 'gt' in data:
+            self.gt = data['gt'].to(self.device, non_blocking=True)
+
+    def optimize_parameters(self, current_iter):
+        self.optimizer_g.zero_grad()
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.use_amp):
+            self.output = self.net_g(self.lq)
+        l_total = 0
+        loss_dict = OrderedDict()
+        if self.cri_pix:
+            l_pix = self.cri_pix(self.output, self.gt)
+            l_total += l_pix
+            loss_dict['l_pix'] = l_pix
+        l_total.backward()
+        self.sync_gradients()
+        if hasattr(self.optimizer_g, 'fp') and self.ema_decay > 0 and self.flat_ema is not None:
+            self.optimizer_g.step(ema=self.flat_ema, ema_decay=self.ema_decay)
+        else:
+            self.optimizer_g.step()
+            if self.ema_decay > 0:
+                self.model_ema(decay=self.ema_decay)
+        self.log_dict = self.reduce_loss_dict(loss_dict)
+
+    def test(self):
+        net = self.net_g_ema if hasattr(self, 'net_g_ema') else self.net_g
+        was_training = self.net_g.training
+        net.eval()
+        with torch.no_grad():
+            self.output = net(self.lq)
+        if net is self.net_g and was_training:
+            self.net_g.train()
+
+    def nondist_validation(self, dataloader, current_iter, tb_logger, save_img):
+        dataset_name = dataloader.dataset.opt['name']
+        with_metrics = self.opt['val'].get('metrics') is not None
+        if with_metrics:
+            if not hasattr(self, 'metric_results'):
+                self.metric_results = {metric: 0 for metric in self.opt['val']['metrics'].keys()}
+            self._initialize_best_metric_results(dataset_name)
+            self.metric_results = {metric: 0 for metric in self.metric_results}
+        metric_data = dict()
+        idx = -1
+        for idx, val_data in enumerate(dataloader):
+            img_name = osp.splitext(osp.basename(val_data['lq_path'][0]))[0] if 'lq_path' in val_data else str(idx)
+            self.feed_data(val_data)
+            self.test()
+            visuals = self.get_current_visuals(current_iter)
+            sr_img = tensor2img([visuals['result']])
+            metric_data['img'] = sr_img
+            if 'gt' in visuals:
+                metric_data['img2'] = tensor2img([visuals['gt']])
+                del self.gt
+            del self.lq
+            del self.output
+            if save_img:
+                save_img_path = osp.join(self.opt['path']['visualization'], img_name, f'{img_name}_{current_iter}.png')
+                imwrite(sr_img, save_img_path)
+            if with_metrics:
+                for name, opt_ in self.opt['val']['metrics'].items():
+                    self.metric_results[name] += calculate_metric(metric_data, opt_)
+        if with_metrics:
+            for metric in self.metric_results.keys():
+                self.metric_results[metric] /= (idx + 1)
+                self._update_best_metric_result(dataset_name, metric, self.metric_results[metric], current_iter)
+
+    def get_current_visuals(self, current_iter=None):
+        out_dict = OrderedDict()
+        out_dict['lq'] = self.lq.detach().cpu()
+        out_dict['result'] = self.output.detach().float().cpu()
+        if hasattr(self, 'gt'):
+            out_dict['gt'] = self.gt.detach().cpu()
+        return out_dict
+
+    def save(self, epoch, current_iter):
+        if hasattr(self, 'net_g_ema'):
+            self.save_network([self.net_g, self.net_g_ema], 'net_g', current_iter, param_key=['params', 'params_ema'])
+        else:
+            self.save_network(self.net_g, 'net_g', current_iter)
+        self.save_training_state(epoch, current_iter)

@@ -1,0 +1,189 @@
+"""Flat fp32 parameter / gradient storage, fused Adam+EMA, bucketed gradient all-reduce.
+
+The reference's train step (basicsr/models/sr_model.py:91-118) is: zero_grad, forward, loss,
+backward (DDP all-reduce of every gradient, basicsr/models/base_model.py:87-105), Adam step
+(torch.optim.Adam, base_model.py:107-124), EMA (base_model.py:75-82).  Here the parameters
+of the net (and of its EMA copy) are re-pointed into ONE contiguous fp32 buffer each, and
+their ``.grad`` into one contiguous gradient buffer, so that
+
+* the gradient all-reduce runs on contiguous bucket slices of that buffer, launched from
+  post-accumulate-grad hooks while backward is still running (RCCL over xGMI when the
+  process group is NCCL; gloo on CPU for tests);
+* Adam + EMA is ONE HIP kernel over the flat vectors (sr_adam_ema), with the DDP 1/world
+  average folded in as a gradient scale.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+from .. import _lib
+from ..ops.conv import bump_param_epoch
+
+
+def _params(module):
+    return [p for p in module.parameters() if p.requires_grad]
+
+
+class FlatParams:
+    """Re-point ``module``'s trainable parameters (and grads) into contiguous fp32 buffers."""
+
+    def __init__(self, module, with_grad=True):
+        self.params = _params(module)
+        self.numels = [p.numel() for p in self.params]
+        self.offsets = [0]
+        for n in self.numels:
+            self.offsets.append(self.offsets[-1] + n)
+        dev = self.params[0].device
+        self.flat = torch.empty(self.offsets[-1], dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(self.offsets[-1], dtype=torch.float32, device=dev) if with_grad else None
+        with torch.no_grad():
+            for p, o, n in zip(self.params, self.offsets, self.numels):
+                self.flat[o:o + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + n].view_as(p)
+                if with_grad:
+                    p.grad = self.grad[o:o + n].view_as(p)
+
+    def view(self, buf, i):
+        return buf[self.offsets[i]:self.offsets[i] + self.numels[i]].view_as(self.params[i])
+
+    def zero_grad(self):
+        self.grad.zero_()
+        for i, p in enumerate(self.params):  # autograd may have replaced a view; restore it
+            if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[i]:
+                p.grad = self.view(self.grad, i)
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (no amsgrad / weight decay) as one HIP kernel over a FlatParams.
+
+    ``state_dict()`` has torch.optim.Adam's layout (per-param ``step``, ``exp_avg``,
+    ``exp_avg_sq``), so training states saved by the reference load here and vice versa.
+    ``step(ema=FlatParams, ema_decay=d)`` also applies the EMA update in the same pass.
+    """
+
+    def __init__(self, flat, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False):
+        if weight_decay != 0 or amsgrad:
+            raise NotImplementedError('FusedAdam: weight_decay / amsgrad are not used by the SR configs')
+        super().__init__(flat.params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False))
+        self.fp = flat
+        self.m = torch.zeros_like(flat.flat)
+        self.v = torch.zeros_like(flat.flat)
+        self.nstep = 0
+        self.grad_scale = 1.0
+        self._bind_state()
+
+    def _bind_state(self):
+        for i, p in enumerate(self.fp.params):
+            self.state[p] = {'step': torch.tensor(float(self.nstep)), 'exp_avg': self.fp.view(self.m, i),
+                             'exp_avg_sq': self.fp.view(self.v, i)}
+
+    def zero_grad(self, set_to_none=False):
+        self.fp.zero_grad()
+
+    @torch.no_grad()
+    def step(self, closure=None, ema=None, ema_decay=0.0):
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        b1, b2 = g['betas']
+        self.nstep += 1
+        lib = _lib.load()
+        _lib.check(
+            lib.sr_adam_ema(_lib.ptr(self.fp.flat), _lib.ptr(self.fp.grad), _lib.ptr(self.m), _lib.ptr(self.v),
+                            _lib.ptr(ema.flat if ema is not None else None), self.fp.flat.numel(), float(g['lr']),
+                            float(b1), float(b2), float(g['eps']), 1.0 - b1**self.nstep, 1.0 - b2**self.nstep,
+                            float(ema_decay), float(self.grad_scale), _lib.stream()))
+        for p in self.fp.params:
+            self.state[p]['step'].fill_(float(self.nstep))
+        bump_param_epoch()
+        return loss
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        steps = [float(s['step']) for s in self.state.values() if 'step' in s]
+        with torch.no_grad():
+            for i, p in enumerate(self.fp.params):
+                st = self.state[p]
+                self.fp.view(self.m, i).copy_(st['exp_avg'])
+                self.fp.view(self.v, i).copy_(st['exp_avg_sq'])
+        self.nstep = int(max(steps)) if steps else 0
+        self._bind_state()
+
+
+def ema_copy(flat_dst, flat_src, decay):
+    """EMA of parameters only (base_model.py:75-82): dst = dst*decay + src*(1-decay)."""
+    with torch.no_grad():
+        flat_dst.flat.mul_(decay).add_(flat_src.flat, alpha=1 - decay)
+    bump_param_epoch()
+
+
+class GradBucketReducer:
+    """Bucketed gradient all-reduce overlapped with backward (DDP semantics: average).
+
+    Buckets are contiguous slices of ``flat.grad`` in reverse parameter order (the order
+    backward produces them), ``bucket_mb`` MiB each (DDP default 25).  A bucket's
+    ``all_reduce`` is issued (async) from the post-accumulate-grad hook of the last of its
+    parameters to finish; ``wait()`` joins them before the optimizer.  The 1/world average is
+    left to the optimizer (FusedAdam.grad_scale) so no extra pass over the gradients runs.
+    """
+
+    def __init__(self, flat, group=None, bucket_mb=25.0):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group)
+        n = len(flat.params)
+        cap = int(bucket_mb * 1024 * 1024 / 4)
+        self.buckets = []  # (lo, hi, param indices)
+        cur, lo_idx = [], None
+        for i in reversed(range(n)):
+            cur.append(i)
+            lo, hi = flat.offsets[min(cur)], flat.offsets[max(cur) + 1]
+            if hi - lo >= cap:
+                self.buckets.append((lo, hi, list(cur)))
+                cur = []
+        if cur:
+            self.buckets.append((flat.offsets[min(cur)], flat.offsets[max(cur) + 1], list(cur)))
+        self.bucket_of = {}
+        for b, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self.bucket_of[i] = b
+        self.pending = [0] * len(self.buckets)
+        self.handles = []
+        self.hooks = []
+        for i, p in enumerate(flat.params):
+            self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.reset()
+
+    def reset(self):
+        self.pending = [len(idx) for (_, _, idx) in self.buckets]
+        self.handles = []
+
+    def _make_hook(self, i):
+
+        def hook(_p):
+            b = self.bucket_of[i]
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                lo, hi, _ = self.buckets[b]
+                self.handles.append(dist.all_reduce(self.flat.grad[lo:hi], group=self.group, async_op=True))
+
+        return hook
+
+    def wait(self):
+        """Join outstanding bucket reductions; reduce any bucket whose hooks did not fire
+        (parameters unused in this step) so every rank issues the same collectives."""
+        for b, n in enumerate(self.pending):
+            if n > 0:
+                lo, hi, _ = self.buckets[b]
+                self.handles.append(dist.all_reduce(self.flat.grad[lo:hi], group=self.group, async_op=True))
+        for h in self.handles:
+            h.wait()
+        self.reset()
+
+    def broadcast_params(self, src=0):
+        dist.broadcast(self.flat.flat, src=src, group=self.group)
+        bump_param_epoch()
+
+
+def bucket_count(nbytes, bucket_mb=25.0):
+    return max(1, math.ceil(nbytes / (bucket_mb * 1024 * 1024)))

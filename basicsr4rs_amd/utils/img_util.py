@@ -1,0 +1,61 @@
+"""Tensor <-> uint8 image helpers (mirror of basicsr/utils/img_util.py:40-96).
+
+OpenCV is not available in this image: RGB->BGR is a channel flip and ``imwrite`` writes
+PNG with the standard library (zlib) so validation images can still be saved.
+"""
+import os
+import struct
+import zlib
+
+import numpy as np
+import torch
+
+
+def tensor2img(tensor, rgb2bgr=True, out_type=np.uint8, min_max=(0, 1)):
+    """Clamp to min_max, scale to [0,1], CHW->HWC, RGB->BGR, *255 and round for uint8."""
+    if not (torch.is_tensor(tensor) or (isinstance(tensor, list) and all(torch.is_tensor(t) for t in tensor))):
+        raise TypeError(f'tensor or list of tensors expected, got {type(tensor)}')
+    if torch.is_tensor(tensor):
+        tensor = [tensor]
+    result = []
+    for t in tensor:
+        t = t.squeeze(0).float().detach().cpu().clamp_(*min_max)
+        t = (t - min_max[0]) / (min_max[1] - min_max[0])
+        if t.dim() == 3:
+            img = t.numpy().transpose(1, 2, 0)
+            if img.shape[2] == 1:
+                img = np.squeeze(img, axis=2)
+            elif rgb2bgr:
+                img = img[..., ::-1]
+        elif t.dim() == 2:
+            img = t.numpy()
+        else:
+            raise TypeError(f'Only support 3D or 2D tensor. But received with dimension: {t.dim()}')
+        if out_type == np.uint8:
+            img = (img * 255.0).round()
+        result.append(np.ascontiguousarray(img).astype(out_type))
+    return result[0] if len(result) == 1 else result
+
+
+def imwrite(img, file_path, params=None, auto_mkdir=True):
+    """Write a uint8 HWC BGR (or HW gray) image as PNG."""
+    if auto_mkdir:
+        os.makedirs(os.path.dirname(os.path.abspath(file_path)), exist_ok=True)
+    img = np.asarray(img, dtype=np.uint8)
+    if img.ndim == 3:
+        img = img[..., ::-1]  # BGR -> RGB for PNG
+        h, w, c = img.shape
+        ctype = {3: 2, 4: 6, 1: 0}[c]
+    else:
+        h, w = img.shape
+        c, ctype = 1, 0
+    raw = b''.join(b'\x00' + img[y].tobytes() for y in range(h))
+
+    def chunk(tag, data):
+        return struct.pack('>I', len(data)) + tag + data + struct.pack('>I', zlib.crc32(tag + data) & 0xffffffff)
+
+    png = b'\x89PNG\r\n\x1a\n' + chunk(b'IHDR', struct.pack('>IIBBBBB', w, h, 8, ctype, 0, 0, 0))
+    png += chunk(b'IDAT', zlib.compress(raw, 6)) + chunk(b'IEND', b'')
+    with open(file_path, 'wb') as f:
+        f.write(png)
+    return True

@@ -1,0 +1,180 @@
+"""North-star benchmark: HR-pixels/sec of the x4 SR train step (BASELINE.json:metric).
+
+Workload (BASELINE.json configs[1]): EDSR_Lx4 (32 ResidualBlockNoBN, nf=256, res_scale=0.1)
+train step in bf16, per-GPU batch 32 x 3 x 64 x 64 LR -> 32 x 3 x 256 x 256 HR (HR tile
+256 = gt_size).  A step = SRModel.optimize_parameters: forward, L1 loss,
+backward, gradient all-reduce (N>1, RCCL), fused Adam(0.9, 0.99) + EMA(0.999).  Inputs
+are synthetic U[0,1) tiles already resident in HBM (seed 0 / 1, + rank).
+
+Run: python bench.py --gpus N --steps K --warmup W   (N>1 under torch.distributed.run).
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events over
+the timed region) and the CPU baseline (oracle restatement on the host cores, bounded
+sample, rank 0 at N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+EDSR_L = dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=256, num_block=32, upscale=4, res_scale=0.1,
+              img_range=255., rgb_mean=[0.4488, 0.4371, 0.4040])
+
+
+def make_opt(world, batch):
+    return dict(
+        model_type='SRModel', is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
+        network_g=dict(EDSR_L),
+        train=dict(ema_decay=0.999, use_amp=True,
+                   optim_g=dict(type='Adam', lr=1e-4, weight_decay=0, betas=[0.9, 0.99]),
+                   scheduler=dict(type='MultiStepLR', milestones=[200000], gamma=0.5),
+                   pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')),
+        path={})
+
+
+def cpu_baseline(seconds=20.0):
+    """Oracle EDSR_Lx4 train step (fwd + L1 + bwd + Adam) in torch-CPU fp32 at batch 1."""
+    from basicsr4rs_amd.archs import build_network
+    from oracle import nets as O
+    torch.manual_seed(42)
+    net = build_network(dict(EDSR_L))
+    params = {k: v.detach().clone().requires_grad_(True) for k, v in net.state_dict().items()}
+    opt = torch.optim.Adam(list(params.values()), lr=1e-4, betas=(0.9, 0.99))
+    g0, g1 = torch.Generator().manual_seed(0), torch.Generator().manual_seed(1)
+    lq = torch.rand(1, 3, 64, 64, generator=g0)
+    gt = torch.rand(1, 3, 256, 256, generator=g1)
+
+    def step():
+        opt.zero_grad()
+        out = O.edsr(params, lq, num_block=32, upscale=4, res_scale=0.1)
+        O.l1_loss(out, gt).backward()
+        opt.step()
+
+    step()  # warm-up
+    times = []
+    t_all = time.time()
+    while len(times) < 3 or (time.time() - t_all < seconds and len(times) < 10):
+        t = time.time()
+        step()
+        times.append(time.time() - t)
+        if time.time() - t_all > seconds and len(times) >= 1:
+            break
+    times.sort()
+    t_med = times[len(times) // 2]
+    return {'value': 256 * 256 / t_med, 'unit': 'HR-pixels/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'sample': f'oracle EDSR_Lx4 fp32 train step, batch 1 (64x64 LR -> 256x256 HR), median of {len(times)} '
+                      f'steps after 1 warm-up, torch CPU threads={torch.get_num_threads()}'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-trace', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        from basicsr4rs_amd.utils.dist_util import init_dist
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        init_dist('pytorch', backend='nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    from basicsr4rs_amd.utils import ktrace
+
+    torch.manual_seed(42)
+    opt = make_opt(world, args.batch)
+    opt['rank'] = rank
+    model = build_model(opt)
+    B = args.batch
+    g0 = torch.Generator(device=dev).manual_seed(0 + rank)
+    g1 = torch.Generator(device=dev).manual_seed(1 + rank)
+    lq = torch.rand(B, 3, 64, 64, generator=g0, device=dev)
+    gt = torch.rand(B, 3, 256, 256, generator=g1, device=dev)
+    model.feed_data({'lq': lq, 'gt': gt})
+
+    it = 0
+    for _ in range(args.warmup):
+        it += 1
+        model.update_learning_rate(it)
+        model.optimize_parameters(it)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if not args.no_trace:
+        ktrace.start()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        it += 1
+        model.update_learning_rate(it)
+        model.optimize_parameters(it)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kstats = ktrace.stop() if not args.no_trace else {}
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    loss = model.get_current_log().get('l_pix', float('nan'))
+
+    hr_px = world * B * 256 * 256 * args.steps
+    value = hr_px / dt
+    roof = None
+    if kstats:
+        name, st = max(kstats.items(), key=lambda kv: kv[1]['ms'])
+        avg_ms = st['ms'] / st['count']
+        achieved = st['flops'] / (st['ms'] * 1e-3) / 1e12
+        roof = {'bound': 'mfma', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS,
+                'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+                'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // args.steps,
+                'flops_per_launch': st['flops'] / st['count'],
+                'share_of_step': round(st['ms'] * 1e-3 / dt, 3)}
+        roof['kernels'] = {
+            k: {'count': v['count'] // args.steps, 'avg_us': round(v['ms'] / v['count'] * 1e3, 1),
+                'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 else None,
+                'ms_per_step': round(v['ms'] / args.steps, 3)}
+            for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]['ms'])
+        }
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+    if rank == 0:
+        line = {
+            'metric': 'HR-pixels/sec/node (x4 SR train step)', 'value': round(value, 1), 'unit': 'HR-pixels/s',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
+            'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
+            'config': {'workload': 'EDSR_Lx4 train step (32 RB, nf 256, res_scale 0.1), LR 64x64 -> HR 256x256',
+                       'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world}',
+                       'model': 'EDSR_Lx4'},
+            'train_flops_per_hr_px': 18.85e6, 'model_tflops': round(18.85e6 * value / 1e12, 1),
+            'last_loss': loss, 'roofline': roof, 'cpu_baseline': cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

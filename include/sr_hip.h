@@ -126,11 +126,12 @@ size_t sr_l1_loss_workspace(int64_t n);
 int sr_act_backward(int dtype, const void* dy, const void* y, int64_t n, int act, float slope, float alpha,
                     void* out, void* stream);
 /* Fused Adam (torch.optim.Adam semantics, no amsgrad/weight decay) + EMA of a flat fp32
- * parameter vector: p, exp_avg, exp_avg_sq updated in place; if ema != NULL,
- * ema = ema*decay + p*(1-decay) after the step (basicsr/models/base_model.py:75-82). */
+ * parameter vector: g is scaled by grad_scale (DDP 1/world_size averaging), p, exp_avg,
+ * exp_avg_sq updated in place; if ema != NULL, ema = ema*decay + p*(1-decay) after the step
+ * (basicsr/models/base_model.py:75-82).  bc1/bc2 = 1 - beta^step. */
 int sr_adam_ema(float* p, const float* g, float* m, float* v, float* ema, int64_t n, float lr,
                 float beta1, float beta2, float eps, float bc1, float bc2, float ema_decay,
-                void* stream);
+                float grad_scale, void* stream);
 
 #ifdef __cplusplus
 }
