@@ -65,6 +65,109 @@ SR_DEV void mfma_chunk<float>(const u32x4& a, const u32x4& b, f32x4& acc) {
 // Byte offset of chunk c of row r inside a [rows][128 B] swizzled image.
 SR_DEV uint32_t swz128(uint32_t r, uint32_t c) { return r * 128u + ((c ^ (r & 7u)) << 4); }
 
+// Fused epilogue over a [ROWS][BN] fp32 tile staged in LDS (row stride CSTR floats):
+// bias, activation, gate, alpha, residual, then a plain / pixel-shuffled NHWC store of
+// 8-channel (16-byte bf16 / 32-byte f32) groups, or the fp32 NCHW affine store.
+template <typename T, int ROWS, int BN, int NT>
+SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, int n0, int tid) {
+  constexpr int SZ = Elt<T>::SIZE;
+  if (a.out_nchw) {
+    float* y = (float*)a.y;
+    const int HW = a.H * a.W;
+    for (int idx = tid; idx < ROWS * BN; idx += NT) {
+      const int row = idx % ROWS, col = idx / ROWS;
+      const int m = m0 + row, n = n0 + col;
+      if (m >= a.M || n >= a.Cout_real) continue;
+      float v = Cs[row * CSTR + col] + (a.bias ? a.bias[n] : 0.f);
+      v = act_apply(v, a.act, a.slope) * a.alpha;
+      v = v * (a.aff_scale ? a.aff_scale[n] : 1.f) + (a.aff_shift ? a.aff_shift[n] : 0.f);
+      const int img = m / HW, pix = m - img * HW;
+      y[((size_t)img * a.Cout_real + n) * HW + pix] = v;
+    }
+    return;
+  }
+  constexpr int CG = BN / 8;  // 8-channel groups per row
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  for (int idx = tid; idx < ROWS * CG; idx += NT) {
+    const int row = idx / CG, cg = idx % CG;
+    const int m = m0 + row, n = n0 + cg * 8;
+    if (m >= a.M || n >= a.Cout) continue;
+    float v[8];
+    const f32x4 c0 = *(const f32x4*)(Cs + row * CSTR + cg * 8);
+    const f32x4 c1 = *(const f32x4*)(Cs + row * CSTR + cg * 8 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = c0[j]; v[4 + j] = c1[j]; }
+    if (a.bias) {
+      const f32x4 b0 = *(const f32x4*)(a.bias + n);
+      const f32x4 b1 = *(const f32x4*)(a.bias + n + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+    if (a.gate) {
+      float g[8];
+      const uint32_t off = (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ);
+      if constexpr (SZ == 2) {
+        u32x4 gg = buf_load16(gr, off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          g[2 * j] = bf16_to_f32(gg[j] & 0xffff);
+          g[2 * j + 1] = bf16_to_f32(gg[j] >> 16);
+        }
+      } else {
+        u32x4 g0 = buf_load16(gr, off), g1 = buf_load16(gr, off + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { g[j] = __uint_as_float(g0[j]); g[4 + j] = __uint_as_float(g1[j]); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+    if (a.res) {
+      float rv[8];
+      const uint32_t off = (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ);
+      if constexpr (SZ == 2) {
+        u32x4 rr4 = buf_load16(rr, off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          rv[2 * j] = bf16_to_f32(rr4[j] & 0xffff);
+          rv[2 * j + 1] = bf16_to_f32(rr4[j] >> 16);
+        }
+      } else {
+        u32x4 r0 = buf_load16(rr, off), r1 = buf_load16(rr, off + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { rv[j] = __uint_as_float(r0[j]); rv[4 + j] = __uint_as_float(r1[j]); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = a.beta * rv[j] + v[j];
+    }
+    size_t dst;  // element offset of the 8-channel group
+    if (a.out_ps == 0) {
+      dst = (size_t)m * a.ldy + a.ycoff + n;
+    } else {
+      const int r = a.out_ps;
+      const int s = (int)fdiv((uint32_t)n, a.fd_cps);
+      const int c = n - s * a.fd_cps.d;
+      const int si = s / r, sj = s - (s / r) * r;
+      const int xq = (int)fdiv((uint32_t)m, a.fd_W);
+      const int xx = m - xq * a.W;  // xq = n*H + y
+      dst = ((size_t)(xq * r + si) * (a.W * r) + xx * r + sj) * a.ldy + a.ycoff + c;
+    }
+    if constexpr (SZ == 2) {
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      *(u32x4*)((bf16_t*)a.y + dst) = o;
+    } else {
+      *(f32x4*)((float*)a.y + dst) = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)((float*)a.y + dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int PER = Elt<T>::PER16;
@@ -200,103 +303,161 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         Cs[row * CSTR + col] = acc[i][j][r];
       }
   __syncthreads();
+  epilogue_tile<T, BM, BN, 256>(a, Cs, CSTR, m0, n0, tid);
+}
 
-  if (a.out_nchw) {
-    // fp32 NCHW store with per-channel affine; consecutive threads -> consecutive pixels.
-    float* y = (float*)a.y;
-    const int HW = a.H * a.W;
-    for (int idx = tid; idx < BM * BN; idx += 256) {
-      const int row = idx % BM, col = idx / BM;
-      const int m = m0 + row, n = n0 + col;
-      if (m >= a.M || n >= a.Cout_real) continue;
-      float v = Cs[row * CSTR + col] + (a.bias ? a.bias[n] : 0.f);
-      v = act_apply(v, a.act, a.slope) * a.alpha;
-      v = v * (a.aff_scale ? a.aff_scale[n] : 1.f) + (a.aff_shift ? a.aff_shift[n] : 0.f);
-      const int img = m / HW, pix = m - img * HW;
-      y[((size_t)img * a.Cout_real + n) * HW + pix] = v;
+// ------------------------------------------------------------------------------------
+// 256 x 256 tile forward / dgrad kernel for bf16 with Cout >= 256 (EDSR-L body and
+// upsample convs).  8 waves as 2 (M) x 4 (N), each wave a 128 x 64 output sub-tile
+// (8 x 4 v_mfma_f32_16x16x32_bf16 accumulators).  Operands go HBM/L2 -> LDS by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no VGPR staging, the range check zero-fills the padding),
+// two 64 KB stages in flight, each retired by a counted `s_waitcnt vmcnt` + raw s_barrier
+// (cdna_hip_programming.md §5 "Pipelining across barriers").  The DMA image is lane-linear,
+// so the XOR swizzle of the ds_read_b128 fragment reads is applied to the per-lane SOURCE
+// chunk (rule 21).  Epilogue: the fp32 tile is staged through LDS in two 128-row halves.
+// ------------------------------------------------------------------------------------
+constexpr int BIG_STAGE = 65536;
+
+// One buffer_load_dwordx4 ... lds per call, exactly (inline asm: hipcc cannot split it into
+// exec-divergent copies, which would break the hand-counted vmcnt).  M0 is written and
+// restored inside the statement (cdna_hip_programming.md §5.7).  `lds` must be wave-uniform.
+SR_DEV void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(__builtin_amdgcn_readfirstlane(dst)), "s"(r)
+      : "memory");
+}
+
+__global__ __launch_bounds__(512) void conv3x3_fwd_big_kernel(FwdArgs a) {
+  constexpr int MI = 8, NI = 4;
+  constexpr int CSTR = 256 + 4;
+  constexpr int SMEM = 128 * CSTR * 4;  // epilogue half tile; >= 2 stages of 64 KB
+  static_assert(SMEM >= 2 * BIG_STAGE, "LDS too small");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (int)(tile / a.tiles_n) * 256;
+  const int n0 = (int)(tile % a.tiles_n) * 256;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  // DMA image rows of this lane: w*32 + j*8 + (lane>>3), j = 0..3; logical 16-B chunk c
+  const int c = (lane & 7) ^ (lane >> 3);
+  int ay[4], ax[4], anh[4];
+  uint32_t boff[4];
+  bool bval[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = w * 32 + j * 8 + (lane >> 3);
+    const int m = m0 + r;
+    if (m < a.M) {
+      uint32_t q = fdiv((uint32_t)m, a.fd_W);
+      ax[j] = m - (int)q * a.W;
+      uint32_t n = fdiv(q, a.fd_H);
+      ay[j] = (int)q - (int)n * a.H;
+      anh[j] = (int)n * a.H;
+    } else {
+      ax[j] = 0; ay[j] = -100000; anh[j] = 0;
     }
-    return;
+    const int n = n0 + r;
+    bval[j] = n < a.Cout;
+    boff[j] = (uint32_t)(n * a.ldw) * 2u + (uint32_t)c * 16u;
   }
 
-  constexpr int CG = BN / 8;  // 8-channel groups per row
-  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
-  for (int idx = tid; idx < BM * CG; idx += 256) {
-    const int row = idx / CG, cg = idx % CG;
-    const int m = m0 + row, n = n0 + cg * 8;
-    if (m >= a.M || n >= a.Cout) continue;
-    float v[8];
-    const f32x4 c0 = *(const f32x4*)(Cs + row * CSTR + cg * 8);
-    const f32x4 c1 = *(const f32x4*)(Cs + row * CSTR + cg * 8 + 4);
+  f32x4 acc[MI][NI];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = c0[j]; v[4 + j] = c1[j]; }
-    if (a.bias) {
-      const f32x4 b0 = *(const f32x4*)(a.bias + n);
-      const f32x4 b1 = *(const f32x4*)(a.bias + n + 4);
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
-    }
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.nkc + 7) >> 3;
+
+  auto issue = [&](int ks, int buf) {
+    const int q = ks * 8 + c;
+    const int tap = (int)fdiv((uint32_t)q, a.fd_cpt);
+    const int cc = q - tap * a.cpt;
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    const bool kval = q < a.nkc;
+    const int ch = cc * 8;
+    char* As = smem + buf * BIG_STAGE + w * 4096;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
-    if (a.gate) {
-      float g[8];
-      const uint32_t off = (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ);
-      if constexpr (SZ == 2) {
-        u32x4 gg = buf_load16(gr, off);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          g[2 * j] = bf16_to_f32(gg[j] & 0xffff);
-          g[2 * j + 1] = bf16_to_f32(gg[j] >> 16);
-        }
+    for (int j = 0; j < 4; ++j) {
+      const int yy = ay[j] + dy, xx = ax[j] + dx;
+      const bool v = kval && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      uint32_t off;
+      if (a.in_ps == 0) {
+        off = (uint32_t)((((anh[j] + yy) * a.W + xx) * a.ldx + a.xcoff + ch) * 2);
       } else {
-        u32x4 g0 = buf_load16(gr, off), g1 = buf_load16(gr, off + 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { g[j] = __uint_as_float(g0[j]); g[4 + j] = __uint_as_float(g1[j]); }
+        const int r = a.in_ps;
+        const int s = (int)fdiv((uint32_t)ch, a.fd_cps);
+        const int cch = ch - s * a.fd_cps.d;
+        const int si = s / r, sj = s - (s / r) * r;
+        off = (uint32_t)((((anh[j] + yy) * r + si) * (a.W * r) + xx * r + sj) * a.ldx + a.xcoff + cch) * 2;
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
+      glds16(xr, As + j * 1024, v ? off : SR_OOB);
     }
+    char* Bs = smem + buf * BIG_STAGE + 32768 + w * 4096;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
-    if (a.res) {
-      float rv[8];
-      const uint32_t off = (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ);
-      if constexpr (SZ == 2) {
-        u32x4 rr4 = buf_load16(rr, off);
+    for (int j = 0; j < 4; ++j)
+      glds16(wr, Bs + j * 1024, (kval && bval[j]) ? boff[j] + (uint32_t)ks * 128u : SR_OOB);
+  };
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * BIG_STAGE;
+    const char* Bs = As + 32768;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          rv[2 * j] = bf16_to_f32(rr4[j] & 0xffff);
-          rv[2 * j + 1] = bf16_to_f32(rr4[j] >> 16);
-        }
-      } else {
-        u32x4 r0 = buf_load16(rr, off), r1 = buf_load16(rr, off + 16);
+    for (int kk = 0; kk < 2; ++kk) {
+      const uint32_t cq = kk * 4 + (lane >> 4);
+      u32x4 fa[MI], fb[NI];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { rv[j] = __uint_as_float(r0[j]); rv[4 + j] = __uint_as_float(r1[j]); }
-      }
+      for (int j = 0; j < NI; ++j) fb[j] = *(const u32x4*)(Bs + swz128(wn * 64 + j * 16 + (lane & 15), cq));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = a.beta * rv[j] + v[j];
+      for (int i = 0; i < MI; ++i) fa[i] = *(const u32x4*)(As + swz128(wm * 128 + i * 16 + (lane & 15), cq));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) mfma_chunk<bf16_t>(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
-    size_t dst;  // element offset of the 8-channel group
-    if (a.out_ps == 0) {
-      dst = (size_t)m * a.ldy + a.ycoff + n;
-    } else {
-      const int r = a.out_ps;
-      const int s = (int)fdiv((uint32_t)n, a.fd_cps);
-      const int c = n - s * a.fd_cps.d;
-      const int si = s / r, sj = s - (s / r) * r;
-      const int xq = (int)fdiv((uint32_t)m, a.fd_W);
-      const int xx = m - xq * a.W;  // xq = n*H + y
-      dst = ((size_t)(xq * r + si) * (a.W * r) + xx * r + sj) * a.ldy + a.ycoff + c;
-    }
-    if constexpr (SZ == 2) {
-      u32x4 o;
+  };
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    compute(ks & 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + 2 < nk) issue(ks + 2, ks & 1);
+  }
+
+  float* Cs = (float*)smem;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
-      *(u32x4*)((bf16_t*)a.y + dst) = o;
-    } else {
-      *(f32x4*)((float*)a.y + dst) = f32x4{v[0], v[1], v[2], v[3]};
-      *(f32x4*)((float*)a.y + dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + (lane >> 4) * 4 + r) * CSTR + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
     }
+    __syncthreads();
+    epilogue_tile<bf16_t, 128, 256, 512>(a, Cs, CSTR, m0 + h * 128, n0, tid);
   }
 }
 
@@ -627,8 +788,20 @@ hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
+  FwdArgs a = a0;
+  const int tm = (a.M + 255) / 256;
+  a.tiles_n = (a.Cout + 255) / 256;
+  a.tiles = tm * a.tiles_n;
+  hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
+bool g_disable_big = false;  // set by sr_conv3x3_set_variant (tests / A-B timing)
+
 template <typename T>
 hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
+  if (sizeof(T) == 2 && !a.out_nchw && a.Cout >= 256 && !g_disable_big) return launch_fwd_big(a, s);
   if (a.out_nchw || a.Cout <= 16) return launch_fwd<T, 256, 16, 4, 1>(a, s);
   if (a.Cout <= 32) return launch_fwd<T, 256, 32, 4, 1>(a, s);
   if (a.Cout <= 64) return launch_fwd<T, 128, 64, 2, 2>(a, s);
@@ -740,6 +913,12 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = d->dtype == SR_BF16 ? dispatch_fwd<bf16_t>(a, s) : dispatch_fwd<float>(a, s);
   return sr_check(e, "conv3x3_fwd launch");
+}
+
+// Kernel-variant switch for A/B tests: variant 0 = automatic, 1 = never use the 256x256 kernel.
+int sr_conv3x3_set_variant(int variant) {
+  g_disable_big = variant == 1;
+  return SR_OK;
 }
 
 size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d) {

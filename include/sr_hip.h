@@ -76,6 +76,10 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
                    const void* gate, const void* res, const float* aff_scale,
                    const float* aff_shift, void* y, void* stream);
 
+/* Kernel-variant selection for A/B tests: 0 = automatic (default), 1 = never use the
+ * 256x256 LDS-DMA kernel (all shapes on the 128-row register-staged kernels). */
+int sr_conv3x3_set_variant(int variant);
+
 /* Weight gradient: dw[co][ci][ky][kx] = scale * sum_pixels dy[p][co'] * x[p + tap][ci]
  * (param layout, fp32, co = perm(co') undoing out_ps), db[co] = scale * sum_p dy[p][co'].
  * dy is read in GEMM column order (gathered when out_ps > 0).  Needs a workspace of

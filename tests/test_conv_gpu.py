@@ -148,3 +148,30 @@ def test_edsr_m_parity_fp32(cuda):
     (out - gt.to(cuda)).abs().mean().backward()
     for n, p in gnet.named_parameters():
         assert rel_err(p.grad.cpu(), sd[n].grad) < 1e-3, n
+
+
+@pytest.mark.parametrize('shape', [(2, 64, 64, 256, 256, 0), (1, 20, 36, 256, 512, 0), (3, 17, 9, 256, 768, 0),
+                                   (1, 16, 16, 1024, 256, 2), (2, 8, 24, 256, 1024, 2)])
+def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
+    """The 256x256 LDS-DMA kernel and the 128x128 register-staged kernel sum K in the same
+    order, so their bf16 outputs must be bitwise identical (partial tiles, in_ps gather)."""
+    N, H, W, cin, cout, in_ps = shape
+    torch.manual_seed(3)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    if in_ps:
+        x = torch.randn(N, H * in_ps, W * in_ps, cin // (in_ps * in_ps), device=cuda).to(dt)
+    else:
+        x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    wf = (torch.randn(cout, 9 * cin, device=cuda) * 0.05).to(dt)
+    bg = torch.randn(cout, device=cuda)
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    outs = []
+    for variant in (0, 1):
+        _lib.check(lib.sr_conv3x3_set_variant(variant))
+        y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+        C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, res=res, alpha=0.5, in_ps=in_ps, ldx=x.shape[-1])
+        outs.append(y)
+    _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
