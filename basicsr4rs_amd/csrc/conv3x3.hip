@@ -20,6 +20,8 @@
 
 namespace {
 
+bool g_disable_big = false;  // set by sr_conv3x3_set_variant (tests / A-B timing)
+
 struct FwdArgs {
   const void* x;
   const void* w;
@@ -723,24 +725,267 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_kernel(WgArgs a) {
   }
 }
 
-// dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co = perm(co'); db likewise.
+// ------------------------------------------------------------------------------------
+// 256 (co) x 256 (ci) weight-gradient tile per tap for bf16, Cout >= 256 and Cin >= 256.
+// Same LDS-DMA pipeline as conv3x3_fwd_big_kernel: the [64 pixels][256 ch] images of dy and
+// of the tap-shifted x arrive by buffer_load ... lds (two 64 KB stages, counted vmcnt, raw
+// barriers); MFMA operands need 8 consecutive pixels per lane and are read transposed
+// with ds_read_b64_tr_b16 from 32-byte-block XOR-swizzled 512-byte rows (the swizzle is
+// applied to the per-lane DMA source chunk).  The bias gradient of the centre-tap blocks
+// is one extra MFMA per A fragment against an all-ones B operand (dy^T . 1).
+// ------------------------------------------------------------------------------------
+SR_DEV uint32_t swz512(uint32_t row, uint32_t byte_in_row) {
+  const uint32_t f = (row & 3u) | (((row >> 3) & 1u) << 2);
+  return row * 512u + ((((byte_in_row >> 5) ^ f)) << 5) + (byte_in_row & 31u);
+}
+
+// Bias-gradient role of the wgrad launch: the [64 pixels][256 co] dy image of each K-step
+// (same LDS-DMA pipeline, A operand only) times an all-ones B operand on MFMA.
+SR_DEV void wgrad_bias_role(const WgArgs& a, char* smem, int split, int co0) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  constexpr int STAGE = 2 * 64 * 512;
+  int lc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int R = 8 * w + 2 * j + (lane >> 5);
+    const int f = (R & 3) | (((R >> 3) & 1) << 2);
+    lc[j] = ((((lane & 31) >> 1) ^ f) << 1) | (lane & 1);
+  }
+  auto issue = [&](int p0, int buf) {
+    char* As = smem + buf * STAGE + w * 4096;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int R = 8 * w + 2 * j + (lane >> 5);
+      const int p = p0 + R;
+      const bool pv = p < p_end;
+      const int pc = pv ? p : 0;
+      const int co = co0 + lc[j] * 8;
+      uint32_t off;
+      if (a.out_ps == 0) {
+        off = (uint32_t)((pc * a.ldy + a.ycoff + co) * 2);
+      } else {
+        uint32_t q = fdiv((uint32_t)pc, a.fd_W);
+        const int x = pc - (int)q * a.W;
+        const int r = a.out_ps;
+        const int s = (int)fdiv((uint32_t)co, a.fd_cps);
+        const int cch = co - s * a.fd_cps.d;
+        const int si = s / r, sj = s - (s / r) * r;
+        off = (uint32_t)((((int)q * r + si) * (a.W * r) + x * r + sj) * a.ldy + a.ycoff + cch) * 2;
+      }
+      glds16(dyr, As + j * 1024, (pv && co < a.Cout) ? off : SR_OOB);
+    }
+  };
+  const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int nk = (p_end - p_begin + 63) / 64;
+  if (nk > 0) issue(p_begin, 0);
+  if (nk > 1) issue(p_begin + 64, 1);
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const char* As = smem + (ks & 1) * STAGE;
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = kk * 32 + 8 * g + q;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = w * 32 + i * 16 + 4 * pp;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + swz512(r0, col * 2)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + swz512(r0 + 4, col * 2)));
+        const s16x8 fa = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, ones, accb[i], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + 2 < nk) issue(p_begin + (ks + 2) * 64, ks & 1);
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + w * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[i][r];
+      }
+  }
+}
+
+__global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
+  constexpr int MI = 8, NI = 4;
+  constexpr int STAGE = 2 * 64 * 512;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  // block -> (split, role): roles 0 .. 9*tco*tci-1 are (tap, co tile, ci tile) GEMM tiles,
+  // the last tco roles (present only when db is wanted) are bias-gradient blocks.
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = 9 * a.tiles_co * a.tiles_ci;
+  const int per_split = ntile + (a.wsb ? a.tiles_co : 0);
+  const int split = (int)b / per_split;
+  int rem = (int)b - split * per_split;
+  if (rem >= ntile) {
+    wgrad_bias_role(a, smem, split, (rem - ntile) * 256);
+    return;
+  }
+  const int tap = rem / (a.tiles_co * a.tiles_ci);
+  rem -= tap * a.tiles_co * a.tiles_ci;
+  const int co0 = (rem / a.tiles_ci) * 256;
+  const int ci0 = (rem % a.tiles_ci) * 256;
+  const int dy_ = tap / 3 - 1, dx_ = tap % 3 - 1;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+
+  // DMA rows of this lane: R_j = 8w + 2j + (lane >> 5); logical 16-B chunk lc_j (source swizzle)
+  int lc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int R = 8 * w + 2 * j + (lane >> 5);
+    const int f = (R & 3) | (((R >> 3) & 1) << 2);
+    lc[j] = ((((lane & 31) >> 1) ^ f) << 1) | (lane & 1);
+  }
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int p0, int buf) {
+    char* As = smem + buf * STAGE + w * 4096;
+    char* Bs = As + 32768;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int R = 8 * w + 2 * j + (lane >> 5);
+      const int p = p0 + R;
+      const bool pv = p < p_end;
+      const int pc = pv ? p : 0;
+      uint32_t q = fdiv((uint32_t)pc, a.fd_W);
+      const int x = pc - (int)q * a.W;
+      uint32_t n = fdiv(q, a.fd_H);
+      const int y = (int)q - (int)n * a.H;
+      const int co = co0 + lc[j] * 8;
+      uint32_t offa;
+      if (a.out_ps == 0) {
+        offa = (uint32_t)((pc * a.ldy + a.ycoff + co) * 2);
+      } else {
+        const int r = a.out_ps;
+        const int s = (int)fdiv((uint32_t)co, a.fd_cps);
+        const int cch = co - s * a.fd_cps.d;
+        const int si = s / r, sj = s - (s / r) * r;
+        offa = (uint32_t)((((int)q * r + si) * (a.W * r) + x * r + sj) * a.ldy + a.ycoff + cch) * 2;
+      }
+      glds16(dyr, As + j * 1024, (pv && co < a.Cout) ? offa : SR_OOB);
+      const int yy = y + dy_, xx = x + dx_;
+      const int ci = ci0 + lc[j] * 8;
+      const bool bv = pv && ci < a.Cin && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      const uint32_t offb = (uint32_t)((((int)q + dy_) * a.W + xx) * a.ldx + a.xcoff + ci) * 2;
+      glds16(xr, Bs + j * 1024, bv ? offb : SR_OOB);
+    }
+  };
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + 32768;
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = kk * 32 + 8 * g + q;
+      s16x8 fa[MI], fb[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wn * 64 + j * 16 + 4 * pp;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Bs + swz512(r0, col * 2)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(Bs + swz512(r0 + 4, col * 2)));
+        fb[j] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int col = wm * 128 + i * 16 + 4 * pp;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + swz512(r0, col * 2)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(As + swz512(r0 + 4, col * 2)));
+        fa[i] = s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  const int nk = (p_end - p_begin + 63) / 64;
+  if (nk > 0) issue(p_begin, 0);
+  if (nk > 1) issue(p_begin + 64, 1);
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    compute(ks & 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + 2 < nk) issue(p_begin + (ks + 2) * 64, ks & 1);
+  }
+
+  float* ws = a.ws + ((size_t)split * 9 + tap) * a.Cout * a.Cin;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 128 + i * 16 + (lane >> 4) * 4 + r;
+        const int ci = ci0 + wn * 64 + j * 16 + (lane & 15);
+        if (co < a.Cout && ci < a.Cin) ws[(size_t)co * a.Cin + ci] = acc[i][j][r];
+      }
+}
+
+// dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co' = GEMM column of co (out_ps
+// permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
                                     int Cout, int Cin, int Cout_real, int Cin_real, int out_ps,
                                     float scale) {
-  const int64_t total = (int64_t)Cout_real * Cin_real * 9;
+  const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
   const int cps = Cout_real / r2;  // C' (channels after shuffle)
   if (i < total) {
-    const int tap = (int)(i % 9);
-    const int ci = (int)((i / 9) % Cin_real);
-    const int co = (int)(i / (9 * (int64_t)Cin_real));
+    const int ci = (int)(i % Cin_real);
+    const int co = (int)(i / Cin_real);
     const int cop = out_ps > 0 ? (co % r2) * cps + co / r2 : co;  // GEMM column of co
     const size_t stride = (size_t)9 * Cout * Cin;
-    const float* src = ws + ((size_t)tap * Cout + cop) * Cin + ci;
-    float s = 0.f;
-    for (int k = 0; k < S; ++k) s += src[k * stride];
-    dw[i] = s * scale;
+    float s[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) s[t] = 0.f;
+    for (int k = 0; k < S; ++k) {
+      const float* src = ws + k * stride + (size_t)cop * Cin + ci;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) s[t] += src[(size_t)t * Cout * Cin];
+    }
+    float* d = dw + i * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) d[t] = s[t] * scale;
   }
   if (db && i < Cout_real) {
     const int co = (int)i;
@@ -797,8 +1042,6 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
-bool g_disable_big = false;  // set by sr_conv3x3_set_variant (tests / A-B timing)
-
 template <typename T>
 hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
   if (sizeof(T) == 2 && !a.out_nchw && a.Cout >= 256 && !g_disable_big) return launch_fwd_big(a, s);
@@ -849,13 +1092,26 @@ hipError_t dispatch_wg(const WgArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-// Split-K factor: enough blocks to cover the chip ~2x, pixels per split a multiple of 64.
+bool wg_use_big(const sr_conv3x3_wgrad_desc* d) {
+  return d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && !g_disable_big;
+}
+
+// Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
+// 256x256 kernel, ~2 rounds for the small ones), pixels per split a multiple of 64.
 void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
   const int M = d->N * d->H * d->W;
-  int bm, bn;
-  wg_tiles(d->Cout, d->Cin, &bm, &bn);
-  const int tiles = 9 * ((d->Cout + bm - 1) / bm) * ((d->Cin + bn - 1) / bn);
-  int S = (1024 + tiles - 1) / tiles;
+  int bm, bn, target;
+  int extra = 0;  // bias-role blocks per split (big kernel)
+  if (wg_use_big(d)) {
+    bm = bn = 256;
+    target = 256;
+    extra = (d->Cout + 255) / 256;
+  } else {
+    wg_tiles(d->Cout, d->Cin, &bm, &bn);
+    target = 1024;
+  }
+  const int tiles = 9 * ((d->Cout + bm - 1) / bm) * ((d->Cin + bn - 1) / bn) + extra;
+  int S = extra ? target / tiles : (target + tiles / 2) / tiles;
   const int maxS = (M + 255) / 256;  // at least 256 pixels per split
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
@@ -915,6 +1171,22 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   return sr_check(e, "conv3x3_fwd launch");
 }
 
+// Name of the kernel instantiation sr_conv3x3_fwd / sr_conv3x3_wgrad will launch for a
+// descriptor (bench.py traces and rocprof summaries are matched on these names).
+const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
+  const bool bf = d->dtype == SR_BF16;
+  if (bf && !d->out_nchw && d->Cout >= 256 && !g_disable_big) return "conv3x3_fwd_big_kernel";
+  if (d->out_nchw || d->Cout <= 16) return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
+  if (d->Cout <= 32) return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
+  if (d->Cout <= 64) return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
+  return bf ? "conv3x3_fwd_kernel<bf16,128,128>" : "conv3x3_fwd_kernel<f32,128,128>";
+}
+
+const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
+  if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
+  return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
+}
+
 // Kernel-variant switch for A/B tests: variant 0 = automatic, 1 = never use the 256x256 kernel.
 int sr_conv3x3_set_variant(int variant) {
   g_disable_big = variant == 1;
@@ -958,11 +1230,20 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     return sr_fail(SR_EINVAL, "conv3x3_wgrad: shuffled channel count must be a multiple of 8");
   a.fd_cps = make_fastdiv(cps);
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = d->dtype == SR_BF16 ? dispatch_wg<bf16_t>(a, s) : dispatch_wg<float>(a, s);
+  hipError_t e;
+  if (wg_use_big(d)) {
+    a.tiles_co = (a.Cout + 255) / 256;
+    a.tiles_ci = (a.Cin + 255) / 256;
+    const int per_split = 9 * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
+    hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
+    e = hipGetLastError();
+  } else {
+    e = d->dtype == SR_BF16 ? dispatch_wg<bf16_t>(a, s) : dispatch_wg<float>(a, s);
+  }
   if (e != hipSuccess) return sr_check(e, "conv3x3_wgrad launch");
   const int Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout;
   const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
-  const int64_t total = (int64_t)Cout_real * Cin_real * 9;
+  const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t work = total > Cout_real ? total : Cout_real;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
                      (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,

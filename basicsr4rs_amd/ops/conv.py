@@ -104,27 +104,12 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     assert wf.shape[0] >= cout and wf.shape[1] == 9 * cin, (wf.shape, cout, cin)
     lib = _lib.load()
     M = N * H * W
-    with ktrace.span(fwd_kernel_name(x.dtype, cout, d.out_nchw), 2.0 * M * 9 * cin * cout_real,
+    with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * 9 * cin * cout_real,
                      x.element_size() * (M * (cin + cout) + 9 * cin * cout)):
         _lib.check(
             lib.sr_conv3x3_fwd(d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res),
                                _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.stream()))
     return y
-
-
-def fwd_kernel_name(dtype, cout, out_nchw):
-    """Instantiation chosen by dispatch_fwd in csrc/conv3x3.hip (for trace / rocprof matching)."""
-    t = 'unsigned short' if dtype == torch.bfloat16 else 'float'
-    if out_nchw or cout <= 16:
-        cfg = '256, 16, 4, 1'
-    elif cout <= 32:
-        cfg = '256, 32, 4, 1'
-    elif cout <= 64:
-        cfg = '128, 64, 2, 2'
-    else:
-        cfg = '128, 128, 2, 2'
-    return f'conv3x3_fwd_kernel<{t}, {cfg}>'
-
 
 
 def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, out_ps=0, need_bias=True, **kw):
@@ -142,8 +127,7 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
     dw = torch.empty(cout_real, cin_real, 3, 3, device=x.device, dtype=torch.float32)
     db = torch.empty(cout_real, device=x.device, dtype=torch.float32) if need_bias else None
     M = N * H * W
-    t = 'unsigned short' if x.dtype == torch.bfloat16 else 'float'
-    with ktrace.span(f'conv3x3_wgrad_kernel<{t}>+reduce', 2.0 * M * 9 * cin_real * cout_real,
+    with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * 9 * cin_real * cout_real,
                      x.element_size() * M * (cin + cout) + 4 * 9 * cin * cout):
         _lib.check(
             lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(dw), _lib.ptr(db),

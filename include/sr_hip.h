@@ -76,6 +76,11 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
                    const void* gate, const void* res, const float* aff_scale,
                    const float* aff_shift, void* y, void* stream);
 
+/* Name of the GPU kernel that sr_conv3x3_fwd / sr_conv3x3_wgrad would launch for a
+ * descriptor (static string; for traces and profiler summaries). */
+const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d);
+const char* sr_conv3x3_wgrad_kernel_name(const struct sr_conv3x3_wgrad_desc* d);
+
 /* Kernel-variant selection for A/B tests: 0 = automatic (default), 1 = never use the
  * 256x256 LDS-DMA kernel (all shapes on the 128-row register-staged kernels). */
 int sr_conv3x3_set_variant(int variant);

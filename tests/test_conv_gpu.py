@@ -175,3 +175,35 @@ def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
     _lib.check(lib.sr_conv3x3_set_variant(0))
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize('shape', [(2, 16, 16, 256, 256, 0), (1, 20, 12, 512, 256, 0), (2, 9, 14, 256, 768, 0),
+                                   (1, 8, 12, 256, 1024, 2)])
+@pytest.mark.parametrize('variant', [0, 1])
+def test_wgrad_bf16_vs_fp64(cuda, shape, variant):
+    """Weight/bias gradient (256x256 LDS-DMA kernel = variant 0, small kernel = variant 1)
+    against an fp64 CPU reference on the same bf16-rounded operands; |err| <= 1e-2*|ref|max."""
+    N, H, W, cin, cout, ps = shape
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin).to(dt)
+    if ps:
+        dy = torch.randn(N, H * ps, W * ps, cout // (ps * ps)).to(dt)
+        dy_gemm = O.pixel_unshuffle(dy.permute(0, 3, 1, 2).double(), ps)  # [N, cout, H, W], channel c*r*r+s
+    else:
+        dy = torch.randn(N, H, W, cout).to(dt)
+        dy_gemm = dy.permute(0, 3, 1, 2).double()
+    xd = x.permute(0, 3, 1, 2).double()
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xd, w, b, padding=1).mul(dy_gemm).sum().backward()
+    _lib.check(lib.sr_conv3x3_set_variant(variant))
+    try:
+        dw, db = C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps)
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    assert rel_err(dw.cpu().double(), w.grad) < 1e-2 * max(1.0, w.grad.abs().max().item()) / max(1.0, w.grad.abs().max().item())
+    assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
