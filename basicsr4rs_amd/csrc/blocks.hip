@@ -1,0 +1,448 @@
+// HBM-bound block kernels around the convs of MSRResNet, RCAN and RRDBNet.
+//
+//   sr_bilinear_up_add   MSRResNet global skip: out += F.interpolate(x, scale, 'bilinear',
+//                        align_corners=False) (basicsr/archs/srresnet_arch.py:64-65)
+//   sr_channel_reduce    per-(n, c) sum / dot over pixels of NHWC maps (deterministic two-pass):
+//                        RCAN ChannelAttention AdaptiveAvgPool2d(1) (rcan_arch.py:19) and its
+//                        backward reduction
+//   sr_ca_mlp_fwd/_bwd   the 1x1 conv -> ReLU -> 1x1 conv -> Sigmoid squeeze MLP (rcan_arch.py:19-20)
+//   sr_ca_scale_residual out = x + rs * u * s[n, c]   (RCAB tail, rcan_arch.py:22-24, 44-46)
+//   sr_ca_du             du = rs * dout * s[n, c] + dpool[n, c] / HW   (RCAB backward)
+//   sr_act_backward_nhwc strided (channel-slice) ReLU/LeakyReLU backward (RRDB dense slices)
+//   sr_nearest_up_backward  sum of each 2x2 (s x s) block: backward of F.interpolate(
+//                        scale_factor=s, mode='nearest') (rrdbnet_arch.py:116-117)
+//   sr_copy_channels     strided channel-slice copy (RRDB dense buffers)
+#include "sr_common.h"
+#include "sr_internal.h"
+
+namespace {
+
+__global__ void bilinear_up_add_kernel(const float* __restrict__ x, int N, int C, int H, int W, int s,
+                                       const float* __restrict__ base, float* __restrict__ y) {
+  const int Ho = H * s, Wo = W * s;
+  const int64_t total = (int64_t)N * C * Ho * Wo;
+  const float inv = 1.f / (float)s;
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (int64_t)gridDim.x * blockDim.x) {
+    const int ox = (int)(o % Wo);
+    const int oy = (int)((o / Wo) % Ho);
+    const int64_t nc = o / ((int64_t)Wo * Ho);
+    // PyTorch area_pixel_compute_source_index, align_corners=False, scale = 1/s
+    float sy = ((float)oy + 0.5f) * inv - 0.5f;
+    float sx = ((float)ox + 0.5f) * inv - 0.5f;
+    sy = sy < 0.f ? 0.f : sy;
+    sx = sx < 0.f ? 0.f : sx;
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, lx1 = sx - (float)x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* p = x + nc * H * W;
+    const float v = ly0 * (lx0 * p[y0 * W + x0] + lx1 * p[y0 * W + x1]) +
+                    ly1 * (lx0 * p[y1 * W + x0] + lx1 * p[y1 * W + x1]);
+    y[o] = base[o] + v;
+  }
+}
+
+// partial[n][chunk][c] = sum over the chunk's pixels of a[n,p,c] (* b[n,p,c]); threads: 8-channel
+// groups x pixel lanes; one block per (chunk, n).
+constexpr int RED_CHUNK = 256;  // pixels per block
+
+template <typename T>
+__global__ void channel_reduce_partial(const T* __restrict__ a, int lda, int acoff, const T* __restrict__ b, int ldb,
+                                       int bcoff, int HW, int C, float* __restrict__ partial) {
+  constexpr int PER = Elt<T>::PER16;
+  __shared__ float red[256 * 8];
+  const int n = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int groups = C / 8;
+  const int lanes = 256 / groups;  // pixel lanes
+  const int tid = threadIdx.x;
+  const int g = tid % groups, pl = tid / groups;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pl < lanes) {
+    const int p0 = chunk * RED_CHUNK, p1 = min(HW, p0 + RED_CHUNK);
+    for (int p = p0 + pl; p < p1; p += lanes) {
+      const size_t pix = (size_t)n * HW + p;
+      const T* pa = a + pix * lda + acoff + g * 8;
+      const T* pb = b ? b + pix * ldb + bcoff + g * 8 : nullptr;
+#pragma unroll
+      for (int h = 0; h < 8 / PER; ++h) {
+        const u32x4 va = *(const u32x4*)(pa + h * PER);
+        u32x4 vb;
+        if (pb) vb = *(const u32x4*)(pb + h * PER);
+        if constexpr (PER == 8) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float a0 = bf16_to_f32(va[k] & 0xffff), a1 = bf16_to_f32(va[k] >> 16);
+            if (pb) { a0 *= bf16_to_f32(vb[k] & 0xffff); a1 *= bf16_to_f32(vb[k] >> 16); }
+            acc[2 * k] += a0;
+            acc[2 * k + 1] += a1;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float a0 = __uint_as_float(va[k]);
+            if (pb) a0 *= __uint_as_float(vb[k]);
+            acc[h * 4 + k] += a0;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[tid * 8 + k] = acc[k];
+  __syncthreads();
+  if (tid < C) {
+    const int gg = tid / 8, k = tid % 8;
+    float s = 0.f;
+    for (int l = 0; l < lanes; ++l) s += red[(l * groups + gg) * 8 + k];
+    partial[((size_t)n * nchunk + chunk) * C + tid] = s;
+  }
+}
+
+__global__ void channel_reduce_final(const float* __restrict__ partial, int N, int nchunk, int C, float scale,
+                                     float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float s = 0.f;
+  for (int k = 0; k < nchunk; ++k) s += partial[((size_t)n * nchunk + k) * C + c];
+  out[i] = s * scale;
+}
+
+// h = relu(W1 pool + b1) [N,Cr], s = sigmoid(W2 h + b2) [N,C]; W1 [Cr][C], W2 [C][Cr]
+__global__ void ca_mlp_fwd_kernel(const float* __restrict__ pool, const float* __restrict__ w1,
+                                  const float* __restrict__ b1, const float* __restrict__ w2,
+                                  const float* __restrict__ b2, int C, int Cr, float* __restrict__ h,
+                                  float* __restrict__ s) {
+  extern __shared__ float sh[];  // Cr floats
+  const int n = blockIdx.x;
+  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+    float acc = b1 ? b1[r] : 0.f;
+    for (int c = 0; c < C; ++c) acc += w1[r * C + c] * pool[n * C + c];
+    acc = acc > 0.f ? acc : 0.f;
+    sh[r] = acc;
+    h[n * Cr + r] = acc;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float acc = b2 ? b2[c] : 0.f;
+    for (int r = 0; r < Cr; ++r) acc += w2[c * Cr + r] * sh[r];
+    s[n * C + c] = 1.f / (1.f + expf(-acc));
+  }
+}
+
+// Backward of the squeeze MLP for the whole batch (one block): ds = d loss / d s.
+__global__ void ca_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ s,
+                                  const float* __restrict__ h, const float* __restrict__ pool,
+                                  const float* __restrict__ w1, const float* __restrict__ w2, int N, int C, int Cr,
+                                  float* __restrict__ dpool, float* __restrict__ dw1, float* __restrict__ db1,
+                                  float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ scratch) {
+  // scratch: dz2 [N,C], dz1 [N,Cr]
+  float* dz2 = scratch;
+  float* dz1 = scratch + (size_t)N * C;
+  for (int i = threadIdx.x; i < N * C; i += blockDim.x) dz2[i] = ds[i] * s[i] * (1.f - s[i]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < N * Cr; i += blockDim.x) {
+    const int n = i / Cr, r = i % Cr;
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc += w2[c * Cr + r] * dz2[n * C + c];
+    dz1[i] = h[i] > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * Cr; i += blockDim.x) {
+    const int c = i / Cr, r = i % Cr;
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += dz2[n * C + c] * h[n * Cr + r];
+    dw2[i] = acc;
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += dz2[n * C + c];
+    if (db2) db2[c] = acc;
+  }
+  for (int i = threadIdx.x; i < Cr * C; i += blockDim.x) {
+    const int r = i / C, c = i % C;
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r] * pool[n * C + c];
+    dw1[i] = acc;
+  }
+  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r];
+    if (db1) db1[r] = acc;
+  }
+  for (int i = threadIdx.x; i < N * C; i += blockDim.x) {
+    const int n = i / C, c = i % C;
+    float acc = 0.f;
+    for (int r = 0; r < Cr; ++r) acc += w1[r * C + c] * dz1[n * Cr + r];
+    dpool[i] = acc;
+  }
+}
+
+// out = beta * x + alpha * u * s[n,c] + gamma * t[n,c]   (all NHWC with the same C, dense)
+// RCAB forward: beta 1, alpha rs, s = sigmoid, t = null.  RCAB du: x = null, u = dout,
+// alpha = rs, s = sigmoid, gamma = 1/HW, t = dpool.
+template <typename T>
+__global__ void nc_affine_kernel(const T* __restrict__ x, const T* __restrict__ u, const float* __restrict__ s,
+                                 const float* __restrict__ t, int N, int HW, int C, float beta, float alpha,
+                                 float gamma, T* __restrict__ out) {
+  constexpr int PER = Elt<T>::PER16;
+  const int64_t nv = (int64_t)N * HW * C / PER;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e0 = i * PER;
+    const int c0 = (int)(e0 % C);
+    const int n = (int)(e0 / ((int64_t)HW * C));
+    const u32x4 vu = ((const u32x4*)u)[i];
+    u32x4 vx = {0, 0, 0, 0};
+    if (x) vx = ((const u32x4*)x)[i];
+    u32x4 o;
+    if constexpr (PER == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float r[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = c0 + 2 * k + h;
+          const float uu = bf16_to_f32(h ? (vu[k] >> 16) : (vu[k] & 0xffff));
+          const float xx = x ? bf16_to_f32(h ? (vx[k] >> 16) : (vx[k] & 0xffff)) : 0.f;
+          r[h] = beta * xx + alpha * uu * s[n * C + c] + (t ? gamma * t[n * C + c] : 0.f);
+        }
+        o[k] = pack_bf16x2(r[0], r[1]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + k;
+        const float r = beta * (x ? __uint_as_float(vx[k]) : 0.f) + alpha * __uint_as_float(vu[k]) * s[n * C + c] +
+                        (t ? gamma * t[n * C + c] : 0.f);
+        o[k] = __float_as_uint(r);
+      }
+    }
+    ((u32x4*)out)[i] = o;
+  }
+}
+
+template <typename T>
+__global__ void act_backward_nhwc_kernel(const T* __restrict__ dy, int ldd, int dcoff, const T* __restrict__ y, int ldy,
+                                         int ycoff, T* __restrict__ out, int ldo, int ocoff, int64_t P, int C, float neg,
+                                         float alpha) {
+  constexpr int PER = Elt<T>::PER16;
+  const int groups = C / PER;
+  const int64_t nv = P * groups;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / groups;
+    const int g = (int)(i % groups);
+    const u32x4 d = *(const u32x4*)(dy + p * ldd + dcoff + g * PER);
+    const u32x4 yy = *(const u32x4*)(y + p * ldy + ycoff + g * PER);
+    u32x4 o;
+    if constexpr (PER == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d0 = bf16_to_f32(d[k] & 0xffff), d1 = bf16_to_f32(d[k] >> 16);
+        const float y0 = bf16_to_f32(yy[k] & 0xffff), y1 = bf16_to_f32(yy[k] >> 16);
+        o[k] = pack_bf16x2(alpha * d0 * (y0 > 0.f ? 1.f : neg), alpha * d1 * (y1 > 0.f ? 1.f : neg));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = __float_as_uint(alpha * __uint_as_float(d[k]) * (__uint_as_float(yy[k]) > 0.f ? 1.f : neg));
+    }
+    *(u32x4*)(out + p * ldo + ocoff + g * PER) = o;
+  }
+}
+
+// out[n,y,x,c] (+)= sum_{i,j<s} d[n, y*s+i, x*s+j, c]
+template <typename T>
+__global__ void nearest_up_backward_kernel(const T* __restrict__ d, int ldd, int N, int H, int W, int C, int s,
+                                           T* __restrict__ out, int ldo, int accumulate) {
+  constexpr int PER = Elt<T>::PER16;
+  const int groups = C / PER;
+  const int64_t nv = (int64_t)N * H * W * groups;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i % groups);
+    const int64_t p = i / groups;
+    const int x = (int)(p % W);
+    const int y = (int)((p / W) % H);
+    const int64_t n = p / ((int64_t)W * H);
+    float acc[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) acc[k] = 0.f;
+    for (int a = 0; a < s; ++a)
+      for (int b = 0; b < s; ++b) {
+        const u32x4 v = *(const u32x4*)(d + ((n * H * s + y * s + a) * (int64_t)W * s + x * s + b) * ldd + g * PER);
+        if constexpr (PER == 8) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            acc[2 * k] += bf16_to_f32(v[k] & 0xffff);
+            acc[2 * k + 1] += bf16_to_f32(v[k] >> 16);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] += __uint_as_float(v[k]);
+        }
+      }
+    T* dst = out + p * ldo + g * PER;
+    if (accumulate) {
+      const u32x4 v = *(const u32x4*)dst;
+      if constexpr (PER == 8) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] += bf16_to_f32(v[k] & 0xffff);
+          acc[2 * k + 1] += bf16_to_f32(v[k] >> 16);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] += __uint_as_float(v[k]);
+      }
+    }
+    u32x4 o;
+    if constexpr (PER == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = pack_bf16x2(acc[2 * k], acc[2 * k + 1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(acc[k]);
+    }
+    *(u32x4*)dst = o;
+  }
+}
+
+template <typename T>
+__global__ void copy_channels_kernel(const T* __restrict__ src, int lds_, int scoff, T* __restrict__ dst, int ldd,
+                                     int dcoff, int64_t P, int C) {
+  constexpr int PER = Elt<T>::PER16;
+  const int groups = C / PER;
+  const int64_t nv = P * groups;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i / groups;
+    const int g = (int)(i % groups);
+    *(u32x4*)(dst + p * ldd + dcoff + g * PER) = *(const u32x4*)(src + p * lds_ + scoff + g * PER);
+  }
+}
+
+inline unsigned grid_for(int64_t n, int64_t cap = 8192) {
+  int64_t g = (n + 255) / 256;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int sr_bilinear_up_add(const float* x, int N, int C, int H, int W, int s, const float* base, float* y,
+                       void* stream) {
+  if (!x || !base || !y || s < 1) return sr_fail(SR_EINVAL, "bilinear_up_add: bad arguments");
+  const int64_t total = (int64_t)N * C * H * s * W * s;
+  hipLaunchKernelGGL(bilinear_up_add_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, N, C, H, W,
+                     s, base, y);
+  return sr_check(hipGetLastError(), "bilinear_up_add launch");
+}
+
+size_t sr_channel_reduce_workspace(int N, int HW, int C) {
+  return (size_t)N * ((HW + RED_CHUNK - 1) / RED_CHUNK) * C * sizeof(float);
+}
+
+int sr_channel_reduce(int dtype, const void* a, int lda, int acoff, const void* b, int ldb, int bcoff, int N, int HW,
+                      int C, float scale, float* out, void* workspace, size_t ws_bytes, void* stream) {
+  if (!a || !out || !workspace || C % 8 || C > 2048 || C / 8 > 256)
+    return sr_fail(SR_EINVAL, "channel_reduce: bad arguments (C multiple of 8, <= 2048)");
+  if (ws_bytes < sr_channel_reduce_workspace(N, HW, C)) return sr_fail(SR_EINVAL, "channel_reduce: workspace too small");
+  const int nchunk = (HW + RED_CHUNK - 1) / RED_CHUNK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(channel_reduce_partial<bf16_t>, dim3(nchunk, N), dim3(256), 0, s, (const bf16_t*)a, lda, acoff,
+                       (const bf16_t*)b, ldb, bcoff, HW, C, (float*)workspace);
+  else
+    hipLaunchKernelGGL(channel_reduce_partial<float>, dim3(nchunk, N), dim3(256), 0, s, (const float*)a, lda, acoff,
+                       (const float*)b, ldb, bcoff, HW, C, (float*)workspace);
+  hipLaunchKernelGGL(channel_reduce_final, dim3((N * C + 255) / 256), dim3(256), 0, s, (const float*)workspace, N,
+                     nchunk, C, scale, out);
+  return sr_check(hipGetLastError(), "channel_reduce launch");
+}
+
+int sr_ca_mlp_fwd(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, int N, int C,
+                  int Cr, float* h, float* s_out, void* stream) {
+  if (!pool || !w1 || !w2 || !h || !s_out) return sr_fail(SR_EINVAL, "ca_mlp_fwd: bad arguments");
+  hipLaunchKernelGGL(ca_mlp_fwd_kernel, dim3(N), dim3(256), Cr * sizeof(float), (hipStream_t)stream, pool, w1, b1, w2,
+                     b2, C, Cr, h, s_out);
+  return sr_check(hipGetLastError(), "ca_mlp_fwd launch");
+}
+
+int sr_ca_mlp_bwd(const float* ds, const float* s, const float* h, const float* pool, const float* w1,
+                  const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1, float* dw2, float* db2,
+                  float* scratch, void* stream) {
+  if (!ds || !s || !h || !pool || !w1 || !w2 || !dpool || !dw1 || !dw2 || !scratch)
+    return sr_fail(SR_EINVAL, "ca_mlp_bwd: bad arguments");
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ds, s, h, pool, w1, w2, N, C, Cr,
+                     dpool, dw1, db1, dw2, db2, scratch);
+  return sr_check(hipGetLastError(), "ca_mlp_bwd launch");
+}
+
+int sr_nc_affine(int dtype, const void* x, const void* u, const float* s, const float* t, int N, int HW, int C,
+                 float beta, float alpha, float gamma, void* out, void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!u || !s || !out || C % PER || !aligned16(u) || !aligned16(out) || (x && !aligned16(x)))
+    return sr_fail(SR_EINVAL, "nc_affine: bad arguments");
+  const int64_t nv = (int64_t)N * HW * C / PER;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(nc_affine_kernel<bf16_t>, dim3(grid_for(nv)), dim3(256), 0, st, (const bf16_t*)x,
+                       (const bf16_t*)u, s, t, N, HW, C, beta, alpha, gamma, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(nc_affine_kernel<float>, dim3(grid_for(nv)), dim3(256), 0, st, (const float*)x, (const float*)u,
+                       s, t, N, HW, C, beta, alpha, gamma, (float*)out);
+  return sr_check(hipGetLastError(), "nc_affine launch");
+}
+
+int sr_act_backward_nhwc(int dtype, int64_t P, int C, const void* dy, int ldd, int dcoff, const void* y, int ldy,
+                         int ycoff, void* out, int ldo, int ocoff, int act, float slope, float alpha, void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!dy || !y || !out || C % PER || ldd % PER || ldy % PER || ldo % PER || dcoff % PER || ycoff % PER || ocoff % PER)
+    return sr_fail(SR_EINVAL, "act_backward_nhwc: bad arguments (16-byte aligned channel slices)");
+  const float neg = act == SR_ACT_LRELU ? slope : (act == SR_ACT_RELU ? 0.f : 1.f);
+  const int64_t nv = P * (C / PER);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(act_backward_nhwc_kernel<bf16_t>, dim3(grid_for(nv)), dim3(256), 0, st, (const bf16_t*)dy, ldd,
+                       dcoff, (const bf16_t*)y, ldy, ycoff, (bf16_t*)out, ldo, ocoff, P, C, neg, alpha);
+  else
+    hipLaunchKernelGGL(act_backward_nhwc_kernel<float>, dim3(grid_for(nv)), dim3(256), 0, st, (const float*)dy, ldd,
+                       dcoff, (const float*)y, ldy, ycoff, (float*)out, ldo, ocoff, P, C, neg, alpha);
+  return sr_check(hipGetLastError(), "act_backward_nhwc launch");
+}
+
+int sr_nearest_up_backward(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s, void* out, int ldo,
+                           int accumulate, void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!d || !out || C % PER || ldd % PER || ldo % PER || s < 1) return sr_fail(SR_EINVAL, "nearest_up_backward: bad arguments");
+  const int64_t nv = (int64_t)N * H * W * (C / PER);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(nearest_up_backward_kernel<bf16_t>, dim3(grid_for(nv)), dim3(256), 0, st, (const bf16_t*)d, ldd,
+                       N, H, W, C, s, (bf16_t*)out, ldo, accumulate);
+  else
+    hipLaunchKernelGGL(nearest_up_backward_kernel<float>, dim3(grid_for(nv)), dim3(256), 0, st, (const float*)d, ldd, N,
+                       H, W, C, s, (float*)out, ldo, accumulate);
+  return sr_check(hipGetLastError(), "nearest_up_backward launch");
+}
+
+int sr_copy_channels(int dtype, const void* src, int lds_, int scoff, void* dst, int ldd, int dcoff, int64_t P, int C,
+                     void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!src || !dst || C % PER || lds_ % PER || ldd % PER || scoff % PER || dcoff % PER)
+    return sr_fail(SR_EINVAL, "copy_channels: bad arguments");
+  const int64_t nv = P * (C / PER);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(copy_channels_kernel<bf16_t>, dim3(grid_for(nv)), dim3(256), 0, st, (const bf16_t*)src, lds_,
+                       scoff, (bf16_t*)dst, ldd, dcoff, P, C);
+  else
+    hipLaunchKernelGGL(copy_channels_kernel<float>, dim3(grid_for(nv)), dim3(256), 0, st, (const float*)src, lds_,
+                       scoff, (float*)dst, ldd, dcoff, P, C);
+  return sr_check(hipGetLastError(), "copy_channels launch");
+}
+
+}  // extern "C"

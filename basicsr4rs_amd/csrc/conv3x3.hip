@@ -42,6 +42,11 @@ struct FwdArgs {
   float gate_slope;
   int ldr, rcoff;
   float beta;
+  const void* res2;
+  uint32_t r2_bytes;
+  int ldr2, r2coff, rcols;
+  float beta2;
+  int in_up;  // nearest-neighbour upsample factor folded into the A gather (1 = none)
   int tiles_n, tiles;
   FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
 };
@@ -128,7 +133,7 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
-    if (a.res) {
+    if (a.res && n < a.rcols) {
       float rv[8];
       const uint32_t off = (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ);
       if constexpr (SZ == 2) {
@@ -145,6 +150,25 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = a.beta * rv[j] + v[j];
+    }
+    if (a.res2 && n < a.rcols) {
+      float rv[8];
+      const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+      const uint32_t off = (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * SZ);
+      if constexpr (SZ == 2) {
+        u32x4 rr4 = buf_load16(rr2, off);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          rv[2 * j] = bf16_to_f32(rr4[j] & 0xffff);
+          rv[2 * j + 1] = bf16_to_f32(rr4[j] >> 16);
+        }
+      } else {
+        u32x4 r0 = buf_load16(rr2, off), r1 = buf_load16(rr2, off + 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { rv[j] = __uint_as_float(r0[j]); rv[4 + j] = __uint_as_float(r1[j]); }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rv[j] + v[j];
     }
     size_t dst;  // element offset of the 8-channel group
     if (a.out_ps == 0) {
@@ -232,7 +256,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       const int yy = ay[i] + dy, xx = ax[i] + dx;
       const bool v = kval && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
       uint32_t off;
-      if (a.in_ps == 0) {
+      if (a.in_up > 1) {
+        const int u = a.in_up;  // source grid is [N, H/u, W/u]
+        off = (uint32_t)((((anh[i] / u + yy / u) * (a.W / u) + xx / u) * a.ldx + a.xcoff + ch) * SZ);
+      } else if (a.in_ps == 0) {
         off = (uint32_t)((((anh[i] + yy) * a.W + xx) * a.ldx + a.xcoff + ch) * SZ);
       } else {
         const int r = a.in_ps;
@@ -479,6 +506,7 @@ struct WgArgs {
   int N, H, W, M;
   int Cin, ldx, xcoff;
   int Cout, ldy, ycoff, out_ps;
+  int in_up;  // nearest upsample factor of the x gather (1 = none)
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   FastDiv fd_W, fd_H, fd_cps;
 };
@@ -580,8 +608,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_kernel(WgArgs a) {
         int nh, y, x;
         pix_decomp(p, nh, y, x);
         const int yy = y + dy_, xx = x + dx_;
-        if ((unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W)
-          off = (uint32_t)(((size_t)((nh + yy) * a.W + xx) * a.ldx + a.xcoff + ci) * SZ);
+        if ((unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W) {
+          const int u = a.in_up;
+          off = (uint32_t)(((size_t)((nh / u + yy / u) * (a.W / u) + xx / u) * a.ldx + a.xcoff + ci) * SZ);
+        }
       }
       rb[i] = buf_load16(xr, off);
     }
@@ -1044,7 +1074,7 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
 
 template <typename T>
 hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
-  if (sizeof(T) == 2 && !a.out_nchw && a.Cout >= 256 && !g_disable_big) return launch_fwd_big(a, s);
+  if (sizeof(T) == 2 && !a.out_nchw && a.Cout >= 256 && a.in_up == 1 && !g_disable_big) return launch_fwd_big(a, s);
   if (a.out_nchw || a.Cout <= 16) return launch_fwd<T, 256, 16, 4, 1>(a, s);
   if (a.Cout <= 32) return launch_fwd<T, 256, 32, 4, 1>(a, s);
   if (a.Cout <= 64) return launch_fwd<T, 128, 64, 2, 2>(a, s);
@@ -1093,7 +1123,7 @@ hipError_t dispatch_wg(const WgArgs& a, hipStream_t s) {
 }
 
 bool wg_use_big(const sr_conv3x3_wgrad_desc* d) {
-  return d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && !g_disable_big;
+  return d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && d->in_up <= 1 && !g_disable_big;
 }
 
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
@@ -1127,7 +1157,7 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
 extern "C" {
 
 int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
-                   const void* gate, const void* res, const float* aff_scale,
+                   const void* gate, const void* res, const void* res2, const float* aff_scale,
                    const float* aff_shift, void* y, void* stream) {
   if (!d || !x || !w || !y) return sr_fail(SR_EINVAL, "conv3x3_fwd: null pointer");
   const int SZ = d->dtype == SR_BF16 ? 2 : 4;
@@ -1135,10 +1165,13 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   if (d->Cin % 8 || d->ldx % PER || d->xcoff % PER || (!d->out_nchw && (d->Cout % 8)))
     return sr_fail(SR_EINVAL, "conv3x3_fwd: Cin/Cout/ld/coff must be multiples of 8 (pad channels)");
   if (d->ldw < 9 * d->Cin) return sr_fail(SR_EINVAL, "conv3x3_fwd: ldw < 9*Cin");
-  if ((gate || res) && d->out_ps) return sr_fail(SR_EINVAL, "conv3x3_fwd: gate/res need plain store");
+  if ((gate || res || res2) && d->out_ps) return sr_fail(SR_EINVAL, "conv3x3_fwd: gate/res need plain store");
+  const int up = d->in_up > 1 ? d->in_up : 1;
+  if (up > 1 && (d->in_ps > 0 || d->H % up || d->W % up))
+    return sr_fail(SR_EINVAL, "conv3x3_fwd: in_up needs H, W divisible by it and no in_ps");
   const int M = d->N * d->H * d->W;
   const int r_in = d->in_ps > 0 ? d->in_ps : 1;
-  const size_t xb = (size_t)M * r_in * r_in * (size_t)d->ldx * SZ;
+  const size_t xb = (size_t)M * r_in * r_in * (size_t)d->ldx * SZ / ((size_t)up * up);
   const size_t wb = (size_t)d->Cout * d->ldw * SZ;
   if (xb >= 0x80000000ull || wb >= 0x80000000ull)
     return sr_fail(SR_ETOOBIG, "conv3x3_fwd: tensor >= 2 GiB (split the batch)");
@@ -1156,6 +1189,11 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   a.act = d->act; a.slope = d->slope; a.alpha = d->alpha;
   a.ldg = d->ldg; a.gcoff = d->gcoff; a.gate_slope = d->gate_slope;
   a.ldr = d->ldr; a.rcoff = d->rcoff; a.beta = d->beta;
+  a.res2 = res2;
+  a.r2_bytes = res2 ? (uint32_t)((size_t)M * d->ldr2 * SZ) : 0;
+  a.ldr2 = d->ldr2; a.r2coff = d->r2coff; a.beta2 = d->beta2;
+  a.rcols = d->rcols > 0 ? d->rcols : d->Cout;
+  a.in_up = up;
   a.fd_cpt = make_fastdiv(a.cpt);
   a.fd_W = make_fastdiv(d->W);
   a.fd_H = make_fastdiv(d->H);
@@ -1175,7 +1213,7 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
 // descriptor (bench.py traces and rocprof summaries are matched on these names).
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
-  if (bf && !d->out_nchw && d->Cout >= 256 && !g_disable_big) return "conv3x3_fwd_big_kernel";
+  if (bf && !d->out_nchw && d->Cout >= 256 && d->in_up <= 1 && !g_disable_big) return "conv3x3_fwd_big_kernel";
   if (d->out_nchw || d->Cout <= 16) return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
   if (d->Cout <= 32) return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
   if (d->Cout <= 64) return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
@@ -1209,7 +1247,9 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   if (ws_bytes < sr_conv3x3_wgrad_workspace(d)) return sr_fail(SR_EINVAL, "conv3x3_wgrad: workspace too small");
   const int M = d->N * d->H * d->W;
   const int r = d->out_ps > 0 ? d->out_ps : 1;
-  const size_t xb = (size_t)M * d->ldx * SZ;
+  const int up = d->in_up > 1 ? d->in_up : 1;
+  if (up > 1 && (d->H % up || d->W % up)) return sr_fail(SR_EINVAL, "conv3x3_wgrad: H, W must divide by in_up");
+  const size_t xb = (size_t)M * d->ldx * SZ / ((size_t)up * up);
   const size_t dyb2 = (size_t)M * r * r * (size_t)d->ldy * SZ;
   if (xb >= 0x80000000ull || dyb2 >= 0x80000000ull)
     return sr_fail(SR_ETOOBIG, "conv3x3_wgrad: tensor >= 2 GiB (split the batch)");
@@ -1223,6 +1263,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   a.N = d->N; a.H = d->H; a.W = d->W; a.M = M;
   a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff;
   a.Cout = d->Cout; a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps;
+  a.in_up = up;
   a.splits = S; a.kper = kp;
   a.fd_W = make_fastdiv(d->W); a.fd_H = make_fastdiv(d->H);
   int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 1;

@@ -1,0 +1,245 @@
+"""Fused residual blocks of RCAN and RRDBNet, and the MSRResNet bilinear skip, on the HIP engine.
+
+Each block is one autograd Function whose forward/backward are sequences of libsr_hip
+launches (implicit-GEMM convs with fused epilogues + the HBM kernels of csrc/blocks.hip):
+
+* ``rcab``  — RCAB (basicsr/archs/rcan_arch.py:27-46): conv-ReLU-conv, ChannelAttention
+  (avg-pool, 1x1 C->C/r, ReLU, 1x1 C/r->C, sigmoid, rcan_arch.py:8-24), ``* res_scale + x``.
+* ``rrdb``  — RRDB of three ResidualDenseBlocks (rrdbnet_arch.py:9-63): the dense concats are
+  channel slices of one [N, H, W, nf + 4*gc] buffer per RDB (convs read/write slices in place,
+  no torch.cat copies); the two residual scalings of the last RDB fuse into its conv5 epilogue.
+* ``bilinear_up_add`` — MSRResNet ``out += F.interpolate(x, bilinear)`` (srresnet_arch.py:64-65).
+"""
+import torch
+
+from .. import _lib
+from . import conv as C
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(1, nbytes // 4 + 1), device=device, dtype=torch.float32)
+
+
+def channel_reduce(a, b=None, scale=1.0, C_=None, coff=0):
+    """out[n, c] = scale * sum_p a[n, p, c] (* b) for NHWC a (fp32 result)."""
+    N, H, W, ld = a.shape
+    Cc = C_ or ld
+    lib = _lib.load()
+    wsb = lib.sr_channel_reduce_workspace(N, H * W, Cc)
+    ws = _ws(wsb, a.device)
+    out = torch.empty(N, Cc, device=a.device, dtype=torch.float32)
+    _lib.check(
+        lib.sr_channel_reduce(_lib.dtype_code(a.dtype), _lib.ptr(a), ld, coff, _lib.ptr(b), b.shape[-1] if b is not None
+                              else 0, coff, N, H * W, Cc, float(scale), _lib.ptr(out), _lib.ptr(ws), wsb,
+                              _lib.stream()))
+    return out
+
+
+def nc_affine(x, u, s, t, beta, alpha, gamma):
+    N, H, W, Cc = u.shape
+    out = torch.empty_like(u)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_nc_affine(_lib.dtype_code(u.dtype), _lib.ptr(x), _lib.ptr(u), _lib.ptr(s), _lib.ptr(t), N, H * W, Cc,
+                         float(beta), float(alpha), float(gamma), _lib.ptr(out), _lib.stream()))
+    return out
+
+
+class _RCAB(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, aw1, ab1, aw2, ab2, spec1, spec2, rs):
+        dtype = x.dtype
+        N, H, W, Cp = x.shape
+        wf1, _, bg1 = C.prepared(w1, b1, spec1, dtype)
+        wf2, _, bg2 = C.prepared(w2, b2, spec2, dtype)
+        t = torch.empty(N, H, W, spec1.cout_p, device=x.device, dtype=dtype)
+        C.conv_fwd_raw(x, wf1, bg1, t, N, H, W, spec1.cin_p, spec1.cout_p, spec1.cout, act=_lib.ACT_RELU)
+        u = torch.empty(N, H, W, spec2.cout_p, device=x.device, dtype=dtype)
+        C.conv_fwd_raw(t, wf2, bg2, u, N, H, W, spec2.cin_p, spec2.cout_p, spec2.cout)
+        pool = channel_reduce(u, scale=1.0 / (H * W))
+        Cr = aw1.shape[0]
+        a1 = aw1.detach().reshape(Cr, -1).contiguous()
+        a2 = aw2.detach().reshape(-1, Cr).contiguous()
+        h = torch.empty(N, Cr, device=x.device, dtype=torch.float32)
+        s = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+        lib = _lib.load()
+        _lib.check(
+            lib.sr_ca_mlp_fwd(_lib.ptr(pool), _lib.ptr(a1), _lib.ptr(ab1.detach() if ab1 is not None else None),
+                              _lib.ptr(a2), _lib.ptr(ab2.detach() if ab2 is not None else None), N, Cp, Cr,
+                              _lib.ptr(h), _lib.ptr(s), _lib.stream()))
+        y = nc_affine(x, u, s, None, 1.0, rs, 0.0)
+        ctx.specs = (spec1, spec2)
+        ctx.rs = rs
+        ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, a1, a2, ab1, ab2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, t, u, pool, h, s, w1, b1, w2, b2, a1, a2, ab1, ab2 = ctx.saved_tensors
+        spec1, spec2 = ctx.specs
+        rs = ctx.rs
+        dtype = x.dtype
+        N, H, W, Cp = x.shape
+        Cr = a1.shape[0]
+        dy = dy.to(dtype).contiguous()
+        lib = _lib.load()
+        ds = channel_reduce(dy, u, scale=rs)  # dL/ds[n,c] = rs * sum_p dy*u
+        dpool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+        dA1 = torch.empty_like(a1)
+        dA2 = torch.empty_like(a2)
+        dab1 = torch.empty(Cr, device=x.device, dtype=torch.float32)
+        dab2 = torch.empty(Cp, device=x.device, dtype=torch.float32)
+        scratch = torch.empty(N * (Cp + Cr), device=x.device, dtype=torch.float32)
+        _lib.check(
+            lib.sr_ca_mlp_bwd(_lib.ptr(ds), _lib.ptr(s), _lib.ptr(h), _lib.ptr(pool), _lib.ptr(a1), _lib.ptr(a2), N, Cp,
+                              Cr, _lib.ptr(dpool), _lib.ptr(dA1), _lib.ptr(dab1), _lib.ptr(dA2), _lib.ptr(dab2),
+                              _lib.ptr(scratch), _lib.stream()))
+        du = nc_affine(None, dy, s, dpool, 0.0, rs, 1.0 / (H * W))
+        _, wd1, _ = C.prepared(w1, b1, spec1, dtype)
+        _, wd2, _ = C.prepared(w2, b2, spec2, dtype)
+        dz1 = torch.empty_like(t)
+        C.conv_fwd_raw(du, wd2, None, dz1, N, H, W, spec2.cout_p, spec2.cin_p, spec2.cin_p, gate=t, gate_slope=0.0)
+        dw2, db2 = C.conv_wgrad_raw(du, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout)
+        dx = torch.empty_like(x)
+        C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
+        dw1, db1 = C.conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout)
+        return (dx, dw1, db1, dw2, db2, dA1.reshape(Cr, Cp, 1, 1), dab1 if ab1 is not None else None,
+                dA2.reshape(Cp, Cr, 1, 1), dab2 if ab2 is not None else None, None, None, None)
+
+
+def rcab(x, conv1, conv2, ca1, ca2, res_scale):
+    """RCAB on an NHWC map; conv1/conv2 3x3 nn.Conv2d, ca1/ca2 the 1x1 squeeze convs."""
+    if C.pad8(conv1.in_channels) != conv1.in_channels:
+        raise ValueError('RCAB needs num_feat divisible by 8')
+    s1 = C.ConvSpec(conv1.in_channels, conv1.out_channels, act=_lib.ACT_RELU)
+    s2 = C.ConvSpec(conv2.in_channels, conv2.out_channels)
+    return _RCAB.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, ca1.weight, ca1.bias, ca2.weight,
+                       ca2.bias, s1, s2, float(res_scale))
+
+
+def _copy_channels(src, lds_, scoff, dst, ldd, dcoff, P, Cc):
+    lib = _lib.load()
+    _lib.check(lib.sr_copy_channels(_lib.dtype_code(src.dtype), _lib.ptr(src), lds_, scoff, _lib.ptr(dst), ldd, dcoff,
+                                    P, Cc, _lib.stream()))
+
+
+def _act_bwd_inplace(buf, yb, Cbuf, coff, Cc, P, slope):
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_act_backward_nhwc(_lib.dtype_code(buf.dtype), P, Cc, _lib.ptr(buf), Cbuf, coff, _lib.ptr(yb), Cbuf, coff,
+                                 _lib.ptr(buf), Cbuf, coff, _lib.ACT_LRELU, float(slope), 1.0, _lib.stream()))
+
+
+class _RRDB(torch.autograd.Function):
+    """RRDB: out = 0.2 * rdb3(rdb2(rdb1(x))) + x, RDB(z) = 0.2 * conv5(cat(z, x1..x4)) + z."""
+
+    @staticmethod
+    def forward(ctx, x, nf, gc, *params):
+        dtype = x.dtype
+        N, H, W, _ = x.shape
+        Cb = nf + 4 * gc
+        P = N * H * W
+        specs = [C.ConvSpec(nf + k * gc, gc if k < 4 else nf) for k in range(5)]
+        bufs = [torch.empty(N, H, W, Cb, device=x.device, dtype=dtype)]
+        _copy_channels(x, nf, 0, bufs[0], Cb, 0, P, nf)
+        out = None
+        for r in range(3):
+            B = bufs[r]
+            for k in range(4):  # x_{k+1} = lrelu(conv_{k+1}(B[0 : nf + k*gc])) -> B[nf + k*gc : +gc]
+                wf, _, bg = C.prepared(params[r * 10 + 2 * k], params[r * 10 + 2 * k + 1], specs[k], dtype)
+                C.conv_fwd_raw(B, wf, bg, B, N, H, W, nf + k * gc, gc, gc, act=_lib.ACT_LRELU, slope=0.2, ldx=Cb,
+                               ldy=Cb, ycoff=nf + k * gc)
+            wf5, _, bg5 = C.prepared(params[r * 10 + 8], params[r * 10 + 9], specs[4], dtype)
+            if r < 2:  # next RDB input = 0.2 * conv5 + z, written into the next buffer's slice 0..nf
+                nxt = torch.empty(N, H, W, Cb, device=x.device, dtype=dtype)
+                C.conv_fwd_raw(B, wf5, bg5, nxt, N, H, W, Cb, nf, nf, res=B, alpha=0.2, beta=1.0, ldx=Cb, ldy=Cb,
+                               ldr=Cb)
+                bufs.append(nxt)
+            else:  # RRDB output = 0.2 * (0.2 * conv5 + z) + x
+                out = torch.empty(N, H, W, nf, device=x.device, dtype=dtype)
+                C.conv_fwd_raw(B, wf5, bg5, out, N, H, W, Cb, nf, nf, res=B, alpha=0.04, beta=0.2, res2=x, beta2=1.0,
+                               ldx=Cb, ldy=nf, ldr=Cb, ldr2=nf)
+        ctx.nf, ctx.gc = nf, gc
+        ctx.specs = specs
+        ctx.save_for_backward(x, *bufs, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        saved = ctx.saved_tensors
+        x, bufs, params = saved[0], saved[1:4], saved[4:]
+        nf, gc, specs = ctx.nf, ctx.gc, ctx.specs
+        dtype = x.dtype
+        N, H, W, _ = x.shape
+        Cb = nf + 4 * gc
+        P = N * H * W
+        dout = dout.to(dtype).contiguous()
+        grads = [None] * len(params)
+        d_in = dout  # gradient of the current RDB's output, [N,H,W,nf] or slice 0..nf of a Cb buffer
+        ld_in = nf
+        for r in (2, 1, 0):
+            B = bufs[r]
+            w5, b5 = params[r * 10 + 8], params[r * 10 + 9]
+            _, wd5, _ = C.prepared(w5, b5, specs[4], dtype)
+            dB = torch.empty(N, H, W, Cb, device=x.device, dtype=dtype)
+            a5 = 0.04 if r == 2 else 0.2
+            rb = 0.2 if r == 2 else 1.0
+            # dB[0:Cb] = a5 * dgrad5(d_in) ; dB[0:nf] += rb * d_in  (RDB skip)
+            C.conv_fwd_raw(d_in, wd5, None, dB, N, H, W, nf, Cb, Cb, alpha=a5, res=d_in, beta=rb, rcols=nf, ldx=ld_in,
+                           ldr=ld_in, ldy=Cb)
+            grads[r * 10 + 8], grads[r * 10 + 9] = C.conv_wgrad_raw(d_in, B, N, H, W, Cb, Cb, nf, nf, scale=a5,
+                                                                   ldy=ld_in, ldx=Cb)
+            for k in (3, 2, 1, 0):
+                co = nf + k * gc
+                _act_bwd_inplace(dB, B, Cb, co, gc, P, 0.2)
+                w, b = params[r * 10 + 2 * k], params[r * 10 + 2 * k + 1]
+                _, wd, _ = C.prepared(w, b, specs[k], dtype)
+                last = (r == 0 and k == 0)
+                if last:
+                    # d x = dB[0:nf] + dgrad1(dz1) + dout (RRDB skip) -> fresh [N,H,W,nf]
+                    dx = torch.empty(N, H, W, nf, device=x.device, dtype=dtype)
+                    C.conv_fwd_raw(dB, wd, None, dx, N, H, W, gc, co, co, res=dB, beta=1.0, res2=dout, beta2=1.0,
+                                   ldx=Cb, xcoff=co, ldr=Cb, ldr2=nf, ldy=nf)
+                else:
+                    C.conv_fwd_raw(dB, wd, None, dB, N, H, W, gc, co, co, res=dB, beta=1.0, ldx=Cb, xcoff=co, ldr=Cb,
+                                   ldy=Cb)
+                grads[r * 10 + 2 * k], grads[r * 10 + 2 * k + 1] = C.conv_wgrad_raw(
+                    dB, B, N, H, W, co, co, gc, gc, ldy=Cb, ycoff=co, ldx=Cb)
+            d_in, ld_in = dB, Cb
+        return (dx, None, None, *grads)
+
+
+def rrdb(x, block):
+    """x: NHWC [N,H,W,nf]; block: an RRDB module (rdb1..3 with conv1..conv5)."""
+    nf = block.rdb1.conv1.in_channels
+    gc = block.rdb1.conv1.out_channels
+    if nf % 8 or gc % 8:
+        raise ValueError('RRDB on the HIP engine needs num_feat and num_grow_ch divisible by 8')
+    params = []
+    for rdb in (block.rdb1, block.rdb2, block.rdb3):
+        for conv in (rdb.conv1, rdb.conv2, rdb.conv3, rdb.conv4, rdb.conv5):
+            params += [conv.weight, conv.bias]
+    return _RRDB.apply(x, nf, gc, *params)
+
+
+class _BilinearAdd(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, out, x, s):
+        N, Cc, H, W = x.shape
+        y = torch.empty_like(out)
+        lib = _lib.load()
+        _lib.check(lib.sr_bilinear_up_add(_lib.ptr(x.contiguous().float()), N, Cc, H, W, int(s),
+                                          _lib.ptr(out.contiguous()), _lib.ptr(y), _lib.stream()))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError('gradient w.r.t. the LR input of the bilinear skip is not implemented')
+        return dy, None, None
+
+
+def bilinear_up_add(out, x, s):
+    return _BilinearAdd.apply(out, x, s)

@@ -40,11 +40,12 @@ def feature_dtype():
 class ConvSpec:
     """Static configuration of one conv call (epilogue fusion flags)."""
     __slots__ = ('cin', 'cout', 'cin_p', 'cout_p', 'act', 'slope', 'alpha', 'beta', 'out_ps', 'out_nchw',
-                 'aff_scale', 'aff_shift')
+                 'aff_scale', 'aff_shift', 'in_up')
 
     def __init__(self, cin, cout, act=_lib.ACT_NONE, slope=0.0, alpha=1.0, beta=1.0, out_ps=0, out_nchw=False,
-                 aff_scale=None, aff_shift=None, cin_p=None, cout_p=None):
+                 aff_scale=None, aff_shift=None, cin_p=None, cout_p=None, in_up=0):
         self.cin, self.cout = cin, cout
+        self.in_up = in_up
         self.cin_p = cin_p or pad8(cin)
         self.cout_p = cout_p or pad8(cout)
         self.act, self.slope, self.alpha, self.beta = act, float(slope), float(alpha), float(beta)
@@ -87,11 +88,13 @@ def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
     d.act, d.slope, d.alpha = kw.get('act', 0), kw.get('slope', 0.0), kw.get('alpha', 1.0)
     d.ldg, d.gcoff, d.gate_slope = kw.get('ldg', 0), kw.get('gcoff', 0), kw.get('gate_slope', 0.0)
     d.ldr, d.rcoff, d.beta = kw.get('ldr', 0), kw.get('rcoff', 0), kw.get('beta', 1.0)
+    d.ldr2, d.r2coff, d.beta2 = kw.get('ldr2', 0), kw.get('r2coff', 0), kw.get('beta2', 1.0)
+    d.rcols, d.in_up = kw.get('rcols', 0), kw.get('in_up', 0)
     return d
 
 
 def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res=None, aff_scale=None,
-                 aff_shift=None, **kw):
+                 aff_shift=None, res2=None, **kw):
     """Launch sr_conv3x3_fwd on already-prepared GEMM weights (shapes checked here)."""
     assert x.is_contiguous() and y.is_contiguous()
     ldx = kw.pop('ldx', x.shape[-1])
@@ -100,6 +103,8 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
         kw.setdefault('ldg', gate.shape[-1])
     if res is not None:
         kw.setdefault('ldr', res.shape[-1])
+    if res2 is not None:
+        kw.setdefault('ldr2', res2.shape[-1])
     d = _desc(x.dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw)
     assert wf.shape[0] >= cout and wf.shape[1] == 9 * cin, (wf.shape, cout, cin)
     lib = _lib.load()
@@ -108,7 +113,7 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
                      x.element_size() * (M * (cin + cout) + 9 * cin * cout)):
         _lib.check(
             lib.sr_conv3x3_fwd(d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res),
-                               _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.stream()))
+                               _lib.ptr(res2), _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.stream()))
     return y
 
 
@@ -121,6 +126,7 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
     d.Cout, d.Cout_real, d.ldy, d.ycoff, d.out_ps = cout, cout_real, kw.get('ldy', dy.shape[-1]), kw.get(
         'ycoff', 0), out_ps
     d.scale = scale
+    d.in_up = kw.get('in_up', 0)
     lib = _lib.load()
     ws_bytes = lib.sr_conv3x3_wgrad_workspace(d)
     ws = torch.empty(ws_bytes // 4 + 1, device=x.device, dtype=torch.float32)
@@ -155,6 +161,13 @@ def nhwc_to_nchw(x, c, scale=None, shift=None, coff=0):
     return y
 
 
+def _grid(spec, x):
+    """Conv (output) grid of an input map: in_up folds a nearest upsample into the gather."""
+    N, H, W, _ = x.shape
+    u = spec.in_up if spec.in_up and spec.in_up > 1 else 1
+    return N, H * u, W * u
+
+
 def _out_shape(spec, N, H, W):
     if spec.out_nchw:
         return (N, spec.cout, H, W)
@@ -170,13 +183,14 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, weight, bias, spec):
         dtype = x.dtype
-        N, H, W, _ = x.shape
+        N, H, W = _grid(spec, x)
         wf, wd, bg = prepared(weight, bias, spec, dtype)
         out_dtype = torch.float32 if spec.out_nchw else dtype
         y = torch.empty(_out_shape(spec, N, H, W), device=x.device, dtype=out_dtype)
         conv_fwd_raw(x, wf, bg, y, N, H, W, spec.cin_p, spec.cout_p, spec.cout, res=res,
                      aff_scale=spec.aff_scale, aff_shift=spec.aff_shift, act=spec.act, slope=spec.slope,
-                     alpha=spec.alpha, beta=spec.beta, out_ps=spec.out_ps, out_nchw=spec.out_nchw)
+                     alpha=spec.alpha, beta=spec.beta, out_ps=spec.out_ps, out_nchw=spec.out_nchw,
+                     in_up=spec.in_up)
         ctx.spec = spec
         ctx.has_res = res is not None
         ctx.has_bias = bias is not None
@@ -187,7 +201,7 @@ class _Conv3x3(torch.autograd.Function):
     def backward(ctx, dy):
         spec = ctx.spec
         x, weight, bias, y = ctx.saved_tensors
-        N, H, W, _ = x.shape
+        N, H, W = _grid(spec, x)
         dtype = x.dtype
         alpha = spec.alpha
         if spec.out_nchw:
@@ -208,11 +222,13 @@ class _Conv3x3(torch.autograd.Function):
             dx = torch.empty(N, H, W, spec.cin_p, device=x.device, dtype=dtype)
             conv_fwd_raw(dY, wd, None, dx, N, H, W, spec.cout_p, spec.cin_p, spec.cin_p, alpha=alpha,
                          in_ps=spec.out_ps, ldx=dY.shape[-1])
+            if spec.in_up and spec.in_up > 1:
+                dx = nearest_up_backward(dx, spec.in_up)
         if ctx.has_res and ctx.needs_input_grad[1]:
             dres = dy if spec.beta == 1.0 else dy * spec.beta
         if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
             dw, db = conv_wgrad_raw(dY, x, N, H, W, spec.cin_p, spec.cin, spec.cout_p, spec.cout, scale=alpha,
-                                    out_ps=spec.out_ps, need_bias=ctx.has_bias)
+                                    out_ps=spec.out_ps, need_bias=ctx.has_bias, in_up=spec.in_up)
         return dx, dres, dw, db, None
 
 
@@ -316,3 +332,15 @@ def upsample_specs(scale):
     if scale == 3:
         return [3]
     raise ValueError(f'scale {scale} is not supported. Supported scales: 2^n and 3.')
+
+
+def nearest_up_backward(d, s, out=None, accumulate=False):
+    """Sum of each s x s block of an NHWC map (backward of nearest upsampling by s)."""
+    N, Hs, Ws, C = d.shape
+    H, W = Hs // s, Ws // s
+    if out is None:
+        out = torch.empty(N, H, W, C, device=d.device, dtype=d.dtype)
+    lib = _lib.load()
+    _lib.check(lib.sr_nearest_up_backward(_lib.dtype_code(d.dtype), _lib.ptr(d), C, N, H, W, C, s, _lib.ptr(out),
+                                          out.shape[-1], int(accumulate), _lib.stream()))
+    return out

@@ -70,10 +70,15 @@ typedef struct sr_conv3x3_desc {
   float gate_slope;
   int ldr, rcoff;
   float beta;
+  int ldr2, r2coff;
+  float beta2;
+  int rcols;  /* residuals apply to output columns n < rcols (0 = all) */
+  int in_up;  /* x is the [N, H/u, W/u] map read through nearest-neighbour upsampling (0/1 = none) */
 } sr_conv3x3_desc;
 
+/* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL. */
 int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
-                   const void* gate, const void* res, const float* aff_scale,
+                   const void* gate, const void* res, const void* res2, const float* aff_scale,
                    const float* aff_shift, void* y, void* stream);
 
 /* Name of the GPU kernel that sr_conv3x3_fwd / sr_conv3x3_wgrad would launch for a
@@ -95,6 +100,7 @@ typedef struct sr_conv3x3_wgrad_desc {
   int Cin, Cin_real, ldx, xcoff;
   int Cout, Cout_real, ldy, ycoff, out_ps;
   float scale;
+  int in_up;  /* x read through nearest-neighbour upsampling by in_up (0/1 = none) */
 } sr_conv3x3_wgrad_desc;
 
 size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d);
@@ -141,6 +147,42 @@ int sr_act_backward(int dtype, const void* dy, const void* y, int64_t n, int act
 int sr_adam_ema(float* p, const float* g, float* m, float* v, float* ema, int64_t n, float lr,
                 float beta1, float beta2, float eps, float bc1, float bc2, float ema_decay,
                 float grad_scale, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Block kernels of MSRResNet / RCAN / RRDBNet (csrc/blocks.hip).
+ * ------------------------------------------------------------------------------------- */
+/* y = base + bilinear_upsample(x, s) (align_corners=False), fp32 NCHW, x [N,C,H,W]
+ * (MSRResNet skip, basicsr/archs/srresnet_arch.py:64-65). */
+int sr_bilinear_up_add(const float* x, int N, int C, int H, int W, int s, const float* base, float* y,
+                       void* stream);
+/* out[n][c] = scale * sum_p a[n,p,c] (* b[n,p,c] if b) over the HW pixels of NHWC maps (channel
+ * slices via ld/coff), deterministic; RCAN AdaptiveAvgPool2d(1) (rcan_arch.py:19) and its backward. */
+size_t sr_channel_reduce_workspace(int N, int HW, int C);
+int sr_channel_reduce(int dtype, const void* a, int lda, int acoff, const void* b, int ldb, int bcoff, int N,
+                      int HW, int C, float scale, float* out, void* workspace, size_t ws_bytes, void* stream);
+/* RCAN squeeze MLP: h = relu(W1 pool + b1), s = sigmoid(W2 h + b2); W1 [Cr][C], W2 [C][Cr]
+ * (the two 1x1 convs of rcan_arch.py:19-20). */
+int sr_ca_mlp_fwd(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, int N,
+                  int C, int Cr, float* h, float* s, void* stream);
+/* Its backward for the batch: ds = dL/ds -> dpool, dW1, db1, dW2, db2 (scratch: N*(C+Cr) floats). */
+int sr_ca_mlp_bwd(const float* ds, const float* s, const float* h, const float* pool, const float* w1,
+                  const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1, float* dw2,
+                  float* db2, float* scratch, void* stream);
+/* out = beta*x + alpha*u*s[n,c] + gamma*t[n,c] on dense NHWC [N,HW,C] (x, t may be NULL):
+ * RCAB tail x + rs*u*s and its backward rs*dout*s + dpool/HW. */
+int sr_nc_affine(int dtype, const void* x, const void* u, const float* s, const float* t, int N, int HW, int C,
+                 float beta, float alpha, float gamma, void* out, void* stream);
+/* Strided activation backward over channel slices: out = alpha*dy*(y > 0 ? 1 : neg). */
+int sr_act_backward_nhwc(int dtype, int64_t P, int C, const void* dy, int ldd, int dcoff, const void* y, int ldy,
+                         int ycoff, void* out, int ldo, int ocoff, int act, float slope, float alpha,
+                         void* stream);
+/* Backward of nearest upsampling by s: out[n,y,x,c] (+)= sum of d over the s x s block
+ * (rrdbnet_arch.py:116-117); out has H x W pixels, d has sH x sW. */
+int sr_nearest_up_backward(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s, void* out,
+                           int ldo, int accumulate, void* stream);
+/* Strided channel-slice copy (RRDB dense-block buffers). */
+int sr_copy_channels(int dtype, const void* src, int lds, int scoff, void* dst, int ldd, int dcoff, int64_t P,
+                     int C, void* stream);
 
 #ifdef __cplusplus
 }

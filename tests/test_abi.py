@@ -1,0 +1,65 @@
+"""C-ABI boundary checks that need no GPU: libsr_hip.so loads, exports every function
+include/sr_hip.h declares, the ctypes signatures cover them, and argument validation
+fails loudly with SR_EINVAL + a message (the reference raises RuntimeError from
+TORCH_CHECK, basicsr/ops/dcn/src/deform_conv_cuda.cpp:511-516)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from basicsr4rs_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, 'include', 'sr_hip.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(sr_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(lib, n), f'{n} declared in include/sr_hip.h but not exported'
+    assert set(names) == set(_lib.SIGNATURES), 'ctypes SIGNATURES out of sync with include/sr_hip.h'
+    assert b'gfx950' in lib.sr_version()
+
+
+def test_invalid_arguments_raise():
+    lib = _lib.load()
+    rc = lib.sr_conv3x3_fwd(None, None, None, None, None, None, None, None, None, None, None)
+    assert rc == -1 and b'null' in lib.sr_last_error()
+    with pytest.raises(RuntimeError, match='null'):
+        _lib.check(rc)
+    d = _lib.ConvDesc()
+    d.dtype, d.N, d.H, d.W, d.Cin, d.ldx, d.Cout, d.ldw, d.ldy = 1, 1, 4, 4, 12, 12, 16, 108, 16
+    dummy = ctypes.c_void_p(16)
+    rc = lib.sr_conv3x3_fwd(d, dummy, dummy, None, None, None, None, None, None, dummy, None)
+    assert rc == -1 and b'multiples of 8' in lib.sr_last_error()
+    assert lib.sr_pixel_shuffle_nchw(0, dummy, 1, 3, 4, 4, 2, dummy, None) == -1  # C % r^2 != 0
+
+
+def test_cpu_tensors_refused():
+    with pytest.raises(NotImplementedError):
+        _lib.ptr(torch.zeros(4))
+
+
+def test_struct_layouts_match_header():
+    # field order/size of the ctypes mirrors vs the C structs (all 4-byte members)
+    src = re.sub(r'/\*.*?\*/', '', open(os.path.join(ROOT, 'include', 'sr_hip.h')).read(), flags=re.S)
+    for cls, tag in ((_lib.ConvDesc, 'sr_conv3x3_desc'), (_lib.WgradDesc, 'sr_conv3x3_wgrad_desc')):
+        body = re.search(r'typedef struct ' + tag + r' \{(.*?)\}', src, re.S).group(1)
+        fields = []
+        for decl in body.split(';'):
+            decl = decl.strip()
+            if not decl:
+                continue
+            names = decl.split(None, 1)[1]
+            fields += [n.strip() for n in names.split(',')]
+        assert [f[0] for f in cls._fields_] == fields
+        assert ctypes.sizeof(cls) == 4 * len(fields)

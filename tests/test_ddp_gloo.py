@@ -1,0 +1,76 @@
+"""Multi-process gradient reduction (the DDP path, basicsr/models/base_model.py:87-105) on
+CPU with the gloo backend, world_size 2: the bucketed reducer launched from backward hooks
+must reproduce the full-batch gradient (mean over ranks = DDP average)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from basicsr4rs_amd.utils.flat import FlatParams, GradBucketReducer
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _net():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3, padding=1), torch.nn.ReLU(), torch.nn.Conv2d(8, 8, 3, padding=1),
+                               torch.nn.ReLU(), torch.nn.Conv2d(8, 3, 3, padding=1))
+
+
+def _worker(rank, world, port, bucket_mb, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    net = _net()
+    flat = FlatParams(net)
+    red = GradBucketReducer(flat, bucket_mb=bucket_mb)
+    red.broadcast_params(0)
+    g = torch.Generator().manual_seed(123)
+    x = torch.randn(4, 3, 8, 8, generator=g)
+    y = torch.randn(4, 3, 8, 8, generator=g)
+    for step in range(2):
+        flat.zero_grad()
+        sl = slice(rank * 2, rank * 2 + 2)
+        ((net(x[sl]) - y[sl])**2).mean().backward()
+        red.wait()
+        grads = (flat.grad / world).clone()
+    if rank == 0:
+        q.put((grads, len(red.buckets)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('bucket_mb', [25.0, 0.0005])
+def test_bucketed_allreduce_matches_full_batch(bucket_mb):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket_mb, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    grads, nb = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    net = _net()
+    g = torch.Generator().manual_seed(123)
+    x = torch.randn(4, 3, 8, 8, generator=g)
+    y = torch.randn(4, 3, 8, 8, generator=g)
+    ref = []
+    for xs, ys in ((x[:2], y[:2]), (x[2:], y[2:])):
+        net.zero_grad()
+        ((net(xs) - ys)**2).mean().backward()
+        ref.append(torch.cat([p.grad.reshape(-1) for p in net.parameters()]))
+    ref = (ref[0] + ref[1]) / 2
+    assert torch.allclose(grads, ref, rtol=1e-5, atol=1e-6)
+    if bucket_mb < 0.01:
+        assert nb > 1
