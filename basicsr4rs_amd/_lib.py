@@ -28,26 +28,27 @@ class ConvDesc(ctypes.Structure):
                 ('in_ps', _i), ('Cout', _i), ('Cout_real', _i), ('ldw', _i), ('ldy', _i), ('ycoff', _i),
                 ('out_ps', _i), ('out_nchw', _i), ('act', _i), ('slope', _f), ('alpha', _f), ('ldg', _i),
                 ('gcoff', _i), ('gate_slope', _f), ('ldr', _i), ('rcoff', _i), ('beta', _f), ('ldr2', _i),
-                ('r2coff', _i), ('beta2', _f), ('rcols', _i), ('in_up', _i)]
+                ('r2coff', _i), ('beta2', _f), ('rcols', _i), ('in_up', _i), ('ksize', _i), ('gate_mode', _i)]
 
 
 class WgradDesc(ctypes.Structure):
     _fields_ = [('dtype', _i), ('N', _i), ('H', _i), ('W', _i), ('Cin', _i), ('Cin_real', _i), ('ldx', _i),
                 ('xcoff', _i), ('Cout', _i), ('Cout_real', _i), ('ldy', _i), ('ycoff', _i), ('out_ps', _i),
-                ('scale', _f), ('in_up', _i)]
+                ('scale', _f), ('in_up', _i), ('ksize', _i)]
 
 
 # name -> (restype, argtypes); must match include/sr_hip.h (checked by tests/test_abi.py)
 SIGNATURES = {
     'sr_version': (ctypes.c_char_p, []),
     'sr_last_error': (ctypes.c_char_p, []),
-    'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_conv3x3_set_variant': (_i, [_i]),
     'sr_conv3x3_fwd_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_wgrad_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad_workspace': (_sz, [ctypes.POINTER(WgradDesc)]),
-    'sr_conv3x3_wgrad': (_i, [ctypes.POINTER(WgradDesc), _vp, _vp, _vp, _sz, _vp, _vp, _vp]),
+    'sr_conv3x3_wgrad': (_i, [ctypes.POINTER(WgradDesc), _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     'sr_conv3x3_prep': (_i, [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    'sr_conv_prep_mapped': (_i, [_i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_nchw_to_nhwc': (_i, [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     'sr_nhwc_to_nchw': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     'sr_pixel_shuffle_nchw': (_i, [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
@@ -64,6 +65,14 @@ SIGNATURES = {
     'sr_act_backward_nhwc': (_i, [_i, _i64, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _f, _f, _vp]),
     'sr_nearest_up_backward': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     'sr_copy_channels': (_i, [_i, _vp, _i, _i, _vp, _i, _i, _i64, _i, _vp]),
+    'sr_layernorm_fwd': (_i, [_i, _vp, _i, _vp, _vp, _i64, _i, _i, _f, _vp, _i, _vp, _vp, _vp]),
+    'sr_layernorm_bwd_workspace': (_sz, [_i64, _i]),
+    'sr_layernorm_bwd': (_i, [_i, _vp, _i, _vp, _i, _vp, _vp, _vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _sz,
+                             _vp]),
+    'sr_window_attn_fwd': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp, _vp]),
+    'sr_window_attn_bwd_workspace': (_sz, [_i, _i, _i, _i, _i]),
+    'sr_window_attn_bwd': (_i, [_i, _vp, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp,
+                               _sz, _vp]),
 }
 
 _LIB = None

@@ -47,6 +47,9 @@ struct FwdArgs {
   int ldr2, r2coff, rcols;
   float beta2;
   int in_up;  // nearest-neighbour upsample factor folded into the A gather (1 = none)
+  int tap0;   // 4 for 1x1 (linear) convs: the single tap is the centre one
+  int gate_mode;  // 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate)
+  void* aux;      // optional store of the pre-activation value (same layout as y)
   int tiles_n, tiles;
   FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
 };
@@ -111,6 +114,18 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
 #pragma unroll
       for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
     }
+    if (a.aux) {  // pre-activation side output (GELU backward needs it)
+      const size_t da = (size_t)m * a.ldy + a.ycoff + n;
+      if constexpr (SZ == 2) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        *(u32x4*)((bf16_t*)a.aux + da) = o;
+      } else {
+        *(f32x4*)((float*)a.aux + da) = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)((float*)a.aux + da + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
     if (a.gate) {
@@ -128,8 +143,13 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
 #pragma unroll
         for (int j = 0; j < 4; ++j) { g[j] = __uint_as_float(g0[j]); g[4 + j] = __uint_as_float(g1[j]); }
       }
+      if (a.gate_mode == 1) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(g[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
+      }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
@@ -246,8 +266,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 
   auto load = [&](int ks) {
     const int q = ks * 8 + cA;  // this thread's K chunk
-    const int tap = (int)fdiv((uint32_t)q, a.fd_cpt);
-    const int cc = q - tap * a.cpt;
+    const int tap_i = (int)fdiv((uint32_t)q, a.fd_cpt);
+    const int cc = q - tap_i * a.cpt;
+    const int tap = tap_i + a.tap0;
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     const bool kval = q < a.nkc;
     const int ch = cc * PER;  // GEMM input channel of the chunk
@@ -410,8 +431,9 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_big_kernel(FwdArgs a) {
 
   auto issue = [&](int ks, int buf) {
     const int q = ks * 8 + c;
-    const int tap = (int)fdiv((uint32_t)q, a.fd_cpt);
-    const int cc = q - tap * a.cpt;
+    const int tap_i = (int)fdiv((uint32_t)q, a.fd_cpt);
+    const int cc = q - tap_i * a.cpt;
+    const int tap = tap_i + a.tap0;
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
     const bool kval = q < a.nkc;
     const int ch = cc * 8;
@@ -507,6 +529,7 @@ struct WgArgs {
   int Cin, ldx, xcoff;
   int Cout, ldy, ycoff, out_ps;
   int in_up;  // nearest upsample factor of the x gather (1 = none)
+  int taps, tap0;  // 9 / 0 for 3x3, 1 / 4 for 1x1 (linear)
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   FastDiv fd_W, fd_H, fd_cps;
 };
@@ -541,17 +564,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_kernel(WgArgs a) {
   // block -> (split, tap, co tile, ci tile); splits outermost so concurrent blocks share
   // the same pixel range (dy / x rows re-read from L2).
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_split = 9 * a.tiles_co * a.tiles_ci;
+  const int per_split = a.taps * a.tiles_co * a.tiles_ci;
   const int split = (int)b / per_split;
   int rem = (int)b - split * per_split;
   const int tap = rem / (a.tiles_co * a.tiles_ci);
   rem -= tap * a.tiles_co * a.tiles_ci;
   const int co0 = (rem / a.tiles_ci) * BMW;
   const int ci0 = (rem % a.tiles_ci) * BNW;
-  const int dy_ = tap / 3 - 1, dx_ = tap % 3 - 1;
+  const int etap = tap + a.tap0;
+  const int dy_ = etap / 3 - 1, dx_ = etap % 3 - 1;
   const int p_begin = split * a.kper;
   const int p_end = min(a.M, p_begin + a.kper);
-  const bool do_bias = (tap == 4) && (ci0 == 0) && a.wsb != nullptr;
+  const bool do_bias = (etap == 4) && (ci0 == 0) && a.wsb != nullptr;
 
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
@@ -727,7 +751,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_kernel(WgArgs a) {
   }
 
   // partial tile -> slab ws[split][tap][co][ci]; C/D layout: row = co, col = ci
-  float* ws = a.ws + ((size_t)split * 9 + tap) * a.Cout * a.Cin;
+  float* ws = a.ws + ((size_t)split * a.taps + tap) * a.Cout * a.Cin;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -861,7 +885,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
   // block -> (split, role): roles 0 .. 9*tco*tci-1 are (tap, co tile, ci tile) GEMM tiles,
   // the last tco roles (present only when db is wanted) are bias-gradient blocks.
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = 9 * a.tiles_co * a.tiles_ci;
+  const int ntile = a.taps * a.tiles_co * a.tiles_ci;
   const int per_split = ntile + (a.wsb ? a.tiles_co : 0);
   const int split = (int)b / per_split;
   int rem = (int)b - split * per_split;
@@ -873,7 +897,8 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
   rem -= tap * a.tiles_co * a.tiles_ci;
   const int co0 = (rem / a.tiles_ci) * 256;
   const int ci0 = (rem % a.tiles_ci) * 256;
-  const int dy_ = tap / 3 - 1, dx_ = tap % 3 - 1;
+  const int etap = tap + a.tap0;
+  const int dy_ = etap / 3 - 1, dx_ = etap % 3 - 1;
   const int p_begin = split * a.kper;
   const int p_end = min(a.M, p_begin + a.kper);
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
@@ -978,7 +1003,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
     if (ks + 2 < nk) issue(p_begin + (ks + 2) * 64, ks & 1);
   }
 
-  float* ws = a.ws + ((size_t)split * 9 + tap) * a.Cout * a.Cin;
+  float* ws = a.ws + ((size_t)split * a.taps + tap) * a.Cout * a.Cin;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -994,8 +1019,8 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
 // dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co' = GEMM column of co (out_ps
 // permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
-                                    int Cout, int Cin, int Cout_real, int Cin_real, int out_ps,
-                                    float scale) {
+                                    int Cout, int Cin, int Cout_real, int Cin_real, int out_ps, int taps,
+                                    const int* co_map, const int* ci_map, float scale) {
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
@@ -1003,23 +1028,26 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
   if (i < total) {
     const int ci = (int)(i % Cin_real);
     const int co = (int)(i / Cin_real);
-    const int cop = out_ps > 0 ? (co % r2) * cps + co / r2 : co;  // GEMM column of co
-    const size_t stride = (size_t)9 * Cout * Cin;
+    const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);  // GEMM column
+    const int cip = ci_map ? ci_map[ci] : ci;                                                // GEMM k channel
+    const size_t stride = (size_t)taps * Cout * Cin;
     float s[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) s[t] = 0.f;
     for (int k = 0; k < S; ++k) {
-      const float* src = ws + k * stride + (size_t)cop * Cin + ci;
+      const float* src = ws + k * stride + (size_t)cop * Cin + cip;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) s[t] += src[(size_t)t * Cout * Cin];
+      for (int t = 0; t < 9; ++t)
+        if (t < taps) s[t] += src[(size_t)t * Cout * Cin];
     }
-    float* d = dw + i * 9;
+    float* d = dw + i * taps;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) d[t] = s[t] * scale;
+    for (int t = 0; t < 9; ++t)
+      if (t < taps) d[t] = s[t] * scale;
   }
   if (db && i < Cout_real) {
     const int co = (int)i;
-    const int cop = out_ps > 0 ? (co % r2) * cps + co / r2 : co;
+    const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
     float s = 0.f;
     for (int k = 0; k < S; ++k) s += wsb[(size_t)k * Cout + cop];
     db[co] = s * scale;
@@ -1027,29 +1055,34 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
 }
 
 template <typename T>
-__global__ void prep_kernel(const float* w, const float* bias, int Cout_real, int Cin_real, int Cout,
-                            int Cin, int out_ps, T* wf, T* wd, float* bias_g) {
+__global__ void prep_kernel(const float* w, const float* bias, int Cout_real, int Cin_real, int Cout, int Cin,
+                            int out_ps, int taps, const int* row_map, const int* col_map, T* wf, T* wd,
+                            float* bias_g) {
   // one thread per (n, ci, tap) of the padded GEMM weight
-  const int64_t total = (int64_t)Cout * Cin * 9;
+  const int64_t total = (int64_t)Cout * Cin * taps;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
   const int cps = Cout_real / r2;
+  auto row_of = [&](int n) -> int {
+    if (row_map) return row_map[n];
+    if (n >= Cout_real) return -1;
+    return out_ps > 0 ? (n % cps) * r2 + n / cps : n;
+  };
   if (i < total) {
-    const int tap = (int)(i % 9);
-    const int ci = (int)((i / 9) % Cin);
-    const int n = (int)(i / (9 * (int64_t)Cin));
-    int co = -1;
-    if (n < Cout_real) co = out_ps > 0 ? (n % cps) * r2 + n / cps : n;
+    const int tap = (int)(i % taps);
+    const int ci = (int)((i / taps) % Cin);
+    const int n = (int)(i / ((int64_t)taps * Cin));
+    const int co = row_of(n);
+    const int cs = col_map ? col_map[ci] : (ci < Cin_real ? ci : -1);
     float v = 0.f;
-    if (co >= 0 && ci < Cin_real) v = w[((size_t)co * Cin_real + ci) * 9 + tap];
-    if (wf) wf[(size_t)n * 9 * Cin + (size_t)tap * Cin + ci] = Elt<T>::from_f(v);
-    if (wd) wd[(size_t)ci * 9 * Cout + (size_t)(8 - tap) * Cout + n] = Elt<T>::from_f(v);
+    if (co >= 0 && cs >= 0) v = w[((size_t)co * Cin_real + cs) * taps + tap];
+    if (wf) wf[(size_t)n * taps * Cin + (size_t)tap * Cin + ci] = Elt<T>::from_f(v);
+    if (wd) wd[(size_t)ci * taps * Cout + (size_t)(taps - 1 - tap) * Cout + n] = Elt<T>::from_f(v);
   }
   if (bias_g && i < Cout) {
     const int n = (int)i;
-    float v = 0.f;
-    if (n < Cout_real && bias) v = bias[out_ps > 0 ? (n % cps) * r2 + n / cps : n];
-    bias_g[n] = v;
+    const int co = row_of(n);
+    bias_g[n] = (co >= 0 && bias) ? bias[co] : 0.f;
   }
 }
 
@@ -1104,7 +1137,7 @@ hipError_t launch_wg(WgArgs a, hipStream_t s) {
   static_assert(BMW / WM >= 16 && BNW / WN >= 16, "wgrad tile too small for 4 waves");
   a.tiles_co = (a.Cout + BMW - 1) / BMW;
   a.tiles_ci = (a.Cin + BNW - 1) / BNW;
-  const int blocks = a.splits * 9 * a.tiles_co * a.tiles_ci;
+  const int blocks = a.splits * a.taps * a.tiles_co * a.tiles_ci;
   hipLaunchKernelGGL((conv3x3_wgrad_kernel<T, BMW, BNW, WM, WN>), dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -1140,7 +1173,8 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     wg_tiles(d->Cout, d->Cin, &bm, &bn);
     target = 1024;
   }
-  const int tiles = 9 * ((d->Cout + bm - 1) / bm) * ((d->Cin + bn - 1) / bn) + extra;
+  const int taps = d->ksize == 1 ? 1 : 9;
+  const int tiles = taps * ((d->Cout + bm - 1) / bm) * ((d->Cin + bn - 1) / bn) + extra;
   int S = extra ? target / tiles : (target + tiles / 2) / tiles;
   const int maxS = (M + 255) / 256;  // at least 256 pixels per split
   if (S > maxS) S = maxS;
@@ -1158,13 +1192,16 @@ extern "C" {
 
 int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
                    const void* gate, const void* res, const void* res2, const float* aff_scale,
-                   const float* aff_shift, void* y, void* stream) {
+                   const float* aff_shift, void* y, void* aux, void* stream) {
   if (!d || !x || !w || !y) return sr_fail(SR_EINVAL, "conv3x3_fwd: null pointer");
   const int SZ = d->dtype == SR_BF16 ? 2 : 4;
   const int PER = 16 / SZ;
   if (d->Cin % 8 || d->ldx % PER || d->xcoff % PER || (!d->out_nchw && (d->Cout % 8)))
     return sr_fail(SR_EINVAL, "conv3x3_fwd: Cin/Cout/ld/coff must be multiples of 8 (pad channels)");
-  if (d->ldw < 9 * d->Cin) return sr_fail(SR_EINVAL, "conv3x3_fwd: ldw < 9*Cin");
+  const int taps = d->ksize == 1 ? 1 : 9;
+  if (d->ksize != 0 && d->ksize != 1 && d->ksize != 3) return sr_fail(SR_EINVAL, "conv3x3_fwd: ksize must be 1 or 3");
+  if (d->ldw < taps * d->Cin) return sr_fail(SR_EINVAL, "conv3x3_fwd: ldw < taps*Cin");
+  if (aux && (d->out_ps || d->out_nchw)) return sr_fail(SR_EINVAL, "conv3x3_fwd: aux needs plain store");
   if ((gate || res || res2) && d->out_ps) return sr_fail(SR_EINVAL, "conv3x3_fwd: gate/res need plain store");
   const int up = d->in_up > 1 ? d->in_up : 1;
   if (up > 1 && (d->in_ps > 0 || d->H % up || d->W % up))
@@ -1183,7 +1220,10 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   a.r_bytes = res ? (uint32_t)((size_t)M * d->ldr * SZ) : 0;
   a.N = d->N; a.H = d->H; a.W = d->W; a.M = M;
   a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff; a.in_ps = d->in_ps;
-  a.cpt = d->Cin / PER; a.nkc = 9 * a.cpt;
+  a.cpt = d->Cin / PER; a.nkc = taps * a.cpt;
+  a.tap0 = taps == 1 ? 4 : 0;
+  a.gate_mode = d->gate_mode;
+  a.aux = aux;
   a.Cout = d->Cout; a.Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout; a.ldw = d->ldw;
   a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps; a.out_nchw = d->out_nchw;
   a.act = d->act; a.slope = d->slope; a.alpha = d->alpha;
@@ -1234,11 +1274,12 @@ int sr_conv3x3_set_variant(int variant) {
 size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d) {
   int S, kp;
   wgrad_plan(d, &S, &kp);
-  return ((size_t)S * 9 * d->Cout * d->Cin + (size_t)S * d->Cout) * sizeof(float) + 256;
+  const int taps = d->ksize == 1 ? 1 : 9;
+  return ((size_t)S * taps * d->Cout * d->Cin + (size_t)S * d->Cout) * sizeof(float) + 256;
 }
 
 int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void* x, void* workspace,
-                     size_t ws_bytes, float* dw, float* db, void* stream) {
+                     size_t ws_bytes, float* dw, float* db, const int* co_map, const int* ci_map, void* stream) {
   if (!d || !dy || !x || !workspace || !dw) return sr_fail(SR_EINVAL, "conv3x3_wgrad: null pointer");
   const int SZ = d->dtype == SR_BF16 ? 2 : 4;
   const int PER = 16 / SZ;
@@ -1258,7 +1299,10 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   int S, kp;
   wgrad_plan(d, &S, &kp);
   a.ws = (float*)workspace;
-  a.wsb = db ? a.ws + (size_t)S * 9 * d->Cout * d->Cin : nullptr;
+  const int taps = d->ksize == 1 ? 1 : 9;
+  a.taps = taps;
+  a.tap0 = taps == 1 ? 4 : 0;
+  a.wsb = db ? a.ws + (size_t)S * taps * d->Cout * d->Cin : nullptr;
   a.dy_bytes = (uint32_t)dyb2; a.x_bytes = (uint32_t)xb;
   a.N = d->N; a.H = d->H; a.W = d->W; a.M = M;
   a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff;
@@ -1275,7 +1319,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   if (wg_use_big(d)) {
     a.tiles_co = (a.Cout + 255) / 256;
     a.tiles_ci = (a.Cin + 255) / 256;
-    const int per_split = 9 * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
+    const int per_split = taps * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
     hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
     e = hipGetLastError();
   } else {
@@ -1288,26 +1332,35 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   const int64_t work = total > Cout_real ? total : Cout_real;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
                      (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
-                     Cin_real, d->out_ps, d->scale);
+                     Cin_real, d->out_ps, taps, co_map, ci_map, d->scale);
   return sr_check(hipGetLastError(), "conv3x3_wgrad reduce launch");
 }
 
-int sr_conv3x3_prep(int dtype, const float* w, const float* bias, int Cout_real, int Cin_real, int Cout,
-                    int Cin, int out_ps, void* wf, void* wd, float* bias_g, void* stream) {
-  if (!w) return sr_fail(SR_EINVAL, "conv3x3_prep: null weight");
-  if (Cout < Cout_real || Cin < Cin_real) return sr_fail(SR_EINVAL, "conv3x3_prep: padded < real");
-  if (out_ps > 0 && (Cout_real % (out_ps * out_ps) || Cout != Cout_real))
-    return sr_fail(SR_EINVAL, "conv3x3_prep: shuffled conv needs Cout == Cout_real divisible by r^2");
-  const int64_t total = (int64_t)Cout * Cin * 9;
+int sr_conv_prep_mapped(int dtype, int ksize, const float* w, const float* bias, int Cout_real, int Cin_real,
+                        int Cout, int Cin, int out_ps, const int* row_map, const int* col_map, void* wf, void* wd,
+                        float* bias_g, void* stream) {
+  if (!w) return sr_fail(SR_EINVAL, "conv_prep: null weight");
+  if (ksize != 1 && ksize != 3) return sr_fail(SR_EINVAL, "conv_prep: ksize must be 1 or 3");
+  if ((!row_map && Cout < Cout_real) || (!col_map && Cin < Cin_real)) return sr_fail(SR_EINVAL, "conv_prep: padded < real");
+  if (out_ps > 0 && (Cout_real % (out_ps * out_ps) || Cout != Cout_real || row_map))
+    return sr_fail(SR_EINVAL, "conv_prep: shuffled conv needs Cout == Cout_real divisible by r^2");
+  const int taps = ksize == 1 ? 1 : 9;
+  const int64_t total = (int64_t)Cout * Cin * taps;
   const int64_t work = total > Cout ? total : Cout;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SR_BF16)
-    hipLaunchKernelGGL(prep_kernel<bf16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w,
-                       bias, Cout_real, Cin_real, Cout, Cin, out_ps, (bf16_t*)wf, (bf16_t*)wd, bias_g);
+    hipLaunchKernelGGL(prep_kernel<bf16_t>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w, bias, Cout_real,
+                       Cin_real, Cout, Cin, out_ps, taps, row_map, col_map, (bf16_t*)wf, (bf16_t*)wd, bias_g);
   else
-    hipLaunchKernelGGL(prep_kernel<float>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w,
-                       bias, Cout_real, Cin_real, Cout, Cin, out_ps, (float*)wf, (float*)wd, bias_g);
-  return sr_check(hipGetLastError(), "conv3x3_prep launch");
+    hipLaunchKernelGGL(prep_kernel<float>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w, bias, Cout_real,
+                       Cin_real, Cout, Cin, out_ps, taps, row_map, col_map, (float*)wf, (float*)wd, bias_g);
+  return sr_check(hipGetLastError(), "conv_prep launch");
+}
+
+int sr_conv3x3_prep(int dtype, const float* w, const float* bias, int Cout_real, int Cin_real, int Cout, int Cin,
+                    int out_ps, void* wf, void* wd, float* bias_g, void* stream) {
+  return sr_conv_prep_mapped(dtype, 3, w, bias, Cout_real, Cin_real, Cout, Cin, out_ps, nullptr, nullptr, wf, wd,
+                             bias_g, stream);
 }
 
 }  // extern "C"

@@ -82,9 +82,16 @@ SR_DEV uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
+SR_DEV float gelu_exact(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+SR_DEV float gelu_grad(float z) {
+  // d/dz [z * Phi(z)] = Phi(z) + z * phi(z)
+  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+}
+
 SR_DEV float act_apply(float v, int act, float slope) {
-  // act: 0 none, 1 relu, 2 leaky relu(slope)
+  // act: 0 none, 1 relu, 2 leaky relu(slope), 3 GELU (exact erf form, nn.GELU default)
   if (act == 1) return v > 0.f ? v : 0.f;
   if (act == 2) return v > 0.f ? v : v * slope;
+  if (act == 3) return gelu_exact(v);
   return v;
 }

@@ -1,0 +1,454 @@
+// SwinIR token-side kernels: LayerNorm and fused (shifted) window attention.
+//
+//   sr_layernorm_fwd / _bwd : nn.LayerNorm(C) over the channel rows of an NHWC token map
+//       (PatchEmbed norm, SwinTransformerBlock norm1/norm2, final norm:
+//       basicsr/archs/swinir_arch.py:240, 251, 600-604, 846), eps 1e-5, fp32 statistics.
+//   sr_window_attn_fwd / _bwd : WindowAttention (swinir_arch.py:144-175) including the block's
+//       cyclic shift and window partition/reverse (:288-314) — the qkv rows are GATHERED by
+//       (window, token) -> pixel index ((wy*ws + i/ws + s) mod H, (wx*ws + i%ws + s) mod W), so
+//       torch.roll / window_partition / window_reverse never materialise; the shift mask
+//       (:262-281, -100 between different regions) is computed from region ids on the fly;
+//       the relative-position bias (:119-133, 157-160) is gathered from the [(2ws-1)^2, nH] table.
+//
+// qkv layout: per token row, [3][nH][hdp] with hdp >= head_dim (zero padded, 16-B aligned
+// heads); out layout [nH][hdp].  Round-1 attention computes in fp32 FMAs (one wave per
+// (image, window, head) unit, lane = query token); the MFMA version is future work.
+#include "sr_common.h"
+#include "sr_internal.h"
+
+namespace {
+
+template <typename T>
+SR_DEV float ld_elt(const T* p) {
+  return Elt<T>::to_f(*p);
+}
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row; lane l holds channels l, l+64, l+128, ... (coalesced across the wave).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int ldx, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, int64_t M, int C, int Cp,
+                                                     float eps, T* __restrict__ y, int ldy,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int MAXE = 8;  // C <= 512
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += nw) {
+    const T* xr = x + row * ldx;
+    float v[MAXE];
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+      const int c = lane + 64 * e;
+      v[e] = c < C ? ld_elt(xr + c) : 0.f;
+      s += v[e];
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mu = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+      const int c = lane + 64 * e;
+      const float d = c < C ? v[e] - mu : 0.f;
+      q += d * d;
+    }
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rs = rsqrtf(q / C + eps);
+    T* yr = y + row * ldy;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+      const int c = lane + 64 * e;
+      if (c < C) yr[c] = Elt<T>::from_f((v[e] - mu) * rs * gamma[c] + beta[c]);
+      else if (c < Cp) yr[c] = Elt<T>::from_f(0.f);
+    }
+    if (lane == 0) {
+      mean_out[row] = mu;
+      rstd_out[row] = rs;
+    }
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; out = dx (+ res).
+// dgamma/dbeta partials per wave -> partial[wave][2][C].
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, int lddy, const T* __restrict__ x,
+                                                     int ldx, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                     int64_t M, int C, int Cp, const T* __restrict__ res, int ldr,
+                                                     T* __restrict__ dx, int lddx, float* __restrict__ partial) {
+  constexpr int MAXE = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float dg[MAXE], db[MAXE];
+#pragma unroll
+  for (int e = 0; e < MAXE; ++e) dg[e] = db[e] = 0.f;
+  for (int64_t row = gw; row < M; row += nw) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[MAXE], g[MAXE];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+      const int c = lane + 64 * e;
+      if (c < C) {
+        const float d = ld_elt(dy + row * lddy + c);
+        xh[e] = (ld_elt(x + row * ldx + c) - mu) * rs;
+        g[e] = d * gamma[c];
+        dg[e] += d * xh[e];
+        db[e] += d;
+      } else {
+        xh[e] = g[e] = 0.f;
+      }
+      s1 += g[e];
+      s2 += g[e] * xh[e];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o);
+      s2 += __shfl_xor(s2, o);
+    }
+    s1 /= C;
+    s2 /= C;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+      const int c = lane + 64 * e;
+      if (c < C) {
+        float v = rs * (g[e] - s1 - xh[e] * s2);
+        if (res) v += ld_elt(res + row * ldr + c);
+        dx[row * lddx + c] = Elt<T>::from_f(v);
+      } else if (c < Cp) {
+        dx[row * lddx + c] = Elt<T>::from_f(0.f);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < MAXE; ++e) {
+    const int c = lane + 64 * e;
+    if (c < C) {
+      partial[(gw * 2 + 0) * C + c] = dg[e];
+      partial[(gw * 2 + 1) * C + c] = db[e];
+    }
+  }
+}
+
+__global__ void ln_bwd_reduce(const float* __restrict__ partial, int nw, int C, float* __restrict__ dgamma,
+                              float* __restrict__ dbeta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * C) return;
+  const int which = i / C, c = i % C;
+  float s = 0.f;
+  for (int w = 0; w < nw; ++w) s += partial[((size_t)w * 2 + which) * C + c];
+  (which ? dbeta : dgamma)[c] = s;
+}
+
+// ---------------------------------------------------------------- window attention
+struct AttnArgs {
+  const void* qkv;
+  const void* out;   // forward output (backward only)
+  const void* dout;  // (backward only)
+  void* y;           // forward: out; backward: dqkv
+  float* lse;        // [units][T]
+  const float* bias_table;
+  float* dbias_part;  // [units][nbins] (backward)
+  int ldq, ldo;
+  int N, H, W, ws, shift, nH, hd, hdp;
+  float scale;
+  int nwx, nwin, units, T, nbins;
+};
+
+SR_DEV int region(int p, int L, int ws, int s) {
+  // slices (0, -ws), (-ws, -s), (-s, None) of swinir_arch.py:266-271
+  return p < L - ws ? 0 : (p < L - s ? 1 : 2);
+}
+
+SR_DEV void unit_decode(const AttnArgs& a, int unit, int& n, int& wy, int& wx, int& h) {
+  h = unit % a.nH;
+  const int t = unit / a.nH;
+  const int win = t % a.nwin;
+  n = t / a.nwin;
+  wy = win / a.nwx;
+  wx = win % a.nwx;
+}
+
+SR_DEV int64_t token_pixel(const AttnArgs& a, int n, int wy, int wx, int i) {
+  const int sy = wy * a.ws + i / a.ws, sx = wx * a.ws + i % a.ws;  // position in the shifted image
+  int oy = sy + a.shift, ox = sx + a.shift;                          // torch.roll(-s): shifted[p] = x[p + s]
+  if (oy >= a.H) oy -= a.H;
+  if (ox >= a.W) ox -= a.W;
+  return ((int64_t)n * a.H + oy) * a.W + ox;
+}
+
+SR_DEV int token_region(const AttnArgs& a, int wy, int wx, int i) {
+  if (a.shift == 0) return 0;
+  return region(wy * a.ws + i / a.ws, a.H, a.ws, a.shift) * 3 + region(wx * a.ws + i % a.ws, a.W, a.ws, a.shift);
+}
+
+SR_DEV int rel_bin(const AttnArgs& a, int i, int j) {
+  const int dy = i / a.ws - j / a.ws + a.ws - 1;
+  const int dx = i % a.ws - j % a.ws + a.ws - 1;
+  return dy * (2 * a.ws - 1) + dx;
+}
+
+constexpr int TMAX = 64, DMAX = 32, DSTR = 33;
+
+// One wave per unit; lane i = query token i of the window.
+template <typename T>
+__global__ __launch_bounds__(64) void wattn_fwd_kernel(AttnArgs a) {
+  __shared__ float sK[TMAX * DSTR], sV[TMAX * DSTR];
+  __shared__ int sR[TMAX];
+  const int unit = blockIdx.x;
+  const int i = threadIdx.x;
+  int n, wy, wx, h;
+  unit_decode(a, unit, n, wy, wx, h);
+  const bool act = i < a.T;
+  const T* qkv = (const T*)a.qkv;
+  float q[DMAX];
+  int64_t pi = 0;
+  if (act) {
+    pi = token_pixel(a, n, wy, wx, i);
+    const T* row = qkv + pi * a.ldq;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      const bool dv = d < a.hd;
+      q[d] = dv ? ld_elt(row + h * a.hdp + d) : 0.f;
+      sK[i * DSTR + d] = dv ? ld_elt(row + (a.nH + h) * a.hdp + d) : 0.f;
+      sV[i * DSTR + d] = dv ? ld_elt(row + (2 * a.nH + h) * a.hdp + d) : 0.f;
+    }
+    sR[i] = token_region(a, wy, wx, i);
+  }
+  __syncthreads();
+  float srow[TMAX];
+  float mx = -3.0e38f;
+  if (act) {
+    const int ri = sR[i];
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) {
+      float s = -3.0e38f;
+      if (j < a.T) {
+        float dot = 0.f;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) dot += q[d] * sK[j * DSTR + d];
+        s = dot * a.scale + a.bias_table[rel_bin(a, i, j) * a.nH + h];
+        if (a.shift && sR[j] != ri) s += -100.f;
+      }
+      srow[j] = s;
+      mx = fmaxf(mx, s);
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) {
+      const float e = j < a.T ? __expf(srow[j] - mx) : 0.f;
+      srow[j] = e;
+      sum += e;
+    }
+    const float inv = 1.f / sum;
+    float o[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) o[d] = 0.f;
+#pragma unroll
+    for (int j = 0; j < TMAX; ++j) {
+      if (j < a.T) {
+        const float p = srow[j] * inv;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) o[d] += p * sV[j * DSTR + d];
+      }
+    }
+    T* orow = (T*)a.y + pi * a.ldo + h * a.hdp;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d)
+      if (d < a.hdp) orow[d] = Elt<T>::from_f(d < a.hd ? o[d] : 0.f);
+    a.lse[(int64_t)unit * a.T + i] = mx + __logf(sum);
+  }
+}
+
+// Backward: recompute P from lse; dV_j = sum_i P_ij dO_i, dP_ij = dO_i . V_j,
+// dS = P (dP - D_i), dQ_i = scale sum_j dS_ij K_j, dK_j = scale sum_i dS_ij Q_i,
+// dbias[bin(i,j)] += dS_ij.  One wave per unit; P and dS staged in LDS.
+template <typename T>
+__global__ __launch_bounds__(64) void wattn_bwd_kernel(AttnArgs a) {
+  __shared__ float sQ[TMAX * DSTR], sK[TMAX * DSTR], sV[TMAX * DSTR], sdO[TMAX * DSTR];
+  __shared__ float sP[TMAX * (TMAX + 1)], sdS[TMAX * (TMAX + 1)];
+  __shared__ float sBin[(2 * 8 - 1) * (2 * 8 - 1)];
+  __shared__ int sR[TMAX];
+  const int unit = blockIdx.x;
+  const int i = threadIdx.x;
+  int n, wy, wx, h;
+  unit_decode(a, unit, n, wy, wx, h);
+  const bool act = i < a.T;
+  const T* qkv = (const T*)a.qkv;
+  int64_t pi = 0;
+  float D = 0.f;
+  for (int b = i; b < a.nbins; b += 64) sBin[b] = 0.f;
+  if (act) {
+    pi = token_pixel(a, n, wy, wx, i);
+    const T* row = qkv + pi * a.ldq;
+    const T* orow = (const T*)a.out + pi * a.ldo + h * a.hdp;
+    const T* drow = (const T*)a.dout + pi * a.ldo + h * a.hdp;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      const bool dv = d < a.hd;
+      sQ[i * DSTR + d] = dv ? ld_elt(row + h * a.hdp + d) : 0.f;
+      sK[i * DSTR + d] = dv ? ld_elt(row + (a.nH + h) * a.hdp + d) : 0.f;
+      sV[i * DSTR + d] = dv ? ld_elt(row + (2 * a.nH + h) * a.hdp + d) : 0.f;
+      const float dov = dv ? ld_elt(drow + d) : 0.f;
+      sdO[i * DSTR + d] = dov;
+      D += dov * (dv ? ld_elt(orow + d) : 0.f);
+    }
+    sR[i] = token_region(a, wy, wx, i);
+  }
+  __syncthreads();
+  if (act) {
+    const float lse = a.lse[(int64_t)unit * a.T + i];
+    const int ri = sR[i];
+    for (int j = 0; j < a.T; ++j) {
+      float dot = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        dot += sQ[i * DSTR + d] * sK[j * DSTR + d];
+        dp += sdO[i * DSTR + d] * sV[j * DSTR + d];
+      }
+      float s = dot * a.scale + a.bias_table[rel_bin(a, i, j) * a.nH + h];
+      if (a.shift && sR[j] != ri) s += -100.f;
+      const float p = __expf(s - lse);
+      const float ds = p * (dp - D);
+      sP[i * (TMAX + 1) + j] = p;
+      sdS[i * (TMAX + 1) + j] = ds;
+      atomicAdd(&sBin[rel_bin(a, i, j)], ds);
+    }
+  }
+  __syncthreads();
+  if (act) {
+    // lane i now plays key/value token j = i for dK_j, dV_j; and query i for dQ_i
+    float dq[DMAX], dk[DMAX], dv[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) dq[d] = dk[d] = dv[d] = 0.f;
+    for (int t = 0; t < a.T; ++t) {
+      const float dsi = sdS[i * (TMAX + 1) + t];  // dS[i][t]
+      const float dsj = sdS[t * (TMAX + 1) + i];  // dS[t][i]
+      const float pj = sP[t * (TMAX + 1) + i];    // P[t][i]
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        dq[d] += dsi * sK[t * DSTR + d];
+        dk[d] += dsj * sQ[t * DSTR + d];
+        dv[d] += pj * sdO[t * DSTR + d];
+      }
+    }
+    T* grow = (T*)a.y + pi * a.ldq;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) {
+      if (d < a.hdp) {
+        const bool valid = d < a.hd;
+        grow[h * a.hdp + d] = Elt<T>::from_f(valid ? dq[d] * a.scale : 0.f);
+        grow[(a.nH + h) * a.hdp + d] = Elt<T>::from_f(valid ? dk[d] * a.scale : 0.f);
+        grow[(2 * a.nH + h) * a.hdp + d] = Elt<T>::from_f(valid ? dv[d] : 0.f);
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = i; b < a.nbins; b += 64) a.dbias_part[(int64_t)unit * a.nbins + b] = sBin[b];
+}
+
+// dbias[bin][h] = sum over units of head h of dbias_part[unit][bin]
+__global__ void wattn_dbias_reduce(const float* __restrict__ part, int units, int nH, int nbins,
+                                   float* __restrict__ dbias) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nbins * nH) return;
+  const int bin = idx / nH, h = idx % nH;
+  float s = 0.f;
+  for (int u = h; u < units; u += nH) s += part[(int64_t)u * nbins + bin];
+  dbias[idx] = s;
+}
+
+bool attn_setup(AttnArgs& a, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp, float scale) {
+  if (ws < 1 || ws > 8 || hd > DMAX || hd > hdp || H % ws || W % ws || shift < 0 || shift >= ws) return false;
+  a.N = N; a.H = H; a.W = W; a.ws = ws; a.shift = shift; a.nH = nH; a.hd = hd; a.hdp = hdp; a.scale = scale;
+  a.nwx = W / ws;
+  a.nwin = (H / ws) * (W / ws);
+  a.units = N * a.nwin * nH;
+  a.T = ws * ws;
+  a.nbins = (2 * ws - 1) * (2 * ws - 1);
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, const float* beta, int64_t M, int C, int Cp,
+                     float eps, void* y, int ldy, float* mean, float* rstd, void* stream) {
+  if (!x || !gamma || !beta || !y || !mean || !rstd || C > 512 || Cp < C) return sr_fail(SR_EINVAL, "layernorm_fwd: bad arguments");
+  const unsigned grid = (unsigned)((M + 3) / 4 < 16384 ? (M + 3) / 4 : 16384);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, gamma, beta, M, C, Cp,
+                       eps, (bf16_t*)y, ldy, mean, rstd);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, ldx, gamma, beta, M, C, Cp,
+                       eps, (float*)y, ldy, mean, rstd);
+  return sr_check(hipGetLastError(), "layernorm_fwd launch");
+}
+
+size_t sr_layernorm_bwd_workspace(int64_t M, int C) {
+  (void)M;
+  return (size_t)2048 * 4 * 2 * C * sizeof(float);
+}
+
+int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean, const float* rstd,
+                     const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr, void* dx, int lddx,
+                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes, void* stream) {
+  if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || C > 512)
+    return sr_fail(SR_EINVAL, "layernorm_bwd: bad arguments");
+  if (ws_bytes < sr_layernorm_bwd_workspace(M, C)) return sr_fail(SR_EINVAL, "layernorm_bwd: workspace too small");
+  const unsigned grid = (unsigned)((M + 3) / 4 < 2048 ? (M + 3) / 4 : 2048);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx,
+                       mean, rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, lddy, (const float*)x, ldx,
+                       mean, rstd, gamma, M, C, Cp, (const float*)res, ldr, (float*)dx, lddx, (float*)workspace);
+  hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * C + 255) / 256), dim3(256), 0, s, (const float*)workspace, (int)grid * 4,
+                     C, dgamma, dbeta);
+  return sr_check(hipGetLastError(), "layernorm_bwd launch");
+}
+
+int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W, int ws, int shift, int nH, int hd,
+                       int hdp, float scale, const float* bias_table, void* out, int ldo, float* lse, void* stream) {
+  AttnArgs a{};
+  if (!qkv || !bias_table || !out || !lse || !attn_setup(a, N, H, W, ws, shift, nH, hd, hdp, scale))
+    return sr_fail(SR_EINVAL, "window_attn_fwd: bad arguments (ws <= 8, head_dim <= 32, H/W divisible by ws)");
+  a.qkv = qkv; a.y = out; a.lse = lse; a.bias_table = bias_table; a.ldq = ldq; a.ldo = ldo;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(wattn_fwd_kernel<bf16_t>, dim3(a.units), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(wattn_fwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
+  return sr_check(hipGetLastError(), "window_attn_fwd launch");
+}
+
+size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH) {
+  const int nb = (2 * ws - 1) * (2 * ws - 1);
+  return (size_t)N * (H / ws) * (W / ws) * nH * nb * sizeof(float);
+}
+
+int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo, const float* lse,
+                       int N, int H, int W, int ws, int shift, int nH, int hd, int hdp, float scale,
+                       const float* bias_table, void* dqkv, float* dbias_table, void* workspace, size_t ws_bytes,
+                       void* stream) {
+  AttnArgs a{};
+  if (!qkv || !out || !dout || !lse || !bias_table || !dqkv || !dbias_table ||
+      !attn_setup(a, N, H, W, ws, shift, nH, hd, hdp, scale))
+    return sr_fail(SR_EINVAL, "window_attn_bwd: bad arguments");
+  if (ws_bytes < sr_window_attn_bwd_workspace(N, H, W, ws, nH)) return sr_fail(SR_EINVAL, "window_attn_bwd: workspace");
+  a.qkv = qkv; a.out = out; a.dout = dout; a.y = dqkv; a.lse = (float*)lse; a.bias_table = bias_table;
+  a.dbias_part = (float*)workspace; a.ldq = ldq; a.ldo = ldo;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(wattn_bwd_kernel<bf16_t>, dim3(a.units), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(wattn_bwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(wattn_dbias_reduce, dim3((a.nbins * nH + 255) / 256), dim3(256), 0, s,
+                     (const float*)workspace, a.units, nH, a.nbins, dbias_table);
+  return sr_check(hipGetLastError(), "window_attn_bwd launch");
+}
+
+}  // extern "C"

@@ -90,11 +90,13 @@ def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
     d.ldr, d.rcoff, d.beta = kw.get('ldr', 0), kw.get('rcoff', 0), kw.get('beta', 1.0)
     d.ldr2, d.r2coff, d.beta2 = kw.get('ldr2', 0), kw.get('r2coff', 0), kw.get('beta2', 1.0)
     d.rcols, d.in_up = kw.get('rcols', 0), kw.get('in_up', 0)
+    d.ksize, d.gate_mode = kw.get('ksize', 3), kw.get('gate_mode', 0)
+    d.ldw = (9 if d.ksize == 3 else 1) * cin
     return d
 
 
 def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res=None, aff_scale=None,
-                 aff_shift=None, res2=None, **kw):
+                 aff_shift=None, res2=None, aux=None, **kw):
     """Launch sr_conv3x3_fwd on already-prepared GEMM weights (shapes checked here)."""
     assert x.is_contiguous() and y.is_contiguous()
     ldx = kw.pop('ldx', x.shape[-1])
@@ -106,14 +108,16 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     if res2 is not None:
         kw.setdefault('ldr2', res2.shape[-1])
     d = _desc(x.dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw)
-    assert wf.shape[0] >= cout and wf.shape[1] == 9 * cin, (wf.shape, cout, cin)
+    assert wf.shape[0] >= cout and wf.shape[1] == d.ldw, (wf.shape, cout, cin)
     lib = _lib.load()
     M = N * H * W
-    with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * 9 * cin * cout_real,
-                     x.element_size() * (M * (cin + cout) + 9 * cin * cout)):
+    taps = 9 if d.ksize == 3 else 1
+    with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * taps * cin * cout_real,
+                     x.element_size() * (M * (cin + cout) + taps * cin * cout)):
         _lib.check(
             lib.sr_conv3x3_fwd(d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res),
-                               _lib.ptr(res2), _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.stream()))
+                               _lib.ptr(res2), _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.ptr(aux),
+                               _lib.stream()))
     return y
 
 
@@ -127,17 +131,19 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
         'ycoff', 0), out_ps
     d.scale = scale
     d.in_up = kw.get('in_up', 0)
+    d.ksize = kw.get('ksize', 3)
     lib = _lib.load()
     ws_bytes = lib.sr_conv3x3_wgrad_workspace(d)
     ws = torch.empty(ws_bytes // 4 + 1, device=x.device, dtype=torch.float32)
-    dw = torch.empty(cout_real, cin_real, 3, 3, device=x.device, dtype=torch.float32)
+    kk = 3 if d.ksize == 3 else 1
+    dw = torch.empty(cout_real, cin_real, kk, kk, device=x.device, dtype=torch.float32)
     db = torch.empty(cout_real, device=x.device, dtype=torch.float32) if need_bias else None
     M = N * H * W
-    with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * 9 * cin_real * cout_real,
-                     x.element_size() * M * (cin + cout) + 4 * 9 * cin * cout):
+    with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * kk * kk * cin_real * cout_real,
+                     x.element_size() * M * (cin + cout) + 4 * kk * kk * cin * cout):
         _lib.check(
             lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(dw), _lib.ptr(db),
-                                 _lib.stream()))
+                                 _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')), _lib.stream()))
     return dw, db
 
 
@@ -344,3 +350,20 @@ def nearest_up_backward(d, s, out=None, accumulate=False):
     _lib.check(lib.sr_nearest_up_backward(_lib.dtype_code(d.dtype), _lib.ptr(d), C, N, H, W, C, s, _lib.ptr(out),
                                           out.shape[-1], int(accumulate), _lib.stream()))
     return out
+
+
+class _ToNCHW(torch.autograd.Function):
+    """NHWC feature map -> NCHW fp32, y = x*scale[c] + shift[c] (first c channels)."""
+
+    @staticmethod
+    def forward(ctx, x, c, scale, shift):
+        ctx.c, ctx.cp, ctx.scale, ctx.dtype = c, x.shape[-1], scale, x.dtype
+        return nhwc_to_nchw(x.contiguous(), c, scale=scale, shift=shift)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return nchw_to_nhwc(dy.contiguous(), ctx.cp, ctx.dtype, scale=ctx.scale), None, None, None
+
+
+def to_nchw(x, c, scale=None, shift=None):
+    return _ToNCHW.apply(x, c, scale, shift)

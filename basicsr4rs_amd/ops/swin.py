@@ -1,0 +1,253 @@
+"""SwinIR token ops on the HIP engine (csrc/swin.hip + 1x1 implicit-GEMM linears).
+
+The token map of SwinIR ([B, H*W, C] after PatchEmbed, basicsr/archs/swinir_arch.py:600-604)
+is exactly our NHWC feature map, so PatchEmbed / PatchUnEmbed are free.  A SwinTransformerBlock
+(swinir_arch.py:283-323) is ONE autograd Function:
+
+    ln1 = LN(x); qkv = Linear(ln1)            -> [M, 3*nH*hdp]   (heads padded to hdp = 32)
+    a   = WindowAttention(qkv)                 (shift / partition / mask / bias in-kernel)
+    x2  = x + Linear_proj(a)                   (residual fused in the GEMM epilogue)
+    ln2 = LN(x2); h = GELU(Linear_fc1(ln2))    (GELU + pre-activation side output fused)
+    out = x2 + Linear_fc2(h)
+
+with a hand-written backward (GELU' fused into fc2's dgrad epilogue, LN residual fused).
+Linears are 1x1 convs: nn.Linear.weight [out][in] is the 1x1 conv weight; the padded head
+layout is produced by index maps in the HIP weight-prep kernel.  DropPath is the identity at
+drop_path_rate 0 / eval (parity mode); SURVEY.md §0.7.
+"""
+import torch
+
+from .. import _lib
+from . import conv as C
+
+GELU = 3
+
+
+class LinearSpec:
+    """GEMM geometry of an nn.Linear on padded token rows, with index maps."""
+
+    def __init__(self, cin, cout, cin_p, cout_p, row_map=None, col_map=None):
+        self.cin, self.cout, self.cin_p, self.cout_p = cin, cout, cin_p, cout_p
+        self.row_map, self.col_map = row_map, col_map  # GEMM index -> param index (or -1)
+        co_map = ci_map = None
+        if row_map is not None:
+            co_map = [0] * cout
+            for n, r in enumerate(row_map):
+                if r >= 0:
+                    co_map[r] = n
+        if col_map is not None:
+            ci_map = [0] * cin
+            for k, c in enumerate(col_map):
+                if c >= 0:
+                    ci_map[c] = k
+        self.co_map, self.ci_map = co_map, ci_map
+        self._dev = {}
+
+    def maps(self, device):
+        key = str(device)
+        if key not in self._dev:
+            t = lambda v: torch.tensor(v, dtype=torch.int32, device=device) if v is not None else None  # noqa: E731
+            self._dev[key] = (t(self.row_map), t(self.col_map), t(self.co_map), t(self.ci_map))
+        return self._dev[key]
+
+
+def qkv_spec(C_, nH, hdp):
+    hd = C_ // nH
+    rows = [(w * C_ + h * hd + d) if d < hd else -1 for w in range(3) for h in range(nH) for d in range(hdp)]
+    return LinearSpec(C_, 3 * C_, C.pad8(C_), 3 * nH * hdp, row_map=rows,
+                      col_map=[k if k < C_ else -1 for k in range(C.pad8(C_))])
+
+
+def proj_spec(C_, nH, hdp):
+    hd = C_ // nH
+    cols = [(h * hd + d) if d < hd else -1 for h in range(nH) for d in range(hdp)]
+    return LinearSpec(C_, C_, nH * hdp, C.pad8(C_), row_map=[n if n < C_ else -1 for n in range(C.pad8(C_))],
+                      col_map=cols)
+
+
+def plain_spec(cin, cout):
+    return LinearSpec(cin, cout, C.pad8(cin), C.pad8(cout), row_map=[n if n < cout else -1 for n in range(C.pad8(cout))],
+                      col_map=[k if k < cin else -1 for k in range(C.pad8(cin))])
+
+
+def prepared_linear(weight, bias, spec, dtype):
+    key = (weight._version, C._PARAM_EPOCH[0], dtype, spec.cin_p, spec.cout_p, weight.data_ptr(), 'lin')
+    cache = getattr(weight, '_sr_prep', None)
+    if cache is not None and cache[0] == key:
+        return cache[1]
+    dev = weight.device
+    rm, cm, _, _ = spec.maps(dev)
+    wf = torch.empty(spec.cout_p, spec.cin_p, device=dev, dtype=dtype)
+    wd = torch.empty(spec.cin_p, spec.cout_p, device=dev, dtype=dtype)
+    bg = torch.empty(spec.cout_p, device=dev, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_conv_prep_mapped(_lib.dtype_code(dtype), 1, _lib.ptr(weight.detach()),
+                                _lib.ptr(bias.detach() if bias is not None else None), spec.cout, spec.cin,
+                                spec.cout_p, spec.cin_p, 0, _lib.ptr(rm), _lib.ptr(cm), _lib.ptr(wf), _lib.ptr(wd),
+                                _lib.ptr(bg), _lib.stream()))
+    weight._sr_prep = (key, (wf, wd, bg))
+    return wf, wd, bg
+
+
+def linear_fwd(x, wf, bg, spec, N, H, W, **kw):
+    y = torch.empty(N, H, W, spec.cout_p, device=x.device, dtype=x.dtype)
+    C.conv_fwd_raw(x, wf, bg, y, N, H, W, spec.cin_p, spec.cout_p, spec.cout_p, ksize=1, **kw)
+    return y
+
+
+def linear_dgrad(dy, wd, spec, N, H, W, **kw):
+    dx = torch.empty(N, H, W, spec.cin_p, device=dy.device, dtype=dy.dtype)
+    C.conv_fwd_raw(dy, wd, None, dx, N, H, W, spec.cout_p, spec.cin_p, spec.cin_p, ksize=1, **kw)
+    return dx
+
+
+def linear_wgrad(dy, x, spec, N, H, W, need_bias=True):
+    _, _, co, ci = spec.maps(dy.device)
+    dw, db = C.conv_wgrad_raw(dy, x, N, H, W, spec.cin_p, spec.cin, spec.cout_p, spec.cout, ksize=1, co_map=co,
+                              ci_map=ci, need_bias=need_bias)
+    return dw.reshape(spec.cout, spec.cin), db
+
+
+def layernorm(x, weight, bias, Creal, eps=1e-5):
+    N, H, W, Cp = x.shape
+    M = N * H * W
+    y = torch.empty_like(x)
+    mean = torch.empty(M, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_layernorm_fwd(_lib.dtype_code(x.dtype), _lib.ptr(x), Cp, _lib.ptr(weight.detach()),
+                             _lib.ptr(bias.detach()), M, Creal, Cp, float(eps), _lib.ptr(y), Cp, _lib.ptr(mean),
+                             _lib.ptr(rstd), _lib.stream()))
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None):
+    N, H, W, Cp = x.shape
+    M = N * H * W
+    dx = torch.empty_like(x)
+    dg = torch.empty(Creal, device=x.device, dtype=torch.float32)
+    db = torch.empty(Creal, device=x.device, dtype=torch.float32)
+    lib = _lib.load()
+    wsb = lib.sr_layernorm_bwd_workspace(M, Creal)
+    ws = torch.empty(wsb // 4 + 1, device=x.device, dtype=torch.float32)
+    _lib.check(
+        lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
+                             _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res),
+                             res.shape[-1] if res is not None else 0, _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db),
+                             _lib.ptr(ws), wsb, _lib.stream()))
+    return dx, dg, db
+
+
+class _LayerNorm(torch.autograd.Function):
+    """Standalone token LayerNorm (PatchEmbed norm / final norm)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, Creal):
+        y, mean, rstd = layernorm(x, weight, bias, Creal)
+        ctx.Creal = Creal
+        ctx.save_for_backward(x, mean, rstd, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, weight = ctx.saved_tensors
+        dx, dg, db = layernorm_bwd(dy.to(x.dtype).contiguous(), x, mean, rstd, weight, ctx.Creal)
+        return dx, dg, db, None
+
+
+def token_layernorm(x, norm):
+    return _LayerNorm.apply(x, norm.weight, norm.bias, norm.normalized_shape[0])
+
+
+class AttnGeom:
+
+    def __init__(self, dim, nH, ws, shift, hdp=32):
+        self.dim, self.nH, self.ws, self.shift, self.hdp = dim, nH, ws, shift, hdp
+        self.hd = dim // nH
+        self.qkv = qkv_spec(dim, nH, hdp)
+        self.proj = proj_spec(dim, nH, hdp)
+
+
+def window_attn(qkv, g, N, H, W, scale, table):
+    out = torch.empty(N, H, W, g.nH * g.hdp, device=qkv.device, dtype=qkv.dtype)
+    lse = torch.empty(N * (H // g.ws) * (W // g.ws) * g.nH * g.ws * g.ws, device=qkv.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(
+        lib.sr_window_attn_fwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], N, H, W, g.ws, g.shift, g.nH,
+                               g.hd, g.hdp, float(scale), _lib.ptr(table), _lib.ptr(out), out.shape[-1], _lib.ptr(lse),
+                               _lib.stream()))
+    return out, lse
+
+
+def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table):
+    dqkv = torch.empty_like(qkv)
+    dtable = torch.empty_like(table)
+    lib = _lib.load()
+    wsb = lib.sr_window_attn_bwd_workspace(N, H, W, g.ws, g.nH)
+    ws = torch.empty(wsb // 4 + 1, device=qkv.device, dtype=torch.float32)
+    _lib.check(
+        lib.sr_window_attn_bwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], _lib.ptr(out), _lib.ptr(dout),
+                               out.shape[-1], _lib.ptr(lse), N, H, W, g.ws, g.shift, g.nH, g.hd, g.hdp, float(scale),
+                               _lib.ptr(table), _lib.ptr(dqkv), _lib.ptr(dtable), _lib.ptr(ws), wsb, _lib.stream()))
+    return dqkv, dtable
+
+
+class _STB(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, geom, fc1s, fc2s, scale, n1w, n1b, qw, qb, table, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b):
+        dtype = x.dtype
+        N, H, W, Cp = x.shape
+        Cr = geom.dim
+        ln1, m1, r1 = layernorm(x, n1w, n1b, Cr)
+        qwf, _, qbg = prepared_linear(qw, qb, geom.qkv, dtype)
+        qkv = linear_fwd(ln1, qwf, qbg, geom.qkv, N, H, W)
+        tab = table.detach().float().contiguous()
+        a, lse = window_attn(qkv, geom, N, H, W, scale, tab)
+        pwf, _, pbg = prepared_linear(pw, pb, geom.proj, dtype)
+        x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0)
+        ln2, m2, r2 = layernorm(x2, n2w, n2b, Cr)
+        f1wf, _, f1bg = prepared_linear(f1w, f1b, fc1s, dtype)
+        z = torch.empty(N, H, W, fc1s.cout_p, device=x.device, dtype=dtype)
+        h = linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)
+        f2wf, _, f2bg = prepared_linear(f2w, f2b, fc2s, dtype)
+        out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0)
+        ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale = geom, fc1s, fc2s, scale
+        ctx.save_for_backward(x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w,
+                              f1b, f2w, f2b)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w, f1b, f2w,
+         f2b) = ctx.saved_tensors
+        g, fc1s, fc2s, scale = ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale
+        dtype = x.dtype
+        N, H, W, Cp = x.shape
+        Cr = g.dim
+        dout = dout.to(dtype).contiguous()
+        _, f2wd, _ = prepared_linear(f2w, f2b, fc2s, dtype)
+        dz = linear_dgrad(dout, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)
+        df2w, df2b = linear_wgrad(dout, h, fc2s, N, H, W)
+        _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
+        dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
+        df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W)
+        dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout)
+        _, pwd, _ = prepared_linear(pw, pb, g.proj, dtype)
+        da = linear_dgrad(dx2, pwd, g.proj, N, H, W)
+        dpw, dpb = linear_wgrad(dx2, a, g.proj, N, H, W)
+        dqkv, dtab = window_attn_bwd(qkv, a, da, lse, g, N, H, W, scale, tab)
+        _, qwd, _ = prepared_linear(qw, qb, g.qkv, dtype)
+        dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
+        dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W)
+        dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2)
+        return (dx, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b)
+
+
+def swin_block(x, blk, geom, fc1s, fc2s):
+    at = blk.attn
+    return _STB.apply(x, geom, fc1s, fc2s, float(at.scale), blk.norm1.weight, blk.norm1.bias, at.qkv.weight,
+                      at.qkv.bias, at.relative_position_bias_table, at.proj.weight, at.proj.bias, blk.norm2.weight,
+                      blk.norm2.bias, blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias)

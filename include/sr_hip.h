@@ -74,12 +74,16 @@ typedef struct sr_conv3x3_desc {
   float beta2;
   int rcols;  /* residuals apply to output columns n < rcols (0 = all) */
   int in_up;  /* x is the [N, H/u, W/u] map read through nearest-neighbour upsampling (0/1 = none) */
+  int ksize;  /* 3 (default, 0 = 3) or 1: a 1x1 conv = nn.Linear over the NHWC tokens */
+  int gate_mode; /* 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate) (gate = pre-activation) */
 } sr_conv3x3_desc;
 
-/* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL. */
+/* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.
+ * act: SR_ACT_* or 3 = GELU (exact erf).  aux (may be NULL): also store the pre-activation
+ * value conv(x, w) + bias in y's layout (GELU backward). */
 int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
                    const void* gate, const void* res, const void* res2, const float* aff_scale,
-                   const float* aff_shift, void* y, void* stream);
+                   const float* aff_shift, void* y, void* aux, void* stream);
 
 /* Name of the GPU kernel that sr_conv3x3_fwd / sr_conv3x3_wgrad would launch for a
  * descriptor (static string; for traces and profiler summaries). */
@@ -101,11 +105,15 @@ typedef struct sr_conv3x3_wgrad_desc {
   int Cout, Cout_real, ldy, ycoff, out_ps;
   float scale;
   int in_up;  /* x read through nearest-neighbour upsampling by in_up (0/1 = none) */
+  int ksize;  /* 3 (0 = 3) or 1 */
 } sr_conv3x3_wgrad_desc;
 
 size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d);
+/* co_map[co] / ci_map[ci] (optional, device int arrays over the real param rows / cols) give
+ * the GEMM column / input channel of each parameter row / column (padded head layouts). */
 int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void* x,
-                     void* workspace, size_t ws_bytes, float* dw, float* db, void* stream);
+                     void* workspace, size_t ws_bytes, float* dw, float* db, const int* co_map,
+                     const int* ci_map, void* stream);
 
 /* Weight preparation from the nn.Conv2d parameter w[Cout_real][Cin_real][3][3] (fp32):
  *   wf[n][tap*Cin + ci]       forward GEMM rows (n = GEMM column, permuted by out_ps)
@@ -115,6 +123,12 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
 int sr_conv3x3_prep(int dtype, const float* w, const float* bias, int Cout_real, int Cin_real,
                     int Cout, int Cin, int out_ps, void* wf, void* wd, float* bias_g,
                     void* stream);
+/* General form: ksize 1 or 3; row_map[n] (n < Cout) = parameter row of GEMM column n or -1
+ * (zero row), col_map[k] (k < Cin) = parameter column of GEMM input channel k or -1; NULL maps
+ * = identity (+ out_ps permutation).  nn.Linear weights are [out][in] = 1x1 conv weights. */
+int sr_conv_prep_mapped(int dtype, int ksize, const float* w, const float* bias, int Cout_real,
+                        int Cin_real, int Cout, int Cin, int out_ps, const int* row_map,
+                        const int* col_map, void* wf, void* wd, float* bias_g, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Layout / elementwise ops (HBM-bound).
@@ -183,6 +197,33 @@ int sr_nearest_up_backward(int dtype, const void* d, int ldd, int N, int H, int 
 /* Strided channel-slice copy (RRDB dense-block buffers). */
 int sr_copy_channels(int dtype, const void* src, int lds, int scoff, void* dst, int ldd, int dcoff, int64_t P,
                      int C, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * SwinIR token kernels (csrc/swin.hip).  Token maps are NHWC rows (= the reference's
+ * [B, H*W, C] after PatchEmbed, swinir_arch.py:600-604).
+ * ------------------------------------------------------------------------------------- */
+/* nn.LayerNorm(C) over rows of [M][ld]: y = (x-mean)*rstd*gamma + beta (channels < C; columns
+ * C..Cp-1 of y set to 0); saves per-row mean / rstd (fp32). */
+int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, const float* beta, int64_t M,
+                     int C, int Cp, float eps, void* y, int ldy, float* mean, float* rstd, void* stream);
+size_t sr_layernorm_bwd_workspace(int64_t M, int C);
+/* dx = LN backward (+ res if not NULL), dgamma / dbeta over all rows (deterministic). */
+int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean,
+                     const float* rstd, const float* gamma, int64_t M, int C, int Cp, const void* res,
+                     int ldr, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
+                     size_t ws_bytes, void* stream);
+/* Shifted-window multi-head attention on [N*H*W][ldq] qkv rows laid out [3][nH][hdp]
+ * (head_dim hd <= hdp, zero padded): cyclic shift by `shift`, ws x ws windows, scale,
+ * relative-position bias table [(2ws-1)^2][nH], -100 shift mask; out rows [nH][hdp];
+ * lse = per-query log-sum-exp (for the backward).  ws <= 8, hd <= 32. */
+int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W, int ws, int shift, int nH,
+                       int hd, int hdp, float scale, const float* bias_table, void* out, int ldo, float* lse,
+                       void* stream);
+size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH);
+int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo,
+                       const float* lse, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp,
+                       float scale, const float* bias_table, void* dqkv, float* dbias_table, void* workspace,
+                       size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -170,3 +170,131 @@ def adam_step(p, g, m, v, step, lr, beta1=0.9, beta2=0.99, eps=1e-8):
     bc2 = 1 - beta2**step
     denom = v.sqrt() / math.sqrt(bc2) + eps
     return p - (lr / bc1) * m / denom, m, v
+
+
+def _ln(x, sd, p):
+    """nn.LayerNorm over the last dim, eps 1e-5."""
+    return F.layer_norm(x, (x.shape[-1], ), sd[f'{p}.weight'], sd[f'{p}.bias'], 1e-5)
+
+
+def _linear(x, sd, p):
+    return F.linear(x, sd[f'{p}.weight'], sd.get(f'{p}.bias'))
+
+
+def window_partition(x, ws):
+    """(b, h, w, c) -> (b * nW, ws, ws, c)  (basicsr/archs/swinir_arch.py:63-75)."""
+    b, h, w, c = x.shape
+    return x.view(b, h // ws, ws, w // ws, ws, c).permute(0, 1, 3, 2, 4, 5).reshape(-1, ws, ws, c)
+
+
+def window_reverse(windows, ws, h, w):
+    """Inverse of window_partition (swinir_arch.py:78-92)."""
+    b = windows.shape[0] // ((h // ws) * (w // ws))
+    return windows.view(b, h // ws, w // ws, ws, ws, -1).permute(0, 1, 3, 2, 4, 5).reshape(b, h, w, -1)
+
+
+def rel_index(ws):
+    """relative_position_index (swinir_arch.py:123-133)."""
+    coords = torch.stack(torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing='ij')).flatten(1)
+    rel = (coords[:, :, None] - coords[:, None, :]).permute(1, 2, 0)
+    return (rel[:, :, 0] + ws - 1) * (2 * ws - 1) + (rel[:, :, 1] + ws - 1)
+
+
+def swin_mask(h, w, ws, s):
+    """calculate_mask (swinir_arch.py:262-281): -100 between tokens of different regions."""
+    img = torch.zeros(1, h, w, 1)
+    cnt = 0
+    for hs in (slice(0, -ws), slice(-ws, -s), slice(-s, None)):
+        for wsl in (slice(0, -ws), slice(-ws, -s), slice(-s, None)):
+            img[:, hs, wsl, :] = cnt
+            cnt += 1
+    mw = window_partition(img, ws).view(-1, ws * ws)
+    m = mw.unsqueeze(1) - mw.unsqueeze(2)
+    return m.masked_fill(m != 0, -100.0).masked_fill(m == 0, 0.0)
+
+
+def window_attention(xw, sd, p, nH, ws, mask):
+    """WindowAttention.forward (swinir_arch.py:144-175)."""
+    b_, n, c = xw.shape
+    hd = c // nH
+    qkv = _linear(xw, sd, f'{p}.qkv').reshape(b_, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv[0] * hd**-0.5, qkv[1], qkv[2]
+    attn = q @ k.transpose(-2, -1)
+    table = sd[f'{p}.relative_position_bias_table']
+    bias = table[rel_index(ws).reshape(-1)].view(n, n, -1).permute(2, 0, 1)
+    attn = attn + bias.unsqueeze(0)
+    if mask is not None:
+        nw = mask.shape[0]
+        attn = attn.view(b_ // nw, nw, nH, n, n) + mask.unsqueeze(1).unsqueeze(0)
+        attn = attn.view(-1, nH, n, n)
+    attn = attn.softmax(-1)
+    out = (attn @ v).transpose(1, 2).reshape(b_, n, c)
+    return _linear(out, sd, f'{p}.proj')
+
+
+def swin_block(x, sd, p, hw, nH, ws, shift):
+    """SwinTransformerBlock.forward in eval mode (swinir_arch.py:283-323), DropPath = identity."""
+    h, w = hw
+    b, _, c = x.shape
+    if min(hw) <= ws:
+        shift, ws = 0, min(hw)
+    sc = x
+    t = _ln(x, sd, f'{p}.norm1').view(b, h, w, c)
+    if shift > 0:
+        t = torch.roll(t, shifts=(-shift, -shift), dims=(1, 2))
+    tw = window_partition(t, ws).view(-1, ws * ws, c)
+    aw = window_attention(tw, sd, f'{p}.attn', nH, ws, swin_mask(h, w, ws, shift) if shift > 0 else None)
+    t = window_reverse(aw.view(-1, ws, ws, c), ws, h, w)
+    if shift > 0:
+        t = torch.roll(t, shifts=(shift, shift), dims=(1, 2))
+    x = sc + t.reshape(b, h * w, c)
+    m = _linear(F.gelu(_linear(_ln(x, sd, f'{p}.norm2'), sd, f'{p}.mlp.fc1')), sd, f'{p}.mlp.fc2')
+    return x + m
+
+
+def swinir(sd, x, cfg):
+    """SwinIR.forward (swinir_arch.py:868-922), 1conv residual, ape False, eval mode."""
+    in_ch = cfg.get('in_chans', 3)
+    img_range = cfg.get('img_range', 1.)
+    ws = cfg.get('window_size', 7)
+    depths, heads = cfg.get('depths', (6, 6, 6, 6)), cfg.get('num_heads', (6, 6, 6, 6))
+    ups, s = cfg.get('upsampler', ''), cfg.get('upscale', 2)
+    mean = torch.tensor((0.4488, 0.4371, 0.4040)).view(1, 3, 1, 1) if in_ch == 3 else torch.zeros(1, 1, 1, 1)
+    x = (x - mean) * img_range
+    b, _, h, w = x.shape
+
+    def features(f):
+        t = f.flatten(2).transpose(1, 2)
+        if cfg.get('patch_norm', True):
+            t = _ln(t, sd, 'patch_embed.norm')
+        for i, d in enumerate(depths):
+            g = t
+            for j in range(d):
+                g = swin_block(g, sd, f'layers.{i}.residual_group.blocks.{j}', (h, w), heads[i], ws,
+                               0 if j % 2 == 0 else ws // 2)
+            g = g.transpose(1, 2).reshape(b, -1, h, w)
+            t = conv(g, sd, f'layers.{i}.conv').flatten(2).transpose(1, 2) + t
+        t = _ln(t, sd, 'norm')
+        return t.transpose(1, 2).reshape(b, -1, h, w)
+
+    if ups == 'pixelshuffle':
+        x = conv(x, sd, 'conv_first')
+        x = conv(features(x), sd, 'conv_after_body') + x
+        x = F.leaky_relu(conv(x, sd, 'conv_before_upsample.0'), 0.01)
+        x = conv(upsample(x, sd, 'upsample', s), sd, 'conv_last')
+    elif ups == 'pixelshuffledirect':
+        x = conv(x, sd, 'conv_first')
+        x = conv(features(x), sd, 'conv_after_body') + x
+        x = pixel_shuffle(conv(x, sd, 'upsample.0'), s)
+    elif ups == 'nearest+conv':
+        x = conv(x, sd, 'conv_first')
+        x = conv(features(x), sd, 'conv_after_body') + x
+        x = F.leaky_relu(conv(x, sd, 'conv_before_upsample.0'), 0.01)
+        x = conv(F.interpolate(x, scale_factor=2, mode='nearest'), sd, 'conv_up1', act='lrelu', slope=0.2)
+        x = conv(F.interpolate(x, scale_factor=2, mode='nearest'), sd, 'conv_up2', act='lrelu', slope=0.2)
+        x = conv(conv(x, sd, 'conv_hr', act='lrelu', slope=0.2), sd, 'conv_last')
+    else:
+        xf = conv(x, sd, 'conv_first')
+        res = conv(features(xf), sd, 'conv_after_body') + xf
+        x = x + conv(res, sd, 'conv_last')
+    return x / img_range + mean

@@ -32,14 +32,14 @@ def test_library_exports_every_header_symbol():
 
 def test_invalid_arguments_raise():
     lib = _lib.load()
-    rc = lib.sr_conv3x3_fwd(None, None, None, None, None, None, None, None, None, None, None)
+    rc = lib.sr_conv3x3_fwd(None, None, None, None, None, None, None, None, None, None, None, None)
     assert rc == -1 and b'null' in lib.sr_last_error()
     with pytest.raises(RuntimeError, match='null'):
         _lib.check(rc)
     d = _lib.ConvDesc()
     d.dtype, d.N, d.H, d.W, d.Cin, d.ldx, d.Cout, d.ldw, d.ldy = 1, 1, 4, 4, 12, 12, 16, 108, 16
     dummy = ctypes.c_void_p(16)
-    rc = lib.sr_conv3x3_fwd(d, dummy, dummy, None, None, None, None, None, None, dummy, None)
+    rc = lib.sr_conv3x3_fwd(d, dummy, dummy, None, None, None, None, None, None, dummy, None, None)
     assert rc == -1 and b'multiples of 8' in lib.sr_last_error()
     assert lib.sr_pixel_shuffle_nchw(0, dummy, 1, 3, 4, 4, 2, dummy, None) == -1  # C % r^2 != 0
 

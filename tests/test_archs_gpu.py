@@ -25,7 +25,7 @@ def _build(case, sd):
     return net
 
 
-@pytest.mark.parametrize('name', [n for n in CASES if n != 'swinir_tiny'])
+@pytest.mark.parametrize('name', list(CASES))
 def test_arch_matches_golden_and_oracle_grads(cuda, name):
     z = np.load(os.path.join(GOLDEN, f'{name}.npz'))
     case = CASES[name]
@@ -38,7 +38,7 @@ def test_arch_matches_golden_and_oracle_grads(cuda, name):
     err = (out.detach().cpu() - y).abs().max().item()
     assert err < 1e-3, err
     # gradients vs oracle autograd on the CPU
-    sdg = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    sdg = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
     ref = run_case_grad(case, sdg, x)
     g = torch.randn_like(ref, generator=None)
     (ref * g).sum().backward()
@@ -80,3 +80,44 @@ def test_bf16_forward_close_to_oracle(cuda, arch):
         out = g(x.to(cuda))
     rng = max(1.0, ref.abs().max().item())
     assert (out.float().cpu() - ref).abs().max().item() < 5e-2 * rng
+
+
+@pytest.mark.parametrize('ups', ['pixelshuffle', 'pixelshuffledirect', 'nearest+conv', ''])
+def test_swinir_upsamplers_fp32(cuda, ups):
+    """SwinIR heads (swinir_arch.py:895-919) + shifted windows (ws 8, shift 4) + 180/6 head layout."""
+    from basicsr4rs_amd.archs import build_network
+    cfg = dict(type='SwinIR', upscale=4 if ups == 'nearest+conv' else 2, in_chans=3, img_size=16, window_size=8,
+               img_range=1., depths=[2], embed_dim=60, num_heads=[6], mlp_ratio=2, upsampler=ups, drop_path_rate=0.)
+    torch.manual_seed(0)
+    net = build_network(cfg)
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    x = torch.rand(2, 3, 16, 16)
+    sdg = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    ref = O.swinir(sdg, x, cfg)
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    gn = copy.deepcopy(net).to(cuda)
+    out = gn(x.to(cuda))
+    assert (out.detach().cpu() - ref.detach()).abs().max().item() < 1e-3
+    (out * g.to(cuda)).sum().backward()
+    for n, p in gn.named_parameters():
+        r = sdg[n].grad
+        e = (p.grad.cpu() - r).abs().max().item() / max(1e-3, r.abs().max().item())
+        assert e < 2e-3, (n, e)
+
+
+def test_swinir_bf16_c4_shape(cuda):
+    """SwinIR-M geometry (embed 180, 6 heads, window 8) in bf16 on a 32x32 tile."""
+    from basicsr4rs_amd.archs import build_network
+    cfg = dict(type='SwinIR', upscale=4, in_chans=3, img_size=32, window_size=8, img_range=1., depths=[2, 2],
+               embed_dim=180, num_heads=[6, 6], mlp_ratio=2, upsampler='pixelshuffle', drop_path_rate=0.)
+    torch.manual_seed(0)
+    net = build_network(cfg)
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    x = torch.rand(1, 3, 32, 32)
+    ref = O.swinir(sd, x, cfg)
+    gn = copy.deepcopy(net).to(cuda)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        out = gn(x.to(cuda))
+    assert (out.float().cpu() - ref).abs().max().item() < 5e-2 * max(1.0, ref.abs().max().item())
+    out.float().mean().backward()
