@@ -37,6 +37,12 @@ class WgradDesc(ctypes.Structure):
                 ('scale', _f), ('in_up', _i), ('ksize', _i)]
 
 
+class DcnDesc(ctypes.Structure):
+    _fields_ = [('dtype', _i), ('N', _i), ('C', _i), ('H', _i), ('W', _i), ('Cp', _i), ('Ho', _i), ('Wo', _i),
+                ('kh', _i), ('kw', _i), ('stride_h', _i), ('stride_w', _i), ('pad_h', _i), ('pad_w', _i),
+                ('dil_h', _i), ('dil_w', _i), ('groups', _i), ('deformable_groups', _i), ('cgp', _i)]
+
+
 # name -> (restype, argtypes); must match include/sr_hip.h (checked by tests/test_abi.py)
 SIGNATURES = {
     'sr_version': (ctypes.c_char_p, []),
@@ -73,6 +79,13 @@ SIGNATURES = {
     'sr_window_attn_bwd_workspace': (_sz, [_i, _i, _i, _i, _i]),
     'sr_window_attn_bwd': (_i, [_i, _vp, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp,
                                _sz, _vp]),
+    'sr_dcn_im2col': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp]),
+    'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_fused_bias_act': (_i, [_i, _vp, _vp, _vp, _vp, _i64, _i, _i, _i, _i, _f, _f, _vp]),
+    'sr_fused_lrelu_bwd_workspace': (_sz, [_i, _i, _i64]),
+    'sr_fused_lrelu_bwd': (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i64, _f, _f, _vp, _sz, _vp]),
+    'sr_upfirdn2d_out_size': (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    'sr_upfirdn2d': (_i, [_i, _vp, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
 }
 
 _LIB = None

@@ -1,0 +1,325 @@
+// Deformable convolution (DCNv1 / DCNv2) sampling kernels for gfx950.
+//
+// The reference (basicsr/ops/dcn/src/deform_conv_cuda.cpp:490-685, kernels
+// deform_conv_cuda_kernel.cu:571-770) loops over the batch: per image it builds an fp32
+// column matrix [C*K, Ho*Wo] with one thread per (c, pixel), runs a serial addmm, and in
+// backward scatters with atomics and re-reads the columns once per offset channel.
+//
+// Here the deformable part is reduced to two batched HBM-bound passes around MFMA GEMMs
+// (the GEMMs are the 1x1 path of conv3x3.hip):
+//   sr_dcn_im2col : cols[p][g][tap][ci] = mask * bilinear(x, p + tap + offset), all images
+//                   in one launch, pixel-major rows so the GEMM reads them as a K-contiguous
+//                   operand; x is NHWC so each bilinear corner is a 16-byte channel vector.
+//   sr_dcn_col2im : the three backward scatters of the reference (col2im for grad_x,
+//                   col2im_coord for grad_offset and grad_mask) fused into one pass over
+//                   dcols: every (pixel, tap, deformable group) item walks its group's
+//                   channels once, accumulating the offset/mask gradients in registers and
+//                   scattering grad_x with hardware fp32 atomics.
+// Offsets and masks are staged through LDS per 64-pixel tile so their NCHW reads and
+// writes stay coalesced while the item loop runs deformable-group-fastest (adjacent lanes
+// touch adjacent channel vectors of the same pixel).
+#include "sr_common.h"
+#include "sr_internal.h"
+
+namespace {
+
+struct DcnArgs {
+  int N, C, H, W, Cp, Ho, Wo;
+  int kh, kw, sh, sw, ph, pw, dh, dw;
+  int G, DG, cg, cgp, cpg;  // conv groups, deformable groups, channels per conv group (+pad), per deform group
+  int K, L, TP;             // taps, column row length (G*K*cgp), pixels per tile
+};
+
+template <typename T, int V> struct Vec;
+template <> struct Vec<bf16_t, 8> {
+  SR_DEV static void load(const bf16_t* p, float* f) {
+    const u32x4 u = *(const u32x4*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(u[i] << 16);
+      f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+  SR_DEV static void store(bf16_t* p, const float* f) {
+    u32x4 u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
+    *(u32x4*)p = u;
+  }
+};
+template <> struct Vec<float, 4> {
+  SR_DEV static void load(const float* p, float* f) {
+    const f32x4 v = *(const f32x4*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = v[i];
+  }
+  SR_DEV static void store(float* p, const float* f) { *(f32x4*)p = f32x4{f[0], f[1], f[2], f[3]}; }
+};
+template <typename T> struct Vec<T, 1> {
+  SR_DEV static void load(const T* p, float* f) { f[0] = Elt<T>::to_f(*p); }
+  SR_DEV static void store(T* p, const float* f) { *p = Elt<T>::from_f(f[0]); }
+};
+
+// Bilinear sampling geometry of one (pixel, tap): the reference's validity rule
+// (h > -1 && w > -1 && h < H && w < W, deform_conv_cuda_kernel.cu:619) and corner rules
+// (dmcn_im2col_bilinear, :468-498).  Corner offsets are pixel indices within the image,
+// -1 where the corner lies outside.
+struct Sample {
+  bool valid;
+  float lh, lw, hh, hw;
+  int o1, o2, o3, o4;
+};
+
+SR_DEV Sample make_sample(float h, float w, int H, int W) {
+  Sample s;
+  s.valid = (h > -1.f && w > -1.f && h < (float)H && w < (float)W);
+  s.o1 = s.o2 = s.o3 = s.o4 = -1;
+  s.lh = s.lw = s.hh = s.hw = 0.f;
+  if (!s.valid) return s;
+  const float fh = floorf(h), fw = floorf(w);
+  const int hl = (int)fh, wl = (int)fw, hh_ = hl + 1, wh = wl + 1;
+  s.lh = h - fh;
+  s.lw = w - fw;
+  s.hh = 1.f - s.lh;
+  s.hw = 1.f - s.lw;
+  if (hl >= 0 && wl >= 0) s.o1 = hl * W + wl;
+  if (hl >= 0 && wh <= W - 1) s.o2 = hl * W + wh;
+  if (hh_ <= H - 1 && wl >= 0) s.o3 = hh_ * W + wl;
+  if (hh_ <= H - 1 && wh <= W - 1) s.o4 = hh_ * W + wh;
+  return s;
+}
+
+// LDS tile of offsets ([DG*2K][TP]) followed by masks ([DG*K][TP]) for pixels
+// [p0, p0+np) of image n; missing mask (DCNv1) reads as 1.
+SR_DEV void load_tile(float* s_off, float* s_msk, const float* off, const float* msk, const DcnArgs& a, int n,
+                      int p0, int np) {
+  const int64_t HWo = (int64_t)a.Ho * a.Wo;
+  const int noff = a.DG * 2 * a.K, nm = a.DG * a.K;
+  for (int i = threadIdx.x; i < (noff + nm) * a.TP; i += blockDim.x) {
+    const int ch = i / a.TP, px = i - ch * a.TP;
+    float v = 0.f;
+    if (px < np) {
+      if (ch < noff) v = off[((int64_t)n * noff + ch) * HWo + p0 + px];
+      else v = msk ? msk[((int64_t)n * nm + ch - noff) * HWo + p0 + px] : 1.f;
+    }
+    if (ch < noff) s_off[ch * a.TP + px] = v;
+    else s_msk[(ch - noff) * a.TP + px] = v;
+  }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) dcn_im2col_kernel(DcnArgs a, const T* __restrict__ x,
+                                                         const float* __restrict__ off, const float* __restrict__ msk,
+                                                         T* __restrict__ cols) {
+  extern __shared__ float s_lds[];
+  float* s_off = s_lds;
+  float* s_msk = s_lds + a.DG * 2 * a.K * a.TP;
+  const int HWo = a.Ho * a.Wo;
+  const int tiles = (HWo + a.TP - 1) / a.TP;
+  const int n = blockIdx.x / tiles, p0 = (blockIdx.x - n * tiles) * a.TP;
+  const int np = min(a.TP, HWo - p0);
+  load_tile(s_off, s_msk, off, msk, a, n, p0, np);
+  __syncthreads();
+  const T* xim = x + (int64_t)n * a.H * a.W * a.Cp;
+  const int items = np * a.K * a.DG;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int dgi = it % a.DG, t2 = it / a.DG, tap = t2 % a.K, px = t2 / a.K;
+    const int p = p0 + px, ho = p / a.Wo, wo = p - ho * a.Wo;
+    const int i = tap / a.kw, j = tap - i * a.kw;
+    const float oh = s_off[(dgi * 2 * a.K + 2 * tap) * a.TP + px];
+    const float ow = s_off[(dgi * 2 * a.K + 2 * tap + 1) * a.TP + px];
+    const float m = s_msk[(dgi * a.K + tap) * a.TP + px];
+    const float h = (float)(ho * a.sh - a.ph + i * a.dh) + oh;
+    const float w = (float)(wo * a.sw - a.pw + j * a.dw) + ow;
+    const Sample s = make_sample(h, w, a.H, a.W);
+    const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+    T* row = cols + ((int64_t)n * HWo + p) * a.L;
+    for (int c = dgi * a.cpg; c < (dgi + 1) * a.cpg; c += V) {
+      float v1[V], v2[V], v3[V], v4[V], r[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) v1[e] = v2[e] = v3[e] = v4[e] = 0.f;
+      if (s.o1 >= 0) Vec<T, V>::load(xim + (int64_t)s.o1 * a.Cp + c, v1);
+      if (s.o2 >= 0) Vec<T, V>::load(xim + (int64_t)s.o2 * a.Cp + c, v2);
+      if (s.o3 >= 0) Vec<T, V>::load(xim + (int64_t)s.o3 * a.Cp + c, v3);
+      if (s.o4 >= 0) Vec<T, V>::load(xim + (int64_t)s.o4 * a.Cp + c, v4);
+#pragma unroll
+      for (int e = 0; e < V; ++e) r[e] = (w1 * v1[e] + w2 * v2[e] + w3 * v3[e] + w4 * v4[e]) * m;
+      const int g = c / a.cg, ci = c - g * a.cg;
+      Vec<T, V>::store(row + (g * a.K + tap) * a.cgp + ci, r);
+    }
+  }
+  if (a.cgp != a.cg) {  // zero the per-group channel padding of the column rows
+    const int padc = a.cgp - a.cg, per = a.G * a.K * padc;
+    for (int it = threadIdx.x; it < np * per; it += blockDim.x) {
+      const int px = it / per, r = it - px * per, gt = r / padc, ci = a.cg + r - gt * padc;
+      cols[((int64_t)n * HWo + p0 + px) * a.L + gt * a.cgp + ci] = Elt<T>::from_f(0.f);
+    }
+  }
+}
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) dcn_col2im_kernel(DcnArgs a, const T* __restrict__ dcols,
+                                                         const T* __restrict__ x, const float* __restrict__ off,
+                                                         const float* __restrict__ msk, float* __restrict__ gx,
+                                                         float* __restrict__ goff, float* __restrict__ gmsk) {
+  extern __shared__ float s_lds[];
+  float* s_off = s_lds;
+  float* s_msk = s_lds + a.DG * 2 * a.K * a.TP;
+  const int HWo = a.Ho * a.Wo;
+  const int tiles = (HWo + a.TP - 1) / a.TP;
+  const int n = blockIdx.x / tiles, p0 = (blockIdx.x - n * tiles) * a.TP;
+  const int np = min(a.TP, HWo - p0);
+  load_tile(s_off, s_msk, off, msk, a, n, p0, np);
+  __syncthreads();
+  const T* xim = x + (int64_t)n * a.H * a.W * a.Cp;
+  float* gim = gx + (int64_t)n * a.H * a.W * a.Cp;
+  const int items = np * a.K * a.DG;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int dgi = it % a.DG, t2 = it / a.DG, tap = t2 % a.K, px = t2 / a.K;
+    const int p = p0 + px, ho = p / a.Wo, wo = p - ho * a.Wo;
+    const int i = tap / a.kw, j = tap - i * a.kw;
+    float* ph = &s_off[(dgi * 2 * a.K + 2 * tap) * a.TP + px];
+    float* pw = &s_off[(dgi * 2 * a.K + 2 * tap + 1) * a.TP + px];
+    float* pm = &s_msk[(dgi * a.K + tap) * a.TP + px];
+    const float m = *pm;
+    const float h = (float)(ho * a.sh - a.ph + i * a.dh) + *ph;
+    const float w = (float)(wo * a.sw - a.pw + j * a.dw) + *pw;
+    const Sample s = make_sample(h, w, a.H, a.W);
+    float acc_h = 0.f, acc_w = 0.f, acc_m = 0.f;
+    if (s.valid) {
+      const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+      const T* row = dcols + ((int64_t)n * HWo + p) * a.L;
+      for (int c = dgi * a.cpg; c < (dgi + 1) * a.cpg; c += V) {
+        float v1[V], v2[V], v3[V], v4[V], dc[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) v1[e] = v2[e] = v3[e] = v4[e] = 0.f;
+        const int g = c / a.cg, ci = c - g * a.cg;
+        Vec<T, V>::load(row + (g * a.K + tap) * a.cgp + ci, dc);
+        if (s.o1 >= 0) Vec<T, V>::load(xim + (int64_t)s.o1 * a.Cp + c, v1);
+        if (s.o2 >= 0) Vec<T, V>::load(xim + (int64_t)s.o2 * a.Cp + c, v2);
+        if (s.o3 >= 0) Vec<T, V>::load(xim + (int64_t)s.o3 * a.Cp + c, v3);
+        if (s.o4 >= 0) Vec<T, V>::load(xim + (int64_t)s.o4 * a.Cp + c, v4);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          // col2im_coord (deform_conv_cuda_kernel.cu:696-770): d bilinear / d h, d w and the
+          // un-masked sample for the mask gradient
+          const float wh = -s.hw * v1[e] - s.lw * v2[e] + s.hw * v3[e] + s.lw * v4[e];
+          const float ww = -s.hh * v1[e] + s.hh * v2[e] - s.lh * v3[e] + s.lh * v4[e];
+          acc_h += wh * dc[e] * m;
+          acc_w += ww * dc[e] * m;
+          acc_m += dc[e] * (w1 * v1[e] + w2 * v2[e] + w3 * v3[e] + w4 * v4[e]);
+          // col2im (:636-694): scatter the masked column gradient to the four corners
+          const float t = dc[e] * m;
+          if (s.o1 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o1 * a.Cp + c + e, w1 * t);
+          if (s.o2 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o2 * a.Cp + c + e, w2 * t);
+          if (s.o3 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o3 * a.Cp + c + e, w3 * t);
+          if (s.o4 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o4 * a.Cp + c + e, w4 * t);
+        }
+      }
+    }
+    // each item owns exactly the LDS words it read: overwrite them with its gradients
+    *ph = acc_h;
+    *pw = acc_w;
+    *pm = acc_m;
+  }
+  __syncthreads();
+  const int64_t HWl = HWo;
+  const int noff = a.DG * 2 * a.K, nm = a.DG * a.K;
+  for (int q = threadIdx.x; q < (noff + nm) * a.TP; q += blockDim.x) {
+    const int ch = q / a.TP, px = q - ch * a.TP;
+    if (px >= np) continue;
+    if (ch < noff) goff[((int64_t)n * noff + ch) * HWl + p0 + px] = s_off[ch * a.TP + px];
+    else if (gmsk) gmsk[((int64_t)n * nm + ch - noff) * HWl + p0 + px] = s_msk[(ch - noff) * a.TP + px];
+  }
+}
+
+int make_args(const sr_dcn_desc* d, DcnArgs& a) {
+  if (!d) return sr_fail(SR_EINVAL, "dcn: null descriptor");
+  a.N = d->N; a.C = d->C; a.H = d->H; a.W = d->W; a.Cp = d->Cp; a.Ho = d->Ho; a.Wo = d->Wo;
+  a.kh = d->kh; a.kw = d->kw; a.sh = d->stride_h; a.sw = d->stride_w; a.ph = d->pad_h; a.pw = d->pad_w;
+  a.dh = d->dil_h; a.dw = d->dil_w; a.G = d->groups; a.DG = d->deformable_groups; a.cgp = d->cgp;
+  if (a.N <= 0 || a.C <= 0 || a.H <= 0 || a.W <= 0 || a.Ho <= 0 || a.Wo <= 0 || a.kh <= 0 || a.kw <= 0 ||
+      a.sh <= 0 || a.sw <= 0 || a.dh <= 0 || a.dw <= 0 || a.ph < 0 || a.pw < 0)
+    return sr_fail(SR_EINVAL, "dcn: non-positive size");
+  if (a.G <= 0 || a.DG <= 0 || a.C % a.G || a.C % a.DG)
+    return sr_fail(SR_EINVAL, "dcn: channels must be divisible by groups and deformable_groups");
+  if (a.Cp < a.C || a.Cp % 8) return sr_fail(SR_EINVAL, "dcn: Cp must be >= C and a multiple of 8");
+  a.cg = a.C / a.G;
+  a.cpg = a.C / a.DG;
+  if (a.cgp < a.cg || a.cgp % 8) return sr_fail(SR_EINVAL, "dcn: cgp must be >= C/groups and a multiple of 8");
+  if (a.Ho != (a.H + 2 * a.ph - (a.dh * (a.kh - 1) + 1)) / a.sh + 1 ||
+      a.Wo != (a.W + 2 * a.pw - (a.dw * (a.kw - 1) + 1)) / a.sw + 1)
+    return sr_fail(SR_EINVAL, "dcn: output size does not match the convolution geometry");
+  a.K = a.kh * a.kw;
+  a.L = a.G * a.K * a.cgp;
+  // pixel tile: offsets + masks of every deformable group in LDS (<= 64 KB)
+  a.TP = 64;
+  while (a.TP > 1 && (size_t)a.DG * 3 * a.K * a.TP * 4 > 65536) a.TP >>= 1;
+  if ((size_t)a.DG * 3 * a.K * a.TP * 4 > 65536) return sr_fail(SR_EINVAL, "dcn: too many deformable groups x taps");
+  return SR_OK;
+}
+
+// vector width: 16-byte channel vectors when every group boundary is vector aligned
+template <typename T> int vec_width(const DcnArgs& a) {
+  const int v = Elt<T>::PER16;
+  return (a.cpg % v == 0 && a.cg % v == 0) ? v : 1;
+}
+
+template <typename T>
+int launch_im2col(const DcnArgs& a, const void* x, const float* off, const float* msk, void* cols, hipStream_t s) {
+  const int tiles = (a.Ho * a.Wo + a.TP - 1) / a.TP;
+  const dim3 grid((unsigned)(a.N * tiles));
+  const size_t lds = (size_t)a.DG * 3 * a.K * a.TP * 4;
+  if (vec_width<T>(a) > 1)
+    hipLaunchKernelGGL((dcn_im2col_kernel<T, Elt<T>::PER16>), grid, dim3(256), lds, s, a, (const T*)x, off, msk,
+                       (T*)cols);
+  else
+    hipLaunchKernelGGL((dcn_im2col_kernel<T, 1>), grid, dim3(256), lds, s, a, (const T*)x, off, msk, (T*)cols);
+  return sr_check(hipGetLastError(), "dcn_im2col launch");
+}
+
+template <typename T>
+int launch_col2im(const DcnArgs& a, const void* dcols, const void* x, const float* off, const float* msk, float* gx,
+                  float* goff, float* gmsk, hipStream_t s) {
+  const int tiles = (a.Ho * a.Wo + a.TP - 1) / a.TP;
+  const dim3 grid((unsigned)(a.N * tiles));
+  const size_t lds = (size_t)a.DG * 3 * a.K * a.TP * 4;
+  if (vec_width<T>(a) > 1)
+    hipLaunchKernelGGL((dcn_col2im_kernel<T, Elt<T>::PER16>), grid, dim3(256), lds, s, a, (const T*)dcols,
+                       (const T*)x, off, msk, gx, goff, gmsk);
+  else
+    hipLaunchKernelGGL((dcn_col2im_kernel<T, 1>), grid, dim3(256), lds, s, a, (const T*)dcols, (const T*)x, off, msk,
+                       gx, goff, gmsk);
+  return sr_check(hipGetLastError(), "dcn_col2im launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+int sr_dcn_im2col(const sr_dcn_desc* d, const void* x, const float* offset, const float* mask, void* cols,
+                  void* stream) {
+  DcnArgs a;
+  int rc = make_args(d, a);
+  if (rc) return rc;
+  if (!x || !offset || !cols) return sr_fail(SR_EINVAL, "dcn_im2col: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == SR_BF16) return launch_im2col<bf16_t>(a, x, offset, mask, cols, s);
+  if (d->dtype == SR_F32) return launch_im2col<float>(a, x, offset, mask, cols, s);
+  return sr_fail(SR_EINVAL, "dcn_im2col: bad dtype");
+}
+
+int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const float* offset, const float* mask,
+                  float* grad_x, float* grad_offset, float* grad_mask, void* stream) {
+  DcnArgs a;
+  int rc = make_args(d, a);
+  if (rc) return rc;
+  if (!dcols || !x || !offset || !grad_x || !grad_offset) return sr_fail(SR_EINVAL, "dcn_col2im: null pointer");
+  if (grad_mask && !mask) return sr_fail(SR_EINVAL, "dcn_col2im: grad_mask needs mask");
+  hipStream_t s = (hipStream_t)stream;
+  if (d->dtype == SR_BF16) return launch_col2im<bf16_t>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, s);
+  if (d->dtype == SR_F32) return launch_col2im<float>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, s);
+  return sr_fail(SR_EINVAL, "dcn_col2im: bad dtype");
+}
+
+}  // extern "C"

@@ -225,6 +225,52 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
                        float scale, const float* bias_table, void* dqkv, float* dbias_table, void* workspace,
                        size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * basicsr/ops native extensions (replacements of deform_conv_ext, fused_act_ext,
+ * upfirdn2d_ext).
+ * ------------------------------------------------------------------------------------- */
+/* Deformable convolution geometry (csrc/dcn.hip).  x is NHWC [N][H][W][Cp] (dtype);
+ * offset [N][DG*2*kh*kw][Ho][Wo] and mask [N][DG*kh*kw][Ho][Wo] are the reference's NCHW
+ * fp32 tensors (channel 2*tap = dy, 2*tap+1 = dx, per deformable group).  Columns are
+ * pixel-major rows [N*Ho*Wo][groups][kh*kw][cgp] (cgp = padded C/groups), the operand of
+ * the 1x1 GEMM (sr_conv3x3_fwd with ksize 1). */
+typedef struct sr_dcn_desc {
+  int dtype;
+  int N, C, H, W, Cp, Ho, Wo;
+  int kh, kw, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w;
+  int groups, deformable_groups, cgp;
+} sr_dcn_desc;
+/* columns = mask * bilinear(x, p + tap + offset); mask NULL = DCNv1 (all ones).
+ * Replaces modulated_deformable_im2col_cuda / deformable_im2col
+ * (deform_conv_cuda_kernel.cu:191-278, :571-634), batched over all images. */
+int sr_dcn_im2col(const sr_dcn_desc* d, const void* x, const float* offset, const float* mask, void* cols,
+                  void* stream);
+/* From dcols (= dy x W, column layout): grad_x += scatter (fp32 NHWC [N][H][W][Cp], caller
+ * zeroes it; atomics), grad_offset / grad_mask written in full (grad_mask NULL for v1).
+ * Replaces the col2im + col2im_coord pair (deform_conv_cuda_kernel.cu:280-466, :636-770). */
+int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const float* offset, const float* mask,
+                  float* grad_x, float* grad_offset, float* grad_mask, void* stream);
+
+/* fused_bias_act_op (basicsr/ops/fused_act/src/fused_bias_act_kernel.cu): out = scale *
+ * act(x + bias[(i / step_b) % size_b]) with act 1 linear / 3 leaky-relu(alpha), grad 0/1/2
+ * (grad 1 gates by ref > 0).  bias / ref may be NULL.  size_x < 2^31 (as the reference). */
+int sr_fused_bias_act(int dtype, const void* x, const void* bias, const void* ref, void* out, int64_t size_x,
+                      int step_b, int size_b, int act, int grad, float alpha, float scale, void* stream);
+/* FusedLeakyReLUFunctionBackward.forward (fused_act.py:30-44) on [R][C][S]:
+ * dx = dy * scale * (out > 0 ? 1 : alpha); grad_bias[c] = sum of dx over R, S (fp32,
+ * deterministic; grad_bias may be NULL). */
+size_t sr_fused_lrelu_bwd_workspace(int R, int C, int64_t S);
+int sr_fused_lrelu_bwd(int dtype, const void* dy, const void* out, void* dx, float* grad_bias, int R, int C,
+                       int64_t S, float alpha, float scale, void* workspace, size_t ws_bytes, void* stream);
+
+/* upfirdn2d (basicsr/ops/upfirdn2d/upfirdn2d.py:97-192): planes [major][in_h][in_w], FIR
+ * kernel fp32 [kh][kw]; out [major][out_h][out_w]. */
+int sr_upfirdn2d_out_size(int in_h, int in_w, int kh, int kw, int up_x, int up_y, int down_x, int down_y,
+                          int pad_x0, int pad_x1, int pad_y0, int pad_y1, int* out_h, int* out_w);
+int sr_upfirdn2d(int dtype, const void* x, int major, int in_h, int in_w, const float* kernel, int kh, int kw,
+                 int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
+                 void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,7 +52,8 @@ def test_cpu_tensors_refused():
 def test_struct_layouts_match_header():
     # field order/size of the ctypes mirrors vs the C structs (all 4-byte members)
     src = re.sub(r'/\*.*?\*/', '', open(os.path.join(ROOT, 'include', 'sr_hip.h')).read(), flags=re.S)
-    for cls, tag in ((_lib.ConvDesc, 'sr_conv3x3_desc'), (_lib.WgradDesc, 'sr_conv3x3_wgrad_desc')):
+    for cls, tag in ((_lib.ConvDesc, 'sr_conv3x3_desc'), (_lib.WgradDesc, 'sr_conv3x3_wgrad_desc'),
+                     (_lib.DcnDesc, 'sr_dcn_desc')):
         body = re.search(r'typedef struct ' + tag + r' \{(.*?)\}', src, re.S).group(1)
         fields = []
         for decl in body.split(';'):

@@ -1,0 +1,225 @@
+"""GPU parity of the basicsr/ops replacements (DCN v1/v2, upfirdn2d, fused_bias_act)
+against the float64 numpy oracle (oracle/ops.py).
+
+Tolerances: fp32 mode — samples and GEMMs in fp32 (exact-f32 MFMA), differences are
+summation order / atomics order: |err| <= 1e-4 * max(1, |ref|max) (north_star: 1e-3).
+bf16 (autocast) DCN — x, columns and weights rounded to bf16: |err| <= 3e-2 * |ref|max.
+upfirdn2d / fused_bias_act fp32: 1e-5 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from basicsr4rs_amd import _lib
+from basicsr4rs_amd.ops import dcn as D
+from basicsr4rs_amd.ops.upfirdn2d import upfirdn2d
+from oracle import ops as O
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.detach().double().cpu().numpy() if torch.is_tensor(a) else a
+    return float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
+
+
+DCN_CASES = [
+    # N, C, H, W, Cout, k, stride, pad, dil, groups, dg, modulated
+    (2, 16, 9, 9, 24, 3, 1, 1, 1, 1, 2, True),  # vector path, 8 ch / deformable group
+    (2, 64, 12, 10, 64, 3, 1, 1, 1, 1, 8, True),  # EDVR PCD shape (scaled down)
+    (1, 6, 7, 8, 16, 3, 2, 1, 1, 2, 1, False),  # DCNv1, groups 2, scalar path (3 ch / group)
+    (1, 8, 6, 6, 8, 3, 1, 2, 2, 1, 1, True),  # dilation 2
+    (2, 5, 5, 5, 7, 1, 1, 0, 1, 1, 1, True),  # 1x1 kernel, odd channels
+]
+
+
+def _dcn_inputs(case, seed=0):
+    N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
+    rng = np.random.default_rng(seed)
+    Ho = (H + 2 * p - (d * (k - 1) + 1)) // s + 1
+    Wo = (W + 2 * p - (d * (k - 1) + 1)) // s + 1
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    off = (rng.standard_normal((N, dg * 2 * k * k, Ho, Wo)) * 2.0).astype(np.float32)
+    msk = rng.uniform(0, 1, (N, dg * k * k, Ho, Wo)).astype(np.float32) if modulated else None
+    w = (rng.standard_normal((Cout, C // groups, k, k)) / np.sqrt(C * k * k)).astype(np.float32)
+    b = rng.standard_normal(Cout).astype(np.float32) if modulated else None
+    dy = rng.standard_normal((N, Cout, Ho, Wo)).astype(np.float32)
+    return x, off, msk, w, b, dy
+
+
+@pytest.mark.parametrize('case', DCN_CASES)
+def test_dcn_fwd_bwd_fp32(cuda, case):
+    N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
+    x, off, msk, w, b, dy = _dcn_inputs(case)
+    t = [torch.tensor(a, device=cuda, requires_grad=True) if a is not None else None for a in (x, off, msk, w, b)]
+    if modulated:
+        out = D.modulated_deform_conv(t[0], t[1], t[2], t[3], t[4], s, p, d, groups, dg)
+    else:
+        out = D.deform_conv(t[0], t[1], t[3], s, p, d, groups, dg)
+    ref = O.dcn_forward(x, off, msk, w, b, s, p, d, groups, dg)
+    assert out.shape == ref.shape and out.dtype == torch.float32
+    assert rel(out, ref) < 1e-4, rel(out, ref)
+    out.backward(torch.tensor(dy, device=cuda))
+    grads = O.dcn_backward(x, off, msk, w, b, s, p, d, groups, dg, dy)
+    for name, g, tt in zip(('x', 'offset', 'mask', 'weight', 'bias'), grads, t):
+        if tt is None:
+            continue
+        assert tt.grad is not None, name
+        assert rel(tt.grad, g) < 1e-4, (name, rel(tt.grad, g))
+
+
+def test_dcn_bf16_autocast(cuda):
+    case = (2, 64, 16, 16, 64, 3, 1, 1, 1, 1, 8, True)
+    x, off, msk, w, b, dy = _dcn_inputs(case, seed=1)
+    t = [torch.tensor(a, device=cuda, requires_grad=True) for a in (x, off, msk, w, b)]
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        out = D.modulated_deform_conv(*t, 1, 1, 1, 1, 8)
+    # oracle on the same bf16-rounded operands (x, weight, incoming gradient)
+    bfr = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()  # noqa: E731
+    xb, wb, dyb = bfr(x), bfr(w), bfr(dy)
+    ref = O.dcn_forward(xb, off, msk, wb, b, 1, 1, 1, 1, 8)
+    assert rel(out, ref) < 3e-2
+    out.backward(torch.tensor(dy, device=cuda))
+    grads = O.dcn_backward(xb, off, msk, wb, b, 1, 1, 1, 1, 8, dyb)
+    for name, g, tt in zip(('x', 'offset', 'mask', 'weight', 'bias'), grads, t):
+        assert rel(tt.grad, g) < 5e-2, (name, rel(tt.grad, g))
+
+
+def test_dcn_packs(cuda):
+    torch.manual_seed(0)
+    m2 = D.ModulatedDeformConvPack(16, 16, 3, padding=1, deformable_groups=2).to(cuda)
+    m1 = D.DeformConvPack(16, 8, 3, padding=1).to(cuda)
+    for m in (m1, m2):  # the packs start at zero offsets; perturb the offset branch
+        with torch.no_grad():
+            m.conv_offset.weight.normal_(0, 0.3)
+            m.conv_offset.bias.normal_(0, 0.5)
+    x = torch.randn(2, 16, 10, 9, device=cuda)
+    xn = x.double().cpu().numpy()
+    for m in (m1, m2):
+        out = m(x)
+        with torch.no_grad():
+            co = torch.nn.functional.conv2d(x.double().cpu(), m.conv_offset.weight.double().cpu(),
+                                            m.conv_offset.bias.double().cpu(), padding=1).numpy()
+        if isinstance(m, D.ModulatedDeformConvPack):
+            o1, o2, mk = np.split(co, 3, axis=1)
+            off, msk = np.concatenate((o1, o2), 1), 1 / (1 + np.exp(-mk))
+            bias = m.bias.double().cpu().detach().numpy()
+            dg = 2
+        else:
+            off, msk, bias, dg = co, None, None, 1
+        ref = O.dcn_forward(xn, off, msk, m.weight.double().cpu().detach().numpy(), bias, 1, 1, 1, 1, dg)
+        assert rel(out, ref) < 1e-4, (type(m).__name__, rel(out, ref))
+        out.sum().backward()
+        assert m.weight.grad is not None and m.conv_offset.weight.grad is not None
+
+
+def test_dcn_small_input_padding(cuda):
+    # DeformConv zero-pads inputs smaller than the kernel and crops the output (deform_conv.py:229-241)
+    torch.manual_seed(1)
+    m = D.DeformConv(4, 8, 3, padding=1).to(cuda)
+    x = torch.randn(1, 4, 2, 2, device=cuda)
+    off = torch.randn(1, 18, 2, 2, device=cuda)
+    out = m(x, off)
+    assert out.shape == (1, 8, 2, 2)
+    xp = np.pad(x.cpu().numpy(), ((0, 0), (0, 0), (0, 1), (0, 1)))
+    op = np.pad(off.cpu().numpy(), ((0, 0), (0, 0), (0, 1), (0, 1)))
+    ref = O.dcn_forward(xp, op, None, m.weight.detach().cpu().numpy(), None, 1, 1, 1, 1, 1)[:, :, :2, :2]
+    assert rel(out, ref) < 1e-4
+
+
+def test_dcn_cpu_raises():
+    with pytest.raises(NotImplementedError):
+        D.modulated_deform_conv(torch.zeros(1, 2, 4, 4), torch.zeros(1, 18, 4, 4), torch.zeros(1, 9, 4, 4),
+                                torch.zeros(2, 2, 3, 3), None, 1, 1, 1, 1, 1)
+
+
+UFD_CASES = [
+    # N, C, H, W, k, up, down, pad  (StyleGAN2 Upsample / Downsample / Blur shapes)
+    (2, 8, 16, 16, 4, 2, 1, (2, 1)),
+    (2, 8, 16, 16, 4, 1, 2, (1, 1)),
+    (1, 4, 33, 70, 4, 1, 1, (2, 1)),
+    (1, 3, 9, 13, 3, 2, 2, (1, 2)),
+    (1, 2, 130, 140, 4, 2, 1, (2, 1)),  # several tiles per plane
+    (2, 4, 4, 4, 4, 1, 1, (-1, 2)),  # negative pad = crop
+]
+
+
+@pytest.mark.parametrize('case', UFD_CASES)
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_upfirdn2d(cuda, case, dtype):
+    N, C, H, W, kk, up, down, pad = case
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((N, C, H, W)).astype(np.float32)
+    k1 = np.array([1, 3, 3, 1, 2, 1][:kk], np.float32)
+    k = np.outer(k1, k1[::-1])
+    k = k / k.sum()
+    xt = torch.tensor(x, device=cuda, dtype=dtype, requires_grad=True)
+    out = upfirdn2d(xt, torch.tensor(k, device=cuda), up=up, down=down, pad=pad)
+    xin = xt.detach().double().cpu().numpy()
+    ref = O.upfirdn2d(xin, k, up, up, down, down, pad[0], pad[1], pad[0], pad[1])
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert out.shape == ref.shape and out.dtype == dtype
+    assert rel(out, ref) < tol, rel(out, ref)
+    # backward = adjoint (checked against <A x, y> = <x, A^T y> with the oracle forward)
+    y = rng.standard_normal(ref.shape).astype(np.float32)
+    (gx, ) = torch.autograd.grad(out, xt, torch.tensor(y, device=cuda, dtype=dtype), create_graph=True)
+    yin = torch.tensor(y, dtype=dtype).double().numpy()
+    lhs = (ref * yin).sum()
+    rhs = (xin * gx.detach().double().cpu().numpy()).sum()
+    assert abs(lhs - rhs) <= tol * max(1.0, abs(lhs)) * 10, (lhs, rhs)
+    # double backward (UpFirDn2dBackward.backward, upfirdn2d.py:61-78): d/dy <A^T y, v> = A v
+    yt = torch.tensor(y, device=cuda, dtype=dtype, requires_grad=True)
+    (gx2, ) = torch.autograd.grad(out, xt, yt, create_graph=True)
+    v = torch.randn_like(gx2)
+    (gy, ) = torch.autograd.grad((gx2 * v).sum(), yt)
+    vin = v.detach().double().cpu().numpy()
+    ref_v = O.upfirdn2d(vin, k, up, up, down, down, pad[0], pad[1], pad[0], pad[1])
+    assert rel(gy, ref_v) < tol, rel(gy, ref_v)
+
+
+def test_upfirdn2d_cpu_raises():
+    with pytest.raises(NotImplementedError):
+        upfirdn2d(torch.zeros(1, 1, 4, 4), torch.ones(2, 2))
+
+
+def _fba(x, b, r, act, grad, alpha, scale):
+    lib = _lib.load()
+    out = torch.empty_like(x)
+    S = x[0, 0].numel() if x.dim() >= 2 else 1
+    _lib.check(
+        lib.sr_fused_bias_act(_lib.dtype_code(x.dtype), _lib.ptr(x), _lib.ptr(b), _lib.ptr(r), _lib.ptr(out), x.numel(),
+                              S, b.numel() if b is not None else 0, act, grad, alpha, scale, _lib.stream()))
+    return out
+
+
+@pytest.mark.parametrize('shape', [(4, 32, 8, 8), (3, 5, 7, 3), (16, 512), (2, 6, 130)])
+def test_fused_bias_act_abi(cuda, shape):
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal(shape).astype(np.float32)
+    b = rng.standard_normal(shape[1]).astype(np.float32)
+    xt, bt = torch.tensor(x, device=cuda), torch.tensor(b, device=cuda)
+    y = _fba(xt, bt, None, 3, 0, 0.2, 2**0.5)
+    ref = O.fused_bias_act(x, b, None, 3, 0, 0.2, 2**0.5)
+    assert rel(y, ref) < 1e-6
+    lin = _fba(xt, bt, None, 1, 0, 0.2, 1.5)
+    assert rel(lin, O.fused_bias_act(x, b, None, 1, 0, 0.2, 1.5)) < 1e-6
+    # first backward + fused bias reduction
+    dy = rng.standard_normal(shape).astype(np.float32)
+    dyt = torch.tensor(dy, device=cuda)
+    R, Cn = shape[0], shape[1]
+    S = int(np.prod(shape[2:])) if len(shape) > 2 else 1
+    lib = _lib.load()
+    dx = torch.empty_like(dyt)
+    db = torch.empty(Cn, device=cuda)
+    wsb = lib.sr_fused_lrelu_bwd_workspace(R, Cn, S)
+    ws = torch.empty(wsb // 4 + 1, device=cuda)
+    _lib.check(
+        lib.sr_fused_lrelu_bwd(0, _lib.ptr(dyt), _lib.ptr(y), _lib.ptr(dx), _lib.ptr(db), R, Cn, S, 0.2, 2**0.5,
+                               _lib.ptr(ws), wsb, _lib.stream()))
+    gi, gb = O.fused_lrelu_backward(dy, ref, 0.2, 2**0.5)
+    assert rel(dx, gi) < 1e-6
+    assert rel(db, gb) < 1e-5
+    # double-backward mode (31 with a bias) and the zero second derivative (32)
+    gg = _fba(dyt, bt, y, 3, 1, 0.2, 2**0.5)
+    assert rel(gg, O.fused_bias_act(dy, b, ref, 3, 1, 0.2, 2**0.5)) < 1e-6
+    assert float(_fba(dyt, bt, y, 3, 2, 0.2, 2**0.5).abs().max()) == 0.0
