@@ -80,7 +80,8 @@ SIGNATURES = {
     'sr_window_attn_bwd': (_i, [_i, _vp, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp,
                                _sz, _vp]),
     'sr_dcn_im2col': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp]),
-    'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_dcn_col2im_workspace': (_sz, [ctypes.POINTER(DcnDesc)]),
+    'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     'sr_fused_bias_act': (_i, [_i, _vp, _vp, _vp, _vp, _i64, _i, _i, _i, _i, _f, _f, _vp]),
     'sr_fused_lrelu_bwd_workspace': (_sz, [_i, _i, _i64]),
     'sr_fused_lrelu_bwd': (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i64, _f, _f, _vp, _sz, _vp]),

@@ -10,14 +10,15 @@
 //   sr_dcn_im2col : cols[p][g][tap][ci] = mask * bilinear(x, p + tap + offset), all images
 //                   in one launch, pixel-major rows so the GEMM reads them as a K-contiguous
 //                   operand; x is NHWC so each bilinear corner is a 16-byte channel vector.
-//   sr_dcn_col2im : the three backward scatters of the reference (col2im for grad_x,
-//                   col2im_coord for grad_offset and grad_mask) fused into one pass over
-//                   dcols: every (pixel, tap, deformable group) item walks its group's
-//                   channels once, accumulating the offset/mask gradients in registers and
-//                   scattering grad_x with hardware fp32 atomics.
-// Offsets and masks are staged through LDS per 64-pixel tile so their NCHW reads and
-// writes stay coalesced while the item loop runs deformable-group-fastest (adjacent lanes
-// touch adjacent channel vectors of the same pixel).
+//   sr_dcn_col2im : the reference's backward scatters as two passes over dcols:
+//                   dcn_coord_grad_kernel (col2im_coord: offset and mask gradients, one
+//                   item per (pixel, tap, deformable group) reducing over the group's
+//                   channels in registers, no atomics) and dcn_grad_x_kernel (col2im:
+//                   bilinear scatter accumulated in an LDS image of the output tile's input
+//                   footprint, flushed with channel-contiguous atomics).
+// Offsets and masks are staged through LDS per pixel tile so their NCHW reads and writes
+// stay coalesced while the item loop runs deformable-group-fastest (adjacent lanes touch
+// adjacent channel vectors of the same pixel).
 #include "sr_common.h"
 #include "sr_internal.h"
 
@@ -157,11 +158,14 @@ __global__ void __launch_bounds__(256) dcn_im2col_kernel(DcnArgs a, const T* __r
   }
 }
 
+// Offset / mask gradients (col2im_coord, deform_conv_cuda_kernel.cu:696-770): one item
+// per (pixel, tap, deformable group) walks the group's channels once and reduces in
+// registers; results replace the item's own LDS words and are stored coalesced.
 template <typename T, int V>
-__global__ void __launch_bounds__(256) dcn_col2im_kernel(DcnArgs a, const T* __restrict__ dcols,
-                                                         const T* __restrict__ x, const float* __restrict__ off,
-                                                         const float* __restrict__ msk, float* __restrict__ gx,
-                                                         float* __restrict__ goff, float* __restrict__ gmsk) {
+__global__ void __launch_bounds__(256) dcn_coord_grad_kernel(DcnArgs a, const T* __restrict__ dcols,
+                                                             const T* __restrict__ x, const float* __restrict__ off,
+                                                             const float* __restrict__ msk, float* __restrict__ goff,
+                                                             float* __restrict__ gmsk, unsigned* __restrict__ amax) {
   extern __shared__ float s_lds[];
   float* s_off = s_lds;
   float* s_msk = s_lds + a.DG * 2 * a.K * a.TP;
@@ -172,8 +176,8 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(DcnArgs a, const T* __r
   load_tile(s_off, s_msk, off, msk, a, n, p0, np);
   __syncthreads();
   const T* xim = x + (int64_t)n * a.H * a.W * a.Cp;
-  float* gim = gx + (int64_t)n * a.H * a.W * a.Cp;
   const int items = np * a.K * a.DG;
+  float vmax = 0.f;  // max |mask * dcols| over the samples this block scatters (grad_x scale)
   for (int it = threadIdx.x; it < items; it += blockDim.x) {
     const int dgi = it % a.DG, t2 = it / a.DG, tap = t2 % a.K, px = t2 / a.K;
     const int p = p0 + px, ho = p / a.Wo, wo = p - ho * a.Wo;
@@ -201,19 +205,15 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(DcnArgs a, const T* __r
         if (s.o4 >= 0) Vec<T, V>::load(xim + (int64_t)s.o4 * a.Cp + c, v4);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          // col2im_coord (deform_conv_cuda_kernel.cu:696-770): d bilinear / d h, d w and the
+          // d bilinear / d h and d w (dmcn_get_coordinate_weight, :527-569) and the
           // un-masked sample for the mask gradient
           const float wh = -s.hw * v1[e] - s.lw * v2[e] + s.hw * v3[e] + s.lw * v4[e];
           const float ww = -s.hh * v1[e] + s.hh * v2[e] - s.lh * v3[e] + s.lh * v4[e];
           acc_h += wh * dc[e] * m;
           acc_w += ww * dc[e] * m;
           acc_m += dc[e] * (w1 * v1[e] + w2 * v2[e] + w3 * v3[e] + w4 * v4[e]);
-          // col2im (:636-694): scatter the masked column gradient to the four corners
-          const float t = dc[e] * m;
-          if (s.o1 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o1 * a.Cp + c + e, w1 * t);
-          if (s.o2 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o2 * a.Cp + c + e, w2 * t);
-          if (s.o3 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o3 * a.Cp + c + e, w3 * t);
-          if (s.o4 >= 0) unsafeAtomicAdd(gim + (int64_t)s.o4 * a.Cp + c + e, w4 * t);
+          vmax = fmaxf(vmax, fabsf(dc[e] * m));
+          if (!(fabsf(dc[e] * m) <= 3.0e38f)) vmax = __builtin_inff();  // NaN / inf: grad_x falls back
         }
       }
     }
@@ -222,14 +222,105 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(DcnArgs a, const T* __r
     *pw = acc_w;
     *pm = acc_m;
   }
+  // block max -> per-image max (non-negative floats order like their bit patterns)
+  for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+  if ((threadIdx.x & 63) == 0 && vmax > 0.f) atomicMax(amax + n, __float_as_uint(vmax));
   __syncthreads();
-  const int64_t HWl = HWo;
   const int noff = a.DG * 2 * a.K, nm = a.DG * a.K;
   for (int q = threadIdx.x; q < (noff + nm) * a.TP; q += blockDim.x) {
     const int ch = q / a.TP, px = q - ch * a.TP;
     if (px >= np) continue;
-    if (ch < noff) goff[((int64_t)n * noff + ch) * HWl + p0 + px] = s_off[ch * a.TP + px];
-    else if (gmsk) gmsk[((int64_t)n * nm + ch - noff) * HWl + p0 + px] = s_msk[(ch - noff) * a.TP + px];
+    if (ch < noff) goff[((int64_t)n * noff + ch) * HWo + p0 + px] = s_off[ch * a.TP + px];
+    else if (gmsk) gmsk[((int64_t)n * nm + ch - noff) * HWo + p0 + px] = s_msk[(ch - noff) * a.TP + px];
+  }
+}
+
+// grad_x (col2im, :636-694): scatter mask * dcols to the four bilinear corners.  The
+// workgroup owns a 2-D output tile; every corner that falls into the tile's input
+// footprint (+ a halo of R pixels for the offsets) accumulates in an LDS image of CPP
+// channels, and the footprint is flushed once per channel pass with channel-contiguous
+// (coalesced) global fp32 atomics.  Corners outside the footprint (offsets larger than the
+// halo) go straight to global atomics, so the result never depends on the offset range.
+//
+// LDS accumulation is int64 fixed point (ds_add_u64): fp32 LDS atomics run at ~1/25 of
+// the integer rate on gfx950 (tools/lds_atomic_bench.hip, tools/atomic_bench2.hip).  The
+// per-image scale 2^e puts max |mask * dcols| (from the coordinate kernel) below 2^48, so a
+// cell sum of <= 2^14 contributions cannot overflow and the in-block sum is exact to
+// 2^-48 of the largest term (finer than fp32 accumulation) and order independent.
+// Non-finite gradients (max = inf) use direct fp32 atomics to propagate NaN / inf.
+struct XGeom {
+  int TT, R, RH, RW, CPP;  // output tile edge, halo, footprint rows / cols, channels per pass
+};
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) dcn_grad_x_kernel(DcnArgs a, XGeom xg, const T* __restrict__ dcols,
+                                                         const float* __restrict__ off, const float* __restrict__ msk,
+                                                         const unsigned* __restrict__ amax, float* __restrict__ gx) {
+  extern __shared__ unsigned long long s_acc[];  // [RH*RW][CPP+1]
+  const int HWo = a.Ho * a.Wo;
+  const int tw = (a.Wo + xg.TT - 1) / xg.TT, th = (a.Ho + xg.TT - 1) / xg.TT;
+  const int n = blockIdx.x / (tw * th), t = blockIdx.x - n * (tw * th);
+  const float mx = __uint_as_float(amax[n]);
+  if (mx == 0.f) return;  // nothing of this image is scattered (uniform per block)
+  const bool direct = !(mx <= 3.0e38f);
+  int ex = 0;
+  frexpf(direct ? 1.f : mx, &ex);
+  const int e = min(127, 48 - ex);
+  const float sc = ldexpf(1.f, e), isc = ldexpf(1.f, -e);
+  const int ho0 = (t / tw) * xg.TT, wo0 = (t - (t / tw) * tw) * xg.TT;
+  const int ry0 = ho0 * a.sh - a.ph - xg.R, rx0 = wo0 * a.sw - a.pw - xg.R;
+  const int RP = xg.RH * xg.RW, ST = xg.CPP + 1;
+  const int npx = xg.TT * xg.TT, nvec = xg.CPP / V;
+  float* gim = gx + (int64_t)n * a.H * a.W * a.Cp;
+  for (int c0 = 0; c0 < a.C; c0 += xg.CPP) {
+    for (int i = threadIdx.x; i < RP * ST; i += blockDim.x) s_acc[i] = 0ull;
+    __syncthreads();
+    const int items = npx * nvec * a.K;
+    for (int it = threadIdx.x; it < items; it += blockDim.x) {
+      const int px = it % npx, r = it / npx, cv = r % nvec, tap = r / nvec;
+      const int ho = ho0 + px / xg.TT, wo = wo0 + px % xg.TT;
+      const int c = c0 + cv * V;
+      if (ho >= a.Ho || wo >= a.Wo || c >= a.C) continue;
+      const int p = ho * a.Wo + wo;
+      const int dgi = c / a.cpg, g = c / a.cg, ci = c - g * a.cg;
+      const int i = tap / a.kw, j = tap - i * a.kw;
+      const float oh = off[(((int64_t)n * a.DG + dgi) * 2 * a.K + 2 * tap) * HWo + p];
+      const float ow = off[(((int64_t)n * a.DG + dgi) * 2 * a.K + 2 * tap + 1) * HWo + p];
+      const float m = msk ? msk[(((int64_t)n * a.DG + dgi) * a.K + tap) * HWo + p] : 1.f;
+      const float h = (float)(ho * a.sh - a.ph + i * a.dh) + oh;
+      const float w = (float)(wo * a.sw - a.pw + j * a.dw) + ow;
+      const Sample s = make_sample(h, w, a.H, a.W);
+      if (!s.valid) continue;
+      float dc[V];
+      Vec<T, V>::load(dcols + ((int64_t)n * HWo + p) * a.L + (g * a.K + tap) * a.cgp + ci, dc);
+      const int hl = (int)floorf(h), wl = (int)floorf(w);
+      const float wt[4] = {s.hh * s.hw, s.hh * s.lw, s.lh * s.hw, s.lh * s.lw};
+      const int oo[4] = {s.o1, s.o2, s.o3, s.o4};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (oo[q] < 0) continue;
+        const int ly = hl + (q >> 1) - ry0, lx = wl + (q & 1) - rx0;
+        if (!direct && ly >= 0 && ly < xg.RH && lx >= 0 && lx < xg.RW) {
+          unsigned long long* dst = s_acc + (ly * xg.RW + lx) * ST + cv * V;
+#pragma unroll
+          for (int e2 = 0; e2 < V; ++e2)
+            atomicAdd(dst + e2, (unsigned long long)__float2ll_rn(wt[q] * (dc[e2] * m) * sc));
+        } else {
+          float* dst = gim + (int64_t)oo[q] * a.Cp + c;
+#pragma unroll
+          for (int e2 = 0; e2 < V; ++e2) unsafeAtomicAdd(dst + e2, wt[q] * (dc[e2] * m));
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < RP * xg.CPP; i += blockDim.x) {
+      const int pix = i / xg.CPP, ch = i - pix * xg.CPP;
+      const int yy = ry0 + pix / xg.RW, xx = rx0 + pix % xg.RW;
+      if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W || c0 + ch >= a.C) continue;
+      const long long v = (long long)s_acc[pix * ST + ch];
+      if (v != 0) unsafeAtomicAdd(gim + ((int64_t)yy * a.W + xx) * a.Cp + c0 + ch, (float)v * isc);
+    }
+    __syncthreads();
   }
 }
 
@@ -254,6 +345,7 @@ int make_args(const sr_dcn_desc* d, DcnArgs& a) {
   a.L = a.G * a.K * a.cgp;
   // pixel tile: offsets + masks of every deformable group in LDS (<= 64 KB)
   a.TP = 64;
+  while (a.TP > 16 && (size_t)a.DG * 3 * a.K * a.TP * 4 > 32768) a.TP >>= 1;
   while (a.TP > 1 && (size_t)a.DG * 3 * a.K * a.TP * 4 > 65536) a.TP >>= 1;
   if ((size_t)a.DG * 3 * a.K * a.TP * 4 > 65536) return sr_fail(SR_EINVAL, "dcn: too many deformable groups x taps");
   return SR_OK;
@@ -278,18 +370,46 @@ int launch_im2col(const DcnArgs& a, const void* x, const float* off, const float
   return sr_check(hipGetLastError(), "dcn_im2col launch");
 }
 
+XGeom grad_x_geom(const DcnArgs& a) {
+  // largest (tile, halo) whose LDS footprint fits 64 KB; halo 0 still covers the
+  // undeformed footprint, anything outside goes to global atomics
+  static const int cfg[][2] = {{16, 4}, {16, 2}, {8, 4}, {8, 2}, {8, 0}, {4, 0}};
+  XGeom g;
+  g.CPP = 8;
+  for (const auto& c : cfg) {
+    g.TT = c[0];
+    g.R = c[1];
+    g.RH = (g.TT - 1) * a.sh + (a.kh - 1) * a.dh + 2 * g.R + 2;
+    g.RW = (g.TT - 1) * a.sw + (a.kw - 1) * a.dw + 2 * g.R + 2;
+    if ((size_t)g.RH * g.RW * (g.CPP + 1) * 8 <= 65536) return g;
+  }
+  g.TT = 4; g.R = 0; g.RH = g.RW = 1;  // degenerate footprint: everything through global atomics
+  return g;
+}
+
 template <typename T>
 int launch_col2im(const DcnArgs& a, const void* dcols, const void* x, const float* off, const float* msk, float* gx,
-                  float* goff, float* gmsk, hipStream_t s) {
+                  float* goff, float* gmsk, unsigned* amax, hipStream_t s) {
+  if (hipMemsetAsync(amax, 0, (size_t)a.N * sizeof(unsigned), s) != hipSuccess)
+    return sr_fail(SR_ELAUNCH, "dcn_col2im: memset failed");
   const int tiles = (a.Ho * a.Wo + a.TP - 1) / a.TP;
-  const dim3 grid((unsigned)(a.N * tiles));
   const size_t lds = (size_t)a.DG * 3 * a.K * a.TP * 4;
-  if (vec_width<T>(a) > 1)
-    hipLaunchKernelGGL((dcn_col2im_kernel<T, Elt<T>::PER16>), grid, dim3(256), lds, s, a, (const T*)dcols,
-                       (const T*)x, off, msk, gx, goff, gmsk);
+  const bool vec = vec_width<T>(a) > 1;
+  if (vec)
+    hipLaunchKernelGGL((dcn_coord_grad_kernel<T, Elt<T>::PER16>), dim3((unsigned)(a.N * tiles)), dim3(256), lds, s, a,
+                       (const T*)dcols, (const T*)x, off, msk, goff, gmsk, amax);
   else
-    hipLaunchKernelGGL((dcn_col2im_kernel<T, 1>), grid, dim3(256), lds, s, a, (const T*)dcols, (const T*)x, off, msk,
-                       gx, goff, gmsk);
+    hipLaunchKernelGGL((dcn_coord_grad_kernel<T, 1>), dim3((unsigned)(a.N * tiles)), dim3(256), lds, s, a,
+                       (const T*)dcols, (const T*)x, off, msk, goff, gmsk, amax);
+  const XGeom xg = grad_x_geom(a);
+  const int xt = ((a.Ho + xg.TT - 1) / xg.TT) * ((a.Wo + xg.TT - 1) / xg.TT);
+  const size_t xlds = (size_t)xg.RH * xg.RW * (xg.CPP + 1) * 8;
+  if (vec)
+    hipLaunchKernelGGL((dcn_grad_x_kernel<T, Elt<T>::PER16>), dim3((unsigned)(a.N * xt)), dim3(256), xlds, s, a, xg,
+                       (const T*)dcols, off, msk, amax, gx);
+  else
+    hipLaunchKernelGGL((dcn_grad_x_kernel<T, 1>), dim3((unsigned)(a.N * xt)), dim3(256), xlds, s, a, xg,
+                       (const T*)dcols, off, msk, amax, gx);
   return sr_check(hipGetLastError(), "dcn_col2im launch");
 }
 
@@ -309,16 +429,23 @@ int sr_dcn_im2col(const sr_dcn_desc* d, const void* x, const float* offset, cons
   return sr_fail(SR_EINVAL, "dcn_im2col: bad dtype");
 }
 
+size_t sr_dcn_col2im_workspace(const sr_dcn_desc* d) { return d ? (size_t)d->N * sizeof(unsigned) : 0; }
+
 int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const float* offset, const float* mask,
-                  float* grad_x, float* grad_offset, float* grad_mask, void* stream) {
+                  float* grad_x, float* grad_offset, float* grad_mask, void* workspace, size_t ws_bytes,
+                  void* stream) {
   DcnArgs a;
   int rc = make_args(d, a);
   if (rc) return rc;
   if (!dcols || !x || !offset || !grad_x || !grad_offset) return sr_fail(SR_EINVAL, "dcn_col2im: null pointer");
+  if (!workspace || ws_bytes < sr_dcn_col2im_workspace(d)) return sr_fail(SR_EINVAL, "dcn_col2im: workspace too small");
+  unsigned* amax = (unsigned*)workspace;
   if (grad_mask && !mask) return sr_fail(SR_EINVAL, "dcn_col2im: grad_mask needs mask");
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == SR_BF16) return launch_col2im<bf16_t>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, s);
-  if (d->dtype == SR_F32) return launch_col2im<float>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, s);
+  if (d->dtype == SR_BF16)
+    return launch_col2im<bf16_t>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, amax, s);
+  if (d->dtype == SR_F32)
+    return launch_col2im<float>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, amax, s);
   return sr_fail(SR_EINVAL, "dcn_col2im: bad dtype");
 }
 

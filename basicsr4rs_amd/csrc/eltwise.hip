@@ -47,6 +47,54 @@ __global__ void nhwc_to_nchw_kernel(const T* __restrict__ x, int N, int H, int W
   }
 }
 
+// Wide-channel variants (feature maps, C >= 16): a 64-pixel x 32-channel tile is
+// transposed through LDS so both the NCHW side (pixels contiguous) and the NHWC side
+// (channels contiguous) are accessed with unit stride; the per-pixel kernels above are
+// kept for the 3-channel image boundary where a tile would be mostly padding.
+template <typename T>
+__global__ void __launch_bounds__(256) nchw_to_nhwc_tiled_kernel(const float* __restrict__ x, int C, int64_t HW,
+                                                                 int Cp, const float* shift, const float* scale,
+                                                                 T* __restrict__ y) {
+  __shared__ float t[32][65];
+  const int64_t p0 = (int64_t)blockIdx.x * 64, n = blockIdx.z;
+  const int c0 = blockIdx.y * 32;
+  for (int i = threadIdx.x; i < 32 * 64; i += 256) {
+    const int c = i >> 6, p = i & 63;
+    float v = 0.f;
+    if (c0 + c < C && p0 + p < HW) {
+      v = x[(n * C + c0 + c) * HW + p0 + p];
+      v = (v - (shift ? shift[c0 + c] : 0.f)) * (scale ? scale[c0 + c] : 1.f);
+    }
+    t[c][p] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 32; i += 256) {
+    const int p = i >> 5, c = i & 31;
+    if (p0 + p < HW && c0 + c < Cp) y[(n * HW + p0 + p) * Cp + c0 + c] = Elt<T>::from_f(t[c][p]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) nhwc_to_nchw_tiled_kernel(const T* __restrict__ x, int64_t HW, int ld,
+                                                                 int coff, int C, const float* scale,
+                                                                 const float* shift, float* __restrict__ y) {
+  __shared__ float t[32][65];
+  const int64_t p0 = (int64_t)blockIdx.x * 64, n = blockIdx.z;
+  const int c0 = blockIdx.y * 32;
+  for (int i = threadIdx.x; i < 64 * 32; i += 256) {
+    const int p = i >> 5, c = i & 31;
+    float v = 0.f;
+    if (p0 + p < HW && c0 + c < C) v = Elt<T>::to_f(x[(n * HW + p0 + p) * ld + coff + c0 + c]);
+    t[c][p] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 32 * 64; i += 256) {
+    const int c = i >> 6, p = i & 63;
+    if (c0 + c < C && p0 + p < HW)
+      y[(n * C + c0 + c) * HW + p0 + p] = t[c][p] * (scale ? scale[c0 + c] : 1.f) + (shift ? shift[c0 + c] : 0.f);
+  }
+}
+
 // out[n, c, h*r+i, w*r+j] = in[n, c*r*r + i*r + j, h, w]   (r > 0, shuffle)
 // out[n, c*s*s + i*s + j, h, w] = in[n, c, h*s+i, w*s+j]   (r = -s, unshuffle)
 template <typename T>
@@ -194,6 +242,17 @@ int sr_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, int C
   if (!x || !y || Cp < C) return sr_fail(SR_EINVAL, "nchw_to_nhwc: bad arguments");
   const int64_t P = (int64_t)N * H * W;
   hipStream_t s = (hipStream_t)stream;
+  if (C >= 16 && N <= 65535) {
+    const int64_t HW = (int64_t)H * W;
+    const dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((Cp + 31) / 32), (unsigned)N);
+    if (dtype == SR_BF16)
+      hipLaunchKernelGGL(nchw_to_nhwc_tiled_kernel<bf16_t>, grid, dim3(256), 0, s, x, C, HW, Cp, shift, scale,
+                         (bf16_t*)y);
+    else
+      hipLaunchKernelGGL(nchw_to_nhwc_tiled_kernel<float>, grid, dim3(256), 0, s, x, C, HW, Cp, shift, scale,
+                         (float*)y);
+    return sr_check(hipGetLastError(), "nchw_to_nhwc launch");
+  }
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, x,
                        N, C, H, W, Cp, shift, scale, (bf16_t*)y);
@@ -208,6 +267,17 @@ int sr_nhwc_to_nchw(int dtype, const void* x, int N, int H, int W, int ld, int c
   if (!x || !y || ld < coff + C) return sr_fail(SR_EINVAL, "nhwc_to_nchw: bad arguments");
   const int64_t P = (int64_t)N * H * W;
   hipStream_t s = (hipStream_t)stream;
+  if (C >= 16 && N <= 65535) {
+    const int64_t HW = (int64_t)H * W;
+    const dim3 grid((unsigned)((HW + 63) / 64), (unsigned)((C + 31) / 32), (unsigned)N);
+    if (dtype == SR_BF16)
+      hipLaunchKernelGGL(nhwc_to_nchw_tiled_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, HW, ld, coff,
+                         C, scale, shift, y);
+    else
+      hipLaunchKernelGGL(nhwc_to_nchw_tiled_kernel<float>, grid, dim3(256), 0, s, (const float*)x, HW, ld, coff, C,
+                         scale, shift, y);
+    return sr_check(hipGetLastError(), "nhwc_to_nchw launch");
+  }
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s,
                        (const bf16_t*)x, N, H, W, ld, coff, C, scale, shift, y);

@@ -163,9 +163,12 @@ def _dcn_backward(grad_out, saved, weight, bias, g, dtype):
     gx = torch.zeros(g.N, g.H, g.W, g.Cp, device=dyh.device, dtype=torch.float32)
     goff = torch.empty_like(off)
     gmask = None if msk is None else torch.empty_like(msk)
+    d = g.desc(dtype)
+    wsb = lib.sr_dcn_col2im_workspace(d)
+    ws = torch.empty(wsb // 4 + 1, device=dyh.device, dtype=torch.int32)
     _lib.check(
-        lib.sr_dcn_col2im(g.desc(dtype), _lib.ptr(dcols), _lib.ptr(xh), _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx),
-                          _lib.ptr(goff), _lib.ptr(gmask), _lib.stream()))
+        lib.sr_dcn_col2im(d, _lib.ptr(dcols), _lib.ptr(xh), _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx),
+                          _lib.ptr(goff), _lib.ptr(gmask), _lib.ptr(ws), wsb, _lib.stream()))
     return C.nhwc_to_nchw(gx, g.C), goff, gmask, grad_weight, grad_bias
 
 

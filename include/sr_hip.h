@@ -246,10 +246,13 @@ typedef struct sr_dcn_desc {
 int sr_dcn_im2col(const sr_dcn_desc* d, const void* x, const float* offset, const float* mask, void* cols,
                   void* stream);
 /* From dcols (= dy x W, column layout): grad_x += scatter (fp32 NHWC [N][H][W][Cp], caller
- * zeroes it; atomics), grad_offset / grad_mask written in full (grad_mask NULL for v1).
+ * zeroes it; LDS fixed-point accumulation + fp32 atomics), grad_offset / grad_mask written in
+ * full (grad_mask NULL for v1).  Workspace: sr_dcn_col2im_workspace bytes (per-image scale).
  * Replaces the col2im + col2im_coord pair (deform_conv_cuda_kernel.cu:280-466, :636-770). */
+size_t sr_dcn_col2im_workspace(const sr_dcn_desc* d);
 int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const float* offset, const float* mask,
-                  float* grad_x, float* grad_offset, float* grad_mask, void* stream);
+                  float* grad_x, float* grad_offset, float* grad_mask, void* workspace, size_t ws_bytes,
+                  void* stream);
 
 /* fused_bias_act_op (basicsr/ops/fused_act/src/fused_bias_act_kernel.cu): out = scale *
  * act(x + bias[(i / step_b) % size_b]) with act 1 linear / 3 leaky-relu(alpha), grad 0/1/2

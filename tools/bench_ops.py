@@ -30,19 +30,22 @@ def timeit(fn, iters=20, warmup=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=16)
+    ap.add_argument('--offset-scale', type=float, default=2.0, help='std of the synthetic offsets (pixels)')
+    ap.add_argument('--only', default='', help='comma list: dcn,ufd,fba')
     args = ap.parse_args()
     dev = torch.device('cuda')
     res = {}
     N, C, H, W, dg = args.batch, 64, 128, 128, 8
     x = torch.randn(N, C, H, W, device=dev, requires_grad=True)
-    off = (torch.randn(N, dg * 18, H, W, device=dev) * 2).requires_grad_()
+    off = (torch.randn(N, dg * 18, H, W, device=dev) * args.offset_scale).requires_grad_()
     msk = torch.rand(N, dg * 9, H, W, device=dev, requires_grad=True)
     w = (torch.randn(C, C, 3, 3, device=dev) * 0.05).requires_grad_()
     b = torch.zeros(C, device=dev, requires_grad=True)
     dy = torch.randn(N, C, H, W, device=dev)
     # minimum bytes: read x, offset, mask, write y (fwd); + read dy, write dx, doff, dmask (bwd)
     fwd_bytes = 4 * (x.numel() + off.numel() + msk.numel() + dy.numel())
-    for mode in ('fp32', 'bf16'):
+    only = set(args.only.split(',')) if args.only else {'dcn', 'ufd', 'fba'}
+    for mode in (('fp32', 'bf16') if 'dcn' in only else ()):
         ac = mode == 'bf16'
 
         def fwd():
@@ -58,6 +61,9 @@ def main():
         tfb = timeit(fwdbwd, iters=10)
         res[f'dcnv2_{mode}'] = {'fwd_ms': tf, 'fwd_bwd_ms': tfb, 'fwd_alg_GBps': fwd_bytes / tf / 1e6,
                                 'fwd_bwd_alg_GBps': 2 * fwd_bytes / tfb / 1e6}
+    if 'ufd' not in only:
+        print(json.dumps(res, indent=1))
+        return
     # upfirdn2d: StyleGAN2 1024 upsample (x2, 4x4 kernel) on [4, 64, 512, 512]
     k = torch.tensor([1., 3., 3., 1.], device=dev)
     k = torch.outer(k, k)
