@@ -20,7 +20,10 @@
 
 namespace {
 
-bool g_disable_big = false;  // set by sr_conv3x3_set_variant (tests / A-B timing)
+// set by sr_conv3x3_set_variant (tests / A-B timing): 0 auto (phase-interleaved 256x256),
+// 1 never a 256x256 kernel, 2 the two-barrier 256x256 kernel (previous schedule)
+int g_variant = 0;
+#define g_disable_big (g_variant == 1)
 
 struct FwdArgs {
   const void* x;
@@ -52,6 +55,7 @@ struct FwdArgs {
   void* aux;      // optional store of the pre-activation value (same layout as y)
   int tiles_n, tiles;
   FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
+  FastDiv fd_r;                        // divide by in_ps (1 when none)
 };
 
 template <typename T>
@@ -507,6 +511,267 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_big_kernel(FwdArgs a) {
           for (int r = 0; r < 4; ++r)
             Cs[(i * 16 + (lane >> 4) * 4 + r) * CSTR + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
     }
+    __syncthreads();
+    epilogue_tile<bf16_t, 128, 256, 512>(a, Cs, CSTR, m0 + h * 128, n0, tid);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// 256 x 256 forward / dgrad kernel, phase-interleaved ("ping-pong") schedule.
+//
+// Same tile, waves, MFMA shape and LDS-DMA staging as conv3x3_fwd_big_kernel, but the
+// K-step is cut into 4 phases (cdna_hip_programming.md §5 "256² 8-phase template"):
+//   * LDS holds per buffer four 16 KB half-tiles A0 (tile rows 0-127), A1 (128-255),
+//     B0 (cols 0-127), B1 (128-255).  Wave (wr = w>>2, wc = w&3) owns rows
+//     {h*128 + wr*64 + [0,64)} x cols {g*128 + wc*32 + [0,32)}, h, g in {0, 1}, so its
+//     quadrant (h, g) reads exactly half-tiles A_h and B_g.
+//   * phase p of K-step t computes quadrant (0,0), (0,1), (1,1), (1,0) (16 MFMAs each)
+//     and issues ONE half-tile of step t+1 (2 LDS-DMA per thread) in the order A0, B0, B1,
+//     A1; a counted `s_waitcnt vmcnt(4)` keeps two half-tiles in flight across every
+//     barrier and retires exactly what the next phase reads.
+//   * waves 4-7 run one barrier behind waves 0-3 (stagger), so the two waves sharing a
+//     SIMD alternate: one issues its fragment reads and DMA while the other runs MFMAs.
+// Reads of a half-tile happen one barrier after the wait that retires it for every wave
+// (two barriers for the lagging group); its slot is re-filled >= 4 phases after its last
+// read.  Fragments: A 32 VGPR (one half), B 2 x 16 VGPR (both halves), acc 128 VGPR.
+// ------------------------------------------------------------------------------------
+SR_DEV void pp_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
+  constexpr int CSTR = 256 + 4;
+  constexpr int SMEM = 128 * CSTR * 4;  // epilogue half tile; >= 2 x 64 KB stages
+  static_assert(SMEM >= 2 * BIG_STAGE, "LDS too small");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (int)(tile / a.tiles_n) * 256;
+  const int n0 = (int)(tile % a.tiles_n) * 256;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
+
+  // DMA rows of this lane inside a half-tile: w*16 + j*8 + (lane>>3), j = 0, 1.
+  // Index k = h*2 + j (A: tile row h*128 + ...; B: output channel n0 + g*128 + ...).
+  // FAST (every 64-deep K-step inside one tap and one shuffle slot): the A source offset is
+  // a per-lane pixel base + a wave-uniform (tap, channel) offset computed on the scalar
+  // unit, and the zero padding a per-lane 9-bit mask of valid taps -- the fragment-read /
+  // DMA segment of a phase then carries ~3 VALU per DMA instead of the full gather math.
+  const int c = (lane & 7) ^ (lane >> 3);  // logical chunk loaded by this lane (row & 7 == lane >> 3)
+  const int rps = a.in_ps > 0 ? a.in_ps : 1;
+  int ay[4], ax[4], anh[4];
+  uint32_t abase[4], amask[4];
+  uint32_t boff[4];
+  bool bval[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = (k >> 1) * 128 + w * 16 + (k & 1) * 8 + (lane >> 3);
+    const int m = m0 + r;
+    amask[k] = 0;
+    abase[k] = 0;
+    if (m < a.M) {
+      uint32_t q = fdiv((uint32_t)m, a.fd_W);
+      ax[k] = m - (int)q * a.W;
+      uint32_t n = fdiv(q, a.fd_H);
+      ay[k] = (int)q - (int)n * a.H;
+      anh[k] = (int)n * a.H;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = ay[k] + t / 3 - 1, xx = ax[k] + t % 3 - 1;
+        if ((unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W) amask[k] |= 1u << t;
+      }
+      abase[k] = (uint32_t)(((anh[k] + ay[k]) * rps * (a.W * rps) + ax[k] * rps) * a.ldx) * 2u + (uint32_t)c * 16u;
+    } else {
+      ax[k] = 0; ay[k] = -100000; anh[k] = 0;
+    }
+    const int n = n0 + r;
+    bval[k] = n < a.Cout;
+    boff[k] = (uint32_t)(n * a.ldw) * 2u + (uint32_t)c * 16u;
+  }
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.nkc + 7) >> 3;
+  constexpr uint32_t SLOT_A0 = 0, SLOT_A1 = 16384, SLOT_B0 = 32768, SLOT_B1 = 49152;
+
+  // FAST: wave-uniform state of the K-step whose A half-tiles are issued next (tap,
+  // channel offset inside the tap, shuffle slot), advanced once per step on the scalar unit.
+  int k_tap = a.tap0, k_chu = 0, k_uoff = 0;
+  auto k_eval = [&]() {
+    const int dy = k_tap / 3 - 1, dx = k_tap - (k_tap / 3) * 3 - 1;
+    if (a.in_ps == 0) {
+      k_uoff = ((dy * a.W + dx) * a.ldx + a.xcoff + k_chu) * 2;
+    } else {
+      const int r = a.in_ps;
+      const int sl = (int)fdiv((uint32_t)k_chu, a.fd_cps);
+      const int cch = k_chu - sl * a.fd_cps.d;
+      const int si = (int)fdiv((uint32_t)sl, a.fd_r), sj = sl - si * r;
+      k_uoff = (((dy * r + si) * (a.W * r) + dx * r + sj) * a.ldx + a.xcoff + cch) * 2;
+    }
+    k_uoff = __builtin_amdgcn_readfirstlane(k_uoff);
+  };
+  auto k_advance = [&]() {
+    k_chu += 64;
+    if (k_chu == a.Cin) { k_chu = 0; ++k_tap; }
+    k_eval();
+  };
+
+  // one A half-tile (h) of K-step ks: 2 DMA per thread (FAST: ks is the step k_* describes)
+  auto issue_a = [&](int ks, int h) {
+    char* dst = smem + (ks & 1) * BIG_STAGE + (h ? SLOT_A1 : SLOT_A0) + w * 2048;
+    if constexpr (FAST) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = h * 2 + j;
+        glds16(xr, dst + j * 1024, ((amask[k] >> k_tap) & 1u) ? abase[k] + (uint32_t)k_uoff : SR_OOB);
+      }
+    } else {
+      const int q = ks * 8 + c;
+      const int tap_i = (int)fdiv((uint32_t)q, a.fd_cpt);
+      const int cc = q - tap_i * a.cpt;
+      const int tap = tap_i + a.tap0;
+      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+      const bool kval = q < a.nkc;
+      const int ch = cc * 8;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = h * 2 + j;
+        const int yy = ay[k] + dy, xx = ax[k] + dx;
+        const bool v = kval && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+        uint32_t off;
+        if (a.in_ps == 0) {
+          off = (uint32_t)((((anh[k] + yy) * a.W + xx) * a.ldx + a.xcoff + ch) * 2);
+        } else {
+          const int r = a.in_ps;
+          const int sl = (int)fdiv((uint32_t)ch, a.fd_cps);
+          const int cch = ch - sl * a.fd_cps.d;
+          const int si = sl / r, sj = sl - (sl / r) * r;
+          off = (uint32_t)((((anh[k] + yy) * r + si) * (a.W * r) + xx * r + sj) * a.ldx + a.xcoff + cch) * 2;
+        }
+        glds16(xr, dst + j * 1024, v ? off : SR_OOB);
+      }
+    }
+  };
+  auto issue_b = [&](int ks, int g) {
+    const bool kval = ks * 8 + c < a.nkc;
+    char* dst = smem + (ks & 1) * BIG_STAGE + (g ? SLOT_B1 : SLOT_B0) + w * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = g * 2 + j;
+      glds16(wr_, dst + j * 1024, (kval && bval[k]) ? boff[k] + (uint32_t)ks * 128u : SR_OOB);
+    }
+  };
+
+  u32x4 fa[2][4], fb[2][2][2];  // fa[kk][i] (current A half), fb[g][kk][j]
+  auto read_a = [&](int buf, int h) {
+    const char* As = smem + buf * BIG_STAGE + (h ? SLOT_A1 : SLOT_A0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[kk][i] = *(const u32x4*)(As + swz128(wr * 64 + i * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+  };
+  auto read_b = [&](int buf, int g) {
+    const char* Bs = smem + buf * BIG_STAGE + (g ? SLOT_B1 : SLOT_B0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[g][kk][j] = *(const u32x4*)(Bs + swz128(wc * 32 + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+  };
+  auto mma = [&](int h, int g) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mfma_chunk<bf16_t>(fa[kk][i], fb[g][kk][j], acc[h][g][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: K-step 0 fully issued; A0, B0 retired for every wave before the first read
+  if constexpr (FAST) k_eval();
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(0, 1);
+  issue_a(0, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  pp_barrier();
+  if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more = t + 1 < nk;
+    // phase 1: quadrant (0,0); issue A0(t+1); retire B1(t)
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (more) {
+      if constexpr (FAST) k_advance();
+      issue_a(t + 1, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    pp_barrier();
+    mma(0, 0);
+    pp_barrier();
+    // phase 2: quadrant (0,1); issue B0(t+1); retire A1(t)
+    read_b(buf, 1);
+    if (more) {
+      issue_b(t + 1, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    mma(0, 1);
+    pp_barrier();
+    // phase 3: quadrant (1,1); issue B1(t+1)
+    read_a(buf, 1);
+    if (more) issue_b(t + 1, 1);
+    pp_barrier();
+    mma(1, 1);
+    pp_barrier();
+    // phase 4: quadrant (1,0); issue A1(t+1); retire A0(t+1), B0(t+1)
+    if (more) {
+      issue_a(t + 1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    pp_barrier();
+    mma(1, 0);
+    pp_barrier();
+  }
+  if (!wr) pp_barrier();  // balance the stagger
+
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CSTR + g * 128 + wc * 32 + j * 16 + (lane & 15)] =
+                acc[h][g][i][j][r];
     __syncthreads();
     epilogue_tile<bf16_t, 128, 256, 512>(a, Cs, CSTR, m0 + h * 128, n0, tid);
   }
@@ -1101,7 +1366,12 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   const int tm = (a.M + 255) / 256;
   a.tiles_n = (a.Cout + 255) / 256;
   a.tiles = tm * a.tiles_n;
-  hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
+  if (g_variant == 2)
+    hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
+  else if (a.Cin % 64 == 0 && (a.in_ps == 0 || a.fd_cps.d % 64 == 0))
+    hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<true>, dim3(a.tiles), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<false>, dim3(a.tiles), dim3(512), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1244,6 +1514,7 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   if ((d->in_ps > 0 || d->out_ps > 0) && cps % PER)
     return sr_fail(SR_EINVAL, "conv3x3_fwd: shuffled channel count must be a multiple of 8");
   a.fd_cps = make_fastdiv(cps);
+  a.fd_r = make_fastdiv(d->in_ps > 0 ? d->in_ps : 1);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = d->dtype == SR_BF16 ? dispatch_fwd<bf16_t>(a, s) : dispatch_fwd<float>(a, s);
   return sr_check(e, "conv3x3_fwd launch");
@@ -1253,7 +1524,8 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
 // descriptor (bench.py traces and rocprof summaries are matched on these names).
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
-  if (bf && !d->out_nchw && d->Cout >= 256 && d->in_up <= 1 && !g_disable_big) return "conv3x3_fwd_big_kernel";
+  if (bf && !d->out_nchw && d->Cout >= 256 && d->in_up <= 1 && !g_disable_big)
+    return g_variant == 2 ? "conv3x3_fwd_big_kernel" : "conv3x3_fwd_pp_kernel";
   if (d->out_nchw || d->Cout <= 16) return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
   if (d->Cout <= 32) return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
   if (d->Cout <= 64) return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
@@ -1265,9 +1537,11 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
 }
 
-// Kernel-variant switch for A/B tests: variant 0 = automatic, 1 = never use the 256x256 kernel.
+// Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
+// 2 = the two-barrier 256x256 forward kernel instead of the phase-interleaved one.
 int sr_conv3x3_set_variant(int variant) {
-  g_disable_big = variant == 1;
+  if (variant < 0 || variant > 2) return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1 or 2");
+  g_variant = variant;
   return SR_OK;
 }
 

@@ -150,12 +150,15 @@ def test_edsr_m_parity_fp32(cuda):
         assert rel_err(p.grad.cpu(), sd[n].grad) < 1e-3, n
 
 
-@pytest.mark.parametrize('shape', [(2, 64, 64, 256, 256, 0), (1, 20, 36, 256, 512, 0), (3, 17, 9, 256, 768, 0),
-                                   (1, 16, 16, 1024, 256, 2), (2, 8, 24, 256, 1024, 2)])
+@pytest.mark.parametrize('shape', [(2, 64, 64, 256, 256, 0, 3), (1, 20, 36, 256, 512, 0, 3), (3, 17, 9, 256, 768, 0, 3),
+                                   (1, 16, 16, 1024, 256, 2, 3), (2, 8, 24, 256, 1024, 2, 3),
+                                   (1, 12, 20, 264, 256, 0, 3), (2, 16, 16, 64, 256, 0, 1), (1, 9, 15, 184, 544, 0, 1)])
 def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
-    """The 256x256 LDS-DMA kernel and the 128x128 register-staged kernel sum K in the same
-    order, so their bf16 outputs must be bitwise identical (partial tiles, in_ps gather)."""
-    N, H, W, cin, cout, in_ps = shape
+    """The phase-interleaved 256x256 kernel (variant 0), the 128x128 register-staged kernel
+    (1) and the two-barrier 256x256 kernel (2) sum K in the same order, so their bf16 outputs
+    must be bitwise identical (partial M/N tiles, K-steps crossing taps, a single K-step,
+    1x1 taps, in_ps gather)."""
+    N, H, W, cin, cout, in_ps, ks = shape
     torch.manual_seed(3)
     dt = torch.bfloat16
     lib = _lib.load()
@@ -163,18 +166,23 @@ def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
         x = torch.randn(N, H * in_ps, W * in_ps, cin // (in_ps * in_ps), device=cuda).to(dt)
     else:
         x = torch.randn(N, H, W, cin, device=cuda).to(dt)
-    wf = (torch.randn(cout, 9 * cin, device=cuda) * 0.05).to(dt)
+    taps = 9 if ks == 3 else 1
+    wf = (torch.randn(cout, taps * cin, device=cuda) * 0.05).to(dt)
     bg = torch.randn(cout, device=cuda)
     res = torch.randn(N, H, W, cout, device=cuda).to(dt)
     outs = []
-    for variant in (0, 1):
-        _lib.check(lib.sr_conv3x3_set_variant(variant))
-        y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
-        C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, res=res, alpha=0.5, in_ps=in_ps, ldx=x.shape[-1])
-        outs.append(y)
-    _lib.check(lib.sr_conv3x3_set_variant(0))
+    try:
+        for variant in (0, 1, 2):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+            C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, res=res, alpha=0.5, in_ps=in_ps, ldx=x.shape[-1],
+                           ksize=ks)
+            outs.append(y)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.parametrize('shape', [(2, 16, 16, 256, 256, 0), (1, 20, 12, 512, 256, 0), (2, 9, 14, 256, 768, 0),

@@ -25,8 +25,11 @@ def timeit(fn, iters=20):
 def main():
     dev = 'cuda'
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    variants = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else '0').split(',')]
+    lib = C._lib.load()
     res = []
-    for dtype in (torch.bfloat16, ):
+    for dtype, variant in [(torch.bfloat16, v) for v in variants]:
+        C._lib.check(lib.sr_conv3x3_set_variant(variant))
         for (cin, cout, hw, ps) in [(256, 256, 64, 0), (256, 1024, 64, 2), (256, 1024, 128, 2), (256, 3, 256, 0),
                                     (64, 64, 64, 0)]:
             conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(dev)
@@ -38,7 +41,7 @@ def main():
             fl = 2.0 * B * hw * hw * cin * cout * 9
             t = timeit(lambda: C.conv_fwd_raw(x, wf, bg, y, B, hw, hw, spec.cin_p, spec.cout_p, cout, out_ps=ps,
                                               out_nchw=spec.out_nchw))
-            res.append(dict(k='fwd', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+            res.append(dict(v=variant, k='fwd', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
             if spec.out_nchw:
                 dy = torch.randn(B, hw, hw, spec.cout_p, device=dev).to(dtype)
                 psx = 0
@@ -48,9 +51,9 @@ def main():
             dx = torch.empty(B, hw, hw, spec.cin_p, device=dev, dtype=dtype)
             t = timeit(lambda: C.conv_fwd_raw(dy, wd, None, dx, B, hw, hw, spec.cout_p, spec.cin_p, spec.cin_p,
                                               in_ps=psx, ldx=dy.shape[-1]))
-            res.append(dict(k='dgrad', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+            res.append(dict(v=variant, k='dgrad', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
             t = timeit(lambda: C.conv_wgrad_raw(dy, x, B, hw, hw, spec.cin_p, cin, spec.cout_p, cout, out_ps=psx))
-            res.append(dict(k='wgrad', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+            res.append(dict(v=variant, k='wgrad', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
     for r in res:
         print(json.dumps(r))
 
