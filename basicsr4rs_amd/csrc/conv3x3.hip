@@ -101,9 +101,50 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     return;
   }
   constexpr int CG = BN / 8;  // 8-channel groups per row
+  constexpr int IT = ROWS * CG / NT;  // groups per thread
+  static_assert(ROWS * CG % NT == 0, "epilogue tiling");
+  constexpr int NV = SZ == 2 ? 1 : 2;  // 16-B loads per 8-channel group
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
-  for (int idx = tid; idx < ROWS * CG; idx += NT) {
+  const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+  // per batch of IB groups: first issue every gate / residual load (range-checked buffer
+  // loads: invalid groups read zeros) so their HBM latency overlaps, then compute + store.
+  constexpr int IB = (SZ == 2 ? 4 : 2) < IT ? (SZ == 2 ? 4 : 2) : IT;  // groups per load batch
+  static_assert(IT % IB == 0, "epilogue batch");
+#pragma unroll 1
+  for (int it0 = 0; it0 < IT; it0 += IB) {
+  u32x4 gv[IB][NV], rv1[IB][NV], rv2[IB][NV];
+#pragma unroll
+  for (int ib = 0; ib < IB; ++ib) {
+    const int it = ib;
+    const int idx = tid + (it0 + ib) * NT;
+    const int row = idx / CG, cg = idx % CG;
+    const int m = m0 + row, n = n0 + cg * 8;
+    const bool ok = m < a.M && n < a.Cout;
+    const bool okr = ok && n < a.rcols;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (a.gate) gv[it][v] = buf_load16(gr, ok ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ) + 16u * v : SR_OOB);
+      if (a.res) rv1[it][v] = buf_load16(rr, okr ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ) + 16u * v : SR_OOB);
+      if (a.res2)
+        rv2[it][v] = buf_load16(rr2, okr ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * SZ) + 16u * v : SR_OOB);
+    }
+  }
+  auto unpack = [&](const u32x4* q, float* o) {
+    if constexpr (SZ == 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[2 * j] = bf16_to_f32(q[0][j] & 0xffff);
+        o[2 * j + 1] = bf16_to_f32(q[0][j] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[j] = __uint_as_float(q[0][j]); o[4 + j] = __uint_as_float(q[NV - 1][j]); }
+    }
+  };
+#pragma unroll
+  for (int it = 0; it < IB; ++it) {
+    const int idx = tid + (it0 + it) * NT;
     const int row = idx / CG, cg = idx % CG;
     const int m = m0 + row, n = n0 + cg * 8;
     if (m >= a.M || n >= a.Cout) continue;
@@ -134,19 +175,7 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
     if (a.gate) {
       float g[8];
-      const uint32_t off = (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ);
-      if constexpr (SZ == 2) {
-        u32x4 gg = buf_load16(gr, off);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          g[2 * j] = bf16_to_f32(gg[j] & 0xffff);
-          g[2 * j + 1] = bf16_to_f32(gg[j] >> 16);
-        }
-      } else {
-        u32x4 g0 = buf_load16(gr, off), g1 = buf_load16(gr, off + 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { g[j] = __uint_as_float(g0[j]); g[4 + j] = __uint_as_float(g1[j]); }
-      }
+      unpack(gv[it], g);
       if (a.gate_mode == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(g[j]);
@@ -159,38 +188,13 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
     if (a.res && n < a.rcols) {
       float rv[8];
-      const uint32_t off = (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ);
-      if constexpr (SZ == 2) {
-        u32x4 rr4 = buf_load16(rr, off);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          rv[2 * j] = bf16_to_f32(rr4[j] & 0xffff);
-          rv[2 * j + 1] = bf16_to_f32(rr4[j] >> 16);
-        }
-      } else {
-        u32x4 r0 = buf_load16(rr, off), r1 = buf_load16(rr, off + 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { rv[j] = __uint_as_float(r0[j]); rv[4 + j] = __uint_as_float(r1[j]); }
-      }
+      unpack(rv1[it], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = a.beta * rv[j] + v[j];
     }
     if (a.res2 && n < a.rcols) {
       float rv[8];
-      const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
-      const uint32_t off = (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * SZ);
-      if constexpr (SZ == 2) {
-        u32x4 rr4 = buf_load16(rr2, off);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          rv[2 * j] = bf16_to_f32(rr4[j] & 0xffff);
-          rv[2 * j + 1] = bf16_to_f32(rr4[j] >> 16);
-        }
-      } else {
-        u32x4 r0 = buf_load16(rr2, off), r1 = buf_load16(rr2, off + 16);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { rv[j] = __uint_as_float(r0[j]); rv[4 + j] = __uint_as_float(r1[j]); }
-      }
+      unpack(rv2[it], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rv[j] + v[j];
     }
@@ -215,6 +219,7 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
       *(f32x4*)((float*)a.y + dst) = f32x4{v[0], v[1], v[2], v[3]};
       *(f32x4*)((float*)a.y + dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
+  }
   }
 }
 
@@ -1281,6 +1286,224 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
       }
 }
 
+// ------------------------------------------------------------------------------------
+// Weight gradient, phase-interleaved 256x256 (co x ci) tile: the schedule of
+// conv3x3_fwd_pp_kernel applied to the per-tap GEMM over pixels.  Half-tiles are
+// [64 pixels][128 channels] images (256-B rows, 32-B-block swizzle, ds_read_b64_tr_b16
+// operand reads): A_h = dy channels co0 + h*128.., B_g = x channels ci0 + g*128.. at the
+// tap-shifted pixel.  Needs W % 64 == 0 (a 64-pixel K-step is one image-row segment, so
+// the tap's zero padding is a wave-uniform row test plus a per-lane column test and every
+// source offset is a scalar per-step base + a per-lane constant) and Cout, Cin (and the
+// shuffle slot width) multiples of 128.  Output: fp32 slab tile staged through LDS and
+// written with 16-B row-contiguous stores.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
+  constexpr int STAGE = 65536;
+  constexpr int CSTR = 256 + 4;
+  constexpr int SMEM = 128 * CSTR * 4;
+  static_assert(SMEM >= 2 * STAGE, "LDS too small");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.taps * a.tiles_co * a.tiles_ci;
+  const int per_split = ntile + (a.wsb ? a.tiles_co : 0);
+  const int split = (int)b / per_split;
+  int rem = (int)b - split * per_split;
+  if (rem >= ntile) {
+    wgrad_bias_role(a, smem, split, (rem - ntile) * 256);
+    return;
+  }
+  const int tap = rem / (a.tiles_co * a.tiles_ci);
+  rem -= tap * a.tiles_co * a.tiles_ci;
+  const int co0 = (rem / a.tiles_ci) * 256;
+  const int ci0 = (rem % a.tiles_ci) * 256;
+  const int etap = tap + a.tap0;
+  const int dy_ = etap / 3 - 1, dx_ = etap % 3 - 1;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const int rps = a.out_ps > 0 ? a.out_ps : 1;
+
+  // DMA rows of this lane: R_j = 8w + 4j + (lane >> 4), 16-B slot lane & 15 holding the
+  // logical chunk lc_j of the swizzled 256-B row.
+  int Rj[2];
+  uint32_t la[2], lb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int R = 8 * w + 4 * j + (lane >> 4);
+    const int f = (R & 3) | (((R >> 3) & 1) << 2);
+    const int sl = lane & 15;
+    const int lc = (((sl >> 1) ^ f) << 1) | (sl & 1);
+    Rj[j] = R;
+    la[j] = (uint32_t)(R * rps * a.ldy) * 2u + (uint32_t)lc * 16u;
+    lb[j] = (uint32_t)(R * a.ldx) * 2u + (uint32_t)lc * 16u;
+  }
+
+  // scalar state of the K-step being issued
+  int s_ua0 = 0, s_ua1 = 0, s_ub = 0, s_x0 = 0, s_left = 0, s_yv = 0;
+  auto k_eval = [&](int ks) {
+    const int p0s = p_begin + ks * 64;
+    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
+    const int x0 = p0s - q * a.W;
+    const int n = (int)fdiv((uint32_t)q, a.fd_H);
+    const int y = q - n * a.H;
+    int ua[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cu = co0 + h * 128;
+      if (a.out_ps == 0) {
+        ua[h] = (p0s * a.ldy + a.ycoff + cu) * 2;
+      } else {
+        const int r = a.out_ps;
+        const int sl = (int)fdiv((uint32_t)cu, a.fd_cps);
+        const int cch = cu - sl * a.fd_cps.d;
+        const int si = sl / r, sj = sl - si * r;
+        ua[h] = (((q * r + si) * (a.W * r) + x0 * r + sj) * a.ldy + a.ycoff + cch) * 2;
+      }
+    }
+    s_ua0 = __builtin_amdgcn_readfirstlane(ua[0]);
+    s_ua1 = __builtin_amdgcn_readfirstlane(ua[1]);
+    s_ub = __builtin_amdgcn_readfirstlane((((q + dy_) * a.W + x0 + dx_) * a.ldx + a.xcoff + ci0) * 2);
+    s_x0 = __builtin_amdgcn_readfirstlane(x0 + dx_);
+    s_left = __builtin_amdgcn_readfirstlane(p_end - p0s);
+    s_yv = __builtin_amdgcn_readfirstlane((unsigned)(y + dy_) < (unsigned)a.H ? 1 : 0);
+  };
+  constexpr uint32_t SLOT_A0 = 0, SLOT_A1 = 16384, SLOT_B0 = 32768, SLOT_B1 = 49152;
+  auto issue_a = [&](int ks, int h) {
+    char* dst = smem + (ks & 1) * STAGE + (h ? SLOT_A1 : SLOT_A0) + w * 2048;
+    const uint32_t ua = (uint32_t)(h ? s_ua1 : s_ua0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(dyr, dst + j * 1024, Rj[j] < s_left ? ua + la[j] : SR_OOB);
+  };
+  auto issue_b = [&](int ks, int g) {
+    char* dst = smem + (ks & 1) * STAGE + (g ? SLOT_B1 : SLOT_B0) + w * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool v = s_yv && Rj[j] < s_left && (unsigned)(s_x0 + Rj[j]) < (unsigned)a.W;
+      glds16(xr, dst + j * 1024, v ? (uint32_t)s_ub + (uint32_t)g * 256u + lb[j] : SR_OOB);
+    }
+  };
+
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  s16x8 fa[2][4], fb[2][2][2];  // fa[kk][i] (current A half), fb[g][kk][j]
+  auto tr8 = [&](const char* base, int r0, int col) -> s16x8 {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0, col * 2, 256)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0 + 4, col * 2, 256)));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto read_a = [&](int buf, int h) {
+    const char* As = smem + buf * STAGE + (h ? SLOT_A1 : SLOT_A0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[kk][i] = tr8(As, kk * 32 + 8 * tg + tq, wr * 64 + i * 16 + 4 * tp);
+  };
+  auto read_b = [&](int buf, int g) {
+    const char* Bs = smem + buf * STAGE + (g ? SLOT_B1 : SLOT_B0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[g][kk][j] = tr8(Bs, kk * 32 + 8 * tg + tq, wc * 32 + j * 16 + 4 * tp);
+  };
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int h, int g) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[h][g][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[g][kk][j], acc[h][g][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = (p_end - p_begin + 63) / 64;  // >= 1 (every split owns >= 1 pixel)
+  k_eval(0);
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(0, 1);
+  issue_a(0, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  pp_barrier();
+  if (wr) pp_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more = t + 1 < nk;
+    read_a(buf, 0);
+    read_b(buf, 0);
+    if (more) {
+      k_eval(t + 1);
+      issue_a(t + 1, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    pp_barrier();
+    mma(0, 0);
+    pp_barrier();
+    read_b(buf, 1);
+    if (more) {
+      issue_b(t + 1, 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    mma(0, 1);
+    pp_barrier();
+    read_a(buf, 1);
+    if (more) issue_b(t + 1, 1);
+    pp_barrier();
+    mma(1, 1);
+    pp_barrier();
+    if (more) {
+      issue_a(t + 1, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    pp_barrier();
+    mma(1, 0);
+    pp_barrier();
+  }
+  if (!wr) pp_barrier();
+
+  float* ws = a.ws + ((size_t)split * a.taps + tap) * a.Cout * a.Cin;
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CSTR + g * 128 + wc * 32 + j * 16 + (lane & 15)] =
+                acc[h][g][i][j][r];
+    __syncthreads();
+    for (int idx = tid; idx < 128 * 64; idx += 512) {
+      const int row = idx >> 6, c4 = (idx & 63) * 4;
+      const int co = co0 + h * 128 + row, ci = ci0 + c4;
+      if (co < a.Cout && ci < a.Cin) *(f32x4*)(ws + (size_t)co * a.Cin + ci) = *(const f32x4*)(Cs + row * CSTR + c4);
+    }
+  }
+}
+
 // dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co' = GEMM column of co (out_ps
 // permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
@@ -1316,6 +1539,48 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
     float s = 0.f;
     for (int k = 0; k < S; ++k) s += wsb[(size_t)k * Cout + cop];
     db[co] = s * scale;
+  }
+}
+
+// Vectorised slab reduction (no ci_map, Cin_real % 4 == 0): one thread per (tap, co, 4 ci),
+// S independent 16-B loads (coalesced along ci) in flight per thread; bias sums by the
+// first Cout_real threads.  Same summation order over splits as wgrad_reduce_kernel.
+__global__ void wgrad_reduce4_kernel(const float* ws, const float* wsb, float* dw, float* db, int S, int Cout,
+                                     int Cin, int Cout_real, int Cin_real, int out_ps, int taps, const int* co_map,
+                                     float scale) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
+  const int cps = Cout_real / r2;
+  const int c4n = Cin_real >> 2;
+  const int64_t total = (int64_t)taps * Cout_real * c4n;
+  if (i < total) {
+    const int ci4 = (int)(i % c4n);
+    const int64_t t2 = i / c4n;
+    const int co = (int)(t2 % Cout_real);
+    const int tap = (int)(t2 / Cout_real);
+    const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
+    const size_t stride = (size_t)taps * Cout * Cin;
+    const float* src = ws + ((size_t)tap * Cout + cop) * Cin + ci4 * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 4 <= S; k += 4) {
+      const f32x4 v0 = *(const f32x4*)(src + (size_t)k * stride);
+      const f32x4 v1 = *(const f32x4*)(src + (size_t)(k + 1) * stride);
+      const f32x4 v2 = *(const f32x4*)(src + (size_t)(k + 2) * stride);
+      const f32x4 v3 = *(const f32x4*)(src + (size_t)(k + 3) * stride);
+      acc += v0; acc += v1; acc += v2; acc += v3;
+    }
+    for (; k < S; ++k) acc += *(const f32x4*)(src + (size_t)k * stride);
+    float* d = dw + ((size_t)co * Cin_real + ci4 * 4) * taps + tap;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = acc[e] * scale;
+  }
+  if (db && i < Cout_real) {
+    const int co = (int)i;
+    const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
+    float sb = 0.f;
+    for (int k = 0; k < S; ++k) sb += wsb[(size_t)k * Cout + cop];
+    db[co] = sb * scale;
   }
 }
 
@@ -1429,6 +1694,14 @@ bool wg_use_big(const sr_conv3x3_wgrad_desc* d) {
   return d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && d->in_up <= 1 && !g_disable_big;
 }
 
+// Phase-interleaved wgrad kernel: W a multiple of 64, channel counts (and the pixel-shuffle
+// slot width) multiples of 128.
+bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
+  if (!wg_use_big(d) || g_variant == 2) return false;
+  const int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 128;
+  return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
+}
+
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
 // 256x256 kernel, ~2 rounds for the small ones), pixels per split a multiple of 64.
 void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
@@ -1533,12 +1806,13 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
 }
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
+  if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
 }
 
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
-// 2 = the two-barrier 256x256 forward kernel instead of the phase-interleaved one.
+// 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
   if (variant < 0 || variant > 2) return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1 or 2");
   g_variant = variant;
@@ -1594,7 +1868,10 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.tiles_co = (a.Cout + 255) / 256;
     a.tiles_ci = (a.Cin + 255) / 256;
     const int per_split = taps * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
-    hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
+    if (wg_use_pp(d))
+      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel, dim3(S * per_split), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
     e = hipGetLastError();
   } else {
     e = d->dtype == SR_BF16 ? dispatch_wg<bf16_t>(a, s) : dispatch_wg<float>(a, s);
@@ -1604,9 +1881,17 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t work = total > Cout_real ? total : Cout_real;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
-                     (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
-                     Cin_real, d->out_ps, taps, co_map, ci_map, d->scale);
+  if (!ci_map && Cin_real % 4 == 0) {
+    const int64_t work4 = (int64_t)taps * Cout_real * (Cin_real / 4);
+    const int64_t w4 = work4 > Cout_real ? work4 : Cout_real;
+    hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)((w4 + 255) / 256)), dim3(256), 0, s, (const float*)a.ws,
+                       (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map,
+                       d->scale);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                       (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
+                       Cin_real, d->out_ps, taps, co_map, ci_map, d->scale);
+  }
   return sr_check(hipGetLastError(), "conv3x3_wgrad reduce launch");
 }
 

@@ -186,10 +186,12 @@ def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
 
 
 @pytest.mark.parametrize('shape', [(2, 16, 16, 256, 256, 0), (1, 20, 12, 512, 256, 0), (2, 9, 14, 256, 768, 0),
-                                   (1, 8, 12, 256, 1024, 2)])
-@pytest.mark.parametrize('variant', [0, 1])
+                                   (1, 8, 12, 256, 1024, 2), (1, 3, 64, 256, 256, 0), (2, 3, 128, 256, 1024, 2),
+                                   (1, 5, 64, 384, 256, 0)])
+@pytest.mark.parametrize('variant', [0, 1, 2])
 def test_wgrad_bf16_vs_fp64(cuda, shape, variant):
-    """Weight/bias gradient (256x256 LDS-DMA kernel = variant 0, small kernel = variant 1)
+    """Weight/bias gradient (256x256 LDS-DMA kernels: phase-interleaved = variant 0 where
+    W % 64 == 0, two-barrier = variant 2; small kernel = variant 1)
     against an fp64 CPU reference on the same bf16-rounded operands; |err| <= 1e-2*|ref|max."""
     N, H, W, cin, cout, ps = shape
     torch.manual_seed(5)
@@ -215,3 +217,25 @@ def test_wgrad_bf16_vs_fp64(cuda, shape, variant):
     assert rel_err(dw.cpu().double(), w.grad) < 1e-2 * max(1.0, w.grad.abs().max().item()) / max(1.0, w.grad.abs().max().item())
     assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize('shape', [(2, 4, 64, 256, 256, 0), (1, 3, 128, 256, 1024, 2), (1, 7, 64, 256, 512, 0)])
+def test_wgrad_pp_bitwise_equals_big(cuda, shape):
+    """The phase-interleaved wgrad kernel sums each pixel K-step in the same order as the
+    two-barrier 256x256 kernel (same splits, same MFMA chain): slabs, dW and db bitwise equal."""
+    N, H, W, cin, cout, ps = shape
+    torch.manual_seed(11)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    dy = torch.randn(N, H * max(ps, 1), W * max(ps, 1), cout // max(ps * ps, 1), device=cuda).to(dt)
+    outs = []
+    try:
+        for variant in (0, 2):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            outs.append(C.conv_wgrad_raw(dy, x, N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
