@@ -140,6 +140,162 @@ __global__ void ln_bwd_reduce(const float* __restrict__ partial, int nw, int C, 
   (which ? dbeta : dgamma)[c] = s;
 }
 
+// Vectorised bf16 LayerNorm for padded widths Cp <= 256 (SwinIR embed 60..180): half a
+// wave per row, lane hl = lane & 31 holds channels 8*hl .. 8*hl+7 (one 16-B load), so a
+// wave covers 2 rows per iteration; statistics by 32-lane butterflies.
+SR_DEV float hsum32(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+
+SR_DEV void unpack8(const u32x4& q, float* o) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[2 * j] = bf16_to_f32(q[j] & 0xffff);
+    o[2 * j + 1] = bf16_to_f32(q[j] >> 16);
+  }
+}
+
+SR_DEV u32x4 pack8(const float* v) {
+  u32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+  return o;
+}
+
+__global__ __launch_bounds__(256) void ln_fwd8_kernel(const bf16_t* __restrict__ x, int ldx, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, int64_t M, int C, int Cp, float eps,
+                                                      bf16_t* __restrict__ y, int ldy, float* __restrict__ mean_out,
+                                                      float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int c0 = hl * 8;
+  float gm[8], bt[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gm[j] = c0 + j < C ? gamma[c0 + j] : 0.f;
+    bt[j] = c0 + j < C ? beta[c0 + j] : 0.f;
+  }
+  const int64_t nrw = (int64_t)gridDim.x * 8;
+  for (int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); row < M; row += nrw) {
+    float v[8];
+    if (c0 < Cp) {
+      unpack8(*(const u32x4*)(x + row * ldx + c0), v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c0 + j >= C) v[j] = 0.f;
+      sm += v[j];
+    }
+    const float mu = hsum32(sm) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = c0 + j < C ? v[j] - mu : 0.f;
+      q += d * d;
+    }
+    const float rs = rsqrtf(hsum32(q) / C + eps);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = c0 + j < C ? (v[j] - mu) * rs * gm[j] + bt[j] : 0.f;
+    if (c0 < Cp) *(u32x4*)(y + row * ldy + c0) = pack8(o);
+    if (hl == 0) {
+      mean_out[row] = mu;
+      rstd_out[row] = rs;
+    }
+  }
+}
+
+// Backward, same mapping; per-block dgamma / dbeta partials (LDS-combined over the block's
+// 8 row slots) -> partial[block][2][C], summed by ln_bwd_reduce8.
+__global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16_t* __restrict__ dy, int lddy, const bf16_t* __restrict__ x,
+                                                      int ldx, const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                      int64_t M, int C, int Cp, const bf16_t* __restrict__ res, int ldr,
+                                                      bf16_t* __restrict__ dx, int lddx, float* __restrict__ partial) {
+  __shared__ float red[8][2][256];
+  const int lane = threadIdx.x & 63, hl = lane & 31, slot = threadIdx.x >> 5;
+  const int c0 = hl * 8;
+  float gm[8], dg[8], db[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gm[j] = c0 + j < C ? gamma[c0 + j] : 0.f;
+    dg[j] = db[j] = 0.f;
+  }
+  const int64_t nrw = (int64_t)gridDim.x * 8;
+  for (int64_t row = (int64_t)blockIdx.x * 8 + slot; row < M; row += nrw) {
+    const float mu = mean[row], rs = rstd[row];
+    float d[8], xv[8], rv[8];
+    if (c0 < Cp) {
+      unpack8(*(const u32x4*)(dy + row * lddy + c0), d);
+      unpack8(*(const u32x4*)(x + row * ldx + c0), xv);
+      if (res) unpack8(*(const u32x4*)(res + row * ldr + c0), rv);
+    }
+    float xh[8], g[8], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c0 + j < C) {
+        xh[j] = (xv[j] - mu) * rs;
+        g[j] = d[j] * gm[j];
+        dg[j] += d[j] * xh[j];
+        db[j] += d[j];
+      } else {
+        xh[j] = g[j] = 0.f;
+      }
+      s1 += g[j];
+      s2 += g[j] * xh[j];
+    }
+    s1 = hsum32(s1) / C;
+    s2 = hsum32(s2) / C;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = c0 + j < C ? rs * (g[j] - s1 - xh[j] * s2) : 0.f;
+      if (res && c0 + j < C) o[j] += rv[j];
+    }
+    if (c0 < Cp) *(u32x4*)(dx + row * lddx + c0) = pack8(o);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[slot][0][c0 + j] = dg[j];
+    red[slot][1][c0 + j] = db[j];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * C; i += 256) {
+    const int which = i / C, c = i - which * C;
+    float sm = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sm += red[k][which][c];
+    partial[((size_t)blockIdx.x * 2 + which) * C + c] = sm;
+  }
+}
+
+// dgamma / dbeta = sum over nb block partials: 64 columns per block, 16 waves split the
+// partial rows, LDS combine.
+__global__ __launch_bounds__(1024) void ln_bwd_reduce8(const float* __restrict__ partial, int nb, int C,
+                                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[16][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
+  float sm = 0.f;
+  if (col < 2 * C) {
+    const int which = col / C, c = col - which * C;
+    for (int b = wv; b < nb; b += 16) sm += partial[((size_t)b * 2 + which) * C + c];
+  }
+  red[wv][threadIdx.x & 63] = sm;
+  __syncthreads();
+  if (wv == 0 && col < 2 * C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+    const int which = col / C, c = col - which * C;
+    (which ? dbeta : dgamma)[c] = t;
+  }
+}
+
 // ---------------------------------------------------------------- window attention
 struct AttnArgs {
   const void* qkv;
@@ -371,6 +527,11 @@ bool attn_setup(AttnArgs& a, int N, int H, int W, int ws, int shift, int nH, int
 
 }  // namespace
 
+namespace {
+constexpr int LN_BWD_BLOCKS = 512;
+bool ln_vec8(int Cp, int ld1, int ld2) { return Cp <= 256 && Cp % 8 == 0 && ld1 % 8 == 0 && ld2 % 8 == 0; }
+}  // namespace
+
 extern "C" {
 
 int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, const float* beta, int64_t M, int C, int Cp,
@@ -378,7 +539,11 @@ int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, cons
   if (!x || !gamma || !beta || !y || !mean || !rstd || C > 512 || Cp < C) return sr_fail(SR_EINVAL, "layernorm_fwd: bad arguments");
   const unsigned grid = (unsigned)((M + 3) / 4 < 16384 ? (M + 3) / 4 : 16384);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == SR_BF16)
+  if (dtype == SR_BF16 && ln_vec8(Cp, ldx, ldy)) {
+    const unsigned g8 = (unsigned)((M + 7) / 8 < 4096 ? (M + 7) / 8 : 4096);
+    hipLaunchKernelGGL(ln_fwd8_kernel, dim3(g8), dim3(256), 0, s, (const bf16_t*)x, ldx, gamma, beta, M, C, Cp, eps,
+                       (bf16_t*)y, ldy, mean, rstd);
+  } else if (dtype == SR_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, ldx, gamma, beta, M, C, Cp,
                        eps, (bf16_t*)y, ldy, mean, rstd);
   else
@@ -400,6 +565,14 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
   if (ws_bytes < sr_layernorm_bwd_workspace(M, C)) return sr_fail(SR_EINVAL, "layernorm_bwd: workspace too small");
   const unsigned grid = (unsigned)((M + 3) / 4 < 2048 ? (M + 3) / 4 : 2048);
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16 && ln_vec8(Cp, ldx, lddx) && lddy % 8 == 0 && (!res || ldr % 8 == 0)) {
+    const unsigned g8 = (unsigned)((M + 7) / 8 < LN_BWD_BLOCKS ? (M + 7) / 8 : LN_BWD_BLOCKS);
+    hipLaunchKernelGGL(ln_bwd8_kernel, dim3(g8), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
+                       rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
+    hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 63) / 64), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
+                       dgamma, dbeta);
+    return sr_check(hipGetLastError(), "layernorm_bwd launch");
+  }
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx,
                        mean, rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);

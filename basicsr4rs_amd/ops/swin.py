@@ -18,6 +18,7 @@ drop_path_rate 0 / eval (parity mode); SURVEY.md §0.7.
 import torch
 
 from .. import _lib
+from ..utils import ktrace
 from . import conv as C
 
 GELU = 3
@@ -116,10 +117,11 @@ def layernorm(x, weight, bias, Creal, eps=1e-5):
     mean = torch.empty(M, device=x.device, dtype=torch.float32)
     rstd = torch.empty(M, device=x.device, dtype=torch.float32)
     lib = _lib.load()
-    _lib.check(
-        lib.sr_layernorm_fwd(_lib.dtype_code(x.dtype), _lib.ptr(x), Cp, _lib.ptr(weight.detach()),
-                             _lib.ptr(bias.detach()), M, Creal, Cp, float(eps), _lib.ptr(y), Cp, _lib.ptr(mean),
-                             _lib.ptr(rstd), _lib.stream()))
+    with ktrace.span('ln_fwd_kernel', 0.0, 2.0 * M * Creal * x.element_size()):
+        _lib.check(
+            lib.sr_layernorm_fwd(_lib.dtype_code(x.dtype), _lib.ptr(x), Cp, _lib.ptr(weight.detach()),
+                                 _lib.ptr(bias.detach()), M, Creal, Cp, float(eps), _lib.ptr(y), Cp, _lib.ptr(mean),
+                                 _lib.ptr(rstd), _lib.stream()))
     return y, mean, rstd
 
 
@@ -132,11 +134,12 @@ def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None):
     lib = _lib.load()
     wsb = lib.sr_layernorm_bwd_workspace(M, Creal)
     ws = torch.empty(wsb // 4 + 1, device=x.device, dtype=torch.float32)
-    _lib.check(
-        lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
-                             _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res),
-                             res.shape[-1] if res is not None else 0, _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db),
-                             _lib.ptr(ws), wsb, _lib.stream()))
+    with ktrace.span('ln_bwd_kernel', 0.0, (4.0 if res is not None else 3.0) * M * Creal * x.element_size()):
+        _lib.check(
+            lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
+                                 _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res),
+                                 res.shape[-1] if res is not None else 0, _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db),
+                                 _lib.ptr(ws), wsb, _lib.stream()))
     return dx, dg, db
 
 
@@ -170,14 +173,23 @@ class AttnGeom:
         self.proj = proj_spec(dim, nH, hdp)
 
 
+def attn_flops(g, N, H, W):
+    """Algorithmic FLOPs of one window-attention forward: QK^T and AV per (window, head),
+    2 * 2 * n^2 * head_dim with n = ws^2 tokens (head_dim unpadded)."""
+    n = g.ws * g.ws
+    units = N * (H // g.ws) * (W // g.ws) * g.nH
+    return 4.0 * units * n * n * g.hd
+
+
 def window_attn(qkv, g, N, H, W, scale, table):
     out = torch.empty(N, H, W, g.nH * g.hdp, device=qkv.device, dtype=qkv.dtype)
     lse = torch.empty(N * (H // g.ws) * (W // g.ws) * g.nH * g.ws * g.ws, device=qkv.device, dtype=torch.float32)
     lib = _lib.load()
-    _lib.check(
-        lib.sr_window_attn_fwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], N, H, W, g.ws, g.shift, g.nH,
-                               g.hd, g.hdp, float(scale), _lib.ptr(table), _lib.ptr(out), out.shape[-1], _lib.ptr(lse),
-                               _lib.stream()))
+    with ktrace.span('wattn_fwd_kernel', attn_flops(g, N, H, W), 4.0 * N * H * W * g.dim * qkv.element_size()):
+        _lib.check(
+            lib.sr_window_attn_fwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], N, H, W, g.ws, g.shift, g.nH,
+                                   g.hd, g.hdp, float(scale), _lib.ptr(table), _lib.ptr(out), out.shape[-1], _lib.ptr(lse),
+                                   _lib.stream()))
     return out, lse
 
 
@@ -187,10 +199,11 @@ def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table):
     lib = _lib.load()
     wsb = lib.sr_window_attn_bwd_workspace(N, H, W, g.ws, g.nH)
     ws = torch.empty(wsb // 4 + 1, device=qkv.device, dtype=torch.float32)
-    _lib.check(
-        lib.sr_window_attn_bwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], _lib.ptr(out), _lib.ptr(dout),
-                               out.shape[-1], _lib.ptr(lse), N, H, W, g.ws, g.shift, g.nH, g.hd, g.hdp, float(scale),
-                               _lib.ptr(table), _lib.ptr(dqkv), _lib.ptr(dtable), _lib.ptr(ws), wsb, _lib.stream()))
+    with ktrace.span('wattn_bwd_kernel', 2.5 * attn_flops(g, N, H, W), 9.0 * N * H * W * g.dim * qkv.element_size()):
+        _lib.check(
+            lib.sr_window_attn_bwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], _lib.ptr(out), _lib.ptr(dout),
+                                   out.shape[-1], _lib.ptr(lse), N, H, W, g.ws, g.shift, g.nH, g.hd, g.hdp, float(scale),
+                                   _lib.ptr(table), _lib.ptr(dqkv), _lib.ptr(dtable), _lib.ptr(ws), wsb, _lib.stream()))
     return dqkv, dtable
 
 

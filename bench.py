@@ -7,6 +7,8 @@ backward, gradient all-reduce (N>1, RCCL), fused Adam(0.9, 0.99) + EMA(0.999).  
 are synthetic U[0,1) tiles already resident in HBM (seed 0 / 1, + rank).
 
 Run: python bench.py --gpus N --steps K --warmup W   (N>1 under torch.distributed.run).
+`--workload` selects another BASELINE.json config in the same HR-pixels/s unit (rcan = C3,
+swinir = C4, rrdb = C5); the default (edsr = C2) is the north-star line.
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events over
 the timed region) and the CPU baseline (oracle restatement on the host cores, bounded
 sample, rank 0 at N=1).
@@ -31,12 +33,33 @@ EDSR_L = dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=256, num_block=32
               img_range=255., rgb_mean=[0.4488, 0.4371, 0.4040])
 
 
-def make_opt(world, batch):
+RCAN_X4 = dict(type='RCAN', num_in_ch=3, num_out_ch=3, num_feat=64, num_group=10, num_block=20, squeeze_factor=16,
+               upscale=4, res_scale=1, img_range=255., rgb_mean=[0.4488, 0.4371, 0.4040])
+SWINIR_M = dict(type='SwinIR', upscale=4, in_chans=3, img_size=64, window_size=8, img_range=1.,
+                depths=[6, 6, 6, 6, 6, 6], embed_dim=180, num_heads=[6, 6, 6, 6, 6, 6], mlp_ratio=2,
+                upsampler='pixelshuffle', resi_connection='1conv')
+RRDB_X4 = dict(type='RRDBNet', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=23, num_grow_ch=32, scale=4)
+
+# workload -> (network, model_type, lr, per-GPU batch, LR tile, train FLOPs per HR pixel, label)
+WORKLOADS = {
+    'edsr': (EDSR_L, 'SRModel', 1e-4, 32, 64, 18.85e6,
+             'EDSR_Lx4 train step (32 RB, nf 256, res_scale 0.1), LR 64x64 -> HR 256x256'),
+    'rcan': (RCAN_X4, 'SRModel', 1e-4, 32, 64, 5.97e6,
+             'RCAN x4 train step (10 groups x 20 RCAB, nf 64, squeeze 16), LR 64x64 -> HR 256x256'),
+    'swinir': (SWINIR_M, 'SwinIRModel', 2e-4, 32, 64, 4.90e6,
+               'SwinIR-M x4 classical-SR train step (embed 180, 6x6 STB, 6 heads, window 8), LR 64x64 -> HR 256x256'),
+    'rrdb': (RRDB_X4, 'SRModel', 1e-4, 16, 128, 6.72e6,
+             'RRDBNet x4 train step (nf 64, gc 32, 23 RRDB), LR 128x128 -> HR 512x512 (remote-sensing tile)'),
+}
+
+
+def make_opt(world, batch, workload='edsr'):
+    net, mtype, lr = WORKLOADS[workload][:3]
     return dict(
-        model_type='SRModel', is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
-        network_g=dict(EDSR_L),
+        model_type=mtype, is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
+        network_g=dict(net),
         train=dict(ema_decay=0.999, use_amp=True,
-                   optim_g=dict(type='Adam', lr=1e-4, weight_decay=0, betas=[0.9, 0.99]),
+                   optim_g=dict(type='Adam', lr=lr, weight_decay=0, betas=[0.9, 0.99]),
                    scheduler=dict(type='MultiStepLR', milestones=[200000], gamma=0.5),
                    pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')),
         path={})
@@ -81,7 +104,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (0: the workload default)')
+    ap.add_argument('--workload', default='edsr', choices=sorted(WORKLOADS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-trace', action='store_true')
     args = ap.parse_args()
@@ -101,14 +125,17 @@ def main():
     from basicsr4rs_amd.utils import ktrace
 
     torch.manual_seed(42)
-    opt = make_opt(world, args.batch)
+    wl = WORKLOADS[args.workload]
+    B = args.batch or wl[3]
+    lr_px = wl[4]
+    hr_px_tile = (4 * lr_px) ** 2
+    opt = make_opt(world, B, args.workload)
     opt['rank'] = rank
     model = build_model(opt)
-    B = args.batch
     g0 = torch.Generator(device=dev).manual_seed(0 + rank)
     g1 = torch.Generator(device=dev).manual_seed(1 + rank)
-    lq = torch.rand(B, 3, 64, 64, generator=g0, device=dev)
-    gt = torch.rand(B, 3, 256, 256, generator=g1, device=dev)
+    lq = torch.rand(B, 3, lr_px, lr_px, generator=g0, device=dev)
+    gt = torch.rand(B, 3, 4 * lr_px, 4 * lr_px, generator=g1, device=dev)
     model.feed_data({'lq': lq, 'gt': gt})
 
     it = 0
@@ -137,26 +164,33 @@ def main():
         dt = t.item()
     loss = model.get_current_log().get('l_pix', float('nan'))
 
-    hr_px = world * B * 256 * 256 * args.steps
+    hr_px = world * B * hr_px_tile * args.steps
     value = hr_px / dt
     roof = None
     if kstats:
         name, st = max(kstats.items(), key=lambda kv: kv[1]['ms'])
         avg_ms = st['ms'] / st['count']
-        achieved = st['flops'] / (st['ms'] * 1e-3) / 1e12
-        roof = {'bound': 'mfma', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS,
-                'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None,
-                'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // args.steps,
-                'flops_per_launch': st['flops'] / st['count'],
-                'share_of_step': round(st['ms'] * 1e-3 / dt, 3)}
+        if st['flops'] > 0:
+            achieved = st['flops'] / (st['ms'] * 1e-3) / 1e12
+            roof = {'bound': 'mfma', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS,
+                    'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+                    'flops_per_launch': st['flops'] / st['count']}
+        else:
+            achieved = st['bytes'] / (st['ms'] * 1e-3) / 1e9
+            roof = {'bound': 'hbm', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS,
+                    'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
+                    'bytes_per_launch': st['bytes'] / st['count']}
+        roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // args.steps,
+                     'share_of_step': round(st['ms'] * 1e-3 / dt, 3)})
         roof['kernels'] = {
             k: {'count': v['count'] // args.steps, 'avg_us': round(v['ms'] / v['count'] * 1e3, 1),
-                'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 else None,
+                'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 and v['flops'] else None,
+                'gbs': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] > 0 and not v['flops'] else None,
                 'ms_per_step': round(v['ms'] / args.steps, 3)}
             for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]['ms'])
         }
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == 'edsr':
         cpu = cpu_baseline()
     if rank == 0:
         line = {
@@ -164,10 +198,9 @@ def main():
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
             'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
-            'config': {'workload': 'EDSR_Lx4 train step (32 RB, nf 256, res_scale 0.1), LR 64x64 -> HR 256x256',
-                       'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None, 'parallelism': f'dp{world}',
-                       'model': 'EDSR_Lx4'},
-            'train_flops_per_hr_px': 18.85e6, 'model_tflops': round(18.85e6 * value / 1e12, 1),
+            'config': {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
+                       'parallelism': f'dp{world}', 'model': wl[0]['type']},
+            'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
             'last_loss': loss, 'roofline': roof, 'cpu_baseline': cpu,
         }
         print(json.dumps(line))

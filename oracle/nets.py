@@ -232,6 +232,34 @@ def window_attention(xw, sd, p, nH, ws, mask):
     return _linear(out, sd, f'{p}.proj')
 
 
+def window_attention_core(qkv, nH, ws, shift, scale, table):
+    """The attention core of SwinTransformerBlock + WindowAttention between the qkv Linear
+    and the proj Linear (swinir_arch.py:288-314 roll / partition / reverse, :151-172
+    scale, q k^T, relative bias, shift mask, softmax, attn @ v), on a token map.
+    qkv: [b, h, w, 3*C] with channel order [3][nH][hd] (swinir_arch.py:151); returns the
+    head-concatenated output [b, h, w, C] (channel h*hd + d, :172) at the un-shifted pixels."""
+    b, h, w, c3 = qkv.shape
+    c = c3 // 3
+    hd = c // nH
+    t = qkv
+    if shift > 0:
+        t = torch.roll(t, shifts=(-shift, -shift), dims=(1, 2))
+    tw = window_partition(t, ws).view(-1, ws * ws, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = tw[0] * scale, tw[1], tw[2]
+    n = ws * ws
+    attn = q @ k.transpose(-2, -1)
+    attn = attn + table[rel_index(ws).reshape(-1)].view(n, n, -1).permute(2, 0, 1).unsqueeze(0)
+    if shift > 0:
+        mask = swin_mask(h, w, ws, shift).to(attn.dtype)
+        nw = mask.shape[0]
+        attn = (attn.view(-1, nw, nH, n, n) + mask.unsqueeze(1).unsqueeze(0)).view(-1, nH, n, n)
+    out = (attn.softmax(-1) @ v).transpose(1, 2).reshape(-1, ws, ws, c)
+    t = window_reverse(out, ws, h, w)
+    if shift > 0:
+        t = torch.roll(t, shifts=(shift, shift), dims=(1, 2))
+    return t
+
+
 def swin_block(x, sd, p, hw, nH, ws, shift):
     """SwinTransformerBlock.forward in eval mode (swinir_arch.py:283-323), DropPath = identity."""
     h, w = hw

@@ -105,3 +105,26 @@ def test_oracle_reproduces_golden(name):
     out = run_case(CASES[name], {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith('sd.')},
                    torch.from_numpy(z['x']))
     assert np.allclose(out.numpy(), z['y'], rtol=1e-5, atol=1e-5)
+
+
+def test_window_attention_core_matches_block_path():
+    """oracle.window_attention_core (token-map form used by the op-level GPU tests) equals the
+    reference-structured path: roll -> window_partition -> WindowAttention -> reverse -> roll."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    b, h, w, nH, hd, ws = 2, 16, 16, 3, 8, 8
+    C = nH * hd
+    sd = {'a.qkv.weight': torch.randn(3 * C, C) * 0.2, 'a.qkv.bias': torch.randn(3 * C) * 0.1,
+          'a.proj.weight': torch.eye(C), 'a.proj.bias': torch.zeros(C),
+          'a.relative_position_bias_table': torch.randn((2 * ws - 1)**2, nH)}
+    x = torch.randn(b, h, w, C, dtype=torch.float64)
+    sd = {k: v.double() for k, v in sd.items()}
+    for shift in (0, 4):
+        t = torch.roll(x, (-shift, -shift), (1, 2)) if shift else x
+        tw = O.window_partition(t, ws).view(-1, ws * ws, C)
+        aw = O.window_attention(tw, sd, 'a', nH, ws, O.swin_mask(h, w, ws, shift).double() if shift else None)
+        r = O.window_reverse(aw.view(-1, ws, ws, C), ws, h, w)
+        r = torch.roll(r, (shift, shift), (1, 2)) if shift else r
+        core = O.window_attention_core(F.linear(x, sd['a.qkv.weight'], sd['a.qkv.bias']), nH, ws, shift, hd**-0.5,
+                                       sd['a.relative_position_bias_table'])
+        assert torch.allclose(core, r, atol=1e-10)

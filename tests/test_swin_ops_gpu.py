@@ -1,0 +1,82 @@
+"""Op-level parity of the SwinIR token kernels (csrc/swin.hip) against the oracle:
+LayerNorm fwd/bwd (bf16 vectorised and fp32 paths) and the fused shifted-window attention
+fwd/bwd (oracle.nets.window_attention_core, fp64 autograd) at the SwinIR-M geometry."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from basicsr4rs_amd.ops import swin as S
+from oracle import nets as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _pad_last(t, cp):
+    return F.pad(t, (0, cp - t.shape[-1]))
+
+
+@pytest.mark.parametrize('C,dtype', [(180, torch.bfloat16), (60, torch.bfloat16), (180, torch.float32),
+                                     (300, torch.bfloat16)])
+@pytest.mark.parametrize('with_res', [False, True])
+def test_layernorm_fwd_bwd(cuda, C, dtype, with_res):
+    torch.manual_seed(1)
+    N, H, W = 2, 7, 13  # odd row count: partial wave / block tails
+    Cp = (C + 7) // 8 * 8
+    x = (torch.randn(N, H, W, C) * 2 + 0.5).to(dtype)
+    dy = torch.randn(N, H, W, C).to(dtype)
+    res = torch.randn(N, H, W, C).to(dtype)
+    gw, gb = torch.randn(C) * 0.5 + 1, torch.randn(C) * 0.1
+    xd = x.double().requires_grad_()
+    gwd, gbd = gw.double().requires_grad_(), gb.double().requires_grad_()
+    ref = F.layer_norm(xd, (C, ), gwd, gbd, 1e-5)
+    ref.backward(dy.double())
+    y, mean, rstd = S.layernorm(_pad_last(x, Cp).to(cuda).contiguous(), gw.to(cuda), gb.to(cuda), C)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    assert (y[..., :C].double().cpu() - ref.detach()).abs().max().item() < tol * ref.abs().max().item()
+    assert y[..., C:].abs().max().item() == 0 if Cp > C else True
+    dx, dg, db = S.layernorm_bwd(_pad_last(dy, Cp).to(cuda).contiguous(), _pad_last(x, Cp).to(cuda).contiguous(), mean,
+                                 rstd, gw.to(cuda), C,
+                                 res=_pad_last(res, Cp).to(cuda).contiguous() if with_res else None)
+    want = xd.grad + (res.double() if with_res else 0)
+    assert (dx[..., :C].double().cpu() - want).abs().max().item() < tol * want.abs().max().item()
+    assert (dg.double().cpu() - gwd.grad).abs().max().item() < tol * gwd.grad.abs().max().item() + 1e-3
+    assert (db.double().cpu() - gbd.grad).abs().max().item() < tol * gbd.grad.abs().max().item() + 1e-3
+
+
+def _qkv_padded(qkv, nH, hd, hdp):
+    """[b,h,w,3*nH*hd] -> kernel layout [b,h,w,3*nH*hdp] (zero-padded heads)."""
+    b, h, w, _ = qkv.shape
+    return F.pad(qkv.view(b, h, w, 3, nH, hd), (0, hdp - hd)).reshape(b, h, w, 3 * nH * hdp)
+
+
+@pytest.mark.parametrize('shift', [0, 4])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('geom', [(2, 16, 24, 6, 30, 8), (1, 8, 8, 2, 16, 8), (1, 12, 12, 3, 20, 4)])
+def test_window_attention_fwd_bwd(cuda, shift, dtype, geom):
+    b, h, w, nH, hd, ws = geom
+    if shift >= ws // 2 + 1 or min(h, w) <= ws:
+        shift = 0 if min(h, w) <= ws else ws // 2
+    torch.manual_seed(2)
+    C = nH * hd
+    hdp = 32
+    scale = hd**-0.5
+    qkv = torch.randn(b, h, w, 3 * C).to(dtype)
+    table = torch.randn((2 * ws - 1)**2, nH) * 0.5
+    dout = torch.randn(b, h, w, C).to(dtype)
+    qd = qkv.double().requires_grad_()
+    td = table.double().requires_grad_()
+    ref = O.window_attention_core(qd, nH, ws, shift, scale, td)
+    ref.backward(dout.double())
+    g = S.AttnGeom(C, nH, ws, shift, hdp)
+    qp = _qkv_padded(qkv, nH, hd, hdp).to(cuda).contiguous()
+    out, lse = S.window_attn(qp, g, b, h, w, scale, table.to(cuda))
+    got = out.view(b, h, w, nH, hdp)[..., :hd].reshape(b, h, w, C).double().cpu()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert (got - ref.detach()).abs().max().item() < tol * max(1.0, ref.abs().max().item())
+    assert out.view(b, h, w, nH, hdp)[..., hd:].abs().max().item() == 0
+    dop = F.pad(dout.view(b, h, w, nH, hd), (0, hdp - hd)).reshape(b, h, w, nH * hdp).to(cuda).contiguous()
+    dqkv, dtab = S.window_attn_bwd(qp, out, dop, lse, g, b, h, w, scale, table.to(cuda))
+    dq = dqkv.view(b, h, w, 3, nH, hdp)[..., :hd].reshape(b, h, w, 3 * C).double().cpu()
+    gref = qd.grad
+    assert (dq - gref).abs().max().item() < tol * max(1.0, gref.abs().max().item())
+    assert (dtab.double().cpu() - td.grad).abs().max().item() < tol * max(1.0, td.grad.abs().max().item())
