@@ -564,7 +564,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
 
   // DMA rows of this lane inside a half-tile: w*16 + j*8 + (lane>>3), j = 0, 1.
   // Index k = h*2 + j (A: tile row h*128 + ...; B: output channel n0 + g*128 + ...).
-  // FAST (every 64-deep K-step inside one tap and one shuffle slot): the A source offset is
+  // FAST (every 64-deep K-step inside one tap and one shuffle slot, or a 1x1 conv): the A source offset is
   // a per-lane pixel base + a wave-uniform (tap, channel) offset computed on the scalar
   // unit, and the zero padding a per-lane 9-bit mask of valid taps -- the fragment-read /
   // DMA segment of a phase then carries ~3 VALU per DMA instead of the full gather math.
@@ -639,10 +639,11 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
   auto issue_a = [&](int ks, int h) {
     char* dst = smem + (ks & 1) * BIG_STAGE + (h ? SLOT_A1 : SLOT_A0) + w * 2048;
     if constexpr (FAST) {
+      const bool kv = c * 8 < a.Cin - k_chu;  // 1x1 convs: Cin need not fill the last step
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int k = h * 2 + j;
-        glds16(xr, dst + j * 1024, ((amask[k] >> k_tap) & 1u) ? abase[k] + (uint32_t)k_uoff : SR_OOB);
+        glds16(xr, dst + j * 1024, (kv && ((amask[k] >> k_tap) & 1u)) ? abase[k] + (uint32_t)k_uoff : SR_OOB);
       }
     } else {
       const int q = ks * 8 + c;
@@ -1633,7 +1634,7 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   a.tiles = tm * a.tiles_n;
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
-  else if (a.Cin % 64 == 0 && (a.in_ps == 0 || a.fd_cps.d % 64 == 0))
+  else if ((a.Cin % 64 == 0 || a.tap0 == 4) && (a.in_ps == 0 || a.fd_cps.d % 64 == 0))
     hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<true>, dim3(a.tiles), dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<false>, dim3(a.tiles), dim3(512), 0, s, a);

@@ -11,8 +11,9 @@
 //       the relative-position bias (:119-133, 157-160) is gathered from the [(2ws-1)^2, nH] table.
 //
 // qkv layout: per token row, [3][nH][hdp] with hdp >= head_dim (zero padded, 16-B aligned
-// heads); out layout [nH][hdp].  Round-1 attention computes in fp32 FMAs (one wave per
-// (image, window, head) unit, lane = query token); the MFMA version is future work.
+// heads); out layout [nH][hdp].  bf16 with window 8 and hdp 32 (SwinIR-M/S/light) runs the
+// MFMA kernels; other shapes and the fp32 parity mode run the fp32-FMA kernels (one wave per
+// (image, window, head) unit, lane = query token).
 #include "sr_common.h"
 #include "sr_internal.h"
 
@@ -503,15 +504,404 @@ __global__ __launch_bounds__(64) void wattn_bwd_kernel(AttnArgs a) {
   for (int b = i; b < a.nbins; b += 64) a.dbias_part[(int64_t)unit * a.nbins + b] = sBin[b];
 }
 
-// dbias[bin][h] = sum over units of head h of dbias_part[unit][bin]
-__global__ void wattn_dbias_reduce(const float* __restrict__ part, int units, int nH, int nbins,
-                                   float* __restrict__ dbias) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nbins * nH) return;
-  const int bin = idx / nH, h = idx % nH;
-  float s = 0.f;
-  for (int u = h; u < units; u += nH) s += part[(int64_t)u * nbins + bin];
-  dbias[idx] = s;
+
+// ---------------------------------------------------------------- MFMA window attention
+// bf16, window 8 (64 tokens), heads padded to hdp = 32: one wave per (image, window, head)
+// unit; every contraction is a v_mfma_f32_16x16x32_bf16 with a 16-row tile per lane group.
+//   fragment layouts (16x16x32): A/B lane l holds row l&15, K = 8*(l>>4) .. +7; C lane l
+//   holds rows 4*(l>>4) + r (r = 0..3) of column l&15.
+//   forward : S^T = K Q^T (A = K rows, B = Q rows, both straight 16-B loads of the qkv
+//             rows), softmax over keys per query column (lane-local + 2 butterflies),
+//             O^T = V^T P^T with B = P^T taken from the C registers (K-slot order
+//             {32s+4g+r, 32s+16+4g+r}) and A = V^T by ds_read_b64_tr_b16 from an LDS copy of V
+//             read in the same key order.
+//   backward: S = Q K^T, dP = dO V^T (direct loads), P from lse, dS = P (dP - D);
+//             dV^T = dO^T P, dK^T = Q^T dS (B from registers, A tr-read), dQ^T = K^T dS^T
+//             (dS^T staged in LDS as bf16, tr-read); dbias by LDS float adds.
+// LDS images: [64 rows][64 B] with the 32-B half swapped on (row >> 2) & 1, and dS^T
+// [64][128 B] with 32-B blocks XORed by (row >> 1) & 3: conflict-free tr reads.
+SR_DEV uint32_t sx_off(int row, int chunk) {  // 16-B chunk (0..3) of a 64-B row
+  return (uint32_t)(row * 64 + ((((chunk >> 1) ^ ((row >> 2) & 1))) << 5) + ((chunk & 1) << 4));
+}
+SR_DEV uint32_t sx_byte(int row, int dim) {  // element dim (multiple of 4) of a 64-B row
+  const int b = dim * 2;
+  return (uint32_t)(row * 64 + ((((b >> 5) ^ ((row >> 2) & 1))) << 5) + (b & 31));
+}
+SR_DEV uint32_t st_byte(int row, int col) {  // element col (multiple of 4) of a 128-B dS^T row
+  const int b = col * 2;
+  return (uint32_t)(row * 128 + ((((b >> 5) ^ ((row >> 1) & 3))) << 5) + (b & 31));
+}
+SR_DEV s16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+// A/B fragment for K-step s from a [64][64 B] image: lane (g, tq, tp) reads rows
+// 32s + 4g + tq (slots 0..3) and 32s + 16 + 4g + tq (slots 4..7) at elements col0 + 4tp.
+SR_DEV s16x8 frag_tr64(const char* img, int s, int g, int tq, int tp, int col0) {
+  const s16x4 lo = tr_read(img + sx_byte(32 * s + 4 * g + tq, col0 + 4 * tp));
+  const s16x4 hi = tr_read(img + sx_byte(32 * s + 16 + 4 * g + tq, col0 + 4 * tp));
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+SR_DEV s16x8 frag_trST(const char* img, int s, int g, int tq, int tp, int col0) {
+  const s16x4 lo = tr_read(img + st_byte(32 * s + 4 * g + tq, col0 + 4 * tp));
+  const s16x4 hi = tr_read(img + st_byte(32 * s + 16 + 4 * g + tq, col0 + 4 * tp));
+  return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// B fragment from C registers of two vertically adjacent 16-row tiles (rows 4g + r)
+SR_DEV s16x8 frag_c2(const f32x4& t0, const f32x4& t1) {
+  u32x4 u;
+  u[0] = pack_bf16x2(t0[0], t0[1]);
+  u[1] = pack_bf16x2(t0[2], t0[3]);
+  u[2] = pack_bf16x2(t1[0], t1[1]);
+  u[3] = pack_bf16x2(t1[2], t1[3]);
+  return __builtin_bit_cast(s16x8, u);
+}
+SR_DEV f32x4 mfma16(const s16x8& a, const s16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+SR_DEV int bin8(int q, int k) { return ((q >> 3) - (k >> 3) + 7) * 15 + ((q & 7) - (k & 7) + 7); }
+
+__global__ __launch_bounds__(64) void wattn_fwd_mfma_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) char sV[64 * 64];
+  __shared__ float sT[225];
+  // XCD-aware: the heads of one window (which share the qkv rows' cache lines) run on one XCD
+  const int unit = (int)xcd_remap(blockIdx.x, gridDim.x), lane = threadIdx.x;
+  const int g = lane >> 4, c = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
+  int n, wy, wx, h;
+  unit_decode(a, unit, n, wy, wx, h);
+  const bf16_t* qkv = (const bf16_t*)a.qkv;
+  int64_t pix[4];
+  s16x8 qf[4], kf[4];
+  u32x4 vf[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pix[i] = token_pixel(a, n, wy, wx, 16 * i + c);
+    const bf16_t* row = qkv + pix[i] * a.ldq + g * 8;
+    qf[i] = __builtin_bit_cast(s16x8, *(const u32x4*)(row + h * 32));
+    kf[i] = __builtin_bit_cast(s16x8, *(const u32x4*)(row + (a.nH + h) * 32));
+    vf[i] = *(const u32x4*)(row + (2 * a.nH + h) * 32);
+  }
+  float tv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) tv[k] = lane + 64 * k < 225 ? a.bias_table[(lane + 64 * k) * a.nH + h] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (lane + 64 * k < 225) sT[lane + 64 * k] = tv[k];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *(u32x4*)(sV + sx_off(16 * i + c, g)) = vf[i];
+  __syncthreads();
+
+  f32x4 acc[4][4];  // S^T[key 16i + 4g + r][query 16j + c]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(kf[i], qf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+
+  // element (key 16i + 4g + r, query 16j + c) has bin bb(g, c) + 30 (j - i) - r: 28 distinct
+  // biases per lane, read once
+  const int bb = ((c >> 3) - (g >> 1) + 7) * 15 + (c & 7) - 4 * (g & 1) + 7;
+  float bt[7][4];
+#pragma unroll
+  for (int d = 0; d < 7; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bt[d][r] = sT[bb + 30 * (d - 3) - r];
+  int rk[4][4], rq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rq[i] = region(wy * 8 + 2 * i + (c >> 3), a.H, 8, a.shift) * 3 + region(wx * 8 + (c & 7), a.W, 8, a.shift);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      rk[i][r] = region(wy * 8 + 2 * i + (g >> 1), a.H, 8, a.shift) * 3 + region(wx * 8 + 4 * (g & 1) + r, a.W, 8, a.shift);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int qq = 16 * j + c;
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[i][j][r] * a.scale + bt[j - i + 3][r];
+        if (a.shift && rk[i][r] != rq[j]) v -= 100.f;
+        acc[i][j][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(acc[i][j][r] - mx);
+        acc[i][j][r] = e;
+        sm += e;
+      }
+    sm += __shfl_xor(sm, 16);
+    sm += __shfl_xor(sm, 32);
+    const float inv = 1.f / sm;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] *= inv;
+    if (g == 0) a.lse[(int64_t)unit * 64 + qq] = mx + __logf(sm);
+  }
+
+  f32x4 o[2][4];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[d][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    s16x8 vt[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) vt[d] = frag_tr64(sV, s, g, tq, tp, 16 * d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x8 pb = frag_c2(acc[2 * s][j], acc[2 * s + 1][j]);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) o[d][j] = mfma16(vt[d], pb, o[d][j]);
+    }
+  }
+  bf16_t* out = (bf16_t*)a.y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      uint2 w2;
+      w2.x = pack_bf16x2(o[d][j][0], o[d][j][1]);
+      w2.y = pack_bf16x2(o[d][j][2], o[d][j][3]);
+      *(uint2*)(out + pix[j] * a.ldo + h * 32 + 16 * d + 4 * g) = w2;
+    }
+}
+
+// Element (query 16i + 4g + r, key 16j + c) of a C tile has relative-position bin
+// base(g, c) + 30 (i - j) + r (bin8), so a lane touches 28 distinct bins: their biases are
+// read once and their dS contributions pre-summed in registers before the LDS adds.
+constexpr int ATT_UPW = 4;  // windows per backward wave
+SR_DEV int bin_base_qk(int g, int c) { return ((g >> 1) - (c >> 3) + 7) * 15 + 4 * (g & 1) - (c & 7) + 7; }
+
+__global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
+  // [0, 4K) K image; [4K, 8K) Q, [8K, 12K) dO -- both later overlaid by the 8 KB dS^T image
+  __shared__ __attribute__((aligned(16))) char smem[3 * 4096];
+  __shared__ float sT[225], sBin[225], sD[64];
+  char* sK = smem;
+  char* sQ = smem + 4096;
+  char* sdO = smem + 8192;
+  char* sdST = smem + 4096;
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, c = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
+  // this wave: head h of ATT_UPW consecutive windows (dbias pre-sums stay in registers)
+  const int part = (int)xcd_remap(blockIdx.x, gridDim.x);  // heads of a window group on one XCD
+  const int h = part % a.nH;
+  const int win0 = (part / a.nH) * ATT_UPW;
+  const int bb = bin_base_qk(g, c);
+  float dbs[7][4];
+#pragma unroll
+  for (int d = 0; d < 7; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dbs[d][r] = 0.f;
+  for (int k = lane; k < 225; k += 64) sBin[k] = 0.f;
+  const bf16_t* qkv = (const bf16_t*)a.qkv;
+  for (int uw = 0; uw < ATT_UPW; ++uw) {
+  const int wg = win0 + uw;  // global window index n * nwin + win
+  if (wg >= a.N * a.nwin) break;
+  const int unit = wg * a.nH + h;
+  const int n = wg / a.nwin, win = wg - n * a.nwin;
+  const int wy = win / a.nwx, wx = win - (win / a.nwx) * a.nwx;
+  int64_t pix[4];
+  s16x8 qf[4], kf[4], vf[4], df[4];
+  u32x4 qu[4], ku[4], du[4], ou[4];
+  f32x4 l4[4];
+  // every global load of the unit first (one round trip), then the LDS images
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pix[i] = token_pixel(a, n, wy, wx, 16 * i + c);
+    const bf16_t* row = qkv + pix[i] * a.ldq + g * 8;
+    qu[i] = *(const u32x4*)(row + h * 32);
+    ku[i] = *(const u32x4*)(row + (a.nH + h) * 32);
+    vf[i] = __builtin_bit_cast(s16x8, *(const u32x4*)(row + (2 * a.nH + h) * 32));
+    const int64_t orow = pix[i] * a.ldo + h * 32 + g * 8;
+    du[i] = *(const u32x4*)((const bf16_t*)a.dout + orow);
+    ou[i] = *(const u32x4*)((const bf16_t*)a.out + orow);
+    l4[i] = *(const f32x4*)(a.lse + (int64_t)unit * 64 + 16 * i + 4 * g);
+  }
+  float tv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) tv[k] = lane + 64 * k < 225 ? a.bias_table[(lane + 64 * k) * a.nH + h] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);  // keep all 28 loads ahead of their first use
+  float dd[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    qf[i] = __builtin_bit_cast(s16x8, qu[i]);
+    kf[i] = __builtin_bit_cast(s16x8, ku[i]);
+    df[i] = __builtin_bit_cast(s16x8, du[i]);
+    *(u32x4*)(sQ + sx_off(16 * i + c, g)) = qu[i];
+    *(u32x4*)(sK + sx_off(16 * i + c, g)) = ku[i];
+    *(u32x4*)(sdO + sx_off(16 * i + c, g)) = du[i];
+    float t = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      t += bf16_to_f32(du[i][e] & 0xffff) * bf16_to_f32(ou[i][e] & 0xffff) +
+           bf16_to_f32(du[i][e] >> 16) * bf16_to_f32(ou[i][e] >> 16);
+    dd[i] = t;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dd[i] += __shfl_xor(dd[i], 16);
+    dd[i] += __shfl_xor(dd[i], 32);
+    if (g == 0) sD[16 * i + c] = dd[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (lane + 64 * k < 225) sT[lane + 64 * k] = tv[k];
+  __syncthreads();
+
+  // S = Q K^T and dP = dO V^T: [query 16i + 4g + r][key 16j + c]
+  f32x4 pa[4][4], ds[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pa[i][j] = mfma16(qf[i], kf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+      ds[i][j] = mfma16(df[i], vf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+  float bt[7][4];
+#pragma unroll
+  for (int d = 0; d < 7; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bt[d][r] = sT[bb + 30 * (d - 3) + r];
+  // shift-mask regions: query (i, r) and key j of this lane
+  int rq[4][4], rk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    rk[i] = region(wy * 8 + 2 * i + (c >> 3), a.H, 8, a.shift) * 3 + region(wx * 8 + (c & 7), a.W, 8, a.shift);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      rq[i][r] = region(wy * 8 + 2 * i + (g >> 1), a.H, 8, a.shift) * 3 + region(wx * 8 + 4 * (g & 1) + r, a.W, 8, a.shift);
+  }
+  float Dq[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x4 d4 = *(const f32x4*)(sD + 16 * i + 4 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Dq[i][r] = d4[r];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = pa[i][j][r] * a.scale + bt[i - j + 3][r];
+        if (a.shift && rq[i][r] != rk[j]) v -= 100.f;
+        const float p = __expf(v - l4[i][r]);
+        const float dsv = p * (ds[i][j][r] - Dq[i][r]);
+        pa[i][j][r] = p;
+        ds[i][j][r] = dsv;
+        dbs[i - j + 3][r] += dsv;
+      }
+
+  // dV^T = dO^T P and dK^T = Q^T dS: [dim 16d + 4g + r][key 16j + c]
+  f32x4 dv[2][4], dk[2][4], dq[2][4];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dv[d][j] = dk[d][j] = dq[d][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    s16x8 at[2], qt[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      at[d] = frag_tr64(sdO, s, g, tq, tp, 16 * d);
+      qt[d] = frag_tr64(sQ, s, g, tq, tp, 16 * d);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x8 pb = frag_c2(pa[2 * s][j], pa[2 * s + 1][j]);
+      const s16x8 sb = frag_c2(ds[2 * s][j], ds[2 * s + 1][j]);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        dv[d][j] = mfma16(at[d], pb, dv[d][j]);
+        dk[d][j] = mfma16(qt[d], sb, dk[d][j]);
+      }
+    }
+  }
+  __syncthreads();  // Q / dO images consumed: overlay dS^T
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint2 w2;
+      w2.x = pack_bf16x2(ds[i][j][0], ds[i][j][1]);
+      w2.y = pack_bf16x2(ds[i][j][2], ds[i][j][3]);
+      *(uint2*)(sdST + st_byte(16 * j + c, 16 * i + 4 * g)) = w2;
+    }
+  __syncthreads();
+  // dQ^T = K^T dS^T: [dim 16d + 4g + r][query 16j + c]
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    s16x8 kt[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) kt[d] = frag_tr64(sK, s, g, tq, tp, 16 * d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x8 sb = frag_trST(sdST, s, g, tq, tp, 16 * j);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) dq[d][j] = mfma16(kt[d], sb, dq[d][j]);
+    }
+  }
+  bf16_t* gq = (bf16_t*)a.y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bf16_t* row = gq + pix[j] * a.ldq + 4 * g;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      uint2 w;
+      w.x = pack_bf16x2(dq[d][j][0] * a.scale, dq[d][j][1] * a.scale);
+      w.y = pack_bf16x2(dq[d][j][2] * a.scale, dq[d][j][3] * a.scale);
+      *(uint2*)(row + h * 32 + 16 * d) = w;
+      w.x = pack_bf16x2(dk[d][j][0] * a.scale, dk[d][j][1] * a.scale);
+      w.y = pack_bf16x2(dk[d][j][2] * a.scale, dk[d][j][3] * a.scale);
+      *(uint2*)(row + (a.nH + h) * 32 + 16 * d) = w;
+      w.x = pack_bf16x2(dv[d][j][0], dv[d][j][1]);
+      w.y = pack_bf16x2(dv[d][j][2], dv[d][j][3]);
+      *(uint2*)(row + (2 * a.nH + h) * 32 + 16 * d) = w;
+    }
+  }
+  __syncthreads();  // LDS images free for the next unit
+  }
+#pragma unroll
+  for (int d = 0; d < 7; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) atomicAdd(&sBin[bb + 30 * (d - 3) + r], dbs[d][r]);
+  __syncthreads();
+  for (int b = lane; b < 225; b += 64) a.dbias_part[(int64_t)part * 225 + b] = sBin[b];
+}
+
+bool attn_mfma_ok(const AttnArgs& a, int dtype) {
+  return dtype == SR_BF16 && a.ws == 8 && a.hdp == 32 && a.ldq % 8 == 0 && a.ldo % 8 == 0;
+}
+
+// dbias[bin][h] = sum over the units of head h of dbias_part[unit][bin]: one block per
+// (head, 64-bin chunk), 16 waves split the units (coalesced 64-bin rows), LDS combine.
+__global__ __launch_bounds__(1024) void wattn_dbias_reduce2(const float* __restrict__ part, int units, int nH, int nbins,
+                                                            float* __restrict__ dbias) {
+  __shared__ float red[16][64];
+  const int h = blockIdx.x % nH, chunk = blockIdx.x / nH;
+  const int bin = chunk * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
+  float sm = 0.f;
+  if (bin < nbins)
+    for (int u = h + wv * nH; u < units; u += 16 * nH) sm += part[(int64_t)u * nbins + bin];
+  red[wv][threadIdx.x & 63] = sm;
+  __syncthreads();
+  if (wv == 0 && bin < nbins) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+    dbias[bin * nH + h] = t;
+  }
 }
 
 bool attn_setup(AttnArgs& a, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp, float scale) {
@@ -591,7 +981,9 @@ int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W,
     return sr_fail(SR_EINVAL, "window_attn_fwd: bad arguments (ws <= 8, head_dim <= 32, H/W divisible by ws)");
   a.qkv = qkv; a.y = out; a.lse = lse; a.bias_table = bias_table; a.ldq = ldq; a.ldo = ldo;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == SR_BF16)
+  if (attn_mfma_ok(a, dtype))
+    hipLaunchKernelGGL(wattn_fwd_mfma_kernel, dim3(a.units), dim3(64), 0, s, a);
+  else if (dtype == SR_BF16)
     hipLaunchKernelGGL(wattn_fwd_kernel<bf16_t>, dim3(a.units), dim3(64), 0, s, a);
   else
     hipLaunchKernelGGL(wattn_fwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
@@ -615,12 +1007,17 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
   a.qkv = qkv; a.out = out; a.dout = dout; a.y = dqkv; a.lse = (float*)lse; a.bias_table = bias_table;
   a.dbias_part = (float*)workspace; a.ldq = ldq; a.ldo = ldo;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == SR_BF16)
+  int parts = a.units;  // dbias partial rows, interleaved by head (row % nH == head)
+  if (attn_mfma_ok(a, dtype)) {
+    parts = nH * ((N * a.nwin + ATT_UPW - 1) / ATT_UPW);
+    hipLaunchKernelGGL(wattn_bwd_mfma_kernel, dim3(parts), dim3(64), 0, s, a);
+  } else if (dtype == SR_BF16) {
     hipLaunchKernelGGL(wattn_bwd_kernel<bf16_t>, dim3(a.units), dim3(64), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL(wattn_bwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(wattn_dbias_reduce, dim3((a.nbins * nH + 255) / 256), dim3(256), 0, s,
-                     (const float*)workspace, a.units, nH, a.nbins, dbias_table);
+  }
+  hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((a.nbins + 63) / 64)), dim3(1024), 0, s,
+                     (const float*)workspace, parts, nH, a.nbins, dbias_table);
   return sr_check(hipGetLastError(), "window_attn_bwd launch");
 }
 
