@@ -1505,6 +1505,163 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Weight gradient for narrow convs (Cout <= 64: RCAN / RRDB / SRResNet bodies), all nine
+// taps in one block.  A 64-pixel K-step is one image-row segment (W % 64 == 0); the block
+// stages dy[64 px][Cout] once and the x halo rows y-1..y+1, cols x0-1..x0+64 of its
+// 64-channel chunk once, and forms every tap's GEMM from LDS (the x bytes are read from
+// L2 once per step instead of once per tap).  Wave w owns ci tile w (16 channels) x all co
+// tiles x 9 taps (36*CO_T accumulators); operands by ds_read_b64_tr_b16.  LDS images are
+// [tile][row][32 B] with row r stored at r ^ ((r >> 3) & 1) << 2: the rows a 32-lane half
+// reads ({b..b+3} u {b+8..b+11}, any base b) hit distinct 32-B bank slots.  Both images are
+// filled by LDS-DMA, two stages in flight.  Nearest-neighbour input upsampling (in_up 2,
+// RRDBNet conv_up*) is folded into the halo gather.
+// ------------------------------------------------------------------------------------
+SR_DEV int hrow(int r) { return r ^ (((r >> 3) & 1) << 2); }
+
+template <int CO_T>
+__global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
+  constexpr int HT = 7 * 1024;      // halo image of one 16-ci tile: 224 rows x 32 B (198 used)
+  constexpr int HALO = 4 * HT;
+  constexpr int DYB = CO_T * 2048;  // dy image: CO_T tiles x 64 rows x 32 B
+  constexpr int STAGE = HALO + DYB + 1024;  // + 1 KB target for padding DMAs
+  constexpr int DYI = (CO_T * 2 + 3) / 4;   // dy DMAs per wave
+  constexpr int NDMA = 7 + DYI;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = (int)b / a.tiles_ci;
+  const int chunk = (int)b - split * a.tiles_ci;
+  const int ci0 = chunk * 64;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const int sh = a.in_up > 1 ? 1 : 0;  // in_up is 1 or 2 here
+  const int Hs = a.H >> sh, Ws = a.W >> sh;
+
+  // halo rows of this lane's 7 DMAs: physical row 32i + (lane >> 1), channel half lane & 1
+  int hty[7], htx[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int hr = hrow(32 * i + (lane >> 1));
+    hty[i] = hr < 198 ? hr / 66 : -100000;
+    htx[i] = hr < 198 ? hr - (hr / 66) * 66 : 0;
+  }
+  const int cil = ci0 + w * 16 + (lane & 1) * 8;
+  const bool civ = cil < a.Cin;
+
+  f32x4 acc[9][CO_T], accb[CO_T];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < CO_T; ++c) accb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.wsb != nullptr && chunk == 0 && w == 0;
+
+  auto issue = [&](int ks, int buf) {
+    const int p0s = p_begin + ks * 64;
+    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
+    const int x0 = p0s - q * a.W;
+    const int n = (int)fdiv((uint32_t)q, a.fd_H);
+    const int y = q - n * a.H;
+    char* hd = smem + buf * STAGE + w * HT;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int yy = y - 1 + hty[i], xx = x0 - 1 + htx[i];
+      const bool v = civ && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      const uint32_t off = (uint32_t)((((n * Hs + (yy >> sh)) * Ws + (xx >> sh)) * a.ldx + a.xcoff + cil) * 2);
+      glds16(xr, hd + i * 1024, v ? off : SR_OOB);
+    }
+    const int left = p_end - p0s;
+#pragma unroll
+    for (int i = 0; i < DYI; ++i) {
+      const int k = w + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
+      char* dst = smem + buf * STAGE + HALO + DYB;
+      uint32_t off = SR_OOB;
+      if (k < CO_T * 2) {
+        const int pr = hrow((k & 1) * 32 + (lane >> 1));
+        const int co = (k >> 1) * 16 + (lane & 1) * 8;
+        dst = smem + buf * STAGE + HALO + k * 1024;
+        if (pr < left && co < a.Cout) off = (uint32_t)(((p0s + pr) * a.ldy + a.ycoff + co) * 2);
+      }
+      glds16(dyr, dst, off);
+    }
+  };
+
+  const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  auto tr2 = [&](const char* img, int r0) -> s16x8 {  // rows r0 + tq (K 0..3), r0 + 4 + tq (K 4..7)
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0 + tq) * 32 + tp * 8));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0 + 4 + tq) * 32 + tp * 8));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  auto compute = [&](int buf) {
+    const char* hs = smem + buf * STAGE + w * HT;
+    const char* ds = smem + buf * STAGE + HALO;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s16x8 fa[CO_T];
+#pragma unroll
+      for (int c = 0; c < CO_T; ++c) fa[c] = tr2(ds + c * 2048, kk * 32 + 8 * g);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const s16x8 fb = tr2(hs, (t / 3) * 66 + (t % 3) + kk * 32 + 8 * g);
+#pragma unroll
+        for (int c = 0; c < CO_T; ++c) acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c], fb, acc[t][c], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (do_bias) {
+#pragma unroll
+        for (int c = 0; c < CO_T; ++c) accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c], ones, accb[c], 0, 0, 0);
+      }
+    }
+  };
+
+  const int nk = (p_end - p_begin + 63) / 64;  // >= 1
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    compute(ks & 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ks + 2 < nk) issue(ks + 2, ks & 1);
+  }
+
+  const int c16 = lane & 15;
+  const int ci = ci0 + w * 16 + c16;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    float* ws = a.ws + ((size_t)split * 9 + t) * a.Cout * a.Cin;
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = c * 16 + g * 4 + r;
+        if (co < a.Cout && ci < a.Cin) ws[(size_t)co * a.Cin + ci] = acc[t][c][r];
+      }
+  }
+  if (do_bias && c16 == 0) {
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = c * 16 + g * 4 + r;
+        if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
+      }
+  }
+}
+
 // dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co' = GEMM column of co (out_ps
 // permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
@@ -1543,45 +1700,79 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
   }
 }
 
-// Vectorised slab reduction (no ci_map, Cin_real % 4 == 0): one thread per (tap, co, 4 ci),
-// S independent 16-B loads (coalesced along ci) in flight per thread; bias sums by the
-// first Cout_real threads.  Same summation order over splits as wgrad_reduce_kernel.
-__global__ void wgrad_reduce4_kernel(const float* ws, const float* wsb, float* dw, float* db, int S, int Cout,
-                                     int Cin, int Cout_real, int Cin_real, int out_ps, int taps, const int* co_map,
-                                     float scale) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Slab reduction for Cin_real % 4 == 0 (16-B loads, or gathered through ci_map): 64 (tap, co, 4 ci) groups per
+// 1024-thread block; the 16 waves take splits k = wave (mod 16) with independent 16-B loads
+// (coalesced along ci), then a fixed-order LDS combine -- deterministic, and S / 16 loads
+// per thread instead of S.  The last ceil(Cout_real / 64) blocks sum the bias slab the same
+// way (one co per lane).
+__global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, const float* wsb, float* dw, float* db,
+                                                             int S, int Cout, int Cin, int Cout_real, int Cin_real,
+                                                             int out_ps, int taps, const int* co_map,
+                                                             const int* ci_map, float scale, int wblocks) {
+  __shared__ f32x4 red[16][64];
+  const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
   const int cps = Cout_real / r2;
+  if ((int)blockIdx.x >= wblocks) {  // bias
+    const int c = ((int)blockIdx.x - wblocks) * 64 + t;
+    float sb = 0.f;
+    if (c < Cout_real) {
+      const int cop = co_map ? co_map[c] : (out_ps > 0 ? (c % r2) * cps + c / r2 : c);
+      for (int k = wv; k < S; k += 16) sb += wsb[(size_t)k * Cout + cop];
+    }
+    red[wv][t] = f32x4{sb, 0.f, 0.f, 0.f};
+    __syncthreads();
+    if (wv == 0 && c < Cout_real) {
+      float sm = red[0][t][0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) sm += red[k][t][0];
+      db[c] = sm * scale;
+    }
+    return;
+  }
+  const int64_t i = (int64_t)blockIdx.x * 64 + t;
   const int c4n = Cin_real >> 2;
   const int64_t total = (int64_t)taps * Cout_real * c4n;
+  int co = 0, ci4 = 0, tap = 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   if (i < total) {
-    const int ci4 = (int)(i % c4n);
+    ci4 = (int)(i % c4n);
     const int64_t t2 = i / c4n;
-    const int co = (int)(t2 % Cout_real);
-    const int tap = (int)(t2 / Cout_real);
+    co = (int)(t2 % Cout_real);
+    tap = (int)(t2 / Cout_real);
     const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
     const size_t stride = (size_t)taps * Cout * Cin;
-    const float* src = ws + ((size_t)tap * Cout + cop) * Cin + ci4 * 4;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    int k = 0;
-    for (; k + 4 <= S; k += 4) {
-      const f32x4 v0 = *(const f32x4*)(src + (size_t)k * stride);
-      const f32x4 v1 = *(const f32x4*)(src + (size_t)(k + 1) * stride);
-      const f32x4 v2 = *(const f32x4*)(src + (size_t)(k + 2) * stride);
-      const f32x4 v3 = *(const f32x4*)(src + (size_t)(k + 3) * stride);
-      acc += v0; acc += v1; acc += v2; acc += v3;
+    const float* row = ws + ((size_t)tap * Cout + cop) * Cin;
+    if (ci_map) {  // GEMM channels of the 4 parameter channels (padded heads): gathered loads
+      int cip[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cip[e] = ci_map[ci4 * 4 + e];
+      for (int k = wv; k < S; k += 16) {
+        const float* sk = row + (size_t)k * stride;
+        acc += f32x4{sk[cip[0]], sk[cip[1]], sk[cip[2]], sk[cip[3]]};
+      }
+    } else {
+      const float* src = row + ci4 * 4;
+      int k = wv;
+      for (; k + 48 < S; k += 64) {
+        const f32x4 v0 = *(const f32x4*)(src + (size_t)k * stride);
+        const f32x4 v1 = *(const f32x4*)(src + (size_t)(k + 16) * stride);
+        const f32x4 v2 = *(const f32x4*)(src + (size_t)(k + 32) * stride);
+        const f32x4 v3 = *(const f32x4*)(src + (size_t)(k + 48) * stride);
+        acc += v0; acc += v1; acc += v2; acc += v3;
+      }
+      for (; k < S; k += 16) acc += *(const f32x4*)(src + (size_t)k * stride);
     }
-    for (; k < S; ++k) acc += *(const f32x4*)(src + (size_t)k * stride);
+  }
+  red[wv][t] = acc;
+  __syncthreads();
+  if (wv == 0 && i < total) {
+    f32x4 sm = red[0][t];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) sm += red[k][t];
     float* d = dw + ((size_t)co * Cin_real + ci4 * 4) * taps + tap;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = acc[e] * scale;
-  }
-  if (db && i < Cout_real) {
-    const int co = (int)i;
-    const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
-    float sb = 0.f;
-    for (int k = 0; k < S; ++k) sb += wsb[(size_t)k * Cout + cop];
-    db[co] = sb * scale;
+    for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = sm[e] * scale;
   }
 }
 
@@ -1703,12 +1894,31 @@ bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
 
+// All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2.
+bool wg_use_halo(const sr_conv3x3_wgrad_desc* d) {
+  return d->dtype == SR_BF16 && d->ksize != 1 && d->Cout <= 64 && d->W % 64 == 0 && d->in_up <= 2 && d->out_ps == 0 &&
+         g_variant != 1;
+}
+
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
 // 256x256 kernel, ~2 rounds for the small ones), pixels per split a multiple of 64.
 void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
   const int M = d->N * d->H * d->W;
   int bm, bn, target;
   int extra = 0;  // bias-role blocks per split (big kernel)
+  if (wg_use_halo(d)) {
+    // ~2 blocks per CU, but at least 8 K-steps per block (the slab costs 8 B per tap-MAC row)
+    const int chunks = (d->Cin + 63) / 64;
+    int S = 512 / chunks;
+    const int maxS = M / 512 > 1 ? M / 512 : 1;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
   if (wg_use_big(d)) {
     bm = bn = 256;
     target = 256;
@@ -1807,6 +2017,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
 }
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
+  if (wg_use_halo(d)) return "conv3x3_wgrad_halo_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
@@ -1865,7 +2076,17 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   a.fd_cps = make_fastdiv(cps);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  if (wg_use_big(d)) {
+  if (wg_use_halo(d)) {
+    a.tiles_co = 1;
+    a.tiles_ci = (a.Cin + 63) / 64;
+    const int ct = (a.Cout + 15) / 16;
+    const dim3 grid(S * a.tiles_ci);
+    if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<1>, grid, dim3(256), 0, s, a);
+    else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<2>, grid, dim3(256), 0, s, a);
+    else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<3>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<4>, grid, dim3(256), 0, s, a);
+    e = hipGetLastError();
+  } else if (wg_use_big(d)) {
     a.tiles_co = (a.Cout + 255) / 256;
     a.tiles_ci = (a.Cin + 255) / 256;
     const int per_split = taps * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
@@ -1882,12 +2103,13 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t work = total > Cout_real ? total : Cout_real;
-  if (!ci_map && Cin_real % 4 == 0) {
+  if (Cin_real % 4 == 0) {
     const int64_t work4 = (int64_t)taps * Cout_real * (Cin_real / 4);
-    const int64_t w4 = work4 > Cout_real ? work4 : Cout_real;
-    hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)((w4 + 255) / 256)), dim3(256), 0, s, (const float*)a.ws,
+    const int wblocks = (int)((work4 + 63) / 64);
+    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s, (const float*)a.ws,
                        (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map,
-                       d->scale);
+                       ci_map, d->scale, wblocks);
   } else {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
                        (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,

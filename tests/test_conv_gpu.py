@@ -239,3 +239,31 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
+                                   (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1)])
+def test_wgrad_halo_vs_fp64(cuda, shape):
+    """All-taps halo wgrad (Cout <= 64, W % 64 == 0): channel slices of wider buffers (ldx,
+    xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather (in_up = 2), ragged
+    last split, against an fp64 CPU reference on the same bf16 operands."""
+    N, H, W, cin, cout, up = shape
+    torch.manual_seed(9)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    xw = torch.randn(N, H // up, W // up, cin + 24).to(dt)  # x = channels [8, 8 + cin) of a wider map
+    dyw = torch.randn(N, H, W, cout + 16).to(dt)            # dy = channels [16, 16 + cout)
+    x = xw[..., 8:8 + cin]
+    dy = dyw[..., 16:16 + cout]
+    xd = x.permute(0, 3, 1, 2).double()
+    if up > 1:
+        xd = F.interpolate(xd, scale_factor=up, mode='nearest')
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xd, w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    dw, db = C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
+                              xcoff=8, ldy=cout + 16, ycoff=16, in_up=up)
+    torch.cuda.synchronize()
+    tol = 1e-3 * w.grad.abs().max().item() + 1e-3
+    assert (dw.cpu().double() - w.grad).abs().max().item() <= tol
+    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
