@@ -34,7 +34,7 @@ class ConvDesc(ctypes.Structure):
 class WgradDesc(ctypes.Structure):
     _fields_ = [('dtype', _i), ('N', _i), ('H', _i), ('W', _i), ('Cin', _i), ('Cin_real', _i), ('ldx', _i),
                 ('xcoff', _i), ('Cout', _i), ('Cout_real', _i), ('ldy', _i), ('ycoff', _i), ('out_ps', _i),
-                ('scale', _f), ('in_up', _i), ('ksize', _i)]
+                ('scale', _f), ('in_up', _i), ('ksize', _i), ('accumulate', _i)]
 
 
 class DcnDesc(ctypes.Structure):

@@ -1666,7 +1666,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
 // permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
                                     int Cout, int Cin, int Cout_real, int Cin_real, int out_ps, int taps,
-                                    const int* co_map, const int* ci_map, float scale) {
+                                    const int* co_map, const int* ci_map, float scale, int accumulate) {
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
@@ -1689,14 +1689,14 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
     float* d = dw + i * taps;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
-      if (t < taps) d[t] = s[t] * scale;
+      if (t < taps) d[t] = s[t] * scale + (accumulate ? d[t] : 0.f);
   }
   if (db && i < Cout_real) {
     const int co = (int)i;
     const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
     float s = 0.f;
     for (int k = 0; k < S; ++k) s += wsb[(size_t)k * Cout + cop];
-    db[co] = s * scale;
+    db[co] = s * scale + (accumulate ? db[co] : 0.f);
   }
 }
 
@@ -1708,7 +1708,8 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
 __global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, const float* wsb, float* dw, float* db,
                                                              int S, int Cout, int Cin, int Cout_real, int Cin_real,
                                                              int out_ps, int taps, const int* co_map,
-                                                             const int* ci_map, float scale, int wblocks) {
+                                                             const int* ci_map, float scale, int wblocks,
+                                                             int accumulate) {
   __shared__ f32x4 red[16][64];
   const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
@@ -1726,7 +1727,7 @@ __global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, co
       float sm = red[0][t][0];
 #pragma unroll
       for (int k = 1; k < 16; ++k) sm += red[k][t][0];
-      db[c] = sm * scale;
+      db[c] = sm * scale + (accumulate ? db[c] : 0.f);
     }
     return;
   }
@@ -1772,7 +1773,7 @@ __global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, co
     for (int k = 1; k < 16; ++k) sm += red[k][t];
     float* d = dw + ((size_t)co * Cin_real + ci4 * 4) * taps + tap;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = sm[e] * scale;
+    for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = sm[e] * scale + (accumulate ? d[(size_t)e * taps] : 0.f);
   }
 }
 
@@ -2109,11 +2110,11 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     const int bblocks = db ? (Cout_real + 63) / 64 : 0;
     hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s, (const float*)a.ws,
                        (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map,
-                       ci_map, d->scale, wblocks);
+                       ci_map, d->scale, wblocks, d->accumulate);
   } else {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
                        (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
-                       Cin_real, d->out_ps, taps, co_map, ci_map, d->scale);
+                       Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, d->accumulate);
   }
   return sr_check(hipGetLastError(), "conv3x3_wgrad reduce launch");
 }

@@ -100,10 +100,10 @@ class _RCAB(torch.autograd.Function):
         _, wd2, _ = C.prepared(w2, b2, spec2, dtype)
         dz1 = torch.empty_like(t)
         C.conv_fwd_raw(du, wd2, None, dz1, N, H, W, spec2.cout_p, spec2.cin_p, spec2.cin_p, gate=t, gate_slope=0.0)
-        dw2, db2 = C.conv_wgrad_raw(du, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout)
+        dw2, db2 = C.conv_wgrad_raw(du, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout, params=(w2, b2))
         dx = torch.empty_like(x)
         C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
-        dw1, db1 = C.conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout)
+        dw1, db1 = C.conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, params=(w1, b1))
         return (dx, dw1, db1, dw2, db2, dA1.reshape(Cr, Cp, 1, 1), dab1 if ab1 is not None else None,
                 dA2.reshape(Cp, Cr, 1, 1), dab2 if ab2 is not None else None, None, None, None)
 
@@ -189,7 +189,7 @@ class _RRDB(torch.autograd.Function):
             C.conv_fwd_raw(d_in, wd5, None, dB, N, H, W, nf, Cb, Cb, alpha=a5, res=d_in, beta=rb, rcols=nf, ldx=ld_in,
                            ldr=ld_in, ldy=Cb)
             grads[r * 10 + 8], grads[r * 10 + 9] = C.conv_wgrad_raw(d_in, B, N, H, W, Cb, Cb, nf, nf, scale=a5,
-                                                                   ldy=ld_in, ldx=Cb)
+                                                                   ldy=ld_in, ldx=Cb, params=(w5, b5))
             for k in (3, 2, 1, 0):
                 co = nf + k * gc
                 _act_bwd_inplace(dB, B, Cb, co, gc, P, 0.2)
@@ -205,7 +205,7 @@ class _RRDB(torch.autograd.Function):
                     C.conv_fwd_raw(dB, wd, None, dB, N, H, W, gc, co, co, res=dB, beta=1.0, ldx=Cb, xcoff=co, ldr=Cb,
                                    ldy=Cb)
                 grads[r * 10 + 2 * k], grads[r * 10 + 2 * k + 1] = C.conv_wgrad_raw(
-                    dB, B, N, H, W, co, co, gc, gc, ldy=Cb, ycoff=co, ldx=Cb)
+                    dB, B, N, H, W, co, co, gc, gc, ldy=Cb, ycoff=co, ldx=Cb, params=(w, b))
             d_in, ld_in = dB, Cb
         return (dx, None, None, *grads)
 

@@ -121,8 +121,45 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     return y
 
 
-def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, out_ps=0, need_bias=True, **kw):
-    """Weight / bias gradient in the nn.Conv2d parameter layout (fp32)."""
+_GRAD_READY = {}  # id(param) -> callbacks run when a kernel has written the param's gradient
+
+
+def on_grad_ready(p, fn):
+    """Register fn(p), called after a HIP kernel accumulated p's gradient in place (the
+    direct-gradient path of conv_wgrad_raw, which bypasses autograd's AccumulateGrad)."""
+    _GRAD_READY.setdefault(id(p), []).append(fn)
+
+
+def grad_ready(p):
+    for fn in _GRAD_READY.get(id(p), ()):
+        fn(p)
+
+
+def grad_target(p):
+    """p.grad when it is a view into a FlatParams gradient buffer (the kernels accumulate the
+    gradient straight into it), else None."""
+    if p is None or not getattr(p, '_sr_flat', False):
+        return None
+    g = p.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous():
+        return None
+    return g
+
+
+def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, out_ps=0, need_bias=True, params=None,
+                   **kw):
+    """Weight / bias gradient in the nn.Conv2d parameter layout (fp32).
+
+    With ``params=(weight, bias)`` whose ``.grad`` live in a FlatParams buffer, the reduction
+    kernel accumulates into those ``.grad`` views directly (no per-parameter AccumulateGrad
+    add kernels), fires the gradient-ready callbacks and returns ``(None, None)`` for autograd.
+    """
+    tw = tb = None
+    if params is not None:
+        tw = grad_target(params[0])
+        tb = grad_target(params[1]) if need_bias else None
+        if tw is None or (need_bias and tb is None):
+            tw = tb = None
     d = _lib.WgradDesc()
     d.dtype = _lib.dtype_code(x.dtype)
     d.N, d.H, d.W = N, H, W
@@ -136,14 +173,23 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
     ws_bytes = lib.sr_conv3x3_wgrad_workspace(d)
     ws = torch.empty(ws_bytes // 4 + 1, device=x.device, dtype=torch.float32)
     kk = 3 if d.ksize == 3 else 1
-    dw = torch.empty(cout_real, cin_real, kk, kk, device=x.device, dtype=torch.float32)
-    db = torch.empty(cout_real, device=x.device, dtype=torch.float32) if need_bias else None
+    if tw is not None:
+        d.accumulate = 1
+        dw, db = tw, tb
+    else:
+        dw = torch.empty(cout_real, cin_real, kk, kk, device=x.device, dtype=torch.float32)
+        db = torch.empty(cout_real, device=x.device, dtype=torch.float32) if need_bias else None
     M = N * H * W
     with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * kk * kk * cin_real * cout_real,
                      x.element_size() * M * (cin + cout) + 4 * kk * kk * cin * cout):
         _lib.check(
             lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(dw), _lib.ptr(db),
                                  _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')), _lib.stream()))
+    if tw is not None:
+        grad_ready(params[0])
+        if need_bias:
+            grad_ready(params[1])
+        return None, None
     return dw, db
 
 
@@ -234,7 +280,8 @@ class _Conv3x3(torch.autograd.Function):
             dres = dy if spec.beta == 1.0 else dy * spec.beta
         if ctx.needs_input_grad[2] or (ctx.has_bias and ctx.needs_input_grad[3]):
             dw, db = conv_wgrad_raw(dY, x, N, H, W, spec.cin_p, spec.cin, spec.cout_p, spec.cout, scale=alpha,
-                                    out_ps=spec.out_ps, need_bias=ctx.has_bias, in_up=spec.in_up)
+                                    out_ps=spec.out_ps, need_bias=ctx.has_bias, in_up=spec.in_up,
+                                    params=(weight, bias))
         return dx, dres, dw, db, None
 
 
@@ -280,10 +327,12 @@ class _ResBlock(torch.autograd.Function):
         dz1 = torch.empty_like(t)
         conv_fwd_raw(dy, wd2, None, dz1, N, H, W, spec2.cout_p, spec2.cin_p, spec2.cin_p, alpha=rs, gate=t,
                      gate_slope=0.0)
-        dw2, db2 = conv_wgrad_raw(dy, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout, scale=rs)
+        dw2, db2 = conv_wgrad_raw(dy, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout, scale=rs,
+                                  params=(w2, b2))
         dx = torch.empty_like(x)
         conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
-        dw1, db1 = conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, scale=1.0)
+        dw1, db1 = conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, scale=1.0,
+                                  params=(w1, b1))
         return dx, dw1, db1, dw2, db2, None, None, None
 
 

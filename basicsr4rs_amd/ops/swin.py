@@ -103,11 +103,11 @@ def linear_dgrad(dy, wd, spec, N, H, W, **kw):
     return dx
 
 
-def linear_wgrad(dy, x, spec, N, H, W, need_bias=True):
+def linear_wgrad(dy, x, spec, N, H, W, need_bias=True, params=None):
     _, _, co, ci = spec.maps(dy.device)
     dw, db = C.conv_wgrad_raw(dy, x, N, H, W, spec.cin_p, spec.cin, spec.cout_p, spec.cout, ksize=1, co_map=co,
-                              ci_map=ci, need_bias=need_bias)
-    return dw.reshape(spec.cout, spec.cin), db
+                              ci_map=ci, need_bias=need_bias, params=params)
+    return (dw.reshape(spec.cout, spec.cin) if dw is not None else None), db
 
 
 def layernorm(x, weight, bias, Creal, eps=1e-5):
@@ -243,18 +243,18 @@ class _STB(torch.autograd.Function):
         dout = dout.to(dtype).contiguous()
         _, f2wd, _ = prepared_linear(f2w, f2b, fc2s, dtype)
         dz = linear_dgrad(dout, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)
-        df2w, df2b = linear_wgrad(dout, h, fc2s, N, H, W)
+        df2w, df2b = linear_wgrad(dout, h, fc2s, N, H, W, params=(f2w, f2b))
         _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
         dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
-        df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W)
+        df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W, params=(f1w, f1b))
         dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout)
         _, pwd, _ = prepared_linear(pw, pb, g.proj, dtype)
         da = linear_dgrad(dx2, pwd, g.proj, N, H, W)
-        dpw, dpb = linear_wgrad(dx2, a, g.proj, N, H, W)
+        dpw, dpb = linear_wgrad(dx2, a, g.proj, N, H, W, params=(pw, pb))
         dqkv, dtab = window_attn_bwd(qkv, a, da, lse, g, N, H, W, scale, tab)
         _, qwd, _ = prepared_linear(qw, qb, g.qkv, dtype)
         dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
-        dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W)
+        dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W, params=(qw, qb))
         dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2)
         return (dx, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b)
 

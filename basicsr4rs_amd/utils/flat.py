@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _lib
-from ..ops.conv import bump_param_epoch
+from ..ops.conv import bump_param_epoch, on_grad_ready
 
 
 def _params(module):
@@ -43,6 +43,7 @@ class FlatParams:
                 p.data = self.flat[o:o + n].view_as(p)
                 if with_grad:
                     p.grad = self.grad[o:o + n].view_as(p)
+                    p._sr_flat = True  # HIP wgrad kernels accumulate straight into this .grad view
 
     def view(self, buf, i):
         return buf[self.offsets[i]:self.offsets[i] + self.numels[i]].view_as(self.params[i])

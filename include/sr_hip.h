@@ -106,6 +106,8 @@ typedef struct sr_conv3x3_wgrad_desc {
   float scale;
   int in_up;  /* x read through nearest-neighbour upsampling by in_up (0/1 = none) */
   int ksize;  /* 3 (0 = 3) or 1 */
+  int accumulate;  /* 1: dw += result, db += result (gradient accumulation in place, e.g. into
+                      a flat .grad buffer); 0: overwrite */
 } sr_conv3x3_wgrad_desc;
 
 size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d);
