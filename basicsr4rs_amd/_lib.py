@@ -62,6 +62,7 @@ SIGNATURES = {
     'sr_l1_loss_workspace': (_sz, [_i64]),
     'sr_act_backward': (_i, [_i, _vp, _vp, _i64, _i, _f, _f, _vp, _vp]),
     'sr_adam_ema': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _f, _f, _f, _vp]),
+    'sr_adam_ema_dev': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _vp]),
     'sr_bilinear_up_add': (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     'sr_channel_reduce_workspace': (_sz, [_i, _i, _i]),
     'sr_channel_reduce': (_i, [_i, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _sz, _vp]),

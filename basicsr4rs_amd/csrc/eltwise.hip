@@ -193,6 +193,36 @@ __global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__
   }
 }
 
+// Same update with the step-dependent scalars read from device memory, so one launch can be
+// captured in a HIP graph and replayed: hyper = {step, lr, grad_scale}; adam_step_kernel
+// increments step (one thread) ahead of the update.
+__global__ void adam_step_kernel(float* hyper) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) hyper[0] += 1.f;
+}
+
+__global__ void adam_ema_dev_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                    float* __restrict__ v, float* __restrict__ ema, int64_t n,
+                                    const float* __restrict__ hyper, float beta1, float beta2, float eps,
+                                    float decay) {
+  const float step = hyper[0], lr = hyper[1], gscale = hyper[2];
+  const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    float mi = m[i], vi = v[i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    vi = vi * beta2 + (1.f - beta2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    const float pi = p[i] - step_size * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (ema) ema[i] = ema[i] * decay + pi * (1.f - decay);
+  }
+}
+
 // dz = alpha * dy * (y > 0 ? 1 : neg) with neg = 0 (ReLU) or slope (LeakyReLU); the sign of the
 // activation output equals the sign of its input for both.  8 bf16 / 4 f32 per 16-byte access.
 template <typename T>
@@ -331,6 +361,16 @@ int sr_adam_ema(float* p, const float* g, float* m, float* v, float* ema, int64_
   hipLaunchKernelGGL(adam_ema_kernel, dim3(grid_for(n, 8192)), dim3(256), 0, s, p, g, m, v, ema, n, lr,
                      beta1, beta2, eps, bc1, bc2, ema_decay, grad_scale);
   return sr_check(hipGetLastError(), "adam_ema launch");
+}
+
+int sr_adam_ema_dev(float* p, const float* g, float* m, float* v, float* ema, int64_t n, float* hyper, float beta1,
+                    float beta2, float eps, float ema_decay, void* stream) {
+  if (!p || !g || !m || !v || !hyper || n <= 0) return sr_fail(SR_EINVAL, "adam_ema_dev: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(64), 0, s, hyper);
+  hipLaunchKernelGGL(adam_ema_dev_kernel, dim3(grid_for(n, 8192)), dim3(256), 0, s, p, g, m, v, ema, n, hyper, beta1,
+                     beta2, eps, ema_decay);
+  return sr_check(hipGetLastError(), "adam_ema_dev launch");
 }
 
 int sr_act_backward(int dtype, const void* dy, const void* y, int64_t n, int act, float slope, float alpha,

@@ -49,6 +49,7 @@ class BaseModel:
         self.optimizers = []
         self.flat_g = None
         self.flat_ema = None
+        self._graph = None
         self._pending_losses = None
         self.log_dict = OrderedDict()
 

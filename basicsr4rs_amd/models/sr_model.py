@@ -50,6 +50,10 @@ class SRModel(BaseModel):
         self.net_g.train()
         train_opt = self.opt['train']
         self.use_amp = bool(train_opt.get('use_amp', False))
+        self._graph = None
+        self._eager_steps = 0
+        # HIP-graph capture of the train step (after 2 eager warm-up steps); single process
+        self.use_graph = bool(train_opt.get('cuda_graph', False)) and not self.opt.get('dist', False)
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)
@@ -75,11 +79,20 @@ class SRModel(BaseModel):
         self.optimizers.append(self.optimizer_g)
 
     def feed_data(self, data):
+        if self._graph is not None:  # captured step: refill its static input buffers
+            self.lq.copy_(data['lq'], non_blocking=True)
+            if 'gt' in data:
+                self.gt.copy_(data['gt'], non_blocking=True)
+            return
         self.lq = data['lq'].to(self.device, non_blocking=True)
         if 'gt' in data:
             self.gt = data['gt'].to(self.device, non_blocking=True)
 
-    def optimize_parameters(self, current_iter):
+    def _fused_step(self):
+        return hasattr(self.optimizer_g, 'device_step')
+
+    def _step_body(self):
+        """Device work of one train step (everything a captured replay re-executes)."""
         self.optimizer_g.zero_grad()
         with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.use_amp):
             self.output = self.net_g(self.lq)
@@ -90,14 +103,49 @@ class SRModel(BaseModel):
             l_total += l_pix
             loss_dict['l_pix'] = l_pix
         l_total.backward()
+        # drop the autograd graph now: a graph kept alive by self.output would pin this step's
+        # AccumulateGrad nodes (and their stream) into the next step / a HIP-graph capture
+        self.output = self.output.detach()
+        return loss_dict
+
+    def optimize_parameters(self, current_iter):
+        if self._graph is not None:
+            self.optimizer_g.host_step()
+            self._graph.replay()
+            self.log_dict = self.reduce_loss_dict(self._graph_losses)
+            return
+        if self.use_graph and self._eager_steps >= 2:
+            self._capture_step()
+            return
+        loss_dict = self._step_body()
         self.sync_gradients()
-        if hasattr(self.optimizer_g, 'fp') and self.ema_decay > 0 and self.flat_ema is not None:
-            self.optimizer_g.step(ema=self.flat_ema, ema_decay=self.ema_decay)
+        if self._fused_step():
+            ema = self.flat_ema if self.ema_decay > 0 else None
+            self.optimizer_g.step(ema=ema, ema_decay=self.ema_decay)
         else:
             self.optimizer_g.step()
             if self.ema_decay > 0:
                 self.model_ema(decay=self.ema_decay)
+        self._eager_steps += 1
         self.log_dict = self.reduce_loss_dict(loss_dict)
+
+    def _capture_step(self):
+        """Capture one whole train step (forward, L1, backward, fused Adam+EMA) in a HIP graph
+        and run it; later steps replay it (train.cuda_graph).  Host-side per-step state (step
+        count, lr) is kept outside the graph (FusedAdam.host_step + device hyper-parameters),
+        the inputs live in static buffers refilled by feed_data.  Single process only: the
+        gradient all-reduce of the distributed path stays eager."""
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        ema = self.flat_ema if self.ema_decay > 0 else None
+        self.optimizer_g.host_step()
+        with torch.cuda.graph(g):
+            losses = self._step_body()
+            self.optimizer_g.device_step(ema=ema, ema_decay=self.ema_decay)
+        self._graph = g
+        self._graph_losses = losses
+        g.replay()
+        self.log_dict = self.reduce_loss_dict(losses)
 
     def test(self):
         net = self.net_g_ema if hasattr(self, 'net_g_ema') else self.net_g

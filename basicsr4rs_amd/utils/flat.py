@@ -72,31 +72,50 @@ class FusedAdam(torch.optim.Optimizer):
         self.v = torch.zeros_like(flat.flat)
         self.nstep = 0
         self.grad_scale = 1.0
+        # {step, lr, grad_scale} on the device: the update kernel reads them there, so the step
+        # can be captured in a HIP graph; lr / grad_scale are re-uploaded only when they change
+        self.hyper = torch.zeros(3, dtype=torch.float32, device=flat.flat.device)
+        self._hyper_host = None
         self._bind_state()
 
     def _bind_state(self):
+        self._step_t = torch.tensor(float(self.nstep))  # one host 'step' tensor shared by all params
         for i, p in enumerate(self.fp.params):
-            self.state[p] = {'step': torch.tensor(float(self.nstep)), 'exp_avg': self.fp.view(self.m, i),
+            self.state[p] = {'step': self._step_t, 'exp_avg': self.fp.view(self.m, i),
                              'exp_avg_sq': self.fp.view(self.v, i)}
+        self.hyper[0] = float(self.nstep)
 
     def zero_grad(self, set_to_none=False):
         self.fp.zero_grad()
 
+    def host_step(self):
+        """Host-side part of a step (step count, lr / grad_scale upload when changed).  Runs
+        on every step, also before each replay of a captured step (models/sr_model.py)."""
+        self.nstep += 1
+        g = self.param_groups[0]
+        hv = (float(g['lr']), float(self.grad_scale))
+        if hv != self._hyper_host:
+            self.hyper[1:3].copy_(torch.tensor(hv, dtype=torch.float32), non_blocking=False)
+            self._hyper_host = hv
+        self._step_t.fill_(float(self.nstep))
+
+    def device_step(self, ema=None, ema_decay=0.0):
+        """The device part (graph-capturable): step counter increment + fused Adam/EMA."""
+        g = self.param_groups[0]
+        b1, b2 = g['betas']
+        lib = _lib.load()
+        _lib.check(
+            lib.sr_adam_ema_dev(_lib.ptr(self.fp.flat), _lib.ptr(self.fp.grad), _lib.ptr(self.m), _lib.ptr(self.v),
+                                _lib.ptr(ema.flat if ema is not None else None), self.fp.flat.numel(),
+                                _lib.ptr(self.hyper), float(b1), float(b2), float(g['eps']), float(ema_decay),
+                                _lib.stream()))
+        bump_param_epoch()
+
     @torch.no_grad()
     def step(self, closure=None, ema=None, ema_decay=0.0):
         loss = closure() if closure is not None else None
-        g = self.param_groups[0]
-        b1, b2 = g['betas']
-        self.nstep += 1
-        lib = _lib.load()
-        _lib.check(
-            lib.sr_adam_ema(_lib.ptr(self.fp.flat), _lib.ptr(self.fp.grad), _lib.ptr(self.m), _lib.ptr(self.v),
-                            _lib.ptr(ema.flat if ema is not None else None), self.fp.flat.numel(), float(g['lr']),
-                            float(b1), float(b2), float(g['eps']), 1.0 - b1**self.nstep, 1.0 - b2**self.nstep,
-                            float(ema_decay), float(self.grad_scale), _lib.stream()))
-        for p in self.fp.params:
-            self.state[p]['step'].fill_(float(self.nstep))
-        bump_param_epoch()
+        self.host_step()
+        self.device_step(ema, ema_decay)
         return loss
 
     def load_state_dict(self, state_dict):

@@ -58,7 +58,7 @@ def make_opt(world, batch, workload='edsr'):
     return dict(
         model_type=mtype, is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
         network_g=dict(net),
-        train=dict(ema_decay=0.999, use_amp=True,
+        train=dict(ema_decay=0.999, use_amp=True, cuda_graph=False,
                    optim_g=dict(type='Adam', lr=lr, weight_decay=0, betas=[0.9, 0.99]),
                    scheduler=dict(type='MultiStepLR', milestones=[200000], gamma=0.5),
                    pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')),
@@ -108,6 +108,8 @@ def main():
     ap.add_argument('--workload', default='edsr', choices=sorted(WORKLOADS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-trace', action='store_true')
+    ap.add_argument('--graph', type=int, default=-1,
+                    help='capture the train step in a HIP graph (1/0; default: on for a single process)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -131,6 +133,8 @@ def main():
     hr_px_tile = (4 * lr_px) ** 2
     opt = make_opt(world, B, args.workload)
     opt['rank'] = rank
+    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    opt['train']['cuda_graph'] = use_graph
     model = build_model(opt)
     g0 = torch.Generator(device=dev).manual_seed(0 + rank)
     g1 = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -138,15 +142,26 @@ def main():
     gt = torch.rand(B, 3, 4 * lr_px, 4 * lr_px, generator=g1, device=dev)
     model.feed_data({'lq': lq, 'gt': gt})
 
+    # With a captured step, the per-kernel HIP-event trace is taken on the last eager warm-up
+    # step (a graph replay runs the same kernels but cannot be instrumented per launch); the
+    # capture happens on warm-up step 3, so at least 3 warm-up steps run.
     it = 0
-    for _ in range(args.warmup):
+    warmup = max(args.warmup, 3) if use_graph else args.warmup
+    kstats, traced_steps = {}, 0
+    for w in range(warmup):
         it += 1
         model.update_learning_rate(it)
-        model.optimize_parameters(it)
+        if use_graph and w == 1 and not args.no_trace:
+            torch.cuda.synchronize()
+            ktrace.start()
+            model.optimize_parameters(it)
+            kstats, traced_steps = ktrace.stop(), 1
+        else:
+            model.optimize_parameters(it)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if not args.no_trace:
+    if not args.no_trace and not use_graph:
         ktrace.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -157,7 +172,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kstats = ktrace.stop() if not args.no_trace else {}
+    if not args.no_trace and not use_graph:
+        kstats, traced_steps = ktrace.stop(), args.steps
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -180,13 +196,16 @@ def main():
             roof = {'bound': 'hbm', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS,
                     'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
                     'bytes_per_launch': st['bytes'] / st['count']}
-        roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // args.steps,
-                     'share_of_step': round(st['ms'] * 1e-3 / dt, 3)})
+        roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // traced_steps,
+                     'share_of_step': round(st['ms'] / traced_steps * 1e-3 / (dt / args.steps), 3),
+                     'timing': 'HIP events on the stream of each launch, ' +
+                               ('one eager step before capture (replays run the same kernels)' if use_graph
+                                else 'over the timed steps')})
         roof['kernels'] = {
-            k: {'count': v['count'] // args.steps, 'avg_us': round(v['ms'] / v['count'] * 1e3, 1),
+            k: {'count': v['count'] // traced_steps, 'avg_us': round(v['ms'] / v['count'] * 1e3, 1),
                 'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 and v['flops'] else None,
                 'gbs': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] > 0 and not v['flops'] else None,
-                'ms_per_step': round(v['ms'] / args.steps, 3)}
+                'ms_per_step': round(v['ms'] / traced_steps, 3)}
             for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]['ms'])
         }
     cpu = None
@@ -195,13 +214,13 @@ def main():
     if rank == 0:
         line = {
             'metric': 'HR-pixels/sec/node (x4 SR train step)', 'value': round(value, 1), 'unit': 'HR-pixels/s',
-            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
+            'n_gpus': world, 'steps': args.steps, 'warmup': warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
             'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
             'config': {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
-                       'parallelism': f'dp{world}', 'model': wl[0]['type']},
+                       'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph},
             'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
-            'last_loss': loss, 'roofline': roof, 'cpu_baseline': cpu,
+            'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu,
         }
         print(json.dumps(line))
     if world > 1:

@@ -163,6 +163,10 @@ int sr_act_backward(int dtype, const void* dy, const void* y, int64_t n, int act
 int sr_adam_ema(float* p, const float* g, float* m, float* v, float* ema, int64_t n, float lr,
                 float beta1, float beta2, float eps, float bc1, float bc2, float ema_decay,
                 float grad_scale, void* stream);
+/* Graph-capturable form: hyper = device float[3] {step, lr, grad_scale}; the call first
+ * increments hyper[0] on the device, then applies the update with bc = 1 - beta^step. */
+int sr_adam_ema_dev(float* p, const float* g, float* m, float* v, float* ema, int64_t n, float* hyper,
+                    float beta1, float beta2, float eps, float ema_decay, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Block kernels of MSRResNet / RCAN / RRDBNet (csrc/blocks.hip).

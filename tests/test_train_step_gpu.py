@@ -77,3 +77,36 @@ def test_sr_model_bf16_step_runs(cuda):
         losses.append(model.get_current_log()['l_pix'])
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize('amp', [False, True])
+def test_sr_model_hip_graph_matches_eager(cuda, amp):
+    """train.cuda_graph: steps 1-2 eager, step 3 captured + run, steps 4-6 graph replays (with an
+    lr milestone crossing) must give bitwise the same parameters, EMA and losses as eager steps."""
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        o = _opt(amp=amp)
+        o['train']['cuda_graph'] = graph
+        o['train']['scheduler'] = dict(type='MultiStepLR', milestones=[4], gamma=0.5)
+        model = build_model(o)
+        losses = []
+        for it in range(1, 7):
+            g0 = torch.Generator().manual_seed(it)
+            model.feed_data({'lq': torch.rand(2, 3, 16, 16, generator=g0), 'gt': torch.rand(2, 3, 64, 64, generator=g0)})
+            model.update_learning_rate(it)
+            model.optimize_parameters(it)
+            losses.append(model.get_current_log()['l_pix'])
+        assert (model._graph is not None) == graph
+        net = model.get_bare_model(model.net_g)
+        runs.append((losses, {k: v.detach().cpu().clone() for k, v in net.state_dict().items()},
+                     {k: v.detach().cpu().clone() for k, v in model.net_g_ema.state_dict().items()},
+                     float(model.optimizer_g.state_dict()['state'][0]['step'])))
+    (l0, p0, e0, s0), (l1, p1, e1, s1) = runs
+    assert l0 == l1
+    assert s0 == s1 == 6.0
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
+        assert torch.equal(e0[k], e1[k]), k
