@@ -130,50 +130,59 @@ __global__ void ca_mlp_fwd_kernel(const float* __restrict__ pool, const float* _
   }
 }
 
-// Backward of the squeeze MLP for the whole batch (one block): ds = d loss / d s.
-__global__ void ca_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ s,
-                                  const float* __restrict__ h, const float* __restrict__ pool,
-                                  const float* __restrict__ w1, const float* __restrict__ w2, int N, int C, int Cr,
-                                  float* __restrict__ dpool, float* __restrict__ dw1, float* __restrict__ db1,
-                                  float* __restrict__ dw2, float* __restrict__ db2, float* __restrict__ scratch) {
-  // scratch: dz2 [N,C], dz1 [N,Cr]
-  float* dz2 = scratch;
-  float* dz1 = scratch + (size_t)N * C;
-  for (int i = threadIdx.x; i < N * C; i += blockDim.x) dz2[i] = ds[i] * s[i] * (1.f - s[i]);
-  __syncthreads();
-  for (int i = threadIdx.x; i < N * Cr; i += blockDim.x) {
-    const int n = i / Cr, r = i % Cr;
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += w2[c * Cr + r] * dz2[n * C + c];
-    dz1[i] = h[i] > 0.f ? acc : 0.f;
+// Backward of the squeeze MLP for the whole batch (one 1024-thread block, everything staged
+// in LDS: N*C <= 4096, Cr <= 64): ds = d loss / d s.
+constexpr int CA_MAXNC = 8192, CA_MAXNR = 1024;
+__global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ s,
+                                                          const float* __restrict__ h, const float* __restrict__ pool,
+                                                          const float* __restrict__ w1, const float* __restrict__ w2,
+                                                          int N, int C, int Cr, float* __restrict__ dpool,
+                                                          float* __restrict__ dw1, float* __restrict__ db1,
+                                                          float* __restrict__ dw2, float* __restrict__ db2) {
+  __shared__ float dz2[CA_MAXNC], pl[CA_MAXNC], dz1[CA_MAXNR], hh[CA_MAXNR], W1[CA_MAXNR], W2[CA_MAXNR];
+  const int t = threadIdx.x, nt = blockDim.x;
+  for (int i = t; i < N * C; i += nt) {
+    const float si = s[i];
+    dz2[i] = ds[i] * si * (1.f - si);
+    pl[i] = pool[i];
+  }
+  for (int i = t; i < N * Cr; i += nt) hh[i] = h[i];
+  for (int i = t; i < C * Cr; i += nt) {
+    W1[i] = w1[i];  // [Cr][C]
+    W2[i] = w2[i];  // [C][Cr]
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C * Cr; i += blockDim.x) {
-    const int c = i / Cr, r = i % Cr;
+  for (int i = t; i < N * Cr; i += nt) {
+    const int n = i / Cr, r = i - n * Cr;
     float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += dz2[n * C + c] * h[n * Cr + r];
-    dw2[i] = acc;
+    for (int c = 0; c < C; ++c) acc += W2[c * Cr + r] * dz2[n * C + c];
+    dz1[i] = hh[i] > 0.f ? acc : 0.f;
   }
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  __syncthreads();
+  for (int i = t; i < C * Cr; i += nt) {
+    const int c = i / Cr, r = i - c * Cr;
+    float a2 = 0.f, a1 = 0.f;
+    for (int n = 0; n < N; ++n) {
+      a2 += dz2[n * C + c] * hh[n * Cr + r];
+      a1 += dz1[n * Cr + r] * pl[n * C + c];
+    }
+    dw2[i] = a2;          // [C][Cr]
+    dw1[r * C + c] = a1;  // [Cr][C]
+  }
+  for (int c = t; c < C; c += nt) {
     float acc = 0.f;
     for (int n = 0; n < N; ++n) acc += dz2[n * C + c];
     if (db2) db2[c] = acc;
   }
-  for (int i = threadIdx.x; i < Cr * C; i += blockDim.x) {
-    const int r = i / C, c = i % C;
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r] * pool[n * C + c];
-    dw1[i] = acc;
-  }
-  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+  for (int r = t; r < Cr; r += nt) {
     float acc = 0.f;
     for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r];
     if (db1) db1[r] = acc;
   }
-  for (int i = threadIdx.x; i < N * C; i += blockDim.x) {
-    const int n = i / C, c = i % C;
+  for (int i = t; i < N * C; i += nt) {
+    const int n = i / C, c = i - n * C;
     float acc = 0.f;
-    for (int r = 0; r < Cr; ++r) acc += w1[r * C + c] * dz1[n * Cr + r];
+    for (int r = 0; r < Cr; ++r) acc += W1[r * C + c] * dz1[n * Cr + r];
     dpool[i] = acc;
   }
 }
@@ -376,8 +385,11 @@ int sr_ca_mlp_bwd(const float* ds, const float* s, const float* h, const float* 
                   float* scratch, void* stream) {
   if (!ds || !s || !h || !pool || !w1 || !w2 || !dpool || !dw1 || !dw2 || !scratch)
     return sr_fail(SR_EINVAL, "ca_mlp_bwd: bad arguments");
-  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ds, s, h, pool, w1, w2, N, C, Cr,
-                     dpool, dw1, db1, dw2, db2, scratch);
+  if (N * C > CA_MAXNC || N * Cr > CA_MAXNR || C * Cr > CA_MAXNR)
+    return sr_fail(SR_EINVAL, "ca_mlp_bwd: N*C <= 8192, N*Cr and C*Cr <= 1024 (split the batch)");
+  (void)scratch;
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, ds, s, h, pool, w1, w2, N, C, Cr,
+                     dpool, dw1, db1, dw2, db2);
   return sr_check(hipGetLastError(), "ca_mlp_bwd launch");
 }
 

@@ -784,6 +784,136 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Forward / dgrad for narrow convs (Cout <= 64: RCAN / RRDB / SRResNet bodies at W 64 or
+// 128).  A block computes 256 consecutive output pixels = R = 256 / W full rows of one image
+// x all Cout channels.  Per 64-channel input chunk it stages the halo rows y0-1 .. y0+R,
+// cols -1 .. W of that image once in LDS by LDS-DMA (XOR-swizzled 128-B rows, zero padding
+// from the range check) and forms all nine taps from it: the A fragment of tap (ty, tx) is
+// the row set shifted by ty*(W+2)+tx -- x is read from L2 once per chunk instead of once per
+// tap.  Each wave owns CW co tiles x PT pixel tiles and keeps its weights in registers one
+// kernel row (3 taps) at a time, the next row in flight, so the weight bytes cross L2 once
+// per wave and chunk, not once per tap and pixel tile.  The fp32 tile goes
+// through the shared fused epilogue (bias, activation, gate, residuals, pixel shuffle).
+// ------------------------------------------------------------------------------------
+template <int CO_T, int DBG = 0>
+__global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
+  constexpr int BN = CO_T * 16;
+  constexpr int CSTR = BN + 4;
+  constexpr int CW = CO_T >= 4 ? CO_T / 2 : 1;  // co tiles per wave
+  constexpr int WC = CO_T / CW;                  // waves along co
+  constexpr int WP = 4 / WC;                     // waves along pixels
+  constexpr int PT = 16 / WP;                    // 16-pixel tiles per wave
+  constexpr int HROWS = 528;  // >= (R+2)*(W+2) rounded up to 8: 400 (W 64), 520 (W 128)
+  constexpr int SMEM_H = HROWS * 128;
+  constexpr int SMEM_E = 128 * CSTR * 4;
+  constexpr int SMEM = SMEM_H > SMEM_E ? SMEM_H : SMEM_E;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = w % WC, wp = w / WC;
+  const int g = lane >> 4, c16 = lane & 15;
+  const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (int)tile * 256;
+  const int W = a.W, H = a.H;
+  const int WPAD = W + 2;
+  const int R = 256 / W;
+  const int HR = (R + 2) * WPAD;
+  const int q0 = m0 / W;  // n*H + y0
+  const int n = q0 / H, y0 = q0 - n * H;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  int hb[PT];  // halo row of pixel 16*(PT*wp+i) + c16 at tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const int q = 16 * (PT * wp + i) + c16;
+    const int rr = q / W;
+    hb[i] = rr * WPAD + (q - rr * W);
+  }
+  f32x4 acc[PT][CW];
+#pragma unroll
+  for (int i = 0; i < PT; ++i)
+#pragma unroll
+    for (int c = 0; c < CW; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lc = (lane & 7) ^ (lane >> 3);  // logical 16-B chunk of this lane's DMA slot
+  const int nch = (a.Cin + 63) >> 6;
+  const int ninstr = (HR + 7) >> 3;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int ci0 = ch * 64;
+    if (ch) __syncthreads();  // every wave is done with the previous chunk's halo
+    const bool cv = ci0 + lc * 8 < a.Cin;
+    for (int k = w; k < ninstr; k += 4) {
+      const int hr = 8 * k + (lane >> 3);
+      const int hy = hr / WPAD, hx = hr - hy * WPAD;
+      const int yy = y0 - 1 + hy, xx = hx - 1;
+      const bool v = cv && hr < HR && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const uint32_t off = (uint32_t)((((n * H + yy) * W + xx) * a.ldx + a.xcoff + ci0 + lc * 8) * 2);
+      if (DBG != 2) glds16(xr, smem + k * 1024, v ? off : SR_OOB);
+    }
+    // this wave's weights, one kernel row (3 taps x 2 K halves x CW co tiles) at a time, the
+    // next row loaded while the current one computes; row 0 overlaps the halo DMA
+    u32x4 bw[2][3][2][CW];
+    auto load_row = [&](int ty, u32x4 (&dst)[3][2][CW]) {
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int c = 0; c < CW; ++c) {
+            const int co = (wc * CW + c) * 16 + c16, ci = ci0 + kk * 32 + 8 * g;
+            const int tap = ty * 3 + tx;
+            const bool v = co < a.Cout && ci < a.Cin && (DBG != 1 || tap == 0);
+            dst[tx][kk][c] = buf_load16(wr, v ? (uint32_t)((co * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB);
+          }
+    };
+    load_row(0, bw[0]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // opaque 0: keeps the 9*2*PT fragment addresses from being hoisted out of the chunk loop
+    // as loop invariants (they would pin ~144 VGPRs); recomputing them is ~4 VALU each
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty) {
+      if (ty < 2) load_row(ty + 1, bw[(ty + 1) & 1]);
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) {
+        const int toff = ty * WPAD + tx;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+          for (int i = 0; i < PT; ++i) {
+            const u32x4 fa = *(const u32x4*)(smem + swz128(hb[i] + z + toff, kk * 4 + g));
+#pragma unroll
+            for (int c = 0; c < CW; ++c) mfma_chunk<bf16_t>(fa, bw[ty & 1][DBG == 1 ? 0 : tx][kk][c], acc[i][c]);
+          }
+        }
+      }
+    }
+  }
+
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int row = 16 * (PT * wp + i) - 128 * h;  // pixel tile origin inside half h
+      if (row >= 0 && row < 128) {
+#pragma unroll
+        for (int c = 0; c < CW; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(row + 4 * g + r) * CSTR + (wc * CW + c) * 16 + c16] = acc[i][c][r];
+      }
+    }
+    __syncthreads();
+    if (DBG != 3) epilogue_tile<bf16_t, 128, BN, 256>(a, Cs, CSTR, m0 + h * 128, 0, tid);
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Weight gradient.  GEMM per tap: C[co][ci] = sum_p dy[p][co] * x[p + tap][ci] over a
 // K-range of pixels (split-K).  LDS images are [pixels][cols] (rows = K); MFMA operands
 // need 8 consecutive K per lane, read with ds_read_b64_tr_b16 (bf16) or ds_read_b32
@@ -1833,8 +1963,29 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Narrow-conv halo kernel: bf16 3x3, Cout <= 64, W 64 or 128, whole-row 256-pixel tiles.
+bool fwd_use_halo(const FwdArgs& a, bool bf) {
+  return bf && !a.out_nchw && a.Cout <= 64 && a.in_up == 1 && a.in_ps == 0 && a.tap0 == 0 && g_variant != 1 &&
+         (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
+}
+
+hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
+  FwdArgs a = a0;
+  a.tiles_n = 1;
+  a.tiles = a.M / 256;
+  const int ct = (a.Cout + 15) / 16;
+  if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, dim3(a.tiles), dim3(256), 0, s, a);
+  else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, dim3(a.tiles), dim3(256), 0, s, a);
+  else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), dim3(a.tiles), dim3(256), 0, s, a);
+  else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), dim3(a.tiles), dim3(256), 0, s, a);
+  else if (g_variant == 13) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 3>), dim3(a.tiles), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<4>, dim3(a.tiles), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
+  if (fwd_use_halo(a, sizeof(T) == 2)) return launch_fwd_halo(a, s);
   if (sizeof(T) == 2 && !a.out_nchw && a.Cout >= 256 && a.in_up == 1 && !g_disable_big) return launch_fwd_big(a, s);
   if (a.out_nchw || a.Cout <= 16) return launch_fwd<T, 256, 16, 4, 1>(a, s);
   if (a.Cout <= 32) return launch_fwd<T, 256, 32, 4, 1>(a, s);
@@ -2009,6 +2160,9 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
 // descriptor (bench.py traces and rocprof summaries are matched on these names).
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
+  if (bf && !d->out_nchw && d->Cout <= 64 && d->in_up <= 1 && d->in_ps == 0 && d->ksize != 1 && g_variant != 1 &&
+      (d->W == 64 || d->W == 128) && d->H % (256 / d->W) == 0)
+    return "conv3x3_fwd_halo_kernel";
   if (bf && !d->out_nchw && d->Cout >= 256 && d->in_up <= 1 && !g_disable_big)
     return g_variant == 2 ? "conv3x3_fwd_big_kernel" : "conv3x3_fwd_pp_kernel";
   if (d->out_nchw || d->Cout <= 16) return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
@@ -2027,7 +2181,8 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || variant > 2) return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1 or 2");
+  if (variant < 0 || (variant > 2 && variant < 11) || variant > 13)
+    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
   g_variant = variant;
   return SR_OK;
 }

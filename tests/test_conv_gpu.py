@@ -267,3 +267,46 @@ def test_wgrad_halo_vs_fp64(cuda, shape):
     tol = 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (dw.cpu().double() - w.grad).abs().max().item() <= tol
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize('shape', [(2, 8, 64, 64, 64), (1, 4, 128, 192, 32), (1, 4, 64, 96, 48), (2, 4, 64, 160, 8),
+                                   (1, 6, 128, 64, 64)])
+@pytest.mark.parametrize('epi', ['plain', 'relu_res'])
+def test_fwd_halo_vs_fp64(cuda, shape, epi):
+    """Narrow-conv halo forward (Cout <= 64, W 64/128): channel-slice input (ldx > Cin, xcoff),
+    output written into a slice of a wider buffer (RRDB dense layout), bias + LeakyReLU or
+    residual epilogues, ragged Cin chunks, against fp64 on the same bf16 operands; and
+    bitwise equal to the 128-row register-staged kernel when Cin == 64 (same K order)."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(4)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    spec = C.ConvSpec(cin, cout)
+    wf, wd, bg = C.prepared(conv.weight, conv.bias, spec, dt)
+    xw = torch.randn(N, H, W, cin + 16, device=cuda).to(dt)
+    x = xw[..., 8:8 + cin]
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    ldy = cout + 24
+    kw = dict(ldx=cin + 16, xcoff=8, ldy=ldy, ycoff=16)
+    if epi == 'relu_res':
+        kw.update(act=_lib.ACT_LRELU, slope=0.2, res=res, alpha=0.2, beta=1.0)
+    outs = []
+    try:
+        for variant in (0, 1):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.zeros(N, H, W, ldy, device=cuda, dtype=dt)
+            C.conv_fwd_raw(xw, wf, bg, y, N, H, W, cin, cout, cout, **kw)
+            outs.append(y)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    xd = x.permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(xd, bf(conv.weight.detach().cpu()).double(), conv.bias.detach().cpu().double(), padding=1)
+    if epi == 'relu_res':
+        ref = 0.2 * F.leaky_relu(ref, 0.2) + res.permute(0, 3, 1, 2).double().cpu()
+    got = outs[0][..., 16:16 + cout].permute(0, 3, 1, 2).double().cpu()
+    assert (got - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())
+    assert outs[0][..., :16].abs().max().item() == 0 and outs[0][..., 16 + cout:].abs().max().item() == 0
+    if cin == 64:
+        assert torch.equal(outs[0], outs[1])
