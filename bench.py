@@ -99,6 +99,18 @@ def cpu_baseline(seconds=20.0):
                       f'steps after 1 warm-up, torch CPU threads={torch.get_num_threads()}'}
 
 
+def _pmc_traffic(workload, kernel):
+    """HBM bytes per launch of ``kernel`` from this round's committed PMC passes
+    (tools/profile_round.sh -> profiles/pmc_traffic.json), or None."""
+    try:
+        rec = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))).get(workload)
+    except (OSError, ValueError):
+        return None
+    if not rec or rec.get('hbm_bytes_per_launch') is None or rec.get('bench_kernel') != kernel:
+        return None
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -201,6 +213,11 @@ def main():
                      'timing': 'HIP events on the stream of each launch, ' +
                                ('one eager step before capture (replays run the same kernels)' if use_graph
                                 else 'over the timed steps')})
+        tr = _pmc_traffic(args.workload, name)
+        if tr:
+            roof['traffic'] = round(tr['hbm_bytes_per_launch'])
+            roof['traffic_source'] = (f"{tr['source']}: rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (own passes) of this "
+                                      f"kernel, per launch, {tr['correction']}; rocprof avg {tr['rocprof_avg_us']:.1f} us")
         roof['kernels'] = {
             k: {'count': v['count'] // traced_steps, 'avg_us': round(v['ms'] / v['count'] * 1e3, 1),
                 'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 and v['flops'] else None,
