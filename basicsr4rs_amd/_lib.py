@@ -37,6 +37,12 @@ class WgradDesc(ctypes.Structure):
                 ('scale', _f), ('in_up', _i), ('ksize', _i), ('accumulate', _i)]
 
 
+class PrepItem(ctypes.Structure):
+    _fields_ = [('w', _vp), ('bias', _vp), ('Cout_real', _i), ('Cin_real', _i), ('Cout', _i), ('Cin', _i),
+                ('out_ps', _i), ('ksize', _i), ('row_map', _vp), ('col_map', _vp), ('wf', _vp), ('wd', _vp),
+                ('bias_g', _vp)]
+
+
 class DcnDesc(ctypes.Structure):
     _fields_ = [('dtype', _i), ('N', _i), ('C', _i), ('H', _i), ('W', _i), ('Cp', _i), ('Ho', _i), ('Wo', _i),
                 ('kh', _i), ('kw', _i), ('stride_h', _i), ('stride_w', _i), ('pad_h', _i), ('pad_w', _i),
@@ -47,12 +53,15 @@ class DcnDesc(ctypes.Structure):
 SIGNATURES = {
     'sr_version': (ctypes.c_char_p, []),
     'sr_last_error': (ctypes.c_char_p, []),
-    'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_conv3x3_fwd_colsum_parts': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_set_variant': (_i, [_i]),
     'sr_conv3x3_fwd_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_wgrad_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad_workspace': (_sz, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad': (_i, [ctypes.POINTER(WgradDesc), _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
+    'sr_conv_prep_blocks': (_i, [ctypes.POINTER(PrepItem)]),
+    'sr_conv_prep_batch': (_i, [_i, _vp, _vp, _i, _i, _vp]),
     'sr_conv3x3_prep': (_i, [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     'sr_conv_prep_mapped': (_i, [_i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_nchw_to_nhwc': (_i, [_i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
@@ -66,8 +75,10 @@ SIGNATURES = {
     'sr_bilinear_up_add': (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     'sr_channel_reduce_workspace': (_sz, [_i, _i, _i]),
     'sr_channel_reduce': (_i, [_i, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _f, _vp, _vp, _sz, _vp]),
-    'sr_ca_mlp_fwd': (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
-    'sr_ca_mlp_bwd': (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_channel_partials_count': (_i, [_i]),
+    'sr_channel_partials': (_i, [_i, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    'sr_ca_mlp_fwd': (_i, [_vp, _i, _f, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    'sr_ca_mlp_bwd': (_i, [_vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
     'sr_nc_affine': (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _f, _f, _f, _vp, _vp]),
     'sr_act_backward_nhwc': (_i, [_i, _i64, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _f, _f, _vp]),
     'sr_nearest_up_backward': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),

@@ -5,7 +5,9 @@
 //   sr_channel_reduce    per-(n, c) sum / dot over pixels of NHWC maps (deterministic two-pass):
 //                        RCAN ChannelAttention AdaptiveAvgPool2d(1) (rcan_arch.py:19) and its
 //                        backward reduction
-//   sr_ca_mlp_fwd/_bwd   the 1x1 conv -> ReLU -> 1x1 conv -> Sigmoid squeeze MLP (rcan_arch.py:19-20)
+//   sr_channel_partials  the first pass alone (consumers sum the per-chunk partials)
+//   sr_ca_mlp_fwd/_bwd   the 1x1 conv -> ReLU -> 1x1 conv -> Sigmoid squeeze MLP (rcan_arch.py:19-20),
+//                        summing partial pools (conv colsum / channel partials) on the way in
 //   sr_ca_scale_residual out = x + rs * u * s[n, c]   (RCAB tail, rcan_arch.py:22-24, 44-46)
 //   sr_ca_du             du = rs * dout * s[n, c] + dpool[n, c] / HW   (RCAB backward)
 //   sr_act_backward_nhwc strided (channel-slice) ReLU/LeakyReLU backward (RRDB dense slices)
@@ -108,42 +110,80 @@ __global__ void channel_reduce_final(const float* __restrict__ partial, int N, i
   out[i] = s * scale;
 }
 
-// h = relu(W1 pool + b1) [N,Cr], s = sigmoid(W2 h + b2) [N,C]; W1 [Cr][C], W2 [C][Cr]
-__global__ void ca_mlp_fwd_kernel(const float* __restrict__ pool, const float* __restrict__ w1,
+// sum over p = p0, p0 + G, ... < P of base[p * ld], fixed order, 8 loads in flight per batch
+SR_DEV float strided_sum(const float* __restrict__ base, int p0, int P, int G, int ld) {
+  float acc = 0.f;
+  int p = p0;
+  for (; p + 7 * G < P; p += 8 * G) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = base[(size_t)(p + k * G) * ld];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k];
+  }
+  for (; p < P; p += G) acc += base[(size_t)p * ld];
+  return acc;
+}
+
+// pool[n][c] = scale * sum_p parts[n*P + p][c] (fixed order: G partial sums per channel, then
+// their sum), h = relu(W1 pool + b1) [N,Cr], s = sigmoid(W2 h + b2); W1 [Cr][C], W2 [C][Cr].
+__global__ __launch_bounds__(1024) void ca_mlp_fwd_kernel(const float* __restrict__ parts, int P, float scale, const float* __restrict__ w1,
                                   const float* __restrict__ b1, const float* __restrict__ w2,
-                                  const float* __restrict__ b2, int C, int Cr, float* __restrict__ h,
-                                  float* __restrict__ s) {
-  extern __shared__ float sh[];  // Cr floats
-  const int n = blockIdx.x;
-  for (int r = threadIdx.x; r < Cr; r += blockDim.x) {
+                                  const float* __restrict__ b2, int C, int Cr, float* __restrict__ pool,
+                                  float* __restrict__ h, float* __restrict__ s) {
+  extern __shared__ float sh[];  // red [max(nt, C)] | pl [C] | hr [Cr]
+  const int n = blockIdx.x, nt = blockDim.x;
+  const int G = C < nt ? nt / C : 1;
+  float* red = sh;
+  float* pl = sh + (C > nt ? C : nt);
+  float* hr = pl + C;
+  const float* pn = parts + (size_t)n * P * C;
+  for (int i = threadIdx.x; i < C * G; i += nt) {
+    const int c = i % C, g = i / C;
+    red[g * C + c] = strided_sum(pn + c, g, P, G, C);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += nt) {
+    float acc = 0.f;
+    for (int g = 0; g < G; ++g) acc += red[g * C + c];
+    acc *= scale;
+    pl[c] = acc;
+    pool[n * C + c] = acc;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < Cr; r += nt) {
     float acc = b1 ? b1[r] : 0.f;
-    for (int c = 0; c < C; ++c) acc += w1[r * C + c] * pool[n * C + c];
+    for (int c = 0; c < C; ++c) acc += w1[r * C + c] * pl[c];
     acc = acc > 0.f ? acc : 0.f;
-    sh[r] = acc;
+    hr[r] = acc;
     h[n * Cr + r] = acc;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+  for (int c = threadIdx.x; c < C; c += nt) {
     float acc = b2 ? b2[c] : 0.f;
-    for (int r = 0; r < Cr; ++r) acc += w2[c * Cr + r] * sh[r];
+    for (int r = 0; r < Cr; ++r) acc += w2[c * Cr + r] * hr[r];
     s[n * C + c] = 1.f / (1.f + expf(-acc));
   }
 }
 
 // Backward of the squeeze MLP for the whole batch (one 1024-thread block, everything staged
-// in LDS: N*C <= 4096, Cr <= 64): ds = d loss / d s.
+// in LDS): ds[n][c] = scale * sum_p parts[n*P + p][c] = d loss / d s.  accumulate: the
+// parameter gradients are added to dw1/db1/dw2/db2 (gradient views of the optimizer).
 constexpr int CA_MAXNC = 8192, CA_MAXNR = 1024;
-__global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restrict__ ds, const float* __restrict__ s,
-                                                          const float* __restrict__ h, const float* __restrict__ pool,
-                                                          const float* __restrict__ w1, const float* __restrict__ w2,
-                                                          int N, int C, int Cr, float* __restrict__ dpool,
-                                                          float* __restrict__ dw1, float* __restrict__ db1,
-                                                          float* __restrict__ dw2, float* __restrict__ db2) {
+__global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restrict__ parts, int P, float scale,
+                                                          const float* __restrict__ s, const float* __restrict__ h,
+                                                          const float* __restrict__ pool, const float* __restrict__ w1,
+                                                          const float* __restrict__ w2, int N, int C, int Cr,
+                                                          float* __restrict__ dpool, float* __restrict__ dw1,
+                                                          float* __restrict__ db1, float* __restrict__ dw2,
+                                                          float* __restrict__ db2, int accumulate) {
   __shared__ float dz2[CA_MAXNC], pl[CA_MAXNC], dz1[CA_MAXNR], hh[CA_MAXNR], W1[CA_MAXNR], W2[CA_MAXNR];
   const int t = threadIdx.x, nt = blockDim.x;
   for (int i = t; i < N * C; i += nt) {
+    const int n = i / C, c = i - n * C;
+    const float ds = strided_sum(parts + (size_t)n * P * C + c, 0, P, 1, C);
     const float si = s[i];
-    dz2[i] = ds[i] * si * (1.f - si);
+    dz2[i] = ds * scale * si * (1.f - si);
     pl[i] = pool[i];
   }
   for (int i = t; i < N * Cr; i += nt) hh[i] = h[i];
@@ -166,18 +206,18 @@ __global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restric
       a2 += dz2[n * C + c] * hh[n * Cr + r];
       a1 += dz1[n * Cr + r] * pl[n * C + c];
     }
-    dw2[i] = a2;          // [C][Cr]
-    dw1[r * C + c] = a1;  // [Cr][C]
+    dw2[i] = (accumulate ? dw2[i] : 0.f) + a2;                  // [C][Cr]
+    dw1[r * C + c] = (accumulate ? dw1[r * C + c] : 0.f) + a1;  // [Cr][C]
   }
   for (int c = t; c < C; c += nt) {
     float acc = 0.f;
     for (int n = 0; n < N; ++n) acc += dz2[n * C + c];
-    if (db2) db2[c] = acc;
+    if (db2) db2[c] = (accumulate ? db2[c] : 0.f) + acc;
   }
   for (int r = t; r < Cr; r += nt) {
     float acc = 0.f;
     for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r];
-    if (db1) db1[r] = acc;
+    if (db1) db1[r] = (accumulate ? db1[r] : 0.f) + acc;
   }
   for (int i = t; i < N * C; i += nt) {
     const int n = i / C, c = i - n * C;
@@ -192,39 +232,50 @@ __global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restric
 // alpha = rs, s = sigmoid, gamma = 1/HW, t = dpool.
 template <typename T>
 __global__ void nc_affine_kernel(const T* __restrict__ x, const T* __restrict__ u, const float* __restrict__ s,
-                                 const float* __restrict__ t, int N, int HW, int C, float beta, float alpha,
-                                 float gamma, T* __restrict__ out) {
+                                 const float* __restrict__ t, uint32_t nv, FastDiv fd_cv, FastDiv fd_hwcv, int C,
+                                 float beta, float alpha, float gamma, T* __restrict__ out) {
   constexpr int PER = Elt<T>::PER16;
-  const int64_t nv = (int64_t)N * HW * C / PER;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e0 = i * PER;
-    const int c0 = (int)(e0 % C);
-    const int n = (int)(e0 / ((int64_t)HW * C));
+  // 32-bit indexing (checked on the host); one 16-byte vector = PER consecutive channels
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
+    const uint32_t q = fdiv(i, fd_cv);
+    const int c0 = (int)(i - q * fd_cv.d) * PER;
+    const int n = (int)fdiv(i, fd_hwcv);
     const u32x4 vu = ((const u32x4*)u)[i];
     u32x4 vx = {0, 0, 0, 0};
     if (x) vx = ((const u32x4*)x)[i];
+    float sv[PER], tv[PER];
+    const float* sp = s + n * C + c0;
+#pragma unroll
+    for (int k = 0; k < PER; k += 4) {
+      const f32x4 q4 = *(const f32x4*)(sp + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sv[k + j] = q4[j];
+    }
+    if (t) {
+      const float* tp = t + n * C + c0;
+#pragma unroll
+      for (int k = 0; k < PER; k += 4) {
+        const f32x4 q4 = *(const f32x4*)(tp + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tv[k + j] = gamma * q4[j];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < PER; ++k) tv[k] = 0.f;
+    }
     u32x4 o;
     if constexpr (PER == 8) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        float r[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = c0 + 2 * k + h;
-          const float uu = bf16_to_f32(h ? (vu[k] >> 16) : (vu[k] & 0xffff));
-          const float xx = x ? bf16_to_f32(h ? (vx[k] >> 16) : (vx[k] & 0xffff)) : 0.f;
-          r[h] = beta * xx + alpha * uu * s[n * C + c] + (t ? gamma * t[n * C + c] : 0.f);
-        }
-        o[k] = pack_bf16x2(r[0], r[1]);
+        const float u0 = bf16_to_f32(vu[k] & 0xffff), u1 = bf16_to_f32(vu[k] >> 16);
+        const float x0 = bf16_to_f32(vx[k] & 0xffff), x1 = bf16_to_f32(vx[k] >> 16);
+        o[k] = pack_bf16x2(beta * x0 + alpha * u0 * sv[2 * k] + tv[2 * k],
+                           beta * x1 + alpha * u1 * sv[2 * k + 1] + tv[2 * k + 1]);
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c = c0 + k;
-        const float r = beta * (x ? __uint_as_float(vx[k]) : 0.f) + alpha * __uint_as_float(vu[k]) * s[n * C + c] +
-                        (t ? gamma * t[n * C + c] : 0.f);
-        o[k] = __float_as_uint(r);
-      }
+      for (int k = 0; k < 4; ++k)
+        o[k] = __float_as_uint(beta * __uint_as_float(vx[k]) + alpha * __uint_as_float(vu[k]) * sv[k] + tv[k]);
     }
     ((u32x4*)out)[i] = o;
   }
@@ -372,40 +423,63 @@ int sr_channel_reduce(int dtype, const void* a, int lda, int acoff, const void* 
   return sr_check(hipGetLastError(), "channel_reduce launch");
 }
 
-int sr_ca_mlp_fwd(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, int N, int C,
-                  int Cr, float* h, float* s_out, void* stream) {
-  if (!pool || !w1 || !w2 || !h || !s_out) return sr_fail(SR_EINVAL, "ca_mlp_fwd: bad arguments");
-  hipLaunchKernelGGL(ca_mlp_fwd_kernel, dim3(N), dim3(256), Cr * sizeof(float), (hipStream_t)stream, pool, w1, b1, w2,
-                     b2, C, Cr, h, s_out);
+int sr_channel_partials_count(int HW) { return (HW + RED_CHUNK - 1) / RED_CHUNK; }
+
+int sr_channel_partials(int dtype, const void* a, int lda, int acoff, const void* b, int ldb, int bcoff, int N,
+                        int HW, int C, float* parts, void* stream) {
+  if (!a || !parts || C % 8 || C > 2048 || N <= 0 || HW <= 0)
+    return sr_fail(SR_EINVAL, "channel_partials: bad arguments (C multiple of 8, <= 2048)");
+  const int nchunk = sr_channel_partials_count(HW);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(channel_reduce_partial<bf16_t>, dim3(nchunk, N), dim3(256), 0, s, (const bf16_t*)a, lda, acoff,
+                       (const bf16_t*)b, ldb, bcoff, HW, C, parts);
+  else
+    hipLaunchKernelGGL(channel_reduce_partial<float>, dim3(nchunk, N), dim3(256), 0, s, (const float*)a, lda, acoff,
+                       (const float*)b, ldb, bcoff, HW, C, parts);
+  return sr_check(hipGetLastError(), "channel_partials launch");
+}
+
+int sr_ca_mlp_fwd(const float* parts, int P, float scale, const float* w1, const float* b1, const float* w2,
+                  const float* b2, int N, int C, int Cr, float* pool, float* h, float* s_out, void* stream) {
+  if (!parts || P < 1 || !w1 || !w2 || !pool || !h || !s_out || C < 1 || Cr < 1)
+    return sr_fail(SR_EINVAL, "ca_mlp_fwd: bad arguments");
+  const int nt = 1024;
+  const size_t smem = ((C > nt ? C : nt) + C + Cr) * sizeof(float);
+  if (smem > 64 * 1024) return sr_fail(SR_EINVAL, "ca_mlp_fwd: C too large");
+  hipLaunchKernelGGL(ca_mlp_fwd_kernel, dim3(N), dim3(nt), smem, (hipStream_t)stream, parts, P, scale, w1, b1, w2, b2,
+                     C, Cr, pool, h, s_out);
   return sr_check(hipGetLastError(), "ca_mlp_fwd launch");
 }
 
-int sr_ca_mlp_bwd(const float* ds, const float* s, const float* h, const float* pool, const float* w1,
-                  const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1, float* dw2, float* db2,
-                  float* scratch, void* stream) {
-  if (!ds || !s || !h || !pool || !w1 || !w2 || !dpool || !dw1 || !dw2 || !scratch)
+int sr_ca_mlp_bwd(const float* parts, int P, float scale, const float* s, const float* h, const float* pool,
+                  const float* w1, const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1,
+                  float* dw2, float* db2, int accumulate, void* stream) {
+  if (!parts || P < 1 || !s || !h || !pool || !w1 || !w2 || !dpool || !dw1 || !dw2)
     return sr_fail(SR_EINVAL, "ca_mlp_bwd: bad arguments");
   if (N * C > CA_MAXNC || N * Cr > CA_MAXNR || C * Cr > CA_MAXNR)
     return sr_fail(SR_EINVAL, "ca_mlp_bwd: N*C <= 8192, N*Cr and C*Cr <= 1024 (split the batch)");
-  (void)scratch;
-  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, ds, s, h, pool, w1, w2, N, C, Cr,
-                     dpool, dw1, db1, dw2, db2);
+  hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, parts, P, scale, s, h, pool, w1,
+                     w2, N, C, Cr, dpool, dw1, db1, dw2, db2, accumulate);
   return sr_check(hipGetLastError(), "ca_mlp_bwd launch");
 }
 
 int sr_nc_affine(int dtype, const void* x, const void* u, const float* s, const float* t, int N, int HW, int C,
                  float beta, float alpha, float gamma, void* out, void* stream) {
   const int PER = dtype == SR_BF16 ? 8 : 4;
-  if (!u || !s || !out || C % PER || !aligned16(u) || !aligned16(out) || (x && !aligned16(x)))
+  if (!u || !s || !out || C % PER || !aligned16(u) || !aligned16(out) || (x && !aligned16(x)) || !aligned16(s) ||
+      (t && !aligned16(t)))
     return sr_fail(SR_EINVAL, "nc_affine: bad arguments");
   const int64_t nv = (int64_t)N * HW * C / PER;
+  if (nv >= 0x7fffffffll) return sr_fail(SR_ETOOBIG, "nc_affine: tensor too large (split the batch)");
+  const FastDiv fcv = make_fastdiv(C / PER), fhw = make_fastdiv((uint32_t)HW * (C / PER));
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(nc_affine_kernel<bf16_t>, dim3(grid_for(nv)), dim3(256), 0, st, (const bf16_t*)x,
-                       (const bf16_t*)u, s, t, N, HW, C, beta, alpha, gamma, (bf16_t*)out);
+                       (const bf16_t*)u, s, t, (uint32_t)nv, fcv, fhw, C, beta, alpha, gamma, (bf16_t*)out);
   else
     hipLaunchKernelGGL(nc_affine_kernel<float>, dim3(grid_for(nv)), dim3(256), 0, st, (const float*)x, (const float*)u,
-                       s, t, N, HW, C, beta, alpha, gamma, (float*)out);
+                       s, t, (uint32_t)nv, fcv, fhw, C, beta, alpha, gamma, (float*)out);
   return sr_check(hipGetLastError(), "nc_affine launch");
 }
 

@@ -53,6 +53,7 @@ struct FwdArgs {
   int tap0;   // 4 for 1x1 (linear) convs: the single tap is the centre one
   int gate_mode;  // 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate)
   void* aux;      // optional store of the pre-activation value (same layout as y)
+  float* colsum;  // optional per-(wave, row chunk) column sums of the stored y (see epilogue_tile)
   int tiles_n, tiles;
   FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
   FastDiv fd_r;                        // divide by in_ps (1 when none)
@@ -111,6 +112,10 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
   // loads: invalid groups read zeros) so their HBM latency overlaps, then compute + store.
   constexpr int IB = (SZ == 2 ? 4 : 2) < IT ? (SZ == 2 ? 4 : 2) : IT;  // groups per load batch
   static_assert(IT % IB == 0, "epilogue batch");
+  // colsum: this thread's 8 channels (cg is fixed: NT % CG == 0) summed over its rows, of the
+  // value as stored (bf16-rounded); reduced over the wave's lanes of the same cg below.
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  static_assert(NT % CG == 0 && 64 % CG == 0, "colsum lane map");
 #pragma unroll 1
   for (int it0 = 0; it0 < IT; it0 += IB) {
   u32x4 gv[IB][NV], rv1[IB][NV], rv2[IB][NV];
@@ -215,11 +220,37 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
       *(u32x4*)((bf16_t*)a.y + dst) = o;
+      if (a.colsum) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cs[2 * j] += bf16_to_f32(o[j] & 0xffff);
+          cs[2 * j + 1] += bf16_to_f32(o[j] >> 16);
+        }
+      }
     } else {
       *(f32x4*)((float*)a.y + dst) = f32x4{v[0], v[1], v[2], v[3]};
       *(f32x4*)((float*)a.y + dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      if (a.colsum) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs[j] += v[j];
+      }
     }
   }
+  }
+  if (a.colsum) {
+    // lanes l, l ^ CG, l ^ 2CG, ... hold the same 8 channels: fixed-order butterfly, then
+    // lane cg writes row (m0 / ROWS) * (NT / 64) + wave of the [parts][Cout] partial matrix.
+    const int lane = tid & 63;
+#pragma unroll
+    for (int off = CG; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
+    const int n = n0 + lane * 8;
+    if (lane < CG && n < a.Cout) {
+      float* dstp = a.colsum + (size_t)((m0 / ROWS) * (NT / 64) + (tid >> 6)) * a.Cout + n;
+      *(f32x4*)dstp = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      *(f32x4*)(dstp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    }
   }
 }
 
@@ -1907,13 +1938,14 @@ __global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, co
   }
 }
 
+// One element (n, ci, tap) of the padded GEMM images of a conv / linear weight (and, for i <
+// Cout, its bias entry): wf [Cout][taps*Cin] forward rows, wd [Cin][taps*Cout] the flipped
+// transposed dgrad rows; row_map / col_map (or the PixelShuffle permutation) give the source
+// output / input channel of each padded row / column (-1: zero padding).
 template <typename T>
-__global__ void prep_kernel(const float* w, const float* bias, int Cout_real, int Cin_real, int Cout, int Cin,
-                            int out_ps, int taps, const int* row_map, const int* col_map, T* wf, T* wd,
-                            float* bias_g) {
-  // one thread per (n, ci, tap) of the padded GEMM weight
+SR_DEV void prep_elem(const float* w, const float* bias, int Cout_real, int Cin_real, int Cout, int Cin, int out_ps,
+                      int taps, const int* row_map, const int* col_map, T* wf, T* wd, float* bias_g, int64_t i) {
   const int64_t total = (int64_t)Cout * Cin * taps;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
   const int cps = Cout_real / r2;
   auto row_of = [&](int n) -> int {
@@ -1937,6 +1969,30 @@ __global__ void prep_kernel(const float* w, const float* bias, int Cout_real, in
     const int co = row_of(n);
     bias_g[n] = (co >= 0 && bias) ? bias[co] : 0.f;
   }
+}
+
+template <typename T>
+__global__ void prep_kernel(const float* w, const float* bias, int Cout_real, int Cin_real, int Cout, int Cin,
+                            int out_ps, int taps, const int* row_map, const int* col_map, T* wf, T* wd,
+                            float* bias_g) {
+  prep_elem<T>(w, bias, Cout_real, Cin_real, Cout, Cin, out_ps, taps, row_map, col_map, wf, wd, bias_g,
+               (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// All of a net's cached GEMM images in one launch (after an optimizer step): block b belongs
+// to the item whose [block_start[k], block_start[k+1]) range holds it.
+template <typename T>
+__global__ void prep_batch_kernel(const sr_prep_item* __restrict__ items, const int* __restrict__ block_start, int n) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;  // last k with block_start[k] <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (block_start[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const sr_prep_item it = items[lo];
+  prep_elem<T>(it.w, it.bias, it.Cout_real, it.Cin_real, it.Cout, it.Cin, it.out_ps, it.ksize == 1 ? 1 : 9,
+               it.row_map, it.col_map, (T*)it.wf, (T*)it.wd, it.bias_g,
+               (int64_t)(b - block_start[lo]) * blockDim.x + threadIdx.x);
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -1983,14 +2039,34 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Kernel family sr_conv3x3_fwd launches for a call (dispatch, kernel names and the
+// epilogue geometry behind colsum all follow this one choice).
+enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128 };
+FwdKind fwd_kind(const FwdArgs& a, bool bf) {
+  if (fwd_use_halo(a, bf)) return FK_HALO;
+  if (bf && !a.out_nchw && a.Cout >= 256 && a.in_up == 1 && !g_disable_big) return FK_BIG;
+  if (a.out_nchw || a.Cout <= 16) return FK_256_16;
+  if (a.Cout <= 32) return FK_256_32;
+  if (a.Cout <= 64) return FK_128_64;
+  return FK_128_128;
+}
+// Rows per epilogue chunk and threads per block of each family: colsum has
+// M / rows * threads / 64 partial rows.
+void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
+  *rows = (k == FK_256_16 || k == FK_256_32) ? 256 : 128;
+  *nt = k == FK_BIG ? 512 : 256;
+}
+
 template <typename T>
 hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
-  if (fwd_use_halo(a, sizeof(T) == 2)) return launch_fwd_halo(a, s);
-  if (sizeof(T) == 2 && !a.out_nchw && a.Cout >= 256 && a.in_up == 1 && !g_disable_big) return launch_fwd_big(a, s);
-  if (a.out_nchw || a.Cout <= 16) return launch_fwd<T, 256, 16, 4, 1>(a, s);
-  if (a.Cout <= 32) return launch_fwd<T, 256, 32, 4, 1>(a, s);
-  if (a.Cout <= 64) return launch_fwd<T, 128, 64, 2, 2>(a, s);
-  return launch_fwd<T, 128, 128, 2, 2>(a, s);
+  switch (fwd_kind(a, sizeof(T) == 2)) {
+    case FK_HALO: return launch_fwd_halo(a, s);
+    case FK_BIG: return launch_fwd_big(a, s);
+    case FK_256_16: return launch_fwd<T, 256, 16, 4, 1>(a, s);
+    case FK_256_32: return launch_fwd<T, 256, 32, 4, 1>(a, s);
+    case FK_128_64: return launch_fwd<T, 128, 64, 2, 2>(a, s);
+    default: return launch_fwd<T, 128, 128, 2, 2>(a, s);
+  }
 }
 
 inline int tile_for(int c) { return c <= 16 ? 16 : c <= 32 ? 32 : c <= 64 ? 64 : 128; }
@@ -2092,13 +2168,52 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
   *kper = kp;
 }
 
+// Shape / flag fields of FwdArgs from a descriptor (no pointers; validated by the caller).
+FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
+  const int SZ = d->dtype == SR_BF16 ? 2 : 4;
+  const int PER = 16 / SZ;
+  const int taps = d->ksize == 1 ? 1 : 9;
+  FwdArgs a{};
+  a.N = d->N; a.H = d->H; a.W = d->W; a.M = d->N * d->H * d->W;
+  a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff; a.in_ps = d->in_ps;
+  a.cpt = d->Cin / PER; a.nkc = taps * a.cpt;
+  a.tap0 = taps == 1 ? 4 : 0;
+  a.gate_mode = d->gate_mode;
+  a.Cout = d->Cout; a.Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout; a.ldw = d->ldw;
+  a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps; a.out_nchw = d->out_nchw;
+  a.act = d->act; a.slope = d->slope; a.alpha = d->alpha;
+  a.ldg = d->ldg; a.gcoff = d->gcoff; a.gate_slope = d->gate_slope;
+  a.ldr = d->ldr; a.rcoff = d->rcoff; a.beta = d->beta;
+  a.ldr2 = d->ldr2; a.r2coff = d->r2coff; a.beta2 = d->beta2;
+  a.rcols = d->rcols > 0 ? d->rcols : d->Cout;
+  a.in_up = d->in_up > 1 ? d->in_up : 1;
+  a.fd_cpt = make_fastdiv(a.cpt > 0 ? a.cpt : 1);
+  a.fd_W = make_fastdiv(d->W > 0 ? d->W : 1);
+  a.fd_H = make_fastdiv(d->H > 0 ? d->H : 1);
+  int cps = 1;
+  if (d->in_ps > 0) cps = d->Cin / (d->in_ps * d->in_ps);
+  if (d->out_ps > 0) cps = d->Cout / (d->out_ps * d->out_ps);
+  a.fd_cps = make_fastdiv(cps > 0 ? cps : 1);
+  a.fd_r = make_fastdiv(d->in_ps > 0 ? d->in_ps : 1);
+  return a;
+}
+
+// Partial rows per image of the colsum output, or 0 when the call cannot produce it.
+int colsum_parts(const sr_conv3x3_desc* d, const FwdArgs& a) {
+  if (d->out_ps || d->out_nchw) return 0;
+  int rows, nt;
+  fwd_epi_geom(fwd_kind(a, d->dtype == SR_BF16), &rows, &nt);
+  const int HW = d->H * d->W;
+  if (HW % rows) return 0;
+  return HW / rows * (nt / 64);
+}
 }  // namespace
 
 extern "C" {
 
 int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
                    const void* gate, const void* res, const void* res2, const float* aff_scale,
-                   const float* aff_shift, void* y, void* aux, void* stream) {
+                   const float* aff_shift, void* y, void* aux, float* colsum, void* stream) {
   if (!d || !x || !w || !y) return sr_fail(SR_EINVAL, "conv3x3_fwd: null pointer");
   const int SZ = d->dtype == SR_BF16 ? 2 : 4;
   const int PER = 16 / SZ;
@@ -2112,63 +2227,48 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   const int up = d->in_up > 1 ? d->in_up : 1;
   if (up > 1 && (d->in_ps > 0 || d->H % up || d->W % up))
     return sr_fail(SR_EINVAL, "conv3x3_fwd: in_up needs H, W divisible by it and no in_ps");
-  const int M = d->N * d->H * d->W;
+  if (d->in_ps > 0 && d->out_ps > 0) return sr_fail(SR_EINVAL, "conv3x3_fwd: in_ps and out_ps exclusive");
+  if (d->in_ps > 0 && (d->Cin / (d->in_ps * d->in_ps)) % PER)
+    return sr_fail(SR_EINVAL, "conv3x3_fwd: shuffled channel count must be a multiple of 8");
+  if (d->out_ps > 0 && (d->Cout / (d->out_ps * d->out_ps)) % PER)
+    return sr_fail(SR_EINVAL, "conv3x3_fwd: shuffled channel count must be a multiple of 8");
+  FwdArgs a = fwd_shape(d);
+  if (colsum && colsum_parts(d, a) == 0)
+    return sr_fail(SR_EINVAL, "conv3x3_fwd: colsum needs a plain store and H*W a multiple of the epilogue rows");
+  const int M = a.M;
   const int r_in = d->in_ps > 0 ? d->in_ps : 1;
   const size_t xb = (size_t)M * r_in * r_in * (size_t)d->ldx * SZ / ((size_t)up * up);
   const size_t wb = (size_t)d->Cout * d->ldw * SZ;
   if (xb >= 0x80000000ull || wb >= 0x80000000ull)
     return sr_fail(SR_ETOOBIG, "conv3x3_fwd: tensor >= 2 GiB (split the batch)");
-  FwdArgs a{};
-  a.x = x; a.w = w; a.bias = bias; a.gate = gate; a.res = res;
-  a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.y = y;
+  a.x = x; a.w = w; a.bias = bias; a.gate = gate; a.res = res; a.res2 = res2;
+  a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.y = y; a.aux = aux; a.colsum = colsum;
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
   a.g_bytes = gate ? (uint32_t)((size_t)M * d->ldg * SZ) : 0;
   a.r_bytes = res ? (uint32_t)((size_t)M * d->ldr * SZ) : 0;
-  a.N = d->N; a.H = d->H; a.W = d->W; a.M = M;
-  a.Cin = d->Cin; a.ldx = d->ldx; a.xcoff = d->xcoff; a.in_ps = d->in_ps;
-  a.cpt = d->Cin / PER; a.nkc = taps * a.cpt;
-  a.tap0 = taps == 1 ? 4 : 0;
-  a.gate_mode = d->gate_mode;
-  a.aux = aux;
-  a.Cout = d->Cout; a.Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout; a.ldw = d->ldw;
-  a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps; a.out_nchw = d->out_nchw;
-  a.act = d->act; a.slope = d->slope; a.alpha = d->alpha;
-  a.ldg = d->ldg; a.gcoff = d->gcoff; a.gate_slope = d->gate_slope;
-  a.ldr = d->ldr; a.rcoff = d->rcoff; a.beta = d->beta;
-  a.res2 = res2;
   a.r2_bytes = res2 ? (uint32_t)((size_t)M * d->ldr2 * SZ) : 0;
-  a.ldr2 = d->ldr2; a.r2coff = d->r2coff; a.beta2 = d->beta2;
-  a.rcols = d->rcols > 0 ? d->rcols : d->Cout;
-  a.in_up = up;
-  a.fd_cpt = make_fastdiv(a.cpt);
-  a.fd_W = make_fastdiv(d->W);
-  a.fd_H = make_fastdiv(d->H);
-  int cps = 1;
-  if (d->in_ps > 0) cps = d->Cin / (d->in_ps * d->in_ps);
-  if (d->out_ps > 0) cps = d->Cout / (d->out_ps * d->out_ps);
-  if (d->in_ps > 0 && d->out_ps > 0) return sr_fail(SR_EINVAL, "conv3x3_fwd: in_ps and out_ps exclusive");
-  if ((d->in_ps > 0 || d->out_ps > 0) && cps % PER)
-    return sr_fail(SR_EINVAL, "conv3x3_fwd: shuffled channel count must be a multiple of 8");
-  a.fd_cps = make_fastdiv(cps);
-  a.fd_r = make_fastdiv(d->in_ps > 0 ? d->in_ps : 1);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = d->dtype == SR_BF16 ? dispatch_fwd<bf16_t>(a, s) : dispatch_fwd<float>(a, s);
   return sr_check(e, "conv3x3_fwd launch");
+}
+
+int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d) {
+  if (!d || d->N <= 0 || d->H <= 0 || d->W <= 0) return 0;
+  return colsum_parts(d, fwd_shape(d));
 }
 
 // Name of the kernel instantiation sr_conv3x3_fwd / sr_conv3x3_wgrad will launch for a
 // descriptor (bench.py traces and rocprof summaries are matched on these names).
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
-  if (bf && !d->out_nchw && d->Cout <= 64 && d->in_up <= 1 && d->in_ps == 0 && d->ksize != 1 && g_variant != 1 &&
-      (d->W == 64 || d->W == 128) && d->H % (256 / d->W) == 0)
-    return "conv3x3_fwd_halo_kernel";
-  if (bf && !d->out_nchw && d->Cout >= 256 && d->in_up <= 1 && !g_disable_big)
-    return g_variant == 2 ? "conv3x3_fwd_big_kernel" : "conv3x3_fwd_pp_kernel";
-  if (d->out_nchw || d->Cout <= 16) return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
-  if (d->Cout <= 32) return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
-  if (d->Cout <= 64) return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
-  return bf ? "conv3x3_fwd_kernel<bf16,128,128>" : "conv3x3_fwd_kernel<f32,128,128>";
+  switch (fwd_kind(fwd_shape(d), bf)) {
+    case FK_HALO: return "conv3x3_fwd_halo_kernel";
+    case FK_BIG: return g_variant == 2 ? "conv3x3_fwd_big_kernel" : "conv3x3_fwd_pp_kernel";
+    case FK_256_16: return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
+    case FK_256_32: return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
+    case FK_128_64: return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
+    default: return bf ? "conv3x3_fwd_kernel<bf16,128,128>" : "conv3x3_fwd_kernel<f32,128,128>";
+  }
 }
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
@@ -2293,6 +2393,23 @@ int sr_conv_prep_mapped(int dtype, int ksize, const float* w, const float* bias,
     hipLaunchKernelGGL(prep_kernel<float>, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, w, bias, Cout_real,
                        Cin_real, Cout, Cin, out_ps, taps, row_map, col_map, (float*)wf, (float*)wd, bias_g);
   return sr_check(hipGetLastError(), "conv_prep launch");
+}
+
+int sr_conv_prep_blocks(const sr_prep_item* it) {
+  const int64_t total = (int64_t)it->Cout * it->Cin * (it->ksize == 1 ? 1 : 9);
+  const int64_t work = total > it->Cout ? total : it->Cout;
+  return (int)((work + 255) / 256);
+}
+
+int sr_conv_prep_batch(int dtype, const sr_prep_item* items, const int* block_start, int n, int total_blocks,
+                       void* stream) {
+  if (!items || !block_start || n <= 0 || total_blocks <= 0) return sr_fail(SR_EINVAL, "conv_prep_batch: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(prep_batch_kernel<bf16_t>, dim3(total_blocks), dim3(256), 0, s, items, block_start, n);
+  else
+    hipLaunchKernelGGL(prep_batch_kernel<float>, dim3(total_blocks), dim3(256), 0, s, items, block_start, n);
+  return sr_check(hipGetLastError(), "conv_prep_batch launch");
 }
 
 int sr_conv3x3_prep(int dtype, const float* w, const float* bias, int Cout_real, int Cin_real, int Cout, int Cin,

@@ -18,6 +18,7 @@ import torch
 from ..archs import build_network
 from ..losses import build_loss
 from ..metrics import calculate_metric
+from ..ops.conv import bump_param_epoch
 from ..utils.flat import FlatParams
 from ..utils.img_util import imwrite, tensor2img
 from ..utils.registry import MODEL_REGISTRY
@@ -112,6 +113,9 @@ class SRModel(BaseModel):
         if self._graph is not None:
             self.optimizer_g.host_step()
             self._graph.replay()
+            # the replay updated the parameters: host-side weight-image caches are now stale
+            # (an eager forward, e.g. validation, rebuilds them in place)
+            bump_param_epoch()
             self.log_dict = self.reduce_loss_dict(self._graph_losses)
             return
         if self.use_graph and self._eager_steps >= 2:

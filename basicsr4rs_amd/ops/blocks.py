@@ -45,6 +45,11 @@ def nc_affine(x, u, s, t, beta, alpha, gamma):
     return out
 
 
+def _colsum_ok(N, H, W, spec, dtype):
+    d = C._desc(dtype, N, H, W, spec.cin_p, spec.cin_p, spec.cout_p, spec.cout, spec.cout_p)
+    return _lib.load().sr_conv3x3_fwd_colsum_parts(d) > 0
+
+
 class _RCAB(torch.autograd.Function):
 
     @staticmethod
@@ -56,45 +61,68 @@ class _RCAB(torch.autograd.Function):
         t = torch.empty(N, H, W, spec1.cout_p, device=x.device, dtype=dtype)
         C.conv_fwd_raw(x, wf1, bg1, t, N, H, W, spec1.cin_p, spec1.cout_p, spec1.cout, act=_lib.ACT_RELU)
         u = torch.empty(N, H, W, spec2.cout_p, device=x.device, dtype=dtype)
-        C.conv_fwd_raw(t, wf2, bg2, u, N, H, W, spec2.cin_p, spec2.cout_p, spec2.cout)
-        pool = channel_reduce(u, scale=1.0 / (H * W))
+        lib = _lib.load()
+        # AdaptiveAvgPool2d(1) of u: per-wave channel partial sums from conv2's epilogue (when the
+        # conv kernel provides them), summed inside the squeeze-MLP kernel
+        cs = _colsum_ok(N, H, W, spec2, dtype)
+        r = C.conv_fwd_raw(t, wf2, bg2, u, N, H, W, spec2.cin_p, spec2.cout_p, spec2.cout, colsum=cs)
+        if cs:
+            parts = r[1]
+        else:
+            parts = torch.empty(N, lib.sr_channel_partials_count(H * W), Cp, device=x.device, dtype=torch.float32)
+            _lib.check(lib.sr_channel_partials(_lib.dtype_code(dtype), _lib.ptr(u), Cp, 0, None, 0, 0, N, H * W, Cp,
+                                               _lib.ptr(parts), _lib.stream()))
         Cr = aw1.shape[0]
-        a1 = aw1.detach().reshape(Cr, -1).contiguous()
-        a2 = aw2.detach().reshape(-1, Cr).contiguous()
+        a1 = aw1.detach().reshape(Cr, -1)
+        a2 = aw2.detach().reshape(-1, Cr)
+        pool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
         h = torch.empty(N, Cr, device=x.device, dtype=torch.float32)
         s = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
-        lib = _lib.load()
         _lib.check(
-            lib.sr_ca_mlp_fwd(_lib.ptr(pool), _lib.ptr(a1), _lib.ptr(ab1.detach() if ab1 is not None else None),
-                              _lib.ptr(a2), _lib.ptr(ab2.detach() if ab2 is not None else None), N, Cp, Cr,
+            lib.sr_ca_mlp_fwd(_lib.ptr(parts), parts.shape[1], 1.0 / (H * W), _lib.ptr(a1),
+                              _lib.ptr(ab1.detach() if ab1 is not None else None), _lib.ptr(a2),
+                              _lib.ptr(ab2.detach() if ab2 is not None else None), N, Cp, Cr, _lib.ptr(pool),
                               _lib.ptr(h), _lib.ptr(s), _lib.stream()))
         y = nc_affine(x, u, s, None, 1.0, rs, 0.0)
         ctx.specs = (spec1, spec2)
         ctx.rs = rs
-        ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, a1, a2, ab1, ab2)
+        ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, t, u, pool, h, s, w1, b1, w2, b2, a1, a2, ab1, ab2 = ctx.saved_tensors
+        x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2 = ctx.saved_tensors
         spec1, spec2 = ctx.specs
         rs = ctx.rs
         dtype = x.dtype
         N, H, W, Cp = x.shape
-        Cr = a1.shape[0]
+        Cr = aw1.shape[0]
+        a1 = aw1.detach().reshape(Cr, -1)
+        a2 = aw2.detach().reshape(-1, Cr)
         dy = dy.to(dtype).contiguous()
         lib = _lib.load()
-        ds = channel_reduce(dy, u, scale=rs)  # dL/ds[n,c] = rs * sum_p dy*u
+        # dL/ds[n,c] = rs * sum_p dy*u: per-chunk dot partials, summed in the MLP backward kernel
+        parts = torch.empty(N, lib.sr_channel_partials_count(H * W), Cp, device=x.device, dtype=torch.float32)
+        _lib.check(lib.sr_channel_partials(_lib.dtype_code(dtype), _lib.ptr(dy), Cp, 0, _lib.ptr(u), Cp, 0, N, H * W,
+                                           Cp, _lib.ptr(parts), _lib.stream()))
         dpool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
-        dA1 = torch.empty_like(a1)
-        dA2 = torch.empty_like(a2)
-        dab1 = torch.empty(Cr, device=x.device, dtype=torch.float32)
-        dab2 = torch.empty(Cp, device=x.device, dtype=torch.float32)
-        scratch = torch.empty(N * (Cp + Cr), device=x.device, dtype=torch.float32)
+        # squeeze-conv gradients: straight into the optimizer's flat .grad views when they exist
+        ca = (aw1, ab1, aw2, ab2)
+        tg = [C.grad_target(p) for p in ca]
+        direct = all(g is not None for g in tg)
+        if direct:
+            dA1, dab1, dA2, dab2 = tg
+        else:
+            dA1, dA2 = torch.empty_like(a1), torch.empty_like(a2)
+            dab1 = torch.empty(Cr, device=x.device, dtype=torch.float32) if ab1 is not None else None
+            dab2 = torch.empty(Cp, device=x.device, dtype=torch.float32) if ab2 is not None else None
         _lib.check(
-            lib.sr_ca_mlp_bwd(_lib.ptr(ds), _lib.ptr(s), _lib.ptr(h), _lib.ptr(pool), _lib.ptr(a1), _lib.ptr(a2), N, Cp,
-                              Cr, _lib.ptr(dpool), _lib.ptr(dA1), _lib.ptr(dab1), _lib.ptr(dA2), _lib.ptr(dab2),
-                              _lib.ptr(scratch), _lib.stream()))
+            lib.sr_ca_mlp_bwd(_lib.ptr(parts), parts.shape[1], rs, _lib.ptr(s), _lib.ptr(h), _lib.ptr(pool),
+                              _lib.ptr(a1), _lib.ptr(a2), N, Cp, Cr, _lib.ptr(dpool), _lib.ptr(dA1), _lib.ptr(dab1),
+                              _lib.ptr(dA2), _lib.ptr(dab2), int(direct), _lib.stream()))
+        if direct:
+            for p in ca:
+                C.grad_ready(p)
         du = nc_affine(None, dy, s, dpool, 0.0, rs, 1.0 / (H * W))
         _, wd1, _ = C.prepared(w1, b1, spec1, dtype)
         _, wd2, _ = C.prepared(w2, b2, spec2, dtype)
@@ -104,8 +132,10 @@ class _RCAB(torch.autograd.Function):
         dx = torch.empty_like(x)
         C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
         dw1, db1 = C.conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, params=(w1, b1))
-        return (dx, dw1, db1, dw2, db2, dA1.reshape(Cr, Cp, 1, 1), dab1 if ab1 is not None else None,
-                dA2.reshape(Cp, Cr, 1, 1), dab2 if ab2 is not None else None, None, None, None)
+        if direct:
+            return dx, dw1, db1, dw2, db2, None, None, None, None, None, None, None
+        return (dx, dw1, db1, dw2, db2, dA1.reshape(Cr, Cp, 1, 1), dab1, dA2.reshape(Cp, Cr, 1, 1), dab2, None, None,
+                None)
 
 
 def rcab(x, conv1, conv2, ca1, ca2, res_scale):

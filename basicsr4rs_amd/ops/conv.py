@@ -12,6 +12,7 @@ to a multiple of 8 (padded channels are exactly zero).  Compute dtype: bf16 when
 autocast is enabled (the reference's AMP path, basicsr/models/srrs_model.py:28-31, uses
 fp16; bf16 is the documented divergence), fp32 otherwise.
 """
+import ctypes
 import math
 
 import torch
@@ -57,25 +58,94 @@ class ConvSpec:
             self.cout_p = cout
 
 
-def prepared(weight, bias, spec, dtype):
-    """GEMM images of a conv parameter pair, cached until the parameter changes."""
-    key = (weight._version, _PARAM_EPOCH[0], dtype, spec.cin_p, spec.cout_p, spec.out_ps, weight.data_ptr())
-    cache = getattr(weight, '_sr_prep', None)
-    if cache is not None and cache[0] == key:
-        return cache[1]
-    dev = weight.device
-    wf = torch.empty(spec.cout_p, 9 * spec.cin_p, device=dev, dtype=dtype)
-    wd = torch.empty(spec.cin_p, 9 * spec.cout_p, device=dev, dtype=dtype)
-    bg = torch.empty(spec.cout_p, device=dev, dtype=torch.float32)
+class _Prep:
+    """Cached GEMM images of one (weight, layout) pair and the arguments that rebuild them."""
+    __slots__ = ('weight', 'bias', 'dtype', 'shape', 'maps', 'val', 'key', 'used')
+
+
+_PREP_ALL = {}  # (id(weight), static key) -> _Prep
+_PREP_TABLE = {}  # dtype -> (entries, device item table, device block starts, total blocks)
+
+
+def prepared_images(weight, bias, dtype, shape, maps=(None, None), tag=''):
+    """GEMM images (wf, wd, bias_g) of a conv / linear weight, cached until it changes.
+
+    ``shape`` = (cout_real, cin_real, cout_p, cin_p, out_ps, ksize); ``maps`` = device
+    (row_map, col_map) or Nones.  A stale entry is rebuilt IN PLACE (captured HIP graphs keep
+    pointing at the same buffers); after an optimizer step ``refresh_prepared`` rebuilds every
+    image used in the previous step in one launch instead of one per parameter."""
+    skey = (dtype, shape, weight.data_ptr(), tag)
+    ents = weight.__dict__.setdefault('_sr_prep', {})
+    dyn = (weight._version, -1 if bias is None else bias._version, _PARAM_EPOCH[0])
+    e = ents.get(skey)
+    if e is not None and e.key == dyn:
+        e.used = _PARAM_EPOCH[0]
+        return e.val
+    cout_real, cin_real, cout_p, cin_p, out_ps, ksize = shape
+    if e is None:
+        dev = weight.device
+        taps = 9 if ksize == 3 else 1
+        e = _Prep()
+        e.weight, e.bias, e.dtype, e.shape, e.maps = weight, bias, dtype, shape, maps
+        e.val = (torch.empty(cout_p, taps * cin_p, device=dev, dtype=dtype),
+                 torch.empty(cin_p, taps * cout_p, device=dev, dtype=dtype),
+                 torch.empty(cout_p, device=dev, dtype=torch.float32))
+        ents[skey] = e
+        _PREP_ALL[(id(weight), skey)] = e
+        _PREP_TABLE.pop(dtype, None)
+    wf, wd, bg = e.val
     lib = _lib.load()
     _lib.check(
-        lib.sr_conv3x3_prep(_lib.dtype_code(dtype), _lib.ptr(weight.detach()),
-                            _lib.ptr(bias.detach() if bias is not None else None), spec.cout, spec.cin,
-                            spec.cout_p, spec.cin_p, spec.out_ps, _lib.ptr(wf), _lib.ptr(wd), _lib.ptr(bg),
-                            _lib.stream()))
-    val = (wf, wd, bg)
-    weight._sr_prep = (key, val)
-    return val
+        lib.sr_conv_prep_mapped(_lib.dtype_code(dtype), ksize, _lib.ptr(weight.detach()),
+                                _lib.ptr(bias.detach() if bias is not None else None), cout_real, cin_real, cout_p,
+                                cin_p, out_ps, _lib.ptr(maps[0]), _lib.ptr(maps[1]), _lib.ptr(wf), _lib.ptr(wd),
+                                _lib.ptr(bg), _lib.stream()))
+    e.key, e.used = dyn, _PARAM_EPOCH[0]
+    return e.val
+
+
+def prepared(weight, bias, spec, dtype):
+    """GEMM images of a 3x3 conv parameter pair (wf, wd, bias in GEMM order)."""
+    return prepared_images(weight, bias, dtype, (spec.cout, spec.cin, spec.cout_p, spec.cin_p, spec.out_ps, 3))
+
+
+def refresh_prepared():
+    """Rebuild, in one launch per dtype, the GEMM images of every weight used during the epoch
+    that just ended (call right after ``bump_param_epoch`` by an optimizer step), and re-key
+    them to the new epoch so the next forward finds them current.  Graph-capturable."""
+    ep = _PARAM_EPOCH[0]
+    live = [e for e in _PREP_ALL.values() if e.used == ep - 1]
+    if not live:
+        return
+    lib = _lib.load()
+    by_dt = {}
+    for e in live:
+        by_dt.setdefault(e.dtype, []).append(e)
+    for dt, ents in by_dt.items():
+        tab = _PREP_TABLE.get(dt)
+        if tab is None or tab[0] != ents:
+            items = (_lib.PrepItem * len(ents))()
+            starts = [0]
+            for it, e in zip(items, ents):
+                cr, ci, cp, cip, ops, ks = e.shape
+                wf, wd, bg = e.val
+                it.w, it.bias = e.weight.data_ptr(), (e.bias.data_ptr() if e.bias is not None else None)
+                it.Cout_real, it.Cin_real, it.Cout, it.Cin, it.out_ps, it.ksize = cr, ci, cp, cip, ops, ks
+                it.row_map = e.maps[0].data_ptr() if e.maps[0] is not None else None
+                it.col_map = e.maps[1].data_ptr() if e.maps[1] is not None else None
+                it.wf, it.wd, it.bias_g = wf.data_ptr(), wd.data_ptr(), bg.data_ptr()
+                starts.append(starts[-1] + lib.sr_conv_prep_blocks(ctypes.byref(it)))
+            dev = ents[0].weight.device
+            raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8).to(dev)
+            st = torch.tensor(starts, dtype=torch.int32).to(dev)
+            tab = (list(ents), raw, st, starts[-1])
+            _PREP_TABLE[dt] = tab
+        _, raw, st, total = tab
+        _lib.check(lib.sr_conv_prep_batch(_lib.dtype_code(dt), _lib.ptr(raw), _lib.ptr(st), len(ents), total,
+                                          _lib.stream()))
+    for e in live:
+        e.key = (e.weight._version, -1 if e.bias is None else e.bias._version, ep)
+        e.used = ep
 
 
 def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
@@ -96,8 +166,11 @@ def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
 
 
 def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res=None, aff_scale=None,
-                 aff_shift=None, res2=None, aux=None, **kw):
-    """Launch sr_conv3x3_fwd on already-prepared GEMM weights (shapes checked here)."""
+                 aff_shift=None, res2=None, aux=None, colsum=False, **kw):
+    """Launch sr_conv3x3_fwd on already-prepared GEMM weights (shapes checked here).
+
+    ``colsum=True`` also returns the [N, P, cout] fp32 partial channel sums of y (as stored;
+    summed over P they are the per-image channel sums): ``(y, parts)``."""
     assert x.is_contiguous() and y.is_contiguous()
     ldx = kw.pop('ldx', x.shape[-1])
     ldy = kw.pop('ldy', y.shape[-1] if not kw.get('out_nchw') else 0)
@@ -112,13 +185,19 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     lib = _lib.load()
     M = N * H * W
     taps = 9 if d.ksize == 3 else 1
+    parts = None
+    if colsum:
+        P = lib.sr_conv3x3_fwd_colsum_parts(d)
+        if P <= 0:
+            raise ValueError(f'conv3x3_fwd: no fused channel sums for this call (N={N} H={H} W={W} cout={cout})')
+        parts = torch.empty(N, P, cout, device=y.device, dtype=torch.float32)
     with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * taps * cin * cout_real,
                      x.element_size() * (M * (cin + cout) + taps * cin * cout)):
         _lib.check(
             lib.sr_conv3x3_fwd(d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res),
                                _lib.ptr(res2), _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.ptr(aux),
-                               _lib.stream()))
-    return y
+                               _lib.ptr(parts), _lib.stream()))
+    return (y, parts) if colsum else y
 
 
 _GRAD_READY = {}  # id(param) -> callbacks run when a kernel has written the param's gradient

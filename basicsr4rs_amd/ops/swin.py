@@ -72,23 +72,10 @@ def plain_spec(cin, cout):
 
 
 def prepared_linear(weight, bias, spec, dtype):
-    key = (weight._version, C._PARAM_EPOCH[0], dtype, spec.cin_p, spec.cout_p, weight.data_ptr(), 'lin')
-    cache = getattr(weight, '_sr_prep', None)
-    if cache is not None and cache[0] == key:
-        return cache[1]
-    dev = weight.device
-    rm, cm, _, _ = spec.maps(dev)
-    wf = torch.empty(spec.cout_p, spec.cin_p, device=dev, dtype=dtype)
-    wd = torch.empty(spec.cin_p, spec.cout_p, device=dev, dtype=dtype)
-    bg = torch.empty(spec.cout_p, device=dev, dtype=torch.float32)
-    lib = _lib.load()
-    _lib.check(
-        lib.sr_conv_prep_mapped(_lib.dtype_code(dtype), 1, _lib.ptr(weight.detach()),
-                                _lib.ptr(bias.detach() if bias is not None else None), spec.cout, spec.cin,
-                                spec.cout_p, spec.cin_p, 0, _lib.ptr(rm), _lib.ptr(cm), _lib.ptr(wf), _lib.ptr(wd),
-                                _lib.ptr(bg), _lib.stream()))
-    weight._sr_prep = (key, (wf, wd, bg))
-    return wf, wd, bg
+    """GEMM images of an nn.Linear through the padded-head index maps (1x1 conv layout)."""
+    rm, cm, _, _ = spec.maps(weight.device)
+    return C.prepared_images(weight, bias, dtype, (spec.cout, spec.cin, spec.cout_p, spec.cin_p, 0, 1), (rm, cm),
+                             tag='lin')
 
 
 def linear_fwd(x, wf, bg, spec, N, H, W, **kw):

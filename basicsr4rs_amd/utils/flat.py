@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _lib
-from ..ops.conv import bump_param_epoch, on_grad_ready
+from ..ops.conv import bump_param_epoch, on_grad_ready, refresh_prepared
 
 
 def _params(module):
@@ -110,6 +110,7 @@ class FusedAdam(torch.optim.Optimizer):
                                 _lib.ptr(self.hyper), float(b1), float(b2), float(g['eps']), float(ema_decay),
                                 _lib.stream()))
         bump_param_epoch()
+        refresh_prepared()  # the next forward's GEMM weight images, one launch
 
     @torch.no_grad()
     def step(self, closure=None, ema=None, ema_decay=0.0):

@@ -80,10 +80,15 @@ typedef struct sr_conv3x3_desc {
 
 /* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.
  * act: SR_ACT_* or 3 = GELU (exact erf).  aux (may be NULL): also store the pre-activation
- * value conv(x, w) + bias in y's layout (GELU backward). */
+ * value conv(x, w) + bias in y's layout (GELU backward).  colsum (may be NULL): fp32
+ * [N * P][Cout] partial channel sums of y as stored, P = sr_conv3x3_fwd_colsum_parts(d) rows per
+ * image, sum_p colsum[n*P + p][c] = sum over image n's pixels of y[n, pixel, c] -- RCAN's
+ * AdaptiveAvgPool2d(1) (rcan_arch.py:19) fused into the conv that produces its input. */
 int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const float* bias,
                    const void* gate, const void* res, const void* res2, const float* aff_scale,
-                   const float* aff_shift, void* y, void* aux, void* stream);
+                   const float* aff_shift, void* y, void* aux, float* colsum, void* stream);
+/* Partial rows per image of sr_conv3x3_fwd's colsum for this descriptor (0: not available). */
+int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d);
 
 /* Name of the GPU kernel that sr_conv3x3_fwd / sr_conv3x3_wgrad would launch for a
  * descriptor (static string; for traces and profiler summaries). */
@@ -125,6 +130,25 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
 int sr_conv3x3_prep(int dtype, const float* w, const float* bias, int Cout_real, int Cin_real,
                     int Cout, int Cin, int out_ps, void* wf, void* wd, float* bias_g,
                     void* stream);
+/* One conv / linear weight of a batched GEMM-image preparation (same meaning as the arguments
+ * of sr_conv_prep_mapped; ksize 1 or 3). */
+typedef struct {
+  const float* w;
+  const float* bias;
+  int Cout_real, Cin_real, Cout, Cin, out_ps, ksize;
+  const int* row_map;
+  const int* col_map;
+  void* wf;
+  void* wd;
+  float* bias_g;
+} sr_prep_item;
+/* 256-thread blocks item needs (host helper for building block_start). */
+int sr_conv_prep_blocks(const sr_prep_item* item);
+/* sr_conv_prep_mapped for n items in ONE launch: items and block_start (n + 1 prefix sums of
+ * sr_conv_prep_blocks, block_start[n] = total_blocks) in device memory, all items of dtype.
+ * Replaces the per-parameter re-preparation after every optimizer step. */
+int sr_conv_prep_batch(int dtype, const sr_prep_item* items, const int* block_start, int n, int total_blocks,
+                       void* stream);
 /* General form: ksize 1 or 3; row_map[n] (n < Cout) = parameter row of GEMM column n or -1
  * (zero row), col_map[k] (k < Cin) = parameter column of GEMM input channel k or -1; NULL maps
  * = identity (+ out_ps permutation).  nn.Linear weights are [out][in] = 1x1 conv weights. */
@@ -180,14 +204,22 @@ int sr_bilinear_up_add(const float* x, int N, int C, int H, int W, int s, const 
 size_t sr_channel_reduce_workspace(int N, int HW, int C);
 int sr_channel_reduce(int dtype, const void* a, int lda, int acoff, const void* b, int ldb, int bcoff, int N,
                       int HW, int C, float scale, float* out, void* workspace, size_t ws_bytes, void* stream);
-/* RCAN squeeze MLP: h = relu(W1 pool + b1), s = sigmoid(W2 h + b2); W1 [Cr][C], W2 [C][Cr]
- * (the two 1x1 convs of rcan_arch.py:19-20). */
-int sr_ca_mlp_fwd(const float* pool, const float* w1, const float* b1, const float* w2, const float* b2, int N,
-                  int C, int Cr, float* h, float* s, void* stream);
-/* Its backward for the batch: ds = dL/ds -> dpool, dW1, db1, dW2, db2 (scratch: N*(C+Cr) floats). */
-int sr_ca_mlp_bwd(const float* ds, const float* s, const float* h, const float* pool, const float* w1,
-                  const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1, float* dw2,
-                  float* db2, float* scratch, void* stream);
+/* First pass of sr_channel_reduce only: parts[n][p][c] partial sums (dots) over pixel chunks,
+ * P = sr_channel_partials_count(HW) chunks per image (the consumer sums them). */
+int sr_channel_partials_count(int HW);
+int sr_channel_partials(int dtype, const void* a, int lda, int acoff, const void* b, int ldb, int bcoff, int N,
+                        int HW, int C, float* parts, void* stream);
+/* RCAN squeeze MLP (the two 1x1 convs of rcan_arch.py:19-20): pool[n][c] = scale * sum_p
+ * parts[n*P + p][c] (P = 1, scale = 1: parts is the pooled vector), h = relu(W1 pool + b1),
+ * s = sigmoid(W2 h + b2); W1 [Cr][C], W2 [C][Cr]. */
+int sr_ca_mlp_fwd(const float* parts, int P, float scale, const float* w1, const float* b1, const float* w2,
+                  const float* b2, int N, int C, int Cr, float* pool, float* h, float* s, void* stream);
+/* Its backward for the batch: ds[n][c] = scale * sum_p parts[n*P + p][c] = dL/ds -> dpool, dW1,
+ * db1, dW2, db2 (db1/db2 may be NULL); accumulate = 1 adds the parameter gradients into
+ * dw1/db1/dw2/db2 (the optimizer's gradient views) instead of storing them. */
+int sr_ca_mlp_bwd(const float* parts, int P, float scale, const float* s, const float* h, const float* pool,
+                  const float* w1, const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1,
+                  float* dw2, float* db2, int accumulate, void* stream);
 /* out = beta*x + alpha*u*s[n,c] + gamma*t[n,c] on dense NHWC [N,HW,C] (x, t may be NULL):
  * RCAB tail x + rs*u*s and its backward rs*dout*s + dpool/HW. */
 int sr_nc_affine(int dtype, const void* x, const void* u, const float* s, const float* t, int N, int HW, int C,

@@ -32,16 +32,33 @@ def test_library_exports_every_header_symbol():
 
 def test_invalid_arguments_raise():
     lib = _lib.load()
-    rc = lib.sr_conv3x3_fwd(None, None, None, None, None, None, None, None, None, None, None, None)
+    rc = lib.sr_conv3x3_fwd(None, None, None, None, None, None, None, None, None, None, None, None, None)
     assert rc == -1 and b'null' in lib.sr_last_error()
     with pytest.raises(RuntimeError, match='null'):
         _lib.check(rc)
     d = _lib.ConvDesc()
     d.dtype, d.N, d.H, d.W, d.Cin, d.ldx, d.Cout, d.ldw, d.ldy = 1, 1, 4, 4, 12, 12, 16, 108, 16
     dummy = ctypes.c_void_p(16)
-    rc = lib.sr_conv3x3_fwd(d, dummy, dummy, None, None, None, None, None, None, dummy, None, None)
+    rc = lib.sr_conv3x3_fwd(d, dummy, dummy, None, None, None, None, None, None, dummy, None, None, None)
     assert rc == -1 and b'multiples of 8' in lib.sr_last_error()
     assert lib.sr_pixel_shuffle_nchw(0, dummy, 1, 3, 4, 4, 2, dummy, None) == -1  # C % r^2 != 0
+
+
+def test_colsum_geometry():
+    """Host-side kernel choice behind the fused channel sums (no GPU launch)."""
+    from basicsr4rs_amd.ops import conv as C
+    lib = _lib.load()
+    bf = torch.bfloat16
+    # RCAN body conv: narrow halo kernel, 128-row epilogue chunks x 4 waves
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 32, 64, 64, 64, 64, 64, 64, 64)) == 4096 // 128 * 4
+    # EDSR-L body conv: 256x256 phase-interleaved kernel, 8 waves per 128-row chunk
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 32, 64, 64, 256, 256, 256, 256, 256)) == 4096 // 128 * 8
+    # Cout 16: 256-row chunks of 4 waves
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 2, 16, 16, 64, 64, 16, 16, 16)) == 1 * 4
+    # pixel-shuffled store and H*W not a multiple of the chunk: unavailable
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 2, 16, 16, 64, 64, 256, 256, 64, out_ps=2)) == 0
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 2, 10, 10, 64, 64, 64, 64, 64)) == 0
+    assert lib.sr_channel_partials_count(4096) == 16 and lib.sr_channel_partials_count(100) == 1
 
 
 def test_cpu_tensors_refused():

@@ -310,3 +310,66 @@ def test_fwd_halo_vs_fp64(cuda, shape, epi):
     assert outs[0][..., :16].abs().max().item() == 0 and outs[0][..., 16 + cout:].abs().max().item() == 0
     if cin == 64:
         assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize('case', [(torch.bfloat16, 2, 8, 64, 64, 64), (torch.bfloat16, 2, 16, 16, 64, 64),
+                                  (torch.float32, 2, 16, 16, 64, 64), (torch.bfloat16, 1, 16, 16, 256, 256),
+                                  (torch.bfloat16, 2, 16, 16, 64, 16), (torch.bfloat16, 1, 8, 128, 64, 32)])
+def test_fwd_colsum_matches_output(cuda, case):
+    """Fused per-image channel sums (RCAN avg-pool input) of every conv kernel family: summed
+    over their partial rows they equal the channel sums of y as stored."""
+    dt, N, H, W, cin, cout = case
+    torch.manual_seed(5)
+    lib = _lib.load()
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    spec = C.ConvSpec(cin, cout)
+    wf, _, bg = C.prepared(conv.weight, conv.bias, spec, dt)
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+    d = C._desc(dt, N, H, W, cin, cin, cout, cout, cout)
+    P = lib.sr_conv3x3_fwd_colsum_parts(d)
+    assert P > 0
+    y2, parts = C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, act=_lib.ACT_RELU, colsum=True)
+    assert parts.shape == (N, P, cout)
+    ref = y.double().sum((1, 2))
+    got = parts.double().sum(1)
+    tol = 1e-5 * y.double().abs().sum((1, 2)).max().item() + 1e-6
+    assert (got - ref).abs().max().item() <= tol
+
+
+def test_refresh_prepared_matches_fresh_prep(cuda):
+    """The one-launch rebuild of every cached weight image after an optimizer step (conv,
+    pixel-shuffled conv, mapped linear) equals per-weight preparation, and re-keys the cache."""
+    from basicsr4rs_amd.ops import swin as SW
+    torch.manual_seed(6)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    c1, c2 = nn.Conv2d(64, 64, 3, 1, 1).to(cuda), nn.Conv2d(64, 256, 3, 1, 1).to(cuda)
+    lin = nn.Linear(180, 540).to(cuda)
+    s1, s2 = C.ConvSpec(64, 64), C.ConvSpec(64, 256, out_ps=2)
+    ls = SW.qkv_spec(180, 6, 32)
+    C.prepared(c1.weight, c1.bias, s1, dt)
+    C.prepared(c2.weight, c2.bias, s2, dt)
+    SW.prepared_linear(lin.weight, lin.bias, ls, dt)
+    with torch.no_grad():  # an optimizer writing behind autograd's back (no version bump)
+        for m in (c1, c2, lin):
+            m.weight.data.mul_(-1.5).add_(0.25)
+            m.bias.data.add_(1.0)
+    C.bump_param_epoch()
+    C.refresh_prepared()
+    got = [C.prepared(c1.weight, c1.bias, s1, dt), C.prepared(c2.weight, c2.bias, s2, dt),
+           SW.prepared_linear(lin.weight, lin.bias, ls, dt)]
+    rm, cm, _, _ = ls.maps(cuda)
+    for (w, b, shape, maps), imgs in zip([(c1.weight, c1.bias, (64, 64, 64, 64, 0, 3), (None, None)),
+                                          (c2.weight, c2.bias, (256, 64, 256, 64, 2, 3), (None, None)),
+                                          (lin.weight, lin.bias, (540, 180, ls.cout_p, ls.cin_p, 0, 1), (rm, cm))],
+                                         got):
+        cr, ci, cp, cip, ops, ks = shape
+        taps = 9 if ks == 3 else 1
+        wf = torch.empty(cp, taps * cip, device=cuda, dtype=dt)
+        wd = torch.empty(cip, taps * cp, device=cuda, dtype=dt)
+        bg = torch.empty(cp, device=cuda)
+        _lib.check(lib.sr_conv_prep_mapped(_lib.dtype_code(dt), ks, _lib.ptr(w.detach()), _lib.ptr(b.detach()), cr, ci,
+                                           cp, cip, ops, _lib.ptr(maps[0]), _lib.ptr(maps[1]), _lib.ptr(wf),
+                                           _lib.ptr(wd), _lib.ptr(bg), _lib.stream()))
+        assert torch.equal(imgs[0], wf) and torch.equal(imgs[1], wd) and torch.equal(imgs[2], bg)
