@@ -260,12 +260,16 @@ def window_attention_core(qkv, nH, ws, shift, scale, table):
     return t
 
 
-def swin_block(x, sd, p, hw, nH, ws, shift):
-    """SwinTransformerBlock.forward in eval mode (swinir_arch.py:283-323), DropPath = identity."""
+def swin_block(x, sd, p, hw, nH, ws, shift, res=None):
+    """SwinTransformerBlock.forward in eval mode (swinir_arch.py:283-323), DropPath = identity.
+    ``res``: the block's constructor input_resolution (img_size / patch_size); the no-shift /
+    shrunken-window rule (swinir_arch.py:234-237) is decided on it, not on the runtime size
+    ``hw`` (which only sets the shapes and the shift mask, :315-318)."""
     h, w = hw
     b, _, c = x.shape
-    if min(hw) <= ws:
-        shift, ws = 0, min(hw)
+    res = hw if res is None else res
+    if min(res) <= ws:
+        shift, ws = 0, min(res)
     sc = x
     t = _ln(x, sd, f'{p}.norm1').view(b, h, w, c)
     if shift > 0:
@@ -290,6 +294,9 @@ def swinir(sd, x, cfg):
     mean = torch.tensor((0.4488, 0.4371, 0.4040)).view(1, 3, 1, 1) if in_ch == 3 else torch.zeros(1, 1, 1, 1)
     x = (x - mean) * img_range
     b, _, h, w = x.shape
+    img = cfg.get('img_size', 64)
+    img = (img, img) if isinstance(img, int) else tuple(img)
+    res = (img[0] // cfg.get('patch_size', 1), img[1] // cfg.get('patch_size', 1))
 
     def features(f):
         t = f.flatten(2).transpose(1, 2)
@@ -299,7 +306,7 @@ def swinir(sd, x, cfg):
             g = t
             for j in range(d):
                 g = swin_block(g, sd, f'layers.{i}.residual_group.blocks.{j}', (h, w), heads[i], ws,
-                               0 if j % 2 == 0 else ws // 2)
+                               0 if j % 2 == 0 else ws // 2, res=res)
             g = g.transpose(1, 2).reshape(b, -1, h, w)
             t = conv(g, sd, f'layers.{i}.conv').flatten(2).transpose(1, 2) + t
         t = _ln(t, sd, 'norm')

@@ -223,3 +223,34 @@ def test_fused_bias_act_abi(cuda, shape):
     gg = _fba(dyt, bt, y, 3, 1, 0.2, 2**0.5)
     assert rel(gg, O.fused_bias_act(dy, b, ref, 3, 1, 0.2, 2**0.5)) < 1e-6
     assert float(_fba(dyt, bt, y, 3, 2, 0.2, 2**0.5).abs().max()) == 0.0
+
+
+@pytest.mark.parametrize('shape', [(4, 32, 8, 8), (16, 512), (2, 6, 130)])
+def test_fused_leaky_relu_module_and_double_backward(cuda, shape):
+    """Python surface of basicsr/ops/fused_act/fused_act.py:30-95: FusedLeakyReLU forward,
+    input/bias gradients, and the gradient of (grad_input, grad_bias) w.r.t. grad_output."""
+    from basicsr4rs_amd.ops.fused_act import FusedLeakyReLU, FusedLeakyReLUFunctionBackward, fused_leaky_relu
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal(shape).astype(np.float32)
+    b = rng.standard_normal(shape[1]).astype(np.float32)
+    dy = rng.standard_normal(shape).astype(np.float32)
+    m = FusedLeakyReLU(shape[1]).to(cuda)
+    with torch.no_grad():
+        m.bias.copy_(torch.tensor(b))
+    xt = torch.tensor(x, device=cuda, requires_grad=True)
+    y = m(xt)
+    ref = O.fused_bias_act(x, b, None, 3, 0, 0.2, 2**0.5)
+    assert rel(y, ref) < 1e-6
+    y.backward(torch.tensor(dy, device=cuda))
+    gi, gb = O.fused_lrelu_backward(dy, ref, 0.2, 2**0.5)
+    assert rel(xt.grad, gi) < 1e-6 and rel(m.bias.grad, gb) < 1e-5
+    # second order: d/d(dy) of <g_in, w1> + <g_b, w2> = fused_bias_act(w1, w2, out, 3, 1)
+    w1 = rng.standard_normal(shape).astype(np.float32)
+    w2 = rng.standard_normal(shape[1]).astype(np.float32)
+    dyt = torch.tensor(dy, device=cuda, requires_grad=True)
+    g_in, g_b = FusedLeakyReLUFunctionBackward.apply(dyt, y.detach(), 0.2, 2**0.5)
+    (gg,) = torch.autograd.grad((g_in * torch.tensor(w1, device=cuda)).sum() + (g_b * torch.tensor(w2, device=cuda)).sum(),
+                                dyt)
+    assert rel(gg, O.fused_bias_act(w1, w2, ref, 3, 1, 0.2, 2**0.5)) < 1e-5
+    # functional form == module
+    assert torch.equal(fused_leaky_relu(xt.detach(), m.bias.detach()), y.detach())
