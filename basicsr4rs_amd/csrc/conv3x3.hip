@@ -577,7 +577,7 @@ SR_DEV void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool FAST>
+template <bool FAST, int DBG = 0>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
   constexpr int CSTR = 256 + 4;
   constexpr int SMEM = 128 * CSTR * 4;  // epilogue half tile; >= 2 x 64 KB stages
@@ -731,6 +731,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
         fb[g][kk][j] = *(const u32x4*)(Bs + swz128(wc * 32 + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
   };
   auto mma = [&](int h, int g) {
+    if constexpr (DBG == 2) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -759,7 +760,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     read_b(buf, 0);
     if (more) {
       if constexpr (FAST) k_advance();
-      issue_a(t + 1, 0);
+      if (DBG != 1) issue_a(t + 1, 0);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -770,7 +771,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     // phase 2: quadrant (0,1); issue B0(t+1); retire A1(t)
     read_b(buf, 1);
     if (more) {
-      issue_b(t + 1, 0);
+      if (DBG != 1) issue_b(t + 1, 0);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -780,13 +781,13 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     pp_barrier();
     // phase 3: quadrant (1,1); issue B1(t+1)
     read_a(buf, 1);
-    if (more) issue_b(t + 1, 1);
+    if (more) if (DBG != 1) issue_b(t + 1, 1);
     pp_barrier();
     mma(1, 1);
     pp_barrier();
     // phase 4: quadrant (1,0); issue A1(t+1); retire A0(t+1), B0(t+1)
     if (more) {
-      issue_a(t + 1, 1);
+      if (DBG != 1) issue_a(t + 1, 1);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     }
     pp_barrier();
@@ -794,6 +795,210 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     pp_barrier();
   }
   if (!wr) pp_barrier();  // balance the stagger
+
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CSTR + g * 128 + wc * 32 + j * 16 + (lane & 15)] =
+                acc[h][g][i][j][r];
+    __syncthreads();
+    epilogue_tile<bf16_t, 128, 256, 512>(a, Cs, CSTR, m0 + h * 128, n0, tid);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// conv3x3_fwd_pph_kernel: the phase-interleaved 256x256 schedule of conv3x3_fwd_pp_kernel
+// with the A operand formed from input HALO rows instead of one DMA'd half-tile per tap.
+// For W == 64 a 256-pixel tile is 4 whole image rows; per 64-channel chunk the 6 rows
+// y0-1 .. y0+4 (64 px x 128 B, XOR-swizzled) are staged in LDS once and all 9 taps read
+// their A fragments from them (the left/right image border reads a zero region).  The K
+// loop is chunk-major (chunk, tap): per K-step only the two B half-tiles (2 x 16 KB) and ONE
+// halo piece per wave (the next chunk's rows, streamed into free row slots) are issued, vs.
+// 4 half-tiles before -- ~40 % fewer L2->LDS bytes and DMA issues per MFMA.
+// Row slots: 11 x 8 KB ring, slot(chunk c, row r) = (6c + r) mod 11: the next chunk's rows
+// 0-4 go to the 5 free slots, its row 5 to the current row 0's slot (dead after the
+// ty = 0 taps, steps 0-2; it is issued at step 5).  Per K-step issue order: B0(t+1) [ph1],
+// B1(t+1) [ph2], halo/dummy piece [ph3]; counted waits vmcnt(3) at ph1 (retires B1(t)) and
+// ph4 (retires B0(t+1) and the previous halo piece).  Last step: dummy pieces keep the counts.
+// ------------------------------------------------------------------------------------
+constexpr int PPH_ROWB = 66 * 128;  // px -1 .. 64 (the two border columns stay zero)
+constexpr int PPH_NSLOT = 11;
+constexpr int PPH_SLOT0 = 2 * 32768;
+constexpr int PPH_ZERO = PPH_SLOT0 + PPH_NSLOT * PPH_ROWB;
+constexpr int PPH_LDS = PPH_ZERO + 1024;
+static_assert(PPH_LDS <= 160 * 1024, "pph LDS");
+
+template <int DBG = 0>
+__global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
+  constexpr int CSTR = 256 + 4;
+  constexpr int SMEM = PPH_LDS > 128 * CSTR * 4 ? PPH_LDS : 128 * CSTR * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (int)(tile / a.tiles_n) * 256;
+  const int n0 = (int)(tile % a.tiles_n) * 256;
+  const int HW = a.H * 64;
+  const int img = m0 / HW;
+  const int y0 = (m0 - img * HW) >> 6;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
+
+  const int c = (lane & 7) ^ (lane >> 3);  // logical 16-B chunk of a B row this lane moves
+  const int ch_h = (lane & 7) ^ (((lane >> 3) + 1) & 7);  // halo: slot px index = px + 1
+  uint32_t boff[4];
+  bool bval[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int n = n0 + (k >> 1) * 128 + w * 16 + (k & 1) * 8 + (lane >> 3);
+    bval[k] = n < a.Cout;
+    boff[k] = (uint32_t)(n * a.ldw) * 2u + (uint32_t)c * 16u;
+  }
+  // halo piece of wave w: pixels 8w .. 8w+7 of a row
+  const uint32_t hlane = (uint32_t)((8 * w + (lane >> 3)) * a.ldx + a.xcoff) * 2u + (uint32_t)ch_h * 16u;
+  const uint32_t rowb = (uint32_t)(64 * a.ldx) * 2u;
+
+  if (tid < 64) *(u32x4*)(smem + PPH_ZERO + tid * 16) = u32x4{0u, 0u, 0u, 0u};
+  if (tid < PPH_NSLOT * 16) {  // border columns (slot px index 0 and 65) of every slot
+    const int sl = tid >> 4, e = tid & 15;
+    *(u32x4*)(smem + PPH_SLOT0 + sl * PPH_ROWB + (e < 8 ? 0 : 65 * 128) + (e & 7) * 16) = u32x4{0u, 0u, 0u, 0u};
+  }
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunk = a.Cin >> 6;
+  const int nk = nchunk * 9;
+  auto issue_row = [&](int cc, int rr) {  // row rr (0..5) of chunk cc into its slot
+    const int y = y0 - 1 + rr;
+    const int slot = (6 * cc + rr) % PPH_NSLOT;
+    glds16(xr, smem + PPH_SLOT0 + slot * PPH_ROWB + 128 + w * 1024,
+           (unsigned)y < (unsigned)a.H ? (uint32_t)(img * a.H + y) * rowb + hlane + (uint32_t)cc * 128u : SR_OOB);
+  };
+  auto issue_dummy = [&]() { glds16(xr, smem + PPH_ZERO, SR_OOB); };
+  // B half g of K-step ks = (chunk ks / 9, tap ks % 9): weight columns tap*Cin + chunk*64
+  auto issue_b = [&](int ks, int g) {
+    char* dst = smem + (ks & 1) * 32768 + g * 16384 + w * 2048;
+    const int cc = ks / 9, tap = ks - cc * 9;
+    const uint32_t kofs = (uint32_t)(tap * a.Cin + cc * 64) * 2u;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = g * 2 + j;
+      glds16(wr_, dst + j * 1024, bval[k] ? boff[k] + kofs : SR_OOB);
+    }
+  };
+  auto issue_b_dummy = [&]() {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) issue_dummy();
+  };
+
+  u32x4 fa[2][4], fb[2][2][2];
+  // A half h of step (cc, ty, tx): output row r = 2h + wr reads halo row r + ty at slot px
+  // index x + tx (= px + 1); per lane and tx the swizzled offset inside a 16-px group is fixed
+  // (16 is a multiple of the 8-row swizzle period): q[tx][kk], + i * 2048 per group.
+  // (named registers, not an array: a runtime-indexed array would live in scratch, and its
+  // scratch loads would make the compiler drain vmcnt -- the DMA pipeline -- at every read)
+  auto qoff = [&](int tx, int kk) -> uint32_t {
+    const uint32_t pxi = (uint32_t)((lane & 15) + tx);
+    return pxi * 128u + ((((uint32_t)(kk * 4 + (lane >> 4))) ^ (pxi & 7u)) << 4);
+  };
+  const uint32_t q00 = qoff(0, 0), q01 = qoff(0, 1), q10 = qoff(1, 0), q11 = qoff(1, 1), q20 = qoff(2, 0),
+                 q21 = qoff(2, 1);
+  auto read_a = [&](int slot, int tx) {
+    const char* Rs = smem + PPH_SLOT0 + slot * PPH_ROWB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const uint32_t qa = kk ? q01 : q00, qb = kk ? q11 : q10, qc = kk ? q21 : q20;
+      const uint32_t qq = tx == 0 ? qa : (tx == 1 ? qb : qc);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[kk][i] = *(const u32x4*)(Rs + qq + i * 2048);
+    }
+  };
+  auto read_b = [&](int buf, int g) {
+    const char* Bs = smem + buf * 32768 + g * 16384;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[g][kk][j] = *(const u32x4*)(Bs + swz128(wc * 32 + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+  };
+  auto mma = [&](int h, int g) {
+    if constexpr (DBG == 2) return;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mfma_chunk<bf16_t>(fa[kk][i], fb[g][kk][j], acc[h][g][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: chunk 0's six halo rows and both B halves of step 0, all landed
+#pragma unroll 1
+  for (int rr = 0; rr < 6; ++rr) issue_row(0, rr);
+  issue_b(0, 0);
+  issue_b(0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
+
+  int cc = 0, tap = 0;
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const bool more = t + 1 < nk;
+    const int ty = tap / 3, tx = tap - ty * 3;
+    int sa = (6 * cc + ty + wr) % PPH_NSLOT;  // slot of this wave's row in half 0
+    int sb = sa + 2;                         // half 1: two rows further
+    if (sb >= PPH_NSLOT) sb -= PPH_NSLOT;
+    // phase 1: quadrant (0,0); issue B0(t+1); retire B1(t)
+    read_a(sa, tx);
+    read_b(buf, 0);
+    if (DBG != 1) { if (more) issue_b(t + 1, 0); else issue_b_dummy(); }
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    pp_barrier();
+    mma(0, 0);
+    pp_barrier();
+    // phase 2: quadrant (0,1); issue B1(t+1)
+    read_b(buf, 1);
+    if (DBG != 1) { if (more) issue_b(t + 1, 1); else issue_b_dummy(); }
+    pp_barrier();
+    mma(0, 1);
+    pp_barrier();
+    // phase 3: quadrant (1,1); issue the next chunk's halo row `tap` (rows 0-5 at taps 0-5)
+    read_a(sb, tx);
+    if (DBG != 1) { if (tap < 6 && cc + 1 < nchunk) issue_row(cc + 1, tap); else issue_dummy(); }
+    pp_barrier();
+    mma(1, 1);
+    pp_barrier();
+    // phase 4: quadrant (1,0); retire B0(t+1) (and the previous halo piece)
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    pp_barrier();
+    mma(1, 0);
+    pp_barrier();
+    if (++tap == 9) { tap = 0; ++cc; }
+  }
+  if (!wr) pp_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   float* Cs = (float*)smem;
 #pragma unroll
@@ -2005,6 +2210,12 @@ hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Halo variant of the 256x256 kernel: whole-row tiles of W = 64 images, 64-channel chunks.
+bool fwd_use_pph(const FwdArgs& a) {
+  return g_variant != 2 && g_variant != 24 && (g_variant < 21 || g_variant > 24) && a.W == 64 && a.H % 4 == 0 && a.Cin % 64 == 0 &&
+         a.in_ps == 0 && a.in_up == 1 && a.tap0 == 0;
+}
+
 hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   FwdArgs a = a0;
   const int tm = (a.M + 255) / 256;
@@ -2012,8 +2223,16 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   a.tiles = tm * a.tiles_n;
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
+  else if (g_variant == 25 && fwd_use_pph(a))
+    hipLaunchKernelGGL(conv3x3_fwd_pph_kernel<1>, dim3(a.tiles), dim3(512), 0, s, a);
+  else if (g_variant == 26 && fwd_use_pph(a))
+    hipLaunchKernelGGL(conv3x3_fwd_pph_kernel<2>, dim3(a.tiles), dim3(512), 0, s, a);
+  else if (fwd_use_pph(a))
+    hipLaunchKernelGGL(conv3x3_fwd_pph_kernel<0>, dim3(a.tiles), dim3(512), 0, s, a);
   else if ((a.Cin % 64 == 0 || a.tap0 == 4) && (a.in_ps == 0 || a.fd_cps.d % 64 == 0))
-    hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<true>, dim3(a.tiles), dim3(512), 0, s, a);
+    if (g_variant == 21) hipLaunchKernelGGL((conv3x3_fwd_pp_kernel<true, 1>), dim3(a.tiles), dim3(512), 0, s, a);
+    else if (g_variant == 22) hipLaunchKernelGGL((conv3x3_fwd_pp_kernel<true, 2>), dim3(a.tiles), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<true>, dim3(a.tiles), dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<false>, dim3(a.tiles), dim3(512), 0, s, a);
   return hipGetLastError();
@@ -2263,7 +2482,10 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
   switch (fwd_kind(fwd_shape(d), bf)) {
     case FK_HALO: return "conv3x3_fwd_halo_kernel";
-    case FK_BIG: return g_variant == 2 ? "conv3x3_fwd_big_kernel" : "conv3x3_fwd_pp_kernel";
+    case FK_BIG: {
+      if (g_variant == 2) return "conv3x3_fwd_big_kernel";
+      return fwd_use_pph(fwd_shape(d)) ? "conv3x3_fwd_pph_kernel" : "conv3x3_fwd_pp_kernel";
+    }
     case FK_256_16: return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
     case FK_256_32: return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
     case FK_128_64: return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
@@ -2281,7 +2503,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || variant > 13)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 26)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
   g_variant = variant;
   return SR_OK;

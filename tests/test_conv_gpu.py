@@ -154,10 +154,10 @@ def test_edsr_m_parity_fp32(cuda):
                                    (1, 16, 16, 1024, 256, 2, 3), (2, 8, 24, 256, 1024, 2, 3),
                                    (1, 12, 20, 264, 256, 0, 3), (2, 16, 16, 64, 256, 0, 1), (1, 9, 15, 184, 544, 0, 1)])
 def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
-    """The phase-interleaved 256x256 kernel (variant 0), the 128x128 register-staged kernel
-    (1) and the two-barrier 256x256 kernel (2) sum K in the same order, so their bf16 outputs
-    must be bitwise identical (partial M/N tiles, K-steps crossing taps, a single K-step,
-    1x1 taps, in_ps gather)."""
+    """The phase-interleaved 256x256 kernel (variant 24: never the halo form), the 128x128
+    register-staged kernel (1) and the two-barrier 256x256 kernel (2) sum K in the same order,
+    so their bf16 outputs must be bitwise identical (partial M/N tiles, K-steps crossing taps,
+    a single K-step, 1x1 taps, in_ps gather)."""
     N, H, W, cin, cout, in_ps, ks = shape
     torch.manual_seed(3)
     dt = torch.bfloat16
@@ -172,7 +172,7 @@ def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
     res = torch.randn(N, H, W, cout, device=cuda).to(dt)
     outs = []
     try:
-        for variant in (0, 1, 2):
+        for variant in (24, 1, 2):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
             y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
             C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, res=res, alpha=0.5, in_ps=in_ps, ldx=x.shape[-1],
@@ -373,3 +373,44 @@ def test_refresh_prepared_matches_fresh_prep(cuda):
                                            cp, cip, ops, _lib.ptr(maps[0]), _lib.ptr(maps[1]), _lib.ptr(wf),
                                            _lib.ptr(wd), _lib.ptr(bg), _lib.stream()))
         assert torch.equal(imgs[0], wf) and torch.equal(imgs[1], wd) and torch.equal(imgs[2], bg)
+
+
+@pytest.mark.parametrize('shape', [(2, 64, 64, 256, 256), (1, 8, 64, 256, 1024), (2, 4, 64, 512, 256),
+                                   (1, 12, 64, 64, 384), (3, 4, 64, 128, 256)])
+def test_fwd_pph_vs_fp64(cuda, shape):
+    """Halo form of the 256x256 kernel (W 64 whole-row tiles, chunk-major K): against fp64 on
+    the same bf16 operands, with a channel-slice input, residual + LeakyReLU epilogue and the
+    fused channel sums; close to the tap-major pp kernel (only the K summation order differs)."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(9)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    xw = torch.randn(N, H, W, cin + 16, device=cuda).to(dt)
+    x = xw[..., 8:8 + cin]
+    wt = torch.randn(cout, cin, 3, 3, device=cuda) * 0.05
+    bias = torch.randn(cout, device=cuda)
+    spec = C.ConvSpec(cin, cout)
+    wf, _, bg = C.prepared(torch.nn.Parameter(wt), torch.nn.Parameter(bias), spec, dt)
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    d = C._desc(dt, N, H, W, cin, cin + 16, cout, cout, cout)
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_pph_kernel'
+    outs = []
+    try:
+        for variant in (0, 24):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+            _, parts = C.conv_fwd_raw(xw, wf, bg, y, N, H, W, cin, cout, cout, ldx=cin + 16, xcoff=8,
+                                      act=_lib.ACT_LRELU, slope=0.2, res=res, beta=1.0, colsum=True)
+            outs.append((y, parts))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    xd = x.permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(xd, bf(wt.cpu()).double(), bias.cpu().double(), padding=1)
+    ref = F.leaky_relu(ref, 0.2) + res.permute(0, 3, 1, 2).double().cpu()
+    y0, p0 = outs[0]
+    got = y0.permute(0, 3, 1, 2).double().cpu()
+    assert (got - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())
+    assert (y0.float() - outs[1][0].float()).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())
+    cs = y0.double().sum((1, 2))
+    assert (p0.double().sum(1) - cs).abs().max().item() <= 1e-5 * y0.double().abs().sum((1, 2)).max().item()

@@ -30,8 +30,10 @@ def main():
     res = []
     for dtype, variant in [(torch.bfloat16, v) for v in variants]:
         C._lib.check(lib.sr_conv3x3_set_variant(variant))
-        for (cin, cout, hw, ps) in [(256, 256, 64, 0), (256, 1024, 64, 2), (256, 1024, 128, 2), (256, 3, 256, 0),
-                                    (64, 64, 64, 0)]:
+        shapes = [(256, 256, 64, 0), (256, 1024, 64, 2), (256, 1024, 128, 2), (256, 3, 256, 0), (64, 64, 64, 0)]
+        if len(sys.argv) > 3:  # e.g. 256,256,64,0 (cin, cout, hw, out_ps)
+            shapes = [tuple(int(v) for v in sys.argv[3].split(','))]
+        for (cin, cout, hw, ps) in shapes:
             conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(dev)
             spec = C.ConvSpec(cin, cout, out_ps=ps, out_nchw=(cout == 3))
             x = torch.randn(B, hw, hw, C.pad8(cin), device=dev).to(dtype)
