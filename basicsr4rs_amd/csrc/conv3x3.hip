@@ -816,31 +816,39 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// conv3x3_fwd_pph_kernel: the phase-interleaved 256x256 schedule of conv3x3_fwd_pp_kernel
+// conv3x3_fwd_pph_kernel<R>: the phase-interleaved 256x256 schedule of conv3x3_fwd_pp_kernel
 // with the A operand formed from input HALO rows instead of one DMA'd half-tile per tap.
-// For W == 64 a 256-pixel tile is 4 whole image rows; per 64-channel chunk the 6 rows
-// y0-1 .. y0+4 (64 px x 128 B, XOR-swizzled) are staged in LDS once and all 9 taps read
-// their A fragments from them (the left/right image border reads a zero region).  The K
-// loop is chunk-major (chunk, tap): per K-step only the two B half-tiles (2 x 16 KB) and ONE
-// halo piece per wave (the next chunk's rows, streamed into free row slots) are issued, vs.
-// 4 half-tiles before -- ~40 % fewer L2->LDS bytes and DMA issues per MFMA.
-// Row slots: 11 x 8 KB ring, slot(chunk c, row r) = (6c + r) mod 11: the next chunk's rows
-// 0-4 go to the 5 free slots, its row 5 to the current row 0's slot (dead after the
-// ty = 0 taps, steps 0-2; it is issued at step 5).  Per K-step issue order: B0(t+1) [ph1],
-// B1(t+1) [ph2], halo/dummy piece [ph3]; counted waits vmcnt(3) at ph1 (retires B1(t)) and
-// ph4 (retires B0(t+1) and the previous halo piece).  Last step: dummy pieces keep the counts.
+// A 256-pixel tile is R whole image rows of W = 256 / R pixels (R = 4: W 64, R = 2: W 128).
+// Per 64-channel chunk the R + 2 rows y0-1 .. y0+R (W + 2 px x 128 B, XOR-swizzled, the
+// two border columns zero) are staged in LDS once and all 9 taps read their A fragments
+// from them.  The K loop is chunk-major (chunk, tap): per K-step only the two B half-tiles
+// (2 x 16 KB) and ONE halo piece per wave are issued, vs. 4 half-tiles in the pp kernel.
+// Row slots form a ring: load k = (R+2)*chunk + row goes to slot k mod S, issued once the
+// slot's previous row is dead (its last tap row done) and >= 2 K-steps before its first use:
+//   R = 4 (S 11, rows of 1 piece per wave): at tap j < 6 of chunk c, row j of chunk c+1;
+//   R = 2 (S 5, rows of 2 pieces): taps 0-1 row 3 of chunk c, 2-3 / 4-5 / 6-7 rows 0 / 1 / 2
+//   of chunk c+1, tap 8 a dummy.
+// Per K-step issue order: B0(t+1) [ph1], B1(t+1) [ph2], halo/dummy piece [ph3]; counted
+// waits vmcnt(3) at ph1 (retires B1(t)) and ph4 (retires B0(t+1) and the older halo piece).
 // ------------------------------------------------------------------------------------
-constexpr int PPH_ROWB = 66 * 128;  // px -1 .. 64 (the two border columns stay zero)
-constexpr int PPH_NSLOT = 11;
 constexpr int PPH_SLOT0 = 2 * 32768;
-constexpr int PPH_ZERO = PPH_SLOT0 + PPH_NSLOT * PPH_ROWB;
-constexpr int PPH_LDS = PPH_ZERO + 1024;
-static_assert(PPH_LDS <= 160 * 1024, "pph LDS");
+template <int R>
+struct PphGeom {
+  static constexpr int W = 256 / R;
+  static constexpr int ROWB = (W + 2) * 128;  // px -1 .. W
+  static constexpr int NSLOT = R == 4 ? 11 : 5;
+  static constexpr int PIECES = W / 64;  // 1-KB pieces per wave per row
+  static constexpr int ZERO = PPH_SLOT0 + NSLOT * ROWB;
+  static constexpr int LDS = ZERO + 1024;
+  static_assert(LDS <= 160 * 1024, "pph LDS");
+};
 
-template <int DBG = 0>
+template <int R, int DBG = 0>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
+  using G = PphGeom<R>;
+  constexpr int W = G::W, RH = R + 2;
   constexpr int CSTR = 256 + 4;
-  constexpr int SMEM = PPH_LDS > 128 * CSTR * 4 ? PPH_LDS : 128 * CSTR * 4;
+  constexpr int SMEM = G::LDS > 128 * CSTR * 4 ? G::LDS : 128 * CSTR * 4;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -849,9 +857,9 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (int)(tile / a.tiles_n) * 256;
   const int n0 = (int)(tile % a.tiles_n) * 256;
-  const int HW = a.H * 64;
+  const int HW = a.H * W;
   const int img = m0 / HW;
-  const int y0 = (m0 - img * HW) >> 6;
+  const int y0 = (m0 - img * HW) / W;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
 
@@ -865,14 +873,16 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
     bval[k] = n < a.Cout;
     boff[k] = (uint32_t)(n * a.ldw) * 2u + (uint32_t)c * 16u;
   }
-  // halo piece of wave w: pixels 8w .. 8w+7 of a row
+  // halo piece p of wave w: pixels 64p + 8w .. +7 of a row
   const uint32_t hlane = (uint32_t)((8 * w + (lane >> 3)) * a.ldx + a.xcoff) * 2u + (uint32_t)ch_h * 16u;
-  const uint32_t rowb = (uint32_t)(64 * a.ldx) * 2u;
+  const uint32_t rowb = (uint32_t)(W * a.ldx) * 2u;
+  const uint32_t pieceb = (uint32_t)(64 * a.ldx) * 2u;
 
-  if (tid < 64) *(u32x4*)(smem + PPH_ZERO + tid * 16) = u32x4{0u, 0u, 0u, 0u};
-  if (tid < PPH_NSLOT * 16) {  // border columns (slot px index 0 and 65) of every slot
+  if (tid < 64) *(u32x4*)(smem + G::ZERO + tid * 16) = u32x4{0u, 0u, 0u, 0u};
+  if (tid < G::NSLOT * 16) {  // border columns (slot px index 0 and W + 1) of every slot
     const int sl = tid >> 4, e = tid & 15;
-    *(u32x4*)(smem + PPH_SLOT0 + sl * PPH_ROWB + (e < 8 ? 0 : 65 * 128) + (e & 7) * 16) = u32x4{0u, 0u, 0u, 0u};
+    *(u32x4*)(smem + PPH_SLOT0 + sl * G::ROWB + (e < 8 ? 0 : (W + 1) * 128) + (e & 7) * 16) =
+        u32x4{0u, 0u, 0u, 0u};
   }
 
   f32x4 acc[2][2][4][2];
@@ -887,18 +897,29 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 
   const int nchunk = a.Cin >> 6;
   const int nk = nchunk * 9;
-  auto issue_row = [&](int cc, int rr) {  // row rr (0..5) of chunk cc into its slot
+  auto issue_row = [&](int cc, int rr, int p) {  // piece p of row rr of chunk cc into its slot
     const int y = y0 - 1 + rr;
-    const int slot = (6 * cc + rr) % PPH_NSLOT;
-    glds16(xr, smem + PPH_SLOT0 + slot * PPH_ROWB + 128 + w * 1024,
-           (unsigned)y < (unsigned)a.H ? (uint32_t)(img * a.H + y) * rowb + hlane + (uint32_t)cc * 128u : SR_OOB);
+    const int slot = (RH * cc + rr) % G::NSLOT;
+    glds16(xr, smem + PPH_SLOT0 + slot * G::ROWB + 128 + p * 8192 + w * 1024,
+           (unsigned)y < (unsigned)a.H
+               ? (uint32_t)(img * a.H + y) * rowb + (uint32_t)p * pieceb + hlane + (uint32_t)cc * 128u
+               : SR_OOB);
   };
-  auto issue_dummy = [&]() { glds16(xr, smem + PPH_ZERO, SR_OOB); };
-  // B half g of K-step ks = (chunk ks / 9, tap ks % 9): weight columns tap*Cin + chunk*64
-  auto issue_b = [&](int ks, int g) {
-    char* dst = smem + (ks & 1) * 32768 + g * 16384 + w * 2048;
-    const int cc = ks / 9, tap = ks - cc * 9;
-    const uint32_t kofs = (uint32_t)(tap * a.Cin + cc * 64) * 2u;
+  auto issue_dummy = [&]() { glds16(xr, smem + G::ZERO, SR_OOB); };
+  // the halo piece issued at tap j of chunk cc (ring schedule above)
+  auto issue_halo = [&](int cc, int j) {
+    if constexpr (R == 4) {
+      if (j < 6 && cc + 1 < nchunk) issue_row(cc + 1, j, 0); else issue_dummy();
+    } else {
+      if (j < 2) issue_row(cc, 3, j);
+      else if (j < 8 && cc + 1 < nchunk) issue_row(cc + 1, (j - 2) >> 1, j & 1);
+      else issue_dummy();
+    }
+  };
+  // B half g of K-step (chunk kc, tap kt): weight columns kt*Cin + kc*64
+  auto issue_b = [&](int buf, int kc, int kt, int g) {
+    char* dst = smem + buf * 32768 + g * 16384 + w * 2048;
+    const uint32_t kofs = (uint32_t)(kt * a.Cin + kc * 64) * 2u;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int k = g * 2 + j;
@@ -911,9 +932,10 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   };
 
   u32x4 fa[2][4], fb[2][2][2];
-  // A half h of step (cc, ty, tx): output row r = 2h + wr reads halo row r + ty at slot px
-  // index x + tx (= px + 1); per lane and tx the swizzled offset inside a 16-px group is fixed
-  // (16 is a multiple of the 8-row swizzle period): q[tx][kk], + i * 2048 per group.
+  // A half h of step (cc, ty, tx): the wave's 64 output pixels are row r, columns x0 .. x0+63
+  // (R = 4: r = 2h + wr, x0 = 0; R = 2: r = h, x0 = 64 wr); they read halo row r + ty at slot px
+  // index x + tx (= px + 1).  Per lane and tx the swizzled offset inside a 16-px group is
+  // fixed (16 is a multiple of the 8-row swizzle period): q<tx><kk>, + i * 2048 per group.
   // (named registers, not an array: a runtime-indexed array would live in scratch, and its
   // scratch loads would make the compiler drain vmcnt -- the DMA pipeline -- at every read)
   auto qoff = [&](int tx, int kk) -> uint32_t {
@@ -922,8 +944,9 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   };
   const uint32_t q00 = qoff(0, 0), q01 = qoff(0, 1), q10 = qoff(1, 0), q11 = qoff(1, 1), q20 = qoff(2, 0),
                  q21 = qoff(2, 1);
+  const int xoff = R == 4 ? 0 : wr * 64 * 128;
   auto read_a = [&](int slot, int tx) {
-    const char* Rs = smem + PPH_SLOT0 + slot * PPH_ROWB;
+    const char* Rs = smem + PPH_SLOT0 + slot * G::ROWB + xoff;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const uint32_t qa = kk ? q01 : q00, qb = kk ? q11 : q10, qc = kk ? q21 : q20;
@@ -952,50 +975,62 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // prologue: chunk 0's six halo rows and both B halves of step 0, all landed
+  // prologue: the rows chunk 0 needs first (R = 4: all six; R = 2: rows 0-2, row 3 follows
+  // at taps 0-1) and both B halves of step 0, all landed
 #pragma unroll 1
-  for (int rr = 0; rr < 6; ++rr) issue_row(0, rr);
-  issue_b(0, 0);
-  issue_b(0, 1);
+  for (int rr = 0; rr < (R == 4 ? 6 : 3); ++rr)
+#pragma unroll
+    for (int p = 0; p < G::PIECES; ++p) issue_row(0, rr, p);
+  issue_b(0, 0, 0, 0);
+  issue_b(0, 0, 0, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
   if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
 
-  int cc = 0, tap = 0;
+  int cc = 0, tap = 0;   // this step
+  int ncc = 0, ntap = 1;  // the next step
 #pragma unroll 1
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const bool more = t + 1 < nk;
     const int ty = tap / 3, tx = tap - ty * 3;
-    int sa = (6 * cc + ty + wr) % PPH_NSLOT;  // slot of this wave's row in half 0
-    int sb = sa + 2;                         // half 1: two rows further
-    if (sb >= PPH_NSLOT) sb -= PPH_NSLOT;
+    int sa, sb;  // slots of this wave's rows in halves 0 / 1
+    if constexpr (R == 4) {
+      sa = (RH * cc + ty + wr) % G::NSLOT;
+      sb = sa + 2;
+    } else {
+      sa = (RH * cc + ty) % G::NSLOT;
+      sb = sa + 1;
+    }
+    if (sb >= G::NSLOT) sb -= G::NSLOT;
     // phase 1: quadrant (0,0); issue B0(t+1); retire B1(t)
     read_a(sa, tx);
     read_b(buf, 0);
-    if (DBG != 1) { if (more) issue_b(t + 1, 0); else issue_b_dummy(); }
+    if (DBG != 1) { if (more) issue_b(buf ^ 1, ncc, ntap, 0); else issue_b_dummy(); }
     asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     pp_barrier();
     mma(0, 0);
     pp_barrier();
     // phase 2: quadrant (0,1); issue B1(t+1)
     read_b(buf, 1);
-    if (DBG != 1) { if (more) issue_b(t + 1, 1); else issue_b_dummy(); }
+    if (DBG != 1) { if (more) issue_b(buf ^ 1, ncc, ntap, 1); else issue_b_dummy(); }
     pp_barrier();
     mma(0, 1);
     pp_barrier();
-    // phase 3: quadrant (1,1); issue the next chunk's halo row `tap` (rows 0-5 at taps 0-5)
+    // phase 3: quadrant (1,1); issue this step's halo piece
     read_a(sb, tx);
-    if (DBG != 1) { if (tap < 6 && cc + 1 < nchunk) issue_row(cc + 1, tap); else issue_dummy(); }
+    if (DBG != 1) issue_halo(cc, tap);
     pp_barrier();
     mma(1, 1);
     pp_barrier();
-    // phase 4: quadrant (1,0); retire B0(t+1) (and the previous halo piece)
+    // phase 4: quadrant (1,0); retire B0(t+1) (and the older halo piece)
     asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     pp_barrier();
     mma(1, 0);
     pp_barrier();
-    if (++tap == 9) { tap = 0; ++cc; }
+    cc = ncc;
+    tap = ntap;
+    if (++ntap == 9) { ntap = 0; ++ncc; }
   }
   if (!wr) pp_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2210,10 +2245,11 @@ hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Halo variant of the 256x256 kernel: whole-row tiles of W = 64 images, 64-channel chunks.
+// Halo variant of the 256x256 kernel: whole-row tiles of W = 64 / 128 images, 64-channel chunks.
 bool fwd_use_pph(const FwdArgs& a) {
-  return g_variant != 2 && g_variant != 24 && (g_variant < 21 || g_variant > 24) && a.W == 64 && a.H % 4 == 0 && a.Cin % 64 == 0 &&
-         a.in_ps == 0 && a.in_up == 1 && a.tap0 == 0;
+  return g_variant != 2 && g_variant != 24 && (g_variant < 21 || g_variant > 24) &&
+         ((a.W == 64 && a.H % 4 == 0) || (a.W == 128 && a.H % 2 == 0)) && a.Cin % 64 == 0 && a.in_ps == 0 &&
+         a.in_up == 1 && a.tap0 == 0;
 }
 
 hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
@@ -2223,12 +2259,14 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   a.tiles = tm * a.tiles_n;
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
+  else if (fwd_use_pph(a) && a.W == 128)
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant == 25 && fwd_use_pph(a))
-    hipLaunchKernelGGL(conv3x3_fwd_pph_kernel<1>, dim3(a.tiles), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 1>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant == 26 && fwd_use_pph(a))
-    hipLaunchKernelGGL(conv3x3_fwd_pph_kernel<2>, dim3(a.tiles), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 2>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a))
-    hipLaunchKernelGGL(conv3x3_fwd_pph_kernel<0>, dim3(a.tiles), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0>), dim3(a.tiles), dim3(512), 0, s, a);
   else if ((a.Cin % 64 == 0 || a.tap0 == 4) && (a.in_ps == 0 || a.fd_cps.d % 64 == 0))
     if (g_variant == 21) hipLaunchKernelGGL((conv3x3_fwd_pp_kernel<true, 1>), dim3(a.tiles), dim3(512), 0, s, a);
     else if (g_variant == 22) hipLaunchKernelGGL((conv3x3_fwd_pp_kernel<true, 2>), dim3(a.tiles), dim3(512), 0, s, a);

@@ -376,9 +376,10 @@ def test_refresh_prepared_matches_fresh_prep(cuda):
 
 
 @pytest.mark.parametrize('shape', [(2, 64, 64, 256, 256), (1, 8, 64, 256, 1024), (2, 4, 64, 512, 256),
-                                   (1, 12, 64, 64, 384), (3, 4, 64, 128, 256)])
+                                   (1, 12, 64, 64, 384), (3, 4, 64, 128, 256), (1, 6, 128, 256, 256),
+                                   (2, 2, 128, 128, 512), (1, 4, 128, 64, 256)])
 def test_fwd_pph_vs_fp64(cuda, shape):
-    """Halo form of the 256x256 kernel (W 64 whole-row tiles, chunk-major K): against fp64 on
+    """Halo form of the 256x256 kernel (W 64 / 128 whole-row tiles, chunk-major K): against fp64 on
     the same bf16 operands, with a channel-slice input, residual + LeakyReLU epilogue and the
     fused channel sums; close to the tap-major pp kernel (only the K summation order differs)."""
     N, H, W, cin, cout = shape
