@@ -1066,7 +1066,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // per wave and chunk, not once per tap and pixel tile.  The fp32 tile goes
 // through the shared fused epilogue (bias, activation, gate, residuals, pixel shuffle).
 // ------------------------------------------------------------------------------------
-template <int CO_T, int DBG = 0>
+template <int CO_T, int DBG = 0, bool KLO = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   constexpr int BN = CO_T * 16;
   constexpr int CSTR = BN + 4;
@@ -1085,6 +1085,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   const int g = lane >> 4, c16 = lane & 15;
   const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (int)tile * 256;
+  const int n0 = blockIdx.y * BN;  // co tile (Cout > 64: one block row per 64 output channels)
   const int W = a.W, H = a.H;
   const int WPAD = W + 2;
   const int R = 256 / W;
@@ -1114,6 +1115,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
     const int ci0 = ch * 64;
     if (ch) __syncthreads();  // every wave is done with the previous chunk's halo
     const bool cv = ci0 + lc * 8 < a.Cin;
+    constexpr bool khi = !KLO;  // KLO: Cin <= 32 (RRDB dense dgrads), the upper half-chunk is empty
     for (int k = w; k < ninstr; k += 4) {
       const int hr = 8 * k + (lane >> 3);
       const int hy = hr / WPAD, hx = hr - hy * WPAD;
@@ -1132,10 +1134,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int c = 0; c < CW; ++c) {
-            const int co = (wc * CW + c) * 16 + c16, ci = ci0 + kk * 32 + 8 * g;
+            const int co = n0 + (wc * CW + c) * 16 + c16, ci = ci0 + kk * 32 + 8 * g;
             const int tap = ty * 3 + tx;
             const bool v = co < a.Cout && ci < a.Cin && (DBG != 1 || tap == 0);
-            dst[tx][kk][c] = buf_load16(wr, v ? (uint32_t)((co * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB);
+            if (kk == 0 || khi)
+              dst[tx][kk][c] = buf_load16(wr, v ? (uint32_t)((co * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB);
           }
     };
     load_row(0, bw[0]);
@@ -1153,6 +1156,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
         const int toff = ty * WPAD + tx;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
+          if (kk == 1 && !khi) continue;
 #pragma unroll
           for (int i = 0; i < PT; ++i) {
             const u32x4 fa = *(const u32x4*)(smem + swz128(hb[i] + z + toff, kk * 4 + g));
@@ -1180,7 +1184,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
       }
     }
     __syncthreads();
-    if (DBG != 3) epilogue_tile<bf16_t, 128, BN, 256>(a, Cs, CSTR, m0 + h * 128, 0, tid);
+    if (DBG != 3) epilogue_tile<bf16_t, 128, BN, 256>(a, Cs, CSTR, m0 + h * 128, n0, tid);
   }
 }
 
@@ -2276,23 +2280,26 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Narrow-conv halo kernel: bf16 3x3, Cout <= 64, W 64 or 128, whole-row 256-pixel tiles.
+// Narrow-conv halo kernel: bf16 3x3, W 64 or 128, whole-row 256-pixel tiles; Cout <= 64 in one
+// block column, Cout 65..255 (RRDB dense-block dgrads) in 64-channel block columns.
 bool fwd_use_halo(const FwdArgs& a, bool bf) {
-  return bf && !a.out_nchw && a.Cout <= 64 && a.in_up == 1 && a.in_ps == 0 && a.tap0 == 0 && g_variant != 1 &&
+  return bf && !a.out_nchw && a.Cout < 256 && a.in_up == 1 && a.in_ps == 0 && a.tap0 == 0 && g_variant != 1 &&
          (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
 }
 
 hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   FwdArgs a = a0;
-  a.tiles_n = 1;
+  a.tiles_n = (a.Cout + 63) / 64;
   a.tiles = a.M / 256;
   const int ct = (a.Cout + 15) / 16;
-  if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, dim3(a.tiles), dim3(256), 0, s, a);
-  else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, dim3(a.tiles), dim3(256), 0, s, a);
-  else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), dim3(a.tiles), dim3(256), 0, s, a);
-  else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), dim3(a.tiles), dim3(256), 0, s, a);
-  else if (g_variant == 13) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 3>), dim3(a.tiles), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<4>, dim3(a.tiles), dim3(256), 0, s, a);
+  const dim3 grid(a.tiles, a.tiles_n);
+  if (a.Cin <= 32 && ct > 2) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 0, true>), grid, dim3(256), 0, s, a);
+  else if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, grid, dim3(256), 0, s, a);
+  else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);
+  else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), grid, dim3(256), 0, s, a);
+  else if (g_variant == 13) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 3>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<4>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -59,3 +59,60 @@ def imwrite(img, file_path, params=None, auto_mkdir=True):
     with open(file_path, 'wb') as f:
         f.write(png)
     return True
+
+
+def imfrombytes(content, flag='color', float32=False):
+    """Decode image bytes to a numpy HWC BGR array (basicsr/utils/img_util.py:99-117 semantics:
+    ``color`` -> 3-channel BGR, ``grayscale`` -> HW, ``unchanged`` keeps depth / alpha;
+    ``float32`` divides by 255).  Decoded with Pillow (OpenCV is not in this image); ``.npy``
+    payloads (HWC arrays, no pickle) are accepted as well."""
+    import io
+    if content[:6] == b'\x93NUMPY':
+        img = np.load(io.BytesIO(content), allow_pickle=False)
+    else:
+        from PIL import Image
+        with Image.open(io.BytesIO(content)) as im:
+            if flag == 'grayscale':
+                img = np.asarray(im.convert('L'))
+            elif flag == 'color':
+                img = np.asarray(im.convert('RGB'))[..., ::-1]
+            else:
+                img = np.asarray(im)
+                if img.ndim == 3 and img.shape[2] in (3, 4):
+                    img = img[..., [2, 1, 0] + ([3] if img.shape[2] == 4 else [])]
+    img = np.ascontiguousarray(img)
+    if float32:
+        img = img.astype(np.float32) / 255.
+    return img
+
+
+def img2tensor(imgs, bgr2rgb=True, float32=True):
+    """Numpy HWC -> tensor CHW (basicsr/utils/img_util.py:11-37), BGR -> RGB for 3 channels."""
+
+    def _one(img):
+        if img.ndim == 2:
+            img = img[..., None]
+        if img.shape[2] == 3 and bgr2rgb:
+            img = img[..., ::-1]
+        t = torch.from_numpy(np.ascontiguousarray(img.transpose(2, 0, 1)))
+        return t.float() if float32 else t
+
+    return [_one(i) for i in imgs] if isinstance(imgs, list) else _one(imgs)
+
+
+def scandir(dir_path, suffix=None, recursive=False, full_path=False):
+    """Sorted-walk file scan relative to ``dir_path`` (basicsr/utils/misc.py:57-91)."""
+    if suffix is not None and not isinstance(suffix, (str, tuple)):
+        raise TypeError('"suffix" must be a string or tuple of strings')
+    root = dir_path
+
+    def _scan(path):
+        for entry in sorted(os.scandir(path), key=lambda e: e.name):
+            if not entry.name.startswith('.') and entry.is_file():
+                rel = entry.path if full_path else os.path.relpath(entry.path, root)
+                if suffix is None or rel.endswith(suffix):
+                    yield rel
+            elif recursive and entry.is_dir():
+                yield from _scan(entry.path)
+
+    return _scan(dir_path)

@@ -270,7 +270,8 @@ def test_wgrad_halo_vs_fp64(cuda, shape):
 
 
 @pytest.mark.parametrize('shape', [(2, 8, 64, 64, 64), (1, 4, 128, 192, 32), (1, 4, 64, 96, 48), (2, 4, 64, 160, 8),
-                                   (1, 6, 128, 64, 64)])
+                                   (1, 6, 128, 64, 64), (1, 4, 128, 32, 96), (1, 4, 128, 32, 192),
+                                   (2, 8, 64, 64, 160), (1, 4, 64, 184, 184)])
 @pytest.mark.parametrize('epi', ['plain', 'relu_res'])
 def test_fwd_halo_vs_fp64(cuda, shape, epi):
     """Narrow-conv halo forward (Cout <= 64, W 64/128): channel-slice input (ldx > Cin, xcoff),
