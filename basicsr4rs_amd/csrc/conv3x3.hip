@@ -1055,6 +1055,161 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// conv3x3_lin_kernel<MT>: 1x1 convs (nn.Linear over NHWC tokens: SwinIR qkv / proj / fc1 /
+// fc2 and their dgrads, DCN column GEMMs) with a short K (<= 576).  These GEMMs are
+// HBM-bound (AI ~ 100-150 FLOP/B); the 2-D tiled kernels re-read the token rows once per
+// N tile and pay a full prologue / epilogue per 2-3 K-steps.  Here a block loads its MT
+// token rows x all K ONCE into LDS (LDS-DMA, [K/64][MT][128 B] XOR-swizzled) and then
+// sweeps every output channel, 128 per pass (32 per wave): W fragments come from L2
+// straight into registers, X^T fragments from LDS, C = W x X^T so each lane ends with 8
+// consecutive channels of one token (the W tile rows are permuted on load: tile t row r ->
+// channel 8(r/4) + 4t + r%4) and stores 16 B directly, with the fused epilogue (bias,
+// activation, pre-activation side output, gate, alpha, residuals) in registers.
+// ------------------------------------------------------------------------------------
+template <int MT, int MAXCG>
+__global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
+  constexpr int NMT = MT / 16;  // token tiles per wave (every wave covers all MT tokens)
+  __shared__ __attribute__((aligned(16))) char smem[MAXCG * MT * 128];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int m0 = (int)xcd_remap(blockIdx.x, gridDim.x) * MT;
+  const int K = a.Cin, KC = K >> 3;  // 16-B chunks of a token row
+  const int CG = (K + 63) >> 6;      // 128-B chunk groups
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  // ---- stage the MT x K token tile: piece p = (chunk group cg, 8-row group rg)
+  {
+    const int npieces = CG * (MT / 8);
+    const int rl = lane >> 3, pc = lane & 7;
+    const int lc = pc ^ rl;  // logical chunk this lane fetches (row & 7 == rl)
+    for (int p = w; p < npieces; p += 4) {
+      const int cg = p / (MT / 8), rg = p - cg * (MT / 8);
+      const int row = rg * 8 + rl, m = m0 + row, ch = cg * 8 + lc;
+      const bool v = m < a.M && ch < KC;
+      glds16(xr, smem + (cg * MT + rg * 8) * 128, v ? (uint32_t)(((size_t)m * a.ldx + a.xcoff + ch * 8) * 2) : SR_OOB);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+  const int nkk = (K + 31) >> 5;
+  const int npass = (a.Cout + 127) >> 7;
+  constexpr int MAXKK = MAXCG * 2;
+  // W fragments of a whole pass (all K) in registers, the next pass's loads in flight while the
+  // current pass computes: an L2 round trip per K-step would otherwise set the pace
+  u32x4 wb[MAXKK][2];
+  auto wload_pass = [&](int pass) {
+    const int r0 = pass * 128 + w * 32 + 8 * (c16 >> 2) + (c16 & 3);
+    const bool wv0 = r0 < a.Cout, wv1 = r0 + 4 < a.Cout;
+#pragma unroll
+    for (int kk = 0; kk < MAXKK; ++kk) {
+      const int k = kk * 32 + 8 * g;
+      const bool kv = kk < nkk && k < K;
+      wb[kk][0] = buf_load16(wr, (wv0 && kv) ? (uint32_t)((r0 * a.ldw + k) * 2) : SR_OOB);
+      wb[kk][1] = buf_load16(wr, (wv1 && kv) ? (uint32_t)(((r0 + 4) * a.ldw + k) * 2) : SR_OOB);
+    }
+  };
+  wload_pass(0);
+#pragma unroll 1
+  for (int pass = 0; pass < npass; ++pass) {
+    const int nb = pass * 128 + w * 32;  // this wave's 32 channels (tile t row r -> nb + 8(r/4) + 4t + r%4)
+    f32x4 acc[NMT][2];
+#pragma unroll
+    for (int i = 0; i < NMT; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < MAXKK; ++kk) {
+      if (kk >= nkk) break;
+      const int ch = kk * 4 + g;  // logical 16-B chunk of the X^T fragment
+      // [cg][row][128 B], physical chunk = logical ^ (row & 7); row & 7 == c16 & 7 for all i
+      const char* base = smem + (ch >> 3) * MT * 128 + c16 * 128 + ((((ch & 7) ^ (c16 & 7))) << 4);
+#pragma unroll
+      for (int i = 0; i < NMT; ++i) {
+        const u32x4 xf = *(const u32x4*)(base + i * 16 * 128);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, wb[kk][0]),
+                                                            __builtin_bit_cast(s16x8, xf), acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, wb[kk][1]),
+                                                            __builtin_bit_cast(s16x8, xf), acc[i][1], 0, 0, 0);
+      }
+    }
+    // the next pass's W fragments load while this pass's epilogue runs
+    if (pass + 1 < npass) wload_pass(pass + 1);
+    // ---- epilogue: lane (g, c16) holds channels nb + 8g .. +7 of token m0 + 16i + c16 and
+    // stores them as one 16-B vector (4 lanes cover 64 contiguous bytes of a token row;
+    // staging whole rows through LDS measured slower: 78 -> 95 us on the qkv shape)
+    const int n = nb + 8 * g;
+    if (n >= a.Cout) continue;
+    float bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[j] = 0.f;
+    if (a.bias) {
+      const f32x4 b0 = *(const f32x4*)(a.bias + n), b1 = *(const f32x4*)(a.bias + n + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { bv[j] = b0[j]; bv[4 + j] = b1[j]; }
+    }
+#pragma unroll
+    for (int i = 0; i < NMT; ++i) {  // fully unrolled: acc must stay register-indexed (no scratch)
+      const int m = m0 + i * 16 + c16;
+      if (m >= a.M) continue;
+      u32x4 gv, rv, rv2;
+      const bool rok = n < a.rcols;
+      if (a.gate) gv = buf_load16(gr, (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2));
+      if (a.res) rv = buf_load16(rr, rok ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
+      if (a.res2) rv2 = buf_load16(rr2, rok ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * 2) : SR_OOB);
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
+      if (a.aux) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        *(u32x4*)((bf16_t*)a.aux + (size_t)m * a.ldy + a.ycoff + n) = o;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+      if (a.gate) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float g0 = bf16_to_f32(gv[j] & 0xffff), g1 = bf16_to_f32(gv[j] >> 16);
+          if (a.gate_mode == 1) {
+            v[2 * j] *= gelu_grad(g0);
+            v[2 * j + 1] *= gelu_grad(g1);
+          } else {
+            v[2 * j] *= g0 > 0.f ? 1.f : a.gate_slope;
+            v[2 * j + 1] *= g1 > 0.f ? 1.f : a.gate_slope;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+      if (a.res) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[2 * j] += a.beta * bf16_to_f32(rv[j] & 0xffff);
+          v[2 * j + 1] += a.beta * bf16_to_f32(rv[j] >> 16);
+        }
+      }
+      if (a.res2) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[2 * j] += a.beta2 * bf16_to_f32(rv2[j] & 0xffff);
+          v[2 * j + 1] += a.beta2 * bf16_to_f32(rv2[j] >> 16);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      *(u32x4*)((bf16_t*)a.y + (size_t)m * a.ldy + a.ycoff + n) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Forward / dgrad for narrow convs (Cout <= 64: RCAN / RRDB / SRResNet bodies at W 64 or
 // 128).  A block computes 256 consecutive output pixels = R = 256 / W full rows of one image
 // x all Cout channels.  Per 64-channel input chunk it stages the halo rows y0-1 .. y0+R,
@@ -2306,8 +2461,14 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
 
 // Kernel family sr_conv3x3_fwd launches for a call (dispatch, kernel names and the
 // epilogue geometry behind colsum all follow this one choice).
-enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128 };
+enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN };
+// short-K 1x1 convs (linears): token tile staged once, all output channels swept
+bool fwd_use_lin(const FwdArgs& a, bool bf) {
+  return bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && a.Cin <= 192 &&
+         g_variant != 1 && g_variant != 27;
+}
 FwdKind fwd_kind(const FwdArgs& a, bool bf) {
+  if (fwd_use_lin(a, bf)) return FK_LIN;
   if (fwd_use_halo(a, bf)) return FK_HALO;
   if (bf && !a.out_nchw && a.Cout >= 256 && a.in_up == 1 && !g_disable_big) return FK_BIG;
   if (a.out_nchw || a.Cout <= 16) return FK_256_16;
@@ -2325,6 +2486,12 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
 template <typename T>
 hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
   switch (fwd_kind(a, sizeof(T) == 2)) {
+    case FK_LIN: {
+      FwdArgs b = a;
+      b.tiles = (a.M + 127) / 128;
+      hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3>), dim3(b.tiles), dim3(256), 0, s, b);
+      return hipGetLastError();
+    }
     case FK_HALO: return launch_fwd_halo(a, s);
     case FK_BIG: return launch_fwd_big(a, s);
     case FK_256_16: return launch_fwd<T, 256, 16, 4, 1>(a, s);
@@ -2465,7 +2632,7 @@ FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
 
 // Partial rows per image of the colsum output, or 0 when the call cannot produce it.
 int colsum_parts(const sr_conv3x3_desc* d, const FwdArgs& a) {
-  if (d->out_ps || d->out_nchw) return 0;
+  if (d->out_ps || d->out_nchw || fwd_kind(a, d->dtype == SR_BF16) == FK_LIN) return 0;
   int rows, nt;
   fwd_epi_geom(fwd_kind(a, d->dtype == SR_BF16), &rows, &nt);
   const int HW = d->H * d->W;
@@ -2527,6 +2694,7 @@ int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d) {
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
   switch (fwd_kind(fwd_shape(d), bf)) {
+    case FK_LIN: return "conv3x3_lin_kernel";
     case FK_HALO: return "conv3x3_fwd_halo_kernel";
     case FK_BIG: {
       if (g_variant == 2) return "conv3x3_fwd_big_kernel";
@@ -2549,7 +2717,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 26)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 27)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
   g_variant = variant;
   return SR_OK;

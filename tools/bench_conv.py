@@ -31,9 +31,24 @@ def main():
     for dtype, variant in [(torch.bfloat16, v) for v in variants]:
         C._lib.check(lib.sr_conv3x3_set_variant(variant))
         shapes = [(256, 256, 64, 0), (256, 1024, 64, 2), (256, 1024, 128, 2), (256, 3, 256, 0), (64, 64, 64, 0)]
-        if len(sys.argv) > 3:  # e.g. 256,256,64,0 (cin, cout, hw, out_ps)
-            shapes = [tuple(int(v) for v in sys.argv[3].split(','))]
-        for (cin, cout, hw, ps) in shapes:
+        if len(sys.argv) > 3:  # e.g. 256,256,64,0 (cin, cout, hw, out_ps[, ksize]); ';'-separated list
+            shapes = [tuple(int(v) for v in sh.split(',')) for sh in sys.argv[3].split(';')]
+        for shp in shapes:
+            cin, cout, hw, ps = shp[:4]
+            ks = shp[4] if len(shp) > 4 else 3
+            if ks == 1:  # 1x1 conv = nn.Linear over tokens: fwd and dgrad only
+                taps = 1
+                x = torch.randn(B, hw, hw, C.pad8(cin), device=dev).to(dtype)
+                wf = (torch.randn(C.pad8(cout), C.pad8(cin), device=dev) * 0.05).to(dtype)
+                wd = (torch.randn(C.pad8(cin), C.pad8(cout), device=dev) * 0.05).to(dtype)
+                y = torch.empty(B, hw, hw, C.pad8(cout), device=dev, dtype=dtype)
+                dx = torch.empty(B, hw, hw, C.pad8(cin), device=dev, dtype=dtype)
+                fl = 2.0 * B * hw * hw * cin * cout
+                t = timeit(lambda: C.conv_fwd_raw(x, wf, None, y, B, hw, hw, C.pad8(cin), C.pad8(cout), cout, ksize=1))
+                res.append(dict(v=variant, k='fwd1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+                t = timeit(lambda: C.conv_fwd_raw(y, wd, None, dx, B, hw, hw, C.pad8(cout), C.pad8(cin), cin, ksize=1))
+                res.append(dict(v=variant, k='dgrad1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+                continue
             conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(dev)
             spec = C.ConvSpec(cin, cout, out_ps=ps, out_nchw=(cout == 3))
             x = torch.randn(B, hw, hw, C.pad8(cin), device=dev).to(dtype)
