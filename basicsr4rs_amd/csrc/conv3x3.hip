@@ -2542,14 +2542,24 @@ hipError_t dispatch_wg(const WgArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// 1x1 (linear) weight gradients with >= 128 channels each side: the 256x256 phase-interleaved
+// kernel with partial tiles (columns past Cout / Cin read neighbouring data that only feeds
+// the discarded rows / columns of the tile) -- far fewer operand re-reads than 128x128 tiles.
+bool wg_use_pp_lin(const sr_conv3x3_wgrad_desc* d) {
+  return d->dtype == SR_BF16 && d->ksize == 1 && d->Cout >= 128 && d->Cin >= 128 && d->W % 64 == 0 &&
+         d->in_up <= 1 && d->out_ps == 0 && !g_disable_big && g_variant != 2 && g_variant != 28;
+}
+
 bool wg_use_big(const sr_conv3x3_wgrad_desc* d) {
-  return d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && d->in_up <= 1 && !g_disable_big;
+  return (d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && d->in_up <= 1 && !g_disable_big) ||
+         wg_use_pp_lin(d);
 }
 
 // Phase-interleaved wgrad kernel: W a multiple of 64, channel counts (and the pixel-shuffle
 // slot width) multiples of 128.
 bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
   if (!wg_use_big(d) || g_variant == 2) return false;
+  if (wg_use_pp_lin(d)) return true;
   const int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 128;
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
@@ -2717,7 +2727,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 27)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 28)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
   g_variant = variant;
   return SR_OK;

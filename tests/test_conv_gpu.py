@@ -416,3 +416,34 @@ def test_fwd_pph_vs_fp64(cuda, shape):
     assert (y0.float() - outs[1][0].float()).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())
     cs = y0.double().sum((1, 2))
     assert (p0.double().sum(1) - cs).abs().max().item() <= 1e-5 * y0.double().abs().sum((1, 2)).max().item()
+
+
+@pytest.mark.parametrize('shape', [(2, 4, 64, 184, 576), (1, 4, 64, 192, 184), (1, 2, 128, 368, 184),
+                                   (2, 2, 64, 184, 368), (1, 3, 64, 128, 136)])
+def test_wgrad_1x1_partial_tiles_vs_fp64(cuda, shape):
+    """Linear-layer weight gradients on the 256x256 kernel with partial co / ci tiles (SwinIR
+    qkv / proj / fc1 / fc2 shapes): dW = dy^T x and db = sum dy against fp64, and equal to
+    the 128x128 kernel (variant 28) within bf16-operand rounding."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(7)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    dy = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W, d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.ksize = (
+        _lib.SR_BF16, N, H, W, cin, cin, cin, cout, cout, cout, 1)
+    assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_pp_kernel'
+    ref_w = dy.reshape(-1, cout).double().cpu().t() @ x.reshape(-1, cin).double().cpu()
+    ref_b = dy.reshape(-1, cout).double().cpu().sum(0)
+    outs = []
+    try:
+        for variant in (0, 28):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            dw, db = C.conv_wgrad_raw(dy, x, N, H, W, cin, cin, cout, cout, ksize=1)
+            outs.append((dw.reshape(cout, cin).cpu().double(), db.cpu().double()))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    for dw, db in outs:
+        assert (dw - ref_w).abs().max().item() <= 1e-3 * ref_w.abs().max().item() + 1e-3
+        assert (db - ref_b).abs().max().item() <= 1e-3 * ref_b.abs().max().item() + 1e-3
