@@ -2542,24 +2542,25 @@ hipError_t dispatch_wg(const WgArgs& a, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-// 1x1 (linear) weight gradients with >= 128 channels each side: the 256x256 phase-interleaved
-// kernel with partial tiles (columns past Cout / Cin read neighbouring data that only feeds
-// the discarded rows / columns of the tile) -- far fewer operand re-reads than 128x128 tiles.
-bool wg_use_pp_lin(const sr_conv3x3_wgrad_desc* d) {
-  return d->dtype == SR_BF16 && d->ksize == 1 && d->Cout >= 128 && d->Cin >= 128 && d->W % 64 == 0 &&
+// Weight gradients with >= 128 channels each side that are not multiples of 128 (SwinIR linears
+// 184 / 368 / 576, its 184-channel 3x3 convs): the 256x256 phase-interleaved kernel with partial
+// tiles (columns past Cout / Cin read neighbouring data that only feeds the discarded rows /
+// columns of the tile) -- far fewer operand re-reads than 128x128 tiles.
+bool wg_use_pp_partial(const sr_conv3x3_wgrad_desc* d) {
+  return d->dtype == SR_BF16 && d->Cout >= 128 && d->Cin >= 128 && d->W % 64 == 0 &&
          d->in_up <= 1 && d->out_ps == 0 && !g_disable_big && g_variant != 2 && g_variant != 28;
 }
 
 bool wg_use_big(const sr_conv3x3_wgrad_desc* d) {
   return (d->dtype == SR_BF16 && d->Cout >= 256 && d->Cin >= 256 && d->in_up <= 1 && !g_disable_big) ||
-         wg_use_pp_lin(d);
+         wg_use_pp_partial(d);
 }
 
 // Phase-interleaved wgrad kernel: W a multiple of 64, channel counts (and the pixel-shuffle
 // slot width) multiples of 128.
 bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
   if (!wg_use_big(d) || g_variant == 2) return false;
-  if (wg_use_pp_lin(d)) return true;
+  if (wg_use_pp_partial(d)) return true;
   const int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 128;
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
