@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
 // per wave and chunk, not once per tap and pixel tile.  The fp32 tile goes
 // through the shared fused epilogue (bias, activation, gate, residuals, pixel shuffle).
 // ------------------------------------------------------------------------------------
-template <int CO_T, int DBG = 0>
+template <int CO_T, int DBG = 0, bool W256 = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   constexpr int BN = CO_T * 16;
   constexpr int CSTR = BN + 4;
@@ -1229,7 +1229,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   constexpr int WC = CO_T / CW;                  // waves along co
   constexpr int WP = 4 / WC;                     // waves along pixels
   constexpr int PT = 16 / WP;                    // 16-pixel tiles per wave
-  constexpr int HROWS = 528;  // >= (R+2)*(W+2) rounded up to 8: 400 (W 64), 520 (W 128)
+  // >= (R+2)*(W+2) rounded up to 8: 400 (W 64), 520 (W 128), 776 (W 256: HR-resolution conv_last)
+  constexpr int HROWS = W256 ? 776 : 528;
   constexpr int SMEM_H = HROWS * 128;
   constexpr int SMEM_E = 128 * CSTR * 4;
   constexpr int SMEM = SMEM_H > SMEM_E ? SMEM_H : SMEM_E;
@@ -2440,8 +2441,10 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
 // Narrow-conv halo kernel: bf16 3x3, W 64 or 128, whole-row 256-pixel tiles; Cout <= 64 in one
 // block column, Cout 65..255 (RRDB dense-block dgrads) in 64-channel block columns.
 bool fwd_use_halo(const FwdArgs& a, bool bf) {
-  return bf && !a.out_nchw && a.Cout < 256 && a.in_up == 1 && a.in_ps == 0 && a.tap0 == 0 && g_variant != 1 &&
-         (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
+  if (!bf || a.in_up != 1 || a.in_ps != 0 || a.tap0 != 0 || g_variant == 1) return false;
+  if (a.W == 256)  // HR-resolution tail convs (conv_last, Cout <= 16, NCHW store): one row per tile
+    return a.Cout <= 16 && g_variant != 29;
+  return !a.out_nchw && a.Cout < 256 && (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
 }
 
 hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
@@ -2450,7 +2453,8 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   a.tiles = a.M / 256;
   const int ct = (a.Cout + 15) / 16;
   const dim3 grid(a.tiles, a.tiles_n);
-  if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
+  if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
+  else if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
   else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, grid, dim3(256), 0, s, a);
   else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);
   else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), grid, dim3(256), 0, s, a);
@@ -2728,7 +2732,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 28)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 29)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
   g_variant = variant;
   return SR_OK;

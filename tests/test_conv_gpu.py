@@ -447,3 +447,39 @@ def test_wgrad_1x1_partial_tiles_vs_fp64(cuda, shape):
     for dw, db in outs:
         assert (dw - ref_w).abs().max().item() <= 1e-3 * ref_w.abs().max().item() + 1e-3
         assert (db - ref_b).abs().max().item() <= 1e-3 * ref_b.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize('shape', [(2, 3, 256, 256, 3), (1, 2, 256, 64, 3), (1, 2, 256, 96, 16)])
+def test_fwd_halo_w256_nchw_tail(cuda, shape):
+    """HR-resolution tail conv (conv_last: Cout <= 16, W 256, fp32 NCHW store with the mean
+    shift / range affine) on the one-row halo tiles, against fp64 and the 256x16 kernel
+    (variant 29)."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(11)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    scale = torch.rand(cout, device=cuda) + 0.5
+    shift = torch.randn(cout, device=cuda)
+    spec = C.ConvSpec(cin, cout, out_nchw=True)
+    wf, _, bg = C.prepared(conv.weight, conv.bias, spec, dt)
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    d = C._desc(dt, N, H, W, cin, cin, spec.cout_p, cout, 0, out_nchw=1)
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_halo_kernel'
+    outs = []
+    try:
+        for variant in (0, 29):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.empty(N, cout, H, W, device=cuda)
+            C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, spec.cout_p, cout, out_nchw=True, aff_scale=scale,
+                           aff_shift=shift)
+            outs.append(y)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double().cpu(), bf(conv.weight.detach().cpu()).double(),
+                   conv.bias.detach().cpu().double(), padding=1)
+    ref = ref * scale.cpu().double().view(1, -1, 1, 1) + shift.cpu().double().view(1, -1, 1, 1)
+    tol = 1e-3 * max(1.0, ref.abs().max().item())
+    assert (outs[0].cpu().double() - ref).abs().max().item() <= tol
+    assert (outs[0] - outs[1]).abs().max().item() <= tol
