@@ -86,11 +86,11 @@ SIGNATURES = {
     'sr_layernorm_fwd': (_i, [_i, _vp, _i, _vp, _vp, _i64, _i, _i, _f, _vp, _i, _vp, _vp, _vp]),
     'sr_layernorm_bwd_workspace': (_sz, [_i64, _i]),
     'sr_layernorm_bwd': (_i, [_i, _vp, _i, _vp, _i, _vp, _vp, _vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _sz,
-                             _vp]),
+                             _i, _vp]),
     'sr_window_attn_fwd': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp, _vp]),
     'sr_window_attn_bwd_workspace': (_sz, [_i, _i, _i, _i, _i]),
     'sr_window_attn_bwd': (_i, [_i, _vp, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp,
-                               _sz, _vp]),
+                               _sz, _i, _vp]),
     'sr_dcn_im2col': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp]),
     'sr_dcn_col2im_workspace': (_sz, [ctypes.POINTER(DcnDesc)]),
     'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),

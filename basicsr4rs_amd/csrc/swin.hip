@@ -132,13 +132,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, i
 }
 
 __global__ void ln_bwd_reduce(const float* __restrict__ partial, int nw, int C, float* __restrict__ dgamma,
-                              float* __restrict__ dbeta) {
+                              float* __restrict__ dbeta, int acc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 2 * C) return;
   const int which = i / C, c = i % C;
   float s = 0.f;
   for (int w = 0; w < nw; ++w) s += partial[((size_t)w * 2 + which) * C + c];
-  (which ? dbeta : dgamma)[c] = s;
+  float* o = which ? dbeta : dgamma;
+  o[c] = (acc ? o[c] : 0.f) + s;
 }
 
 // Vectorised bf16 LayerNorm for padded widths Cp <= 256 (SwinIR embed 60..180): half a
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16_t* __restrict__
 // dgamma / dbeta = sum over nb block partials: 64 columns per block, 16 waves split the
 // partial rows, LDS combine.
 __global__ __launch_bounds__(1024) void ln_bwd_reduce8(const float* __restrict__ partial, int nb, int C,
-                                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int acc) {
   __shared__ float red[16][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
   float sm = 0.f;
@@ -293,7 +294,8 @@ __global__ __launch_bounds__(1024) void ln_bwd_reduce8(const float* __restrict__
 #pragma unroll
     for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
     const int which = col / C, c = col - which * C;
-    (which ? dbeta : dgamma)[c] = t;
+    float* o = which ? dbeta : dgamma;
+    o[c] = (acc ? o[c] : 0.f) + t;
   }
 }
 
@@ -887,7 +889,7 @@ bool attn_mfma_ok(const AttnArgs& a, int dtype) {
 // dbias[bin][h] = sum over the units of head h of dbias_part[unit][bin]: one block per
 // (head, 64-bin chunk), 16 waves split the units (coalesced 64-bin rows), LDS combine.
 __global__ __launch_bounds__(1024) void wattn_dbias_reduce2(const float* __restrict__ part, int units, int nH, int nbins,
-                                                            float* __restrict__ dbias) {
+                                                            float* __restrict__ dbias, int acc) {
   __shared__ float red[16][64];
   const int h = blockIdx.x % nH, chunk = blockIdx.x / nH;
   const int bin = chunk * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
@@ -900,7 +902,7 @@ __global__ __launch_bounds__(1024) void wattn_dbias_reduce2(const float* __restr
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
-    dbias[bin * nH + h] = t;
+    dbias[bin * nH + h] = (acc ? dbias[bin * nH + h] : 0.f) + t;
   }
 }
 
@@ -949,7 +951,7 @@ size_t sr_layernorm_bwd_workspace(int64_t M, int C) {
 
 int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean, const float* rstd,
                      const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr, void* dx, int lddx,
-                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes, void* stream) {
+                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes, int accumulate, void* stream) {
   if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || C > 512)
     return sr_fail(SR_EINVAL, "layernorm_bwd: bad arguments");
   if (ws_bytes < sr_layernorm_bwd_workspace(M, C)) return sr_fail(SR_EINVAL, "layernorm_bwd: workspace too small");
@@ -960,7 +962,7 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
     hipLaunchKernelGGL(ln_bwd8_kernel, dim3(g8), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
                        rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
     hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 63) / 64), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
-                       dgamma, dbeta);
+                       dgamma, dbeta, accumulate);
     return sr_check(hipGetLastError(), "layernorm_bwd launch");
   }
   if (dtype == SR_BF16)
@@ -970,7 +972,7 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)dy, lddy, (const float*)x, ldx,
                        mean, rstd, gamma, M, C, Cp, (const float*)res, ldr, (float*)dx, lddx, (float*)workspace);
   hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * C + 255) / 256), dim3(256), 0, s, (const float*)workspace, (int)grid * 4,
-                     C, dgamma, dbeta);
+                     C, dgamma, dbeta, accumulate);
   return sr_check(hipGetLastError(), "layernorm_bwd launch");
 }
 
@@ -998,7 +1000,7 @@ size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH) {
 int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo, const float* lse,
                        int N, int H, int W, int ws, int shift, int nH, int hd, int hdp, float scale,
                        const float* bias_table, void* dqkv, float* dbias_table, void* workspace, size_t ws_bytes,
-                       void* stream) {
+                       int accumulate, void* stream) {
   AttnArgs a{};
   if (!qkv || !out || !dout || !lse || !bias_table || !dqkv || !dbias_table ||
       !attn_setup(a, N, H, W, ws, shift, nH, hd, hdp, scale))
@@ -1017,7 +1019,7 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
     hipLaunchKernelGGL(wattn_bwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
   }
   hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((a.nbins + 63) / 64)), dim3(1024), 0, s,
-                     (const float*)workspace, parts, nH, a.nbins, dbias_table);
+                     (const float*)workspace, parts, nH, a.nbins, dbias_table, accumulate);
   return sr_check(hipGetLastError(), "window_attn_bwd launch");
 }
 

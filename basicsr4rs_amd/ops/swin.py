@@ -112,12 +112,27 @@ def layernorm(x, weight, bias, Creal, eps=1e-5):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None):
+def _direct(params):
+    """The optimizer's flat .grad views of ``params`` when every one has one (kernels then
+    accumulate into them and the gradient-ready callbacks fire), else None."""
+    if params is None:
+        return None
+    tg = [C.grad_target(p) for p in params]
+    return tg if all(g is not None for g in tg) else None
+
+
+def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None):
+    """dx, dgamma, dbeta; with ``params=(weight, bias)`` held in a FlatParams buffer the
+    parameter gradients are accumulated in place and (dx, None, None) is returned."""
     N, H, W, Cp = x.shape
     M = N * H * W
     dx = torch.empty_like(x)
-    dg = torch.empty(Creal, device=x.device, dtype=torch.float32)
-    db = torch.empty(Creal, device=x.device, dtype=torch.float32)
+    direct = _direct(params)
+    if direct is not None:
+        dg, db = direct
+    else:
+        dg = torch.empty(Creal, device=x.device, dtype=torch.float32)
+        db = torch.empty(Creal, device=x.device, dtype=torch.float32)
     lib = _lib.load()
     wsb = lib.sr_layernorm_bwd_workspace(M, Creal)
     ws = torch.empty(wsb // 4 + 1, device=x.device, dtype=torch.float32)
@@ -126,7 +141,11 @@ def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None):
             lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
                                  _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res),
                                  res.shape[-1] if res is not None else 0, _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db),
-                                 _lib.ptr(ws), wsb, _lib.stream()))
+                                 _lib.ptr(ws), wsb, int(direct is not None), _lib.stream()))
+    if direct is not None:
+        for p in params:
+            C.grad_ready(p)
+        return dx, None, None
     return dx, dg, db
 
 
@@ -137,13 +156,14 @@ class _LayerNorm(torch.autograd.Function):
     def forward(ctx, x, weight, bias, Creal):
         y, mean, rstd = layernorm(x, weight, bias, Creal)
         ctx.Creal = Creal
-        ctx.save_for_backward(x, mean, rstd, weight)
+        ctx.save_for_backward(x, mean, rstd, weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, mean, rstd, weight = ctx.saved_tensors
-        dx, dg, db = layernorm_bwd(dy.to(x.dtype).contiguous(), x, mean, rstd, weight, ctx.Creal)
+        x, mean, rstd, weight, bias = ctx.saved_tensors
+        dx, dg, db = layernorm_bwd(dy.to(x.dtype).contiguous(), x, mean, rstd, weight, ctx.Creal,
+                                   params=(weight, bias))
         return dx, dg, db, None
 
 
@@ -180,9 +200,10 @@ def window_attn(qkv, g, N, H, W, scale, table):
     return out, lse
 
 
-def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table):
+def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table, table_param=None):
     dqkv = torch.empty_like(qkv)
-    dtable = torch.empty_like(table)
+    direct = _direct((table_param,) if table_param is not None else None)
+    dtable = direct[0] if direct is not None else torch.empty_like(table)
     lib = _lib.load()
     wsb = lib.sr_window_attn_bwd_workspace(N, H, W, g.ws, g.nH)
     ws = torch.empty(wsb // 4 + 1, device=qkv.device, dtype=torch.float32)
@@ -190,7 +211,11 @@ def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table):
         _lib.check(
             lib.sr_window_attn_bwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], _lib.ptr(out), _lib.ptr(dout),
                                    out.shape[-1], _lib.ptr(lse), N, H, W, g.ws, g.shift, g.nH, g.hd, g.hdp, float(scale),
-                                   _lib.ptr(table), _lib.ptr(dqkv), _lib.ptr(dtable), _lib.ptr(ws), wsb, _lib.stream()))
+                                   _lib.ptr(table), _lib.ptr(dqkv), _lib.ptr(dtable), _lib.ptr(ws), wsb,
+                                   int(direct is not None), _lib.stream()))
+    if direct is not None:
+        C.grad_ready(table_param)
+        return dqkv, None
     return dqkv, dtable
 
 
@@ -216,13 +241,13 @@ class _STB(torch.autograd.Function):
         out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0)
         ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale = geom, fc1s, fc2s, scale
         ctx.save_for_backward(x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w,
-                              f1b, f2w, f2b)
+                              f1b, f2w, f2b, n1b, n2b, table)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         (x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w, f1b, f2w,
-         f2b) = ctx.saved_tensors
+         f2b, n1b, n2b, table) = ctx.saved_tensors
         g, fc1s, fc2s, scale = ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale
         dtype = x.dtype
         N, H, W, Cp = x.shape
@@ -234,15 +259,15 @@ class _STB(torch.autograd.Function):
         _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
         dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
         df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W, params=(f1w, f1b))
-        dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout)
+        dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b))
         _, pwd, _ = prepared_linear(pw, pb, g.proj, dtype)
         da = linear_dgrad(dx2, pwd, g.proj, N, H, W)
         dpw, dpb = linear_wgrad(dx2, a, g.proj, N, H, W, params=(pw, pb))
-        dqkv, dtab = window_attn_bwd(qkv, a, da, lse, g, N, H, W, scale, tab)
+        dqkv, dtab = window_attn_bwd(qkv, a, da, lse, g, N, H, W, scale, tab, table_param=table)
         _, qwd, _ = prepared_linear(qw, qb, g.qkv, dtype)
         dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
         dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W, params=(qw, qb))
-        dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2)
+        dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2, params=(n1w, n1b))
         return (dx, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b)
 
 

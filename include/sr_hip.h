@@ -245,11 +245,12 @@ int sr_copy_channels(int dtype, const void* src, int lds, int scoff, void* dst, 
 int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, const float* beta, int64_t M,
                      int C, int Cp, float eps, void* y, int ldy, float* mean, float* rstd, void* stream);
 size_t sr_layernorm_bwd_workspace(int64_t M, int C);
-/* dx = LN backward (+ res if not NULL), dgamma / dbeta over all rows (deterministic). */
+/* dx = LN backward (+ res if not NULL), dgamma / dbeta over all rows (deterministic);
+ * accumulate = 1 adds them to dgamma / dbeta (the optimizer's gradient views). */
 int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean,
                      const float* rstd, const float* gamma, int64_t M, int C, int Cp, const void* res,
                      int ldr, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
-                     size_t ws_bytes, void* stream);
+                     size_t ws_bytes, int accumulate, void* stream);
 /* Shifted-window multi-head attention on [N*H*W][ldq] qkv rows laid out [3][nH][hdp]
  * (head_dim hd <= hdp, zero padded): cyclic shift by `shift`, ws x ws windows, scale,
  * relative-position bias table [(2ws-1)^2][nH], -100 shift mask; out rows [nH][hdp];
@@ -261,7 +262,7 @@ size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH);
 int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo,
                        const float* lse, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp,
                        float scale, const float* bias_table, void* dqkv, float* dbias_table, void* workspace,
-                       size_t ws_bytes, void* stream);
+                       size_t ws_bytes, int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * basicsr/ops native extensions (replacements of deform_conv_ext, fused_act_ext,
