@@ -28,7 +28,8 @@ class ConvDesc(ctypes.Structure):
                 ('in_ps', _i), ('Cout', _i), ('Cout_real', _i), ('ldw', _i), ('ldy', _i), ('ycoff', _i),
                 ('out_ps', _i), ('out_nchw', _i), ('act', _i), ('slope', _f), ('alpha', _f), ('ldg', _i),
                 ('gcoff', _i), ('gate_slope', _f), ('ldr', _i), ('rcoff', _i), ('beta', _f), ('ldr2', _i),
-                ('r2coff', _i), ('beta2', _f), ('rcols', _i), ('in_up', _i), ('ksize', _i), ('gate_mode', _i)]
+                ('r2coff', _i), ('beta2', _f), ('rcols', _i), ('in_up', _i), ('ksize', _i), ('gate_mode', _i),
+                ('gcol0', _i), ('gcol1', _i)]
 
 
 class WgradDesc(ctypes.Structure):

@@ -51,7 +51,8 @@ struct FwdArgs {
   float beta2;
   int in_up;  // nearest-neighbour upsample factor folded into the A gather (1 = none)
   int tap0;   // 4 for 1x1 (linear) convs: the single tap is the centre one
-  int gate_mode;  // 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate)
+  int gate_mode;  // 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate); 2: post-residual, gcol0..gcol1
+  int gcol0, gcol1;
   void* aux;      // optional store of the pre-activation value (same layout as y)
   float* colsum;  // optional per-(wave, row chunk) column sums of the stored y (see epilogue_tile)
   int tiles_n, tiles;
@@ -129,7 +130,10 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     const bool okr = ok && n < a.rcols;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      if (a.gate) gv[it][v] = buf_load16(gr, ok ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ) + 16u * v : SR_OOB);
+      if (a.gate) {
+        const bool gok = ok && (a.gate_mode != 2 || (n >= a.gcol0 && n < a.gcol1));
+        gv[it][v] = buf_load16(gr, gok ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * SZ) + 16u * v : SR_OOB);
+      }
       if (a.res) rv1[it][v] = buf_load16(rr, okr ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * SZ) + 16u * v : SR_OOB);
       if (a.res2)
         rv2[it][v] = buf_load16(rr2, okr ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * SZ) + 16u * v : SR_OOB);
@@ -178,7 +182,7 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
-    if (a.gate) {
+    if (a.gate && a.gate_mode != 2) {
       float g[8];
       unpack(gv[it], g);
       if (a.gate_mode == 1) {
@@ -202,6 +206,12 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
       unpack(rv2[it], rv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rv[j] + v[j];
+    }
+    if (a.gate && a.gate_mode == 2 && n >= a.gcol0 && n < a.gcol1) {
+      float g[8];
+      unpack(gv[it], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
     }
     size_t dst;  // element offset of the 8-channel group
     if (a.out_ps == 0) {
@@ -1158,7 +1168,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       if (m >= a.M) continue;
       u32x4 gv, rv, rv2;
       const bool rok = n < a.rcols;
-      if (a.gate) gv = buf_load16(gr, (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2));
+      if (a.gate) gv = buf_load16(gr, (a.gate_mode != 2 || (n >= a.gcol0 && n < a.gcol1))
+                                          ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2) : SR_OOB);
       if (a.res) rv = buf_load16(rr, rok ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
       if (a.res2) rv2 = buf_load16(rr2, rok ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * 2) : SR_OOB);
       float v[8];
@@ -1172,7 +1183,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
-      if (a.gate) {
+      if (a.gate && a.gate_mode != 2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float g0 = bf16_to_f32(gv[j] & 0xffff), g1 = bf16_to_f32(gv[j] >> 16);
@@ -1199,6 +1210,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
         for (int j = 0; j < 4; ++j) {
           v[2 * j] += a.beta2 * bf16_to_f32(rv2[j] & 0xffff);
           v[2 * j + 1] += a.beta2 * bf16_to_f32(rv2[j] >> 16);
+        }
+      }
+      if (a.gate && a.gate_mode == 2 && n >= a.gcol0 && n < a.gcol1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[2 * j] *= bf16_to_f32(gv[j] & 0xffff) > 0.f ? 1.f : a.gate_slope;
+          v[2 * j + 1] *= bf16_to_f32(gv[j] >> 16) > 0.f ? 1.f : a.gate_slope;
         }
       }
       u32x4 o;
@@ -2626,6 +2644,7 @@ FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
   a.cpt = d->Cin / PER; a.nkc = taps * a.cpt;
   a.tap0 = taps == 1 ? 4 : 0;
   a.gate_mode = d->gate_mode;
+  a.gcol0 = d->gcol0; a.gcol1 = d->gcol1;
   a.Cout = d->Cout; a.Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout; a.ldw = d->ldw;
   a.ldy = d->ldy; a.ycoff = d->ycoff; a.out_ps = d->out_ps; a.out_nchw = d->out_nchw;
   a.act = d->act; a.slope = d->slope; a.alpha = d->alpha;

@@ -215,14 +215,14 @@ class _RRDB(torch.autograd.Function):
             dB = torch.empty(N, H, W, Cb, device=x.device, dtype=dtype)
             a5 = 0.04 if r == 2 else 0.2
             rb = 0.2 if r == 2 else 1.0
-            # dB[0:Cb] = a5 * dgrad5(d_in) ; dB[0:nf] += rb * d_in  (RDB skip)
+            # dB[0:Cb] = a5 * dgrad5(d_in) ; dB[0:nf] += rb * d_in  (RDB skip); slice 3 (x4) is complete
+            # here, so its LeakyReLU backward is applied in the same epilogue (post-residual gate)
             C.conv_fwd_raw(d_in, wd5, None, dB, N, H, W, nf, Cb, Cb, alpha=a5, res=d_in, beta=rb, rcols=nf, ldx=ld_in,
-                           ldr=ld_in, ldy=Cb)
+                           ldr=ld_in, ldy=Cb, gate=B, gate_slope=0.2, gate_mode=2, gcol0=nf + 3 * gc, gcol1=Cb)
             grads[r * 10 + 8], grads[r * 10 + 9] = C.conv_wgrad_raw(d_in, B, N, H, W, Cb, Cb, nf, nf, scale=a5,
                                                                    ldy=ld_in, ldx=Cb, params=(w5, b5))
             for k in (3, 2, 1, 0):
-                co = nf + k * gc
-                _act_bwd_inplace(dB, B, Cb, co, gc, P, 0.2)
+                co = nf + k * gc  # slice k (x_{k+1}) arrived complete and activation-backward'ed
                 w, b = params[r * 10 + 2 * k], params[r * 10 + 2 * k + 1]
                 _, wd, _ = C.prepared(w, b, specs[k], dtype)
                 last = (r == 0 and k == 0)
@@ -231,7 +231,11 @@ class _RRDB(torch.autograd.Function):
                     dx = torch.empty(N, H, W, nf, device=x.device, dtype=dtype)
                     C.conv_fwd_raw(dB, wd, None, dx, N, H, W, gc, co, co, res=dB, beta=1.0, res2=dout, beta2=1.0,
                                    ldx=Cb, xcoff=co, ldr=Cb, ldr2=nf, ldy=nf)
-                else:
+                elif k > 0:
+                    # dB[0:co] += dgrad_k; this completes slice k-1, whose LeakyReLU backward rides along
+                    C.conv_fwd_raw(dB, wd, None, dB, N, H, W, gc, co, co, res=dB, beta=1.0, ldx=Cb, xcoff=co, ldr=Cb,
+                                   ldy=Cb, gate=B, gate_slope=0.2, gate_mode=2, gcol0=co - gc, gcol1=co)
+                else:  # k == 0: dB[0:nf] is the RDB input's gradient (no activation)
                     C.conv_fwd_raw(dB, wd, None, dB, N, H, W, gc, co, co, res=dB, beta=1.0, ldx=Cb, xcoff=co, ldr=Cb,
                                    ldy=Cb)
                 grads[r * 10 + 2 * k], grads[r * 10 + 2 * k + 1] = C.conv_wgrad_raw(

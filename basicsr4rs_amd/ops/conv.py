@@ -161,6 +161,7 @@ def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
     d.ldr2, d.r2coff, d.beta2 = kw.get('ldr2', 0), kw.get('r2coff', 0), kw.get('beta2', 1.0)
     d.rcols, d.in_up = kw.get('rcols', 0), kw.get('in_up', 0)
     d.ksize, d.gate_mode = kw.get('ksize', 3), kw.get('gate_mode', 0)
+    d.gcol0, d.gcol1 = kw.get('gcol0', 0), kw.get('gcol1', 0)
     d.ldw = (9 if d.ksize == 3 else 1) * cin
     return d
 

@@ -75,7 +75,11 @@ typedef struct sr_conv3x3_desc {
   int rcols;  /* residuals apply to output columns n < rcols (0 = all) */
   int in_up;  /* x is the [N, H/u, W/u] map read through nearest-neighbour upsampling (0/1 = none) */
   int ksize;  /* 3 (default, 0 = 3) or 1: a 1x1 conv = nn.Linear over the NHWC tokens */
-  int gate_mode; /* 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate) (gate = pre-activation) */
+  int gate_mode; /* 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate) (gate = pre-activation);
+                  2: after the residuals, v *= (gate > 0 ? 1 : gate_slope) on output columns
+                  gcol0 <= n < gcol1 only (activation backward of a dense-block slice whose
+                  gradient this call completes) */
+  int gcol0, gcol1;
 } sr_conv3x3_desc;
 
 /* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.
