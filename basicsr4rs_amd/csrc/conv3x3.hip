@@ -2601,6 +2601,7 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
   int extra = 0;  // bias-role blocks per split (big kernel)
   if (wg_use_halo(d)) {
     // ~2 blocks per CU, but at least 8 K-steps per block (the slab costs 8 B per tap-MAC row)
+    // (A/B on RCAN / RRDB: twice or half as many splits are 6-12 % slower per step)
     const int chunks = (d->Cin + 63) / 64;
     int S = 512 / chunks;
     const int maxS = M / 512 > 1 ? M / 512 : 1;
