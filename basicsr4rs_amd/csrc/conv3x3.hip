@@ -1239,8 +1239,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
 // per wave and chunk, not once per tap and pixel tile.  The fp32 tile goes
 // through the shared fused epilogue (bias, activation, gate, residuals, pixel shuffle).
 // ------------------------------------------------------------------------------------
-template <int CO_T, int DBG = 0, bool W256 = false>
+// DIRECT (CO_T 4, plain store, no colsum): C = W x X^T with the two co tiles of a wave
+// row-permuted (tile c row r -> channel 8(r/4) + 4c + r%4), so each lane ends with 8
+// consecutive channels of one pixel and the fused epilogue stores 16 B from registers -- no
+// LDS staging round trip (which cost ~1/3 of the kernel at nf 64).
+template <int CO_T, int DBG = 0, bool W256 = false, bool DIRECT = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
+  static_assert(!DIRECT || CO_T == 4, "direct epilogue: two co tiles per wave");
   constexpr int BN = CO_T * 16;
   constexpr int CSTR = BN + 4;
   constexpr int CW = CO_T >= 4 ? CO_T / 2 : 1;  // co tiles per wave
@@ -1310,7 +1315,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int c = 0; c < CW; ++c) {
-            const int co = n0 + (wc * CW + c) * 16 + c16, ci = ci0 + kk * 32 + 8 * g;
+            const int co = DIRECT ? n0 + wc * CW * 16 + 8 * (c16 >> 2) + 4 * c + (c16 & 3)
+                                  : n0 + (wc * CW + c) * 16 + c16;
+            const int ci = ci0 + kk * 32 + 8 * g;
             const int tap = ty * 3 + tx;
             const bool v = co < a.Cout && ci < a.Cin && (DBG != 1 || tap == 0);
             if (kk == 0 || khi)
@@ -1337,13 +1344,92 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
           for (int i = 0; i < PT; ++i) {
             const u32x4 fa = *(const u32x4*)(smem + swz128(hb[i] + z + toff, kk * 4 + g));
 #pragma unroll
-            for (int c = 0; c < CW; ++c) mfma_chunk<bf16_t>(fa, bw[ty & 1][DBG == 1 ? 0 : tx][kk][c], acc[i][c]);
+            for (int c = 0; c < CW; ++c) {
+              if constexpr (DIRECT)
+                mfma_chunk<bf16_t>(bw[ty & 1][DBG == 1 ? 0 : tx][kk][c], fa, acc[i][c]);
+              else
+                mfma_chunk<bf16_t>(fa, bw[ty & 1][DBG == 1 ? 0 : tx][kk][c], acc[i][c]);
+            }
           }
         }
       }
     }
   }
 
+  if constexpr (DIRECT) {
+    // lane (g, c16): channels n0 + 32 wc + 8g .. +7 of pixel m0 + 16 (PT wp + i) + c16
+    const int nn = n0 + wc * 32 + 8 * g;
+    if (nn >= a.Cout || DBG == 3) return;
+    const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+    const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+    float bv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[j] = 0.f;
+    if (a.bias) {
+      const f32x4 b0 = *(const f32x4*)(a.bias + nn), b1 = *(const f32x4*)(a.bias + nn + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { bv[j] = b0[j]; bv[4 + j] = b1[j]; }
+    }
+    const bool gok = a.gate_mode != 2 || (nn >= a.gcol0 && nn < a.gcol1);
+    const bool rok = nn < a.rcols;
+    auto unpack8 = [](const u32x4& q, float* o) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[2 * j] = bf16_to_f32(q[j] & 0xffff);
+        o[2 * j + 1] = bf16_to_f32(q[j] >> 16);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int m = m0 + 16 * (PT * wp + i) + c16;
+      if (m >= a.M) continue;
+      u32x4 gv, rv, rv2;
+      if (a.gate) gv = buf_load16(gr, gok ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + nn) * 2) : SR_OOB);
+      if (a.res) rv = buf_load16(rr, rok ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + nn) * 2) : SR_OOB);
+      if (a.res2) rv2 = buf_load16(rr2, rok ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + nn) * 2) : SR_OOB);
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
+      if (a.aux) {
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        *(u32x4*)((bf16_t*)a.aux + (size_t)m * a.ldy + a.ycoff + nn) = o;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+      float gf[8];
+      if (a.gate) unpack8(gv, gf);
+      if (a.gate && a.gate_mode != 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= a.gate_mode == 1 ? gelu_grad(gf[j]) : (gf[j] > 0.f ? 1.f : a.gate_slope);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+      if (a.res && rok) {
+        float rf[8];
+        unpack8(rv, rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a.beta * rf[j] + v[j];
+      }
+      if (a.res2 && rok) {
+        float rf[8];
+        unpack8(rv2, rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rf[j] + v[j];
+      }
+      if (a.gate && a.gate_mode == 2 && gok) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+      }
+      u32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      *(u32x4*)((bf16_t*)a.y + (size_t)m * a.ldy + a.ycoff + nn) = o;
+    }
+    return;
+  }
   float* Cs = (float*)smem;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -2477,6 +2563,8 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);
   else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), grid, dim3(256), 0, s, a);
   else if (g_variant == 13) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 3>), grid, dim3(256), 0, s, a);
+  else if (!a.colsum && !a.out_nchw && a.out_ps == 0 && g_variant != 30)
+    hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 0, false, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<4>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -2752,7 +2840,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 29)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 30)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
   g_variant = variant;
   return SR_OK;
