@@ -2580,7 +2580,10 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
 FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_lin(a, bf)) return FK_LIN;
   if (fwd_use_halo(a, bf)) return FK_HALO;
-  if (bf && !a.out_nchw && a.Cout >= 256 && a.in_up == 1 && !g_disable_big) return FK_BIG;
+  // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
+  // kernel with a partial N tile: x read once (vs twice by 128x128 tiles); 68 -> 57 us and 82 -> 65 us
+  const bool lin_big = a.tap0 == 4 && a.Cin > 192 && a.Cout >= 128 && g_variant != 31;
+  if (bf && !a.out_nchw && (a.Cout >= 256 || lin_big) && a.in_up == 1 && !g_disable_big) return FK_BIG;
   if (a.out_nchw || a.Cout <= 16) return FK_256_16;
   if (a.Cout <= 32) return FK_256_32;
   if (a.Cout <= 64) return FK_128_64;
@@ -2840,8 +2843,8 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 30)
-    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations)");
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 32)
+    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-32: schedule A/B switches)");
   g_variant = variant;
   return SR_OK;
 }

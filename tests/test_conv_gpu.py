@@ -152,12 +152,14 @@ def test_edsr_m_parity_fp32(cuda):
 
 @pytest.mark.parametrize('shape', [(2, 64, 64, 256, 256, 0, 3), (1, 20, 36, 256, 512, 0, 3), (3, 17, 9, 256, 768, 0, 3),
                                    (1, 16, 16, 1024, 256, 2, 3), (2, 8, 24, 256, 1024, 2, 3),
-                                   (1, 12, 20, 264, 256, 0, 3), (2, 16, 16, 64, 256, 0, 1), (1, 9, 15, 184, 544, 0, 1)])
+                                   (1, 12, 20, 264, 256, 0, 3), (2, 16, 16, 64, 256, 0, 1), (1, 9, 15, 184, 544, 0, 1),
+                                   (2, 8, 16, 576, 184, 0, 1), (1, 9, 15, 368, 184, 0, 1), (1, 5, 13, 368, 544, 0, 1)])
 def test_big_tile_kernel_bitwise_equals_small(cuda, shape):
     """The phase-interleaved 256x256 kernel (variant 24: never the halo form), the 128x128
     register-staged kernel (1) and the two-barrier 256x256 kernel (2) sum K in the same order,
     so their bf16 outputs must be bitwise identical (partial M/N tiles, K-steps crossing taps,
-    a single K-step, 1x1 taps, in_ps gather)."""
+    a single K-step, 1x1 taps, in_ps gather).  1x1 shapes with K > 192 and Cout >= 128
+    (SwinIR fc2 / qkv and fc1 dgrads) take the 256x256 kernels with a partial N tile."""
     N, H, W, cin, cout, in_ps, ks = shape
     torch.manual_seed(3)
     dt = torch.bfloat16
