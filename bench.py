@@ -154,16 +154,19 @@ def main():
     gt = torch.rand(B, 3, 4 * lr_px, 4 * lr_px, generator=g1, device=dev)
     model.feed_data({'lq': lq, 'gt': gt})
 
-    # With a captured step, the per-kernel HIP-event trace is taken on the last eager warm-up
-    # step (a graph replay runs the same kernels but cannot be instrumented per launch); the
-    # capture happens on warm-up step 3, so at least 3 warm-up steps run.
+    # The per-kernel HIP-event trace is taken on one untimed warm-up step, never inside the timed
+    # region (per-launch events would slow the timed steps).  With a captured step it is the last
+    # eager warm-up step (a graph replay runs the same kernels but cannot be instrumented per
+    # launch; capture happens on warm-up step 3, so at least 3 warm-up steps run); eager (DDP)
+    # runs trace their last warm-up step.
     it = 0
-    warmup = max(args.warmup, 3) if use_graph else args.warmup
+    warmup = max(args.warmup, 3) if use_graph else max(args.warmup, 0 if args.no_trace else 2)
+    trace_w = 1 if use_graph else warmup - 1
     kstats, traced_steps = {}, 0
     for w in range(warmup):
         it += 1
         model.update_learning_rate(it)
-        if use_graph and w == 1 and not args.no_trace:
+        if w == trace_w and not args.no_trace:
             torch.cuda.synchronize()
             ktrace.start()
             model.optimize_parameters(it)
@@ -173,8 +176,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if not args.no_trace and not use_graph:
-        ktrace.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         it += 1
@@ -184,8 +185,6 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if not args.no_trace and not use_graph:
-        kstats, traced_steps = ktrace.stop(), args.steps
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -212,7 +211,7 @@ def main():
                      'share_of_step': round(st['ms'] / traced_steps * 1e-3 / (dt / args.steps), 3),
                      'timing': 'HIP events on the stream of each launch, ' +
                                ('one eager step before capture (replays run the same kernels)' if use_graph
-                                else 'over the timed steps')})
+                                else 'the last (untimed) warm-up step')})
         tr = _pmc_traffic(args.workload, name)
         if tr:
             roof['traffic'] = round(tr['hbm_bytes_per_launch'])
