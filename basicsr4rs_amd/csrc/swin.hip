@@ -178,36 +178,46 @@ __global__ __launch_bounds__(256) void ln_fwd8_kernel(const bf16_t* __restrict__
     gm[j] = c0 + j < C ? gamma[c0 + j] : 0.f;
     bt[j] = c0 + j < C ? beta[c0 + j] : 0.f;
   }
+  // RU rows per half-wave per iteration, all loads issued before any reduction: one 16-B load
+  // per lane in flight left the kernel at ~2.8 TB/s (too few bytes in flight per CU)
+  constexpr int RU = 4;
   const int64_t nrw = (int64_t)gridDim.x * 8;
-  for (int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); row < M; row += nrw) {
-    float v[8];
-    if (c0 < Cp) {
-      unpack8(*(const u32x4*)(x + row * ldx + c0), v);
-    } else {
+  for (int64_t r0 = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); r0 < M; r0 += RU * nrw) {
+    u32x4 raw[RU];  // packed until use: 4 VGPRs per row in flight instead of 8
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    for (int k = 0; k < RU; ++k) {
+      const int64_t row = r0 + k * nrw;
+      raw[k] = (c0 < Cp && row < M) ? *(const u32x4*)(x + row * ldx + c0) : u32x4{0u, 0u, 0u, 0u};
     }
-    float sm = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (c0 + j >= C) v[j] = 0.f;
-      sm += v[j];
-    }
-    const float mu = hsum32(sm) / C;
-    float q = 0.f;
+    for (int k = 0; k < RU; ++k) {
+      const int64_t row = r0 + k * nrw;
+      float v[1][8];
+      unpack8(raw[k], v[0]);
+      float sm = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d = c0 + j < C ? v[j] - mu : 0.f;
-      q += d * d;
-    }
-    const float rs = rsqrtf(hsum32(q) / C + eps);
-    float o[8];
+      for (int j = 0; j < 8; ++j) {
+        if (c0 + j >= C) v[0][j] = 0.f;
+        sm += v[0][j];
+      }
+      const float mu = hsum32(sm) / C;
+      float q = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = c0 + j < C ? (v[j] - mu) * rs * gm[j] + bt[j] : 0.f;
-    if (c0 < Cp) *(u32x4*)(y + row * ldy + c0) = pack8(o);
-    if (hl == 0) {
-      mean_out[row] = mu;
-      rstd_out[row] = rs;
+      for (int j = 0; j < 8; ++j) {
+        const float d = c0 + j < C ? v[0][j] - mu : 0.f;
+        q += d * d;
+      }
+      const float rs = rsqrtf(hsum32(q) / C + eps);
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = c0 + j < C ? (v[0][j] - mu) * rs * gm[j] + bt[j] : 0.f;
+      if (row < M) {
+        if (c0 < Cp) *(u32x4*)(y + row * ldy + c0) = pack8(o);
+        if (hl == 0) {
+          mean_out[row] = mu;
+          rstd_out[row] = rs;
+        }
+      }
     }
   }
 }
