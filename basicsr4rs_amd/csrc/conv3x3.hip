@@ -2367,6 +2367,60 @@ __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw
   }
 }
 
+// Slab reduction for the RGB head conv (Cin_real <= 8, not a multiple of 4): wgrad_reduce_kernel
+// gives each (co, ci) pair ONE thread that walks all S slabs (RRDB conv_first: 192 threads x
+// S 1024 = 1.28 ms).  Here one block per output channel: 256 threads split the slabs, each
+// keeps 9 x Cin_real (+ bias) partial sums, then a fixed-order LDS tree -- deterministic.
+__global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(const float* ws, const float* wsb, float* dw,
+                                                                  float* db, int S, int Cout, int Cin, int Cin_real,
+                                                                  int out_ps, int taps, const int* co_map,
+                                                                  const int* ci_map, float scale, int accumulate) {
+  constexpr int NV = 9 * 8 + 1;
+  __shared__ float red[NV][256];
+  const int co = blockIdx.x, t = threadIdx.x;
+  const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
+  const int cps = (int)gridDim.x / r2;
+  const int cop = co_map ? co_map[co] : (out_ps > 0 ? (co % r2) * cps + co / r2 : co);
+  int cip[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) cip[c] = c < Cin_real ? (ci_map ? ci_map[c] : c) : 0;
+  float s[9][8], sb = 0.f;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) s[tp][c] = 0.f;
+  const size_t stride = (size_t)taps * Cout * Cin, tstride = (size_t)Cout * Cin;
+  for (int k = t; k < S; k += 256) {
+    const float* src = ws + k * stride + (size_t)cop * Cin;
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (tp < taps && c < Cin_real) s[tp][c] += src[tp * tstride + cip[c]];
+    if (db) sb += wsb[(size_t)k * Cout + cop];
+  }
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) red[tp * 8 + c][t] = s[tp][c];
+  red[NV - 1][t] = sb;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w)
+      for (int v = 0; v < NV; ++v) red[v][t] += red[v][t + w];
+    __syncthreads();
+  }
+  if (t < 9 * 8) {
+    const int tp = t >> 3, c = t & 7;
+    if (tp < taps && c < Cin_real) {
+      float* d = dw + ((size_t)co * Cin_real + c) * taps + tp;
+      *d = red[t][0] * scale + (accumulate ? *d : 0.f);
+    }
+  } else if (t == NV - 1 && db) {
+    db[co] = red[t][0] * scale + (accumulate ? db[co] : 0.f);
+  }
+}
+
 // Slab reduction for Cin_real % 4 == 0 (16-B loads, or gathered through ci_map): 64 (tap, co, 4 ci) groups per
 // 1024-thread block; the 16 waves take splits k = wave (mod 16) with independent 16-B loads
 // (coalesced along ci), then a fixed-order LDS combine -- deterministic, and S / 16 loads
@@ -2843,8 +2897,8 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 32)
-    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-32: schedule A/B switches)");
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 33)
+    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-33: schedule A/B switches)");
   g_variant = variant;
   return SR_OK;
 }
@@ -2928,6 +2982,10 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s, (const float*)a.ws,
                        (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map,
                        ci_map, d->scale, wblocks, d->accumulate);
+  } else if (Cin_real <= 8 && g_variant != 33) {
+    hipLaunchKernelGGL(wgrad_reduce_narrow_kernel, dim3((unsigned)Cout_real), dim3(256), 0, s, (const float*)a.ws,
+                       (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cin_real, d->out_ps, taps, co_map, ci_map,
+                       d->scale, d->accumulate);
   } else {
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
                        (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,

@@ -485,3 +485,32 @@ def test_fwd_halo_w256_nchw_tail(cuda, shape):
     tol = 1e-3 * max(1.0, ref.abs().max().item())
     assert (outs[0].cpu().double() - ref).abs().max().item() <= tol
     assert (outs[0] - outs[1]).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize('shape', [(4, 64, 64, 3, 64), (2, 32, 48, 3, 256), (1, 16, 16, 1, 64)])
+@pytest.mark.parametrize('variant', [0, 33])
+def test_wgrad_rgb_head_reduce_vs_fp64(cuda, shape, variant):
+    """Weight/bias gradient of the RGB head conv (Cin_real 3 or 1, padded to 8 channels): the
+    block-per-channel slab reduce (variant 0) and the one-thread-per-weight reduce (33) against
+    fp64 on the same bf16 operands."""
+    N, H, W, cin_real, cout = shape
+    torch.manual_seed(11)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.zeros(N, H, W, 8)
+    x[..., :cin_real] = torch.randn(N, H, W, cin_real)
+    x = x.to(dt)
+    dy = torch.randn(N, H, W, cout).to(dt)
+    xd = x[..., :cin_real].permute(0, 3, 1, 2).double()
+    w = torch.zeros(cout, cin_real, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xd, w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    _lib.check(lib.sr_conv3x3_set_variant(variant))
+    try:
+        dw, db = C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, 8, cin_real, cout, cout, scale=1.0)
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    dw = dw.cpu().double().reshape(w.shape)
+    assert (dw - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
