@@ -166,8 +166,16 @@ def main():
     for w in range(warmup):
         it += 1
         model.update_learning_rate(it)
-        if w == trace_w and not args.no_trace:
+        if w == trace_w - 1 and not args.no_trace:
+            # a spin kernel ahead of the step BEFORE the traced one lets the host run ahead of
+            # the GPU, so the traced step's launches run back to back and each event pair
+            # brackets its kernel alone (without it, host-issue gaps between short eager kernels
+            # -- RCAN: 2.7k launches -- land inside the spans: 45 us vs rocprof's 27 us); the
+            # untraced step in between brings the clocks back up after the idle spin
             torch.cuda.synchronize()
+            torch.cuda._sleep(int(os.environ.get('SR_TRACE_SLEEP_CYCLES', 400_000_000)))
+            model.optimize_parameters(it)
+        elif w == trace_w and not args.no_trace:
             ktrace.start()
             model.optimize_parameters(it)
             kstats, traced_steps = ktrace.stop(), 1
