@@ -130,7 +130,10 @@ def main():
     if world > 1:
         from basicsr4rs_amd.utils.dist_util import init_dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        init_dist('pytorch', backend='nccl')
+        # RCCL ('nccl') for the real runs; SR_DIST_BACKEND=gloo rehearses the N > 1 path of this
+        # script (barriers, max-over-ranks timing, bucketed reducer) with several ranks on one GPU
+        init_dist('pytorch', backend=os.environ.get('SR_DIST_BACKEND', 'nccl'))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
