@@ -223,13 +223,14 @@ __global__ __launch_bounds__(256) void ln_fwd8_kernel(const bf16_t* __restrict__
 }
 
 // Backward, same mapping; per-block dgamma / dbeta partials (LDS-combined over the block's
-// 8 row slots) -> partial[block][2][C], summed by ln_bwd_reduce8.
-__global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16_t* __restrict__ dy, int lddy, const bf16_t* __restrict__ x,
+// SLOTS row slots) -> partial[block][2][C], summed by ln_bwd_reduce8.
+template <int SLOTS>
+__global__ __launch_bounds__(SLOTS * 32) void ln_bwd8_kernel(const bf16_t* __restrict__ dy, int lddy, const bf16_t* __restrict__ x,
                                                       int ldx, const float* __restrict__ mean,
                                                       const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                       int64_t M, int C, int Cp, const bf16_t* __restrict__ res, int ldr,
                                                       bf16_t* __restrict__ dx, int lddx, float* __restrict__ partial) {
-  __shared__ float red[8][2][256];
+  __shared__ float red[SLOTS][2][256];
   const int lane = threadIdx.x & 63, hl = lane & 31, slot = threadIdx.x >> 5;
   const int c0 = hl * 8;
   float gm[8], dg[8], db[8];
@@ -238,8 +239,8 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16_t* __restrict__
     gm[j] = c0 + j < C ? gamma[c0 + j] : 0.f;
     dg[j] = db[j] = 0.f;
   }
-  const int64_t nrw = (int64_t)gridDim.x * 8;
-  for (int64_t row = (int64_t)blockIdx.x * 8 + slot; row < M; row += nrw) {
+  const int64_t nrw = (int64_t)gridDim.x * SLOTS;
+  for (int64_t row = (int64_t)blockIdx.x * SLOTS + slot; row < M; row += nrw) {
     const float mu = mean[row], rs = rstd[row];
     float d[8], xv[8], rv[8];
     if (c0 < Cp) {
@@ -277,11 +278,11 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(const bf16_t* __restrict__
     red[slot][1][c0 + j] = db[j];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * C; i += 256) {
+  for (int i = threadIdx.x; i < 2 * C; i += SLOTS * 32) {
     const int which = i / C, c = i - which * C;
     float sm = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) sm += red[k][which][c];
+    for (int k = 0; k < SLOTS; ++k) sm += red[k][which][c];
     partial[((size_t)blockIdx.x * 2 + which) * C + c] = sm;
   }
 }
@@ -968,8 +969,10 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
   const unsigned grid = (unsigned)((M + 3) / 4 < 2048 ? (M + 3) / 4 : 2048);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SR_BF16 && ln_vec8(Cp, ldx, lddx) && lddy % 8 == 0 && (!res || ldr % 8 == 0)) {
-    const unsigned g8 = (unsigned)((M + 7) / 8 < LN_BWD_BLOCKS ? (M + 7) / 8 : LN_BWD_BLOCKS);
-    hipLaunchKernelGGL(ln_bwd8_kernel, dim3(g8), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
+    // 16 row slots (512 threads) per block: twice the waves in flight of 8 slots for the same
+    // number of dgamma / dbeta partials (more blocks instead moves the cost into the reduce)
+    const unsigned g8 = (unsigned)((M + 15) / 16 < LN_BWD_BLOCKS ? (M + 15) / 16 : LN_BWD_BLOCKS);
+    hipLaunchKernelGGL(ln_bwd8_kernel<16>, dim3(g8), dim3(512), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
                        rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
     hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 63) / 64), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
                        dgamma, dbeta, accumulate);
