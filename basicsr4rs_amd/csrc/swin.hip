@@ -287,26 +287,37 @@ __global__ __launch_bounds__(SLOTS * 32) void ln_bwd8_kernel(const bf16_t* __res
   }
 }
 
-// dgamma / dbeta = sum over nb block partials: 64 columns per block, 16 waves split the
-// partial rows, LDS combine.
+// dgamma / dbeta = sum over nb block partials: 16 columns per 1024-thread block (23 blocks at
+// C 180 instead of 6 with 64 columns), 64 row lanes per column each summing rows r, r + 64, ...
+// with up to 8 independent loads in flight, then a fixed-order LDS tree -- deterministic.
 __global__ __launch_bounds__(1024) void ln_bwd_reduce8(const float* __restrict__ partial, int nb, int C,
                                                        float* __restrict__ dgamma, float* __restrict__ dbeta, int acc) {
-  __shared__ float red[16][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63), wv = threadIdx.x >> 6;
-  float sm = 0.f;
-  if (col < 2 * C) {
-    const int which = col / C, c = col - which * C;
-    for (int b = wv; b < nb; b += 16) sm += partial[((size_t)b * 2 + which) * C + c];
-  }
-  red[wv][threadIdx.x & 63] = sm;
-  __syncthreads();
-  if (wv == 0 && col < 2 * C) {
-    float t = 0.f;
+  __shared__ float red[64][17];
+  const int cl = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  const bool ok = col < 2 * C;
+  const int which = ok ? col / C : 0, c = ok ? col - which * C : 0;
+  float sm[8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
-    const int which = col / C, c = col - which * C;
+  for (int u = 0; u < 8; ++u) sm[u] = 0.f;
+  if (ok) {
+    for (int b0 = r; b0 < nb; b0 += 64 * 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * 64;
+        if (b < nb) sm[u] += partial[((size_t)b * 2 + which) * C + c];
+      }
+    }
+  }
+  red[r][cl] = ((sm[0] + sm[1]) + (sm[2] + sm[3])) + ((sm[4] + sm[5]) + (sm[6] + sm[7]));
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (r < w) red[r][cl] += red[r + w][cl];
+    __syncthreads();
+  }
+  if (r == 0 && ok) {
     float* o = which ? dbeta : dgamma;
-    o[c] = (acc ? o[c] : 0.f) + t;
+    o[c] = (acc ? o[c] : 0.f) + red[0][cl];
   }
 }
 
@@ -974,7 +985,7 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
     const unsigned g8 = (unsigned)((M + 15) / 16 < LN_BWD_BLOCKS ? (M + 15) / 16 : LN_BWD_BLOCKS);
     hipLaunchKernelGGL(ln_bwd8_kernel<16>, dim3(g8), dim3(512), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
                        rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
-    hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 63) / 64), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
+    hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
                        dgamma, dbeta, accumulate);
     return sr_check(hipGetLastError(), "layernorm_bwd launch");
   }
