@@ -142,21 +142,32 @@ class GradBucketReducer:
     """Bucketed gradient all-reduce overlapped with backward (DDP semantics: average).
 
     Buckets are contiguous slices of ``flat.grad`` in reverse parameter order (the order
-    backward produces them), ``bucket_mb`` MiB each (DDP default 25).  A bucket's
+    backward produces them), ``bucket_mb`` MiB each (DDP default 25), except the bucket of
+    the first parameters: backward finishes those last, so their all-reduce cannot overlap
+    any compute, and it is capped at ``last_bucket_mb`` (1 MiB, DDP's first-bucket size)
+    so that only a short collective is exposed before the optimizer.  A bucket's
     ``all_reduce`` is issued (async) from the post-accumulate-grad hook of the last of its
     parameters to finish; ``wait()`` joins them before the optimizer.  The 1/world average is
     left to the optimizer (FusedAdam.grad_scale) so no extra pass over the gradients runs.
     """
 
-    def __init__(self, flat, group=None, bucket_mb=25.0):
+    def __init__(self, flat, group=None, bucket_mb=25.0, last_bucket_mb=1.0):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group)
         n = len(flat.params)
-        cap = int(bucket_mb * 1024 * 1024 / 4)
-        self.buckets = []  # (lo, hi, param indices)
-        cur, lo_idx = [], None
-        for i in reversed(range(n)):
+        cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
+        cap_last = max(1, min(cap, int(last_bucket_mb * 1024 * 1024 / 4)))
+        # the first parameters (reduced last) fill a small bucket; the rest, walked in backward
+        # order, fill bucket_mb buckets
+        head = []
+        for i in range(n):
+            if head and flat.offsets[i + 1] - flat.offsets[0] > cap_last:
+                break
+            head.append(i)
+        self.buckets = []  # (lo, hi, param indices), in issue order
+        cur = []
+        for i in reversed(range(len(head), n)):
             cur.append(i)
             lo, hi = flat.offsets[min(cur)], flat.offsets[max(cur) + 1]
             if hi - lo >= cap:
@@ -164,6 +175,7 @@ class GradBucketReducer:
                 cur = []
         if cur:
             self.buckets.append((flat.offsets[min(cur)], flat.offsets[max(cur) + 1], list(cur)))
+        self.buckets.append((flat.offsets[head[0]], flat.offsets[head[-1] + 1], list(reversed(head))))
         self.bucket_of = {}
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:

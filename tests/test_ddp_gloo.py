@@ -44,6 +44,11 @@ def _worker(rank, world, port, bucket_mb, q):
         red.wait()
         grads = (flat.grad / world).clone()
     if rank == 0:
+        # buckets tile the flat gradient; the one issued last holds the first parameters
+        spans = sorted((lo, hi) for lo, hi, _ in red.buckets)
+        assert spans[0][0] == 0 and spans[-1][1] == flat.offsets[-1]
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert 0 in red.buckets[-1][2] and red.buckets[-1][0] == 0
         q.put((grads, len(red.buckets)))
     dist.barrier()
     dist.destroy_process_group()
