@@ -29,7 +29,7 @@ class ConvDesc(ctypes.Structure):
                 ('out_ps', _i), ('out_nchw', _i), ('act', _i), ('slope', _f), ('alpha', _f), ('ldg', _i),
                 ('gcoff', _i), ('gate_slope', _f), ('ldr', _i), ('rcoff', _i), ('beta', _f), ('ldr2', _i),
                 ('r2coff', _i), ('beta2', _f), ('rcols', _i), ('in_up', _i), ('ksize', _i), ('gate_mode', _i),
-                ('gcol0', _i), ('gcol1', _i)]
+                ('gcol0', _i), ('gcol1', _i), ('row_scale', _vp)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -71,6 +71,7 @@ SIGNATURES = {
     'sr_l1_loss': (_i, [_vp, _vp, _i64, _f, _i, _vp, _vp, _vp, _sz, _vp]),
     'sr_l1_loss_workspace': (_sz, [_i64]),
     'sr_act_backward': (_i, [_i, _vp, _vp, _i64, _i, _f, _f, _vp, _vp]),
+    'sr_row_scale': (_i, [_i, _vp, _i64, _i, _i, _vp, _vp, _vp]),
     'sr_adam_ema': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _f, _f, _f, _f, _f, _f, _f, _f, _vp]),
     'sr_adam_ema_dev': (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _f, _f, _f, _f, _vp]),
     'sr_bilinear_up_add': (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),

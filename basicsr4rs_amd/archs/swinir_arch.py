@@ -5,8 +5,10 @@ kwargs and initialisation (_init_weights: trunc_normal(0.02) Linear, LN 1/0) fol
 reference so checkpoints load strictly.  Execution: token maps are NHWC feature maps
 (channels padded to a multiple of 8, e.g. 180 -> 184); every SwinTransformerBlock is one fused
 op (ops/swin.py), RSTB convs fuse the group skip, head/tail fuse the mean shift.
-DropPath (stochastic depth) is not applied by the fused blocks: parity is defined in eval
-mode / drop_path_rate 0.
+Stochastic depth (drop_path, swinir_arch.py:14-40, :320-321, linear dpr schedule :796) is
+applied in training: one device draw per forward gives every block its two per-sample
+factors floor(keep + U) / keep, which the fused block applies in its proj / fc2 residual
+epilogues (and to the branch gradients in backward).
 """
 import math
 
@@ -21,12 +23,41 @@ from ..utils.registry import ARCH_REGISTRY
 from .arch_util import Upsample, to_2tuple, trunc_normal_
 
 
+def drop_path_factors(drop_prob, rand):
+    """floor(keep + U) / keep (swinir_arch.py:21-25, the factor x.div(keep) * floor(keep + U)
+    applies to a branch); ``rand`` holds the U[0,1) draws."""
+    keep = 1.0 - drop_prob
+    return torch.floor(rand + keep) / keep
+
+
+class _RowScale(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, x, s):
+        ctx.save_for_backward(s)
+        ctx.shape = x.shape
+        x2 = x.contiguous().view(x.shape[0], -1)
+        return S.row_scale(x2, s, 1).view(ctx.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, = ctx.saved_tensors
+        return S.row_scale(dy.contiguous().view(ctx.shape[0], -1), s, 1).view(ctx.shape), None
+
+
 class DropPath(nn.Module):
-    """Stochastic depth module kept for the module tree (swinir_arch.py:30-40)."""
+    """Stochastic depth per sample (swinir_arch.py:29-40).  Inside SwinIR the fused blocks apply
+    it themselves; this module serves standalone use (HIP row-scale kernel on the device)."""
 
     def __init__(self, drop_prob=None):
         super().__init__()
         self.drop_prob = drop_prob
+
+    def forward(self, x):
+        if not self.drop_prob or not self.training:
+            return x
+        r = torch.rand(x.shape[0], device=x.device, dtype=torch.float32)
+        return _RowScale.apply(x, drop_path_factors(self.drop_prob, r))
 
 
 class Mlp(nn.Module):
@@ -115,8 +146,11 @@ class SwinTransformerBlock(nn.Module):
         self._fc1 = S.plain_spec(dim, mlp_hidden_dim)
         self._fc2 = S.plain_spec(mlp_hidden_dim, dim)
 
+    def drop_prob(self):
+        return self.drop_path.drop_prob if isinstance(self.drop_path, DropPath) else 0.0
+
     def forward(self, x):
-        return S.swin_block(x, self, self._geom, self._fc1, self._fc2)
+        return S.swin_block(x, self, self._geom, self._fc1, self._fc2, dp=getattr(self, '_dp', None))
 
 
 class BasicLayer(nn.Module):
@@ -302,12 +336,40 @@ class SwinIR(nn.Module):
             nn.init.constant_(m.bias, 0)
             nn.init.constant_(m.weight, 1.0)
 
+    def _blocks(self):
+        return [blk for layer in self.layers for blk in layer.residual_group.blocks]
+
+    def drop_path_draws(self, n_blocks, batch, device):
+        """U[0,1) draws of one training forward: [blocks, 2 (attention / MLP branch), batch]."""
+        return torch.rand(n_blocks, 2, batch, device=device, dtype=torch.float32)
+
+    def _set_drop_path(self, batch, device):
+        """Give every block with a non-zero rate its (s1, s2) factors for this forward."""
+        blocks = self._blocks()
+        probs = [blk.drop_prob() for blk in blocks]
+        if not (self.training and any(p > 0 for p in probs)):
+            for blk in blocks:
+                blk._dp = None
+            return
+        rand = self.drop_path_draws(len(blocks), batch, device)
+        cached = getattr(self, '_dp_keep', None)
+        if cached is None or cached[0] != (device, tuple(probs)):  # device constant (no H2D copy under capture)
+            keep = torch.tensor([1.0 - p for p in probs], dtype=torch.float32).view(-1, 1, 1).to(device)
+            self._dp_keep = cached = ((device, tuple(probs)), keep)
+        keep = cached[1]
+        fac = torch.floor(rand + keep) / keep
+        for i, (blk, p) in enumerate(zip(blocks, probs)):
+            blk._dp = (fac[i, 0], fac[i, 1]) if p > 0 else None
+
     def forward_features(self, x):
         if self.ape:
             raise NotImplementedError('absolute position embedding (ape=True) is not on the HIP path yet')
+        self._set_drop_path(x.shape[0], x.device)
         x = self.patch_embed(x)
         for layer in self.layers:
             x = layer(x)
+        for blk in self._blocks():
+            blk._dp = None
         return S.token_layernorm(x, self.norm)
 
     def forward(self, x):

@@ -58,7 +58,14 @@ struct FwdArgs {
   int tiles_n, tiles;
   FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
   FastDiv fd_r;                        // divide by in_ps (1 when none)
+  const float* row_scale;  // optional per-image factor on alpha (SwinIR stochastic depth)
+  FastDiv fd_hw;           // divide by H*W (pixel -> image)
 };
+
+// alpha of output row m: a.alpha, times the per-image row_scale when given
+SR_DEV float row_alpha(const FwdArgs& a, int m) {
+  return a.row_scale ? a.alpha * a.row_scale[fdiv((uint32_t)m, a.fd_hw)] : a.alpha;
+}
 
 template <typename T>
 SR_DEV void mfma_chunk(const u32x4& a, const u32x4& b, f32x4& acc);
@@ -95,7 +102,7 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
       const int m = m0 + row, n = n0 + col;
       if (m >= a.M || n >= a.Cout_real) continue;
       float v = Cs[row * CSTR + col] + (a.bias ? a.bias[n] : 0.f);
-      v = act_apply(v, a.act, a.slope) * a.alpha;
+      v = act_apply(v, a.act, a.slope) * row_alpha(a, m);
       v = v * (a.aff_scale ? a.aff_scale[n] : 1.f) + (a.aff_shift ? a.aff_shift[n] : 0.f);
       const int img = m / HW, pix = m - img * HW;
       y[((size_t)img * a.Cout_real + n) * HW + pix] = v;
@@ -193,8 +200,11 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
         for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
       }
     }
+    {
+      const float al = row_alpha(a, m);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+      for (int j = 0; j < 8; ++j) v[j] *= al;
+    }
     if (a.res && n < a.rcols) {
       float rv[8];
       unpack(rv1[it], rv);
@@ -1196,8 +1206,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
           }
         }
       }
+      const float al = row_alpha(a, m);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+      for (int j = 0; j < 8; ++j) v[j] *= al;
       if (a.res) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1405,8 +1416,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= a.gate_mode == 1 ? gelu_grad(gf[j]) : (gf[j] > 0.f ? 1.f : a.gate_slope);
       }
+      const float al = row_alpha(a, m);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] *= a.alpha;
+      for (int j = 0; j < 8; ++j) v[j] *= al;
       if (a.res && rok) {
         float rf[8];
         unpack8(rv, rf);
@@ -2807,6 +2819,8 @@ FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
   if (d->out_ps > 0) cps = d->Cout / (d->out_ps * d->out_ps);
   a.fd_cps = make_fastdiv(cps > 0 ? cps : 1);
   a.fd_r = make_fastdiv(d->in_ps > 0 ? d->in_ps : 1);
+  a.row_scale = d->row_scale;
+  a.fd_hw = make_fastdiv(d->H * d->W > 0 ? d->H * d->W : 1);
   return a;
 }
 

@@ -256,6 +256,27 @@ __global__ void act_backward_kernel(const T* __restrict__ dy, const T* __restric
   }
 }
 
+// out[m][c] = x[m][c] * scale[m / HW] on a dense [M][C] map (C a multiple of the 16-B chunk):
+// the per-sample factor of SwinIR stochastic depth applied to a residual-branch gradient.
+template <typename T>
+__global__ void row_scale_kernel(const T* __restrict__ x, const float* __restrict__ scale, uint32_t nv,
+                                 FastDiv fd_vpr, FastDiv fd_hw, T* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
+    const float f = scale[fdiv(fdiv(i, fd_vpr), fd_hw)];
+    const u32x4 d = ((const u32x4*)x)[i];
+    u32x4 o;
+    if constexpr (Elt<T>::PER16 == 8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = pack_bf16x2(f * bf16_to_f32(d[k] & 0xffff), f * bf16_to_f32(d[k] >> 16));
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(f * __uint_as_float(d[k]));
+    }
+    ((u32x4*)out)[i] = o;
+  }
+}
+
 inline unsigned grid_for(int64_t n, int64_t cap = 4096) {
   int64_t g = (n + 255) / 256;
   if (g > cap) g = cap;
@@ -387,6 +408,25 @@ int sr_act_backward(int dtype, const void* dy, const void* y, int64_t n, int act
     hipLaunchKernelGGL(act_backward_kernel<float>, dim3(grid_for(n / 4 + 1, 8192)), dim3(256), 0, s,
                        (const float*)dy, (const float*)y, n, neg, alpha, (float*)out);
   return sr_check(hipGetLastError(), "act_backward launch");
+}
+
+int sr_row_scale(int dtype, const void* x, int64_t M, int C, int HW, const float* scale, void* out, void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!x || !scale || !out || M < 0 || C <= 0 || HW <= 0 || C % PER || M % HW)
+    return sr_fail(SR_EINVAL, "row_scale: bad arguments (C must be a multiple of the 16-B chunk, M of HW)");
+  if (((uintptr_t)x | (uintptr_t)out) & 15) return sr_fail(SR_EINVAL, "row_scale: tensors must be 16-byte aligned");
+  const int64_t nv = M * C / PER;
+  if (nv >= 0x80000000ll) return sr_fail(SR_ETOOBIG, "row_scale: tensor too large");
+  if (nv == 0) return SR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const FastDiv fv = make_fastdiv((uint32_t)(C / PER)), fh = make_fastdiv((uint32_t)HW);
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(row_scale_kernel<bf16_t>, dim3(grid_for(nv, 8192)), dim3(256), 0, s, (const bf16_t*)x, scale,
+                       (uint32_t)nv, fv, fh, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(row_scale_kernel<float>, dim3(grid_for(nv, 8192)), dim3(256), 0, s, (const float*)x, scale,
+                       (uint32_t)nv, fv, fh, (float*)out);
+  return sr_check(hipGetLastError(), "row_scale launch");
 }
 
 }  // extern "C"

@@ -2,9 +2,9 @@
 from copy import deepcopy
 
 from ..utils.registry import METRIC_REGISTRY
-from .psnr_ssim import calculate_psnr, calculate_psnr_pt
+from .psnr_ssim import calculate_psnr, calculate_psnr_pt, calculate_ssim, calculate_ssim_pt
 
-__all__ = ['calculate_psnr', 'calculate_psnr_pt', 'calculate_metric']
+__all__ = ['calculate_psnr', 'calculate_psnr_pt', 'calculate_ssim', 'calculate_ssim_pt', 'calculate_metric']
 
 
 def calculate_metric(data, opt):

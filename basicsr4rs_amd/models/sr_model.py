@@ -80,11 +80,9 @@ class SRModel(BaseModel):
         self.optimizers.append(self.optimizer_g)
 
     def feed_data(self, data):
-        if self._graph is not None:  # captured step: refill its static input buffers
-            self.lq.copy_(data['lq'], non_blocking=True)
-            if 'gt' in data:
-                self.gt.copy_(data['gt'], non_blocking=True)
-            return
+        # plain assignment also when a step is captured: the graph's static inputs live under
+        # private names (_g_lq / _g_gt) and are refilled by optimize_parameters, so validation
+        # batches of any shape never touch them
         self.lq = data['lq'].to(self.device, non_blocking=True)
         if 'gt' in data:
             self.gt = data['gt'].to(self.device, non_blocking=True)
@@ -109,16 +107,25 @@ class SRModel(BaseModel):
         self.output = self.output.detach()
         return loss_dict
 
+    def _graph_inputs_match(self):
+        return (self.lq.shape == self._g_lq.shape and self.lq.dtype == self._g_lq.dtype
+                and self.gt.shape == self._g_gt.shape and self.gt.dtype == self._g_gt.dtype)
+
     def optimize_parameters(self, current_iter):
-        if self._graph is not None:
+        if self._graph is not None and self._graph_inputs_match():
+            if self.lq is not self._g_lq:
+                self._g_lq.copy_(self.lq, non_blocking=True)
+            if self.gt is not self._g_gt:
+                self._g_gt.copy_(self.gt, non_blocking=True)
             self.optimizer_g.host_step()
             self._graph.replay()
             # the replay updated the parameters: host-side weight-image caches are now stale
             # (an eager forward, e.g. validation, rebuilds them in place)
             bump_param_epoch()
+            self.output = self._g_out
             self.log_dict = self.reduce_loss_dict(self._graph_losses)
             return
-        if self.use_graph and self._eager_steps >= 2:
+        if self.use_graph and self._graph is None and self._eager_steps >= 2:
             self._capture_step()
             return
         loss_dict = self._step_body()
@@ -143,10 +150,13 @@ class SRModel(BaseModel):
         g = torch.cuda.CUDAGraph()
         ema = self.flat_ema if self.ema_decay > 0 else None
         self.optimizer_g.host_step()
+        # the captured step reads these two tensors at replay: keep them under private names
+        self._g_lq, self._g_gt = self.lq, self.gt
         with torch.cuda.graph(g):
             losses = self._step_body()
             self.optimizer_g.device_step(ema=ema, ema_decay=self.ema_decay)
         self._graph = g
+        self._g_out = self.output
         self._graph_losses = losses
         g.replay()
         self.log_dict = self.reduce_loss_dict(losses)

@@ -65,6 +65,15 @@ class _Prep:
 
 _PREP_ALL = {}  # (id(weight), static key) -> _Prep
 _PREP_TABLE = {}  # dtype -> (entries, device item table, device block starts, total blocks)
+# tables replaced since: a captured HIP graph may still launch the batched refresh on one of
+# them, so their device buffers are kept alive instead of returning to the allocator
+_PREP_TABLE_RETIRED = []
+
+
+def _retire_table(dtype):
+    tab = _PREP_TABLE.pop(dtype, None)
+    if tab is not None:
+        _PREP_TABLE_RETIRED.append(tab)
 
 
 def prepared_images(weight, bias, dtype, shape, maps=(None, None), tag=''):
@@ -92,7 +101,7 @@ def prepared_images(weight, bias, dtype, shape, maps=(None, None), tag=''):
                  torch.empty(cout_p, device=dev, dtype=torch.float32))
         ents[skey] = e
         _PREP_ALL[(id(weight), skey)] = e
-        _PREP_TABLE.pop(dtype, None)
+        _retire_table(dtype)
     wf, wd, bg = e.val
     lib = _lib.load()
     _lib.check(
@@ -139,6 +148,7 @@ def refresh_prepared():
             raw = torch.frombuffer(bytearray(bytes(items)), dtype=torch.uint8).to(dev)
             st = torch.tensor(starts, dtype=torch.int32).to(dev)
             tab = (list(ents), raw, st, starts[-1])
+            _retire_table(dt)
             _PREP_TABLE[dt] = tab
         _, raw, st, total = tab
         _lib.check(lib.sr_conv_prep_batch(_lib.dtype_code(dt), _lib.ptr(raw), _lib.ptr(st), len(ents), total,
@@ -163,6 +173,10 @@ def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
     d.ksize, d.gate_mode = kw.get('ksize', 3), kw.get('gate_mode', 0)
     d.gcol0, d.gcol1 = kw.get('gcol0', 0), kw.get('gcol1', 0)
     d.ldw = (9 if d.ksize == 3 else 1) * cin
+    rs = kw.get('row_scale')
+    if rs is not None:
+        assert rs.dtype == torch.float32 and rs.is_cuda and rs.numel() == N, 'row_scale: fp32 [N] on the device'
+        d.row_scale = rs.data_ptr()
     return d
 
 
@@ -201,29 +215,38 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     return (y, parts) if colsum else y
 
 
-_GRAD_READY = {}  # id(param) -> callbacks run when a kernel has written the param's gradient
-
-
 def on_grad_ready(p, fn):
     """Register fn(p), called after a HIP kernel accumulated p's gradient in place (the
-    direct-gradient path of conv_wgrad_raw, which bypasses autograd's AccumulateGrad)."""
-    _GRAD_READY.setdefault(id(p), []).append(fn)
+    direct-gradient path of conv_wgrad_raw and the LN / attention / CA backwards, which bypass
+    autograd's AccumulateGrad).  Kept on the parameter object itself."""
+    cbs = p.__dict__.get('_sr_grad_ready')
+    if cbs is None:
+        cbs = p._sr_grad_ready = []
+    cbs.append(fn)
 
 
 def grad_ready(p):
-    for fn in _GRAD_READY.get(id(p), ()):
+    for fn in p.__dict__.get('_sr_grad_ready', ()):
         fn(p)
 
 
 def grad_target(p):
-    """p.grad when it is a view into a FlatParams gradient buffer (the kernels accumulate the
-    gradient straight into it), else None."""
+    """The FlatParams gradient view of p (the kernels accumulate the gradient straight into it),
+    else None.  If something replaced p.grad since FlatParams bound it (``zero_grad`` with
+    set_to_none, an autograd-created tensor), the view is re-bound first, carrying over the
+    current gradient value (None = zero), so the optimizer's flat buffer stays authoritative."""
     if p is None or not getattr(p, '_sr_flat', False):
         return None
+    view = p._sr_grad_view
     g = p.grad
-    if g is None or g.dtype != torch.float32 or not g.is_contiguous():
-        return None
-    return g
+    if g is None or g.data_ptr() != view.data_ptr():
+        with torch.no_grad():
+            if g is None:
+                view.zero_()
+            else:
+                view.copy_(g)
+        p.grad = view
+    return view
 
 
 def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, out_ps=0, need_bias=True, params=None,

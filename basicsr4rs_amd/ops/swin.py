@@ -12,8 +12,13 @@ is exactly our NHWC feature map, so PatchEmbed / PatchUnEmbed are free.  A SwinT
 
 with a hand-written backward (GELU' fused into fc2's dgrad epilogue, LN residual fused).
 Linears are 1x1 convs: nn.Linear.weight [out][in] is the 1x1 conv weight; the padded head
-layout is produced by index maps in the HIP weight-prep kernel.  DropPath is the identity at
-drop_path_rate 0 / eval (parity mode); SURVEY.md §0.7.
+layout is produced by index maps in the HIP weight-prep kernel.
+
+Stochastic depth (DropPath, swinir_arch.py:14-40 applied at :320-321): in training the two
+residual branches are scaled per sample, x2 = x + s1[n]*proj(a), out = x2 + s2[n]*fc2(h), with
+s = floor(keep + U[0,1)) / keep drawn per forward (archs/swinir_arch.py).  The factor rides in
+the proj / fc2 GEMM epilogues (sr_conv3x3_desc.row_scale); the backward scales the branch
+gradients once (sr_row_scale) and feeds them to both the dgrad and the wgrad.
 """
 import torch
 
@@ -88,6 +93,17 @@ def linear_dgrad(dy, wd, spec, N, H, W, **kw):
     dx = torch.empty(N, H, W, spec.cin_p, device=dy.device, dtype=dy.dtype)
     C.conv_fwd_raw(dy, wd, None, dx, N, H, W, spec.cout_p, spec.cin_p, spec.cin_p, ksize=1, **kw)
     return dx
+
+
+def row_scale(x, scale, HW):
+    """out[m] = x[m] * scale[m // HW] over the rows of a dense NHWC map (HIP kernel)."""
+    out = torch.empty_like(x)
+    M = x.numel() // x.shape[-1]
+    lib = _lib.load()
+    with ktrace.span('row_scale_kernel', 0.0, 2.0 * x.numel() * x.element_size()):
+        _lib.check(lib.sr_row_scale(_lib.dtype_code(x.dtype), _lib.ptr(x), M, x.shape[-1], HW, _lib.ptr(scale),
+                                    _lib.ptr(out), _lib.stream()))
+    return out
 
 
 def linear_wgrad(dy, x, spec, N, H, W, need_bias=True, params=None):
@@ -222,7 +238,7 @@ def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table, table_param=N
 class _STB(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, x, geom, fc1s, fc2s, scale, n1w, n1b, qw, qb, table, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b):
+    def forward(ctx, x, geom, fc1s, fc2s, scale, dp, n1w, n1b, qw, qb, table, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b):
         dtype = x.dtype
         N, H, W, Cp = x.shape
         Cr = geom.dim
@@ -232,14 +248,15 @@ class _STB(torch.autograd.Function):
         tab = table.detach().float().contiguous()
         a, lse = window_attn(qkv, geom, N, H, W, scale, tab)
         pwf, _, pbg = prepared_linear(pw, pb, geom.proj, dtype)
-        x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0)
+        s1, s2 = dp if dp is not None else (None, None)  # per-sample DropPath factors (fp32 [N])
+        x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0, row_scale=s1)
         ln2, m2, r2 = layernorm(x2, n2w, n2b, Cr)
         f1wf, _, f1bg = prepared_linear(f1w, f1b, fc1s, dtype)
         z = torch.empty(N, H, W, fc1s.cout_p, device=x.device, dtype=dtype)
         h = linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)
         f2wf, _, f2bg = prepared_linear(f2w, f2b, fc2s, dtype)
-        out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0)
-        ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale = geom, fc1s, fc2s, scale
+        out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0, row_scale=s2)
+        ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale, ctx.dp = geom, fc1s, fc2s, scale, dp
         ctx.save_for_backward(x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w,
                               f1b, f2w, f2b, n1b, n2b, table)
         return out
@@ -253,26 +270,30 @@ class _STB(torch.autograd.Function):
         N, H, W, Cp = x.shape
         Cr = g.dim
         dout = dout.to(dtype).contiguous()
+        s1, s2 = ctx.dp if ctx.dp is not None else (None, None)
+        g2 = row_scale(dout, s2, H * W) if s2 is not None else dout  # fc2-branch gradient
         _, f2wd, _ = prepared_linear(f2w, f2b, fc2s, dtype)
-        dz = linear_dgrad(dout, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)
-        df2w, df2b = linear_wgrad(dout, h, fc2s, N, H, W, params=(f2w, f2b))
+        dz = linear_dgrad(g2, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)
+        df2w, df2b = linear_wgrad(g2, h, fc2s, N, H, W, params=(f2w, f2b))
         _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
         dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
         df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W, params=(f1w, f1b))
         dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b))
+        g1 = row_scale(dx2, s1, H * W) if s1 is not None else dx2  # proj-branch gradient
         _, pwd, _ = prepared_linear(pw, pb, g.proj, dtype)
-        da = linear_dgrad(dx2, pwd, g.proj, N, H, W)
-        dpw, dpb = linear_wgrad(dx2, a, g.proj, N, H, W, params=(pw, pb))
+        da = linear_dgrad(g1, pwd, g.proj, N, H, W)
+        dpw, dpb = linear_wgrad(g1, a, g.proj, N, H, W, params=(pw, pb))
         dqkv, dtab = window_attn_bwd(qkv, a, da, lse, g, N, H, W, scale, tab, table_param=table)
         _, qwd, _ = prepared_linear(qw, qb, g.qkv, dtype)
         dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
         dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W, params=(qw, qb))
         dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2, params=(n1w, n1b))
-        return (dx, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b)
+        return (dx, None, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b)
 
 
-def swin_block(x, blk, geom, fc1s, fc2s):
+def swin_block(x, blk, geom, fc1s, fc2s, dp=None):
+    """dp: None, or the (s1, s2) per-sample DropPath factors of this forward."""
     at = blk.attn
-    return _STB.apply(x, geom, fc1s, fc2s, float(at.scale), blk.norm1.weight, blk.norm1.bias, at.qkv.weight,
+    return _STB.apply(x, geom, fc1s, fc2s, float(at.scale), dp, blk.norm1.weight, blk.norm1.bias, at.qkv.weight,
                       at.qkv.bias, at.relative_position_bias_table, at.proj.weight, at.proj.bias, blk.norm2.weight,
                       blk.norm2.bias, blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias)

@@ -43,6 +43,7 @@ class FlatParams:
                 p.data = self.flat[o:o + n].view_as(p)
                 if with_grad:
                     p.grad = self.grad[o:o + n].view_as(p)
+                    p._sr_grad_view = p.grad
                     p._sr_flat = True  # HIP wgrad kernels accumulate straight into this .grad view
 
     def view(self, buf, i):
@@ -52,7 +53,7 @@ class FlatParams:
         self.grad.zero_()
         for i, p in enumerate(self.params):  # autograd may have replaced a view; restore it
             if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[i]:
-                p.grad = self.view(self.grad, i)
+                p.grad = p._sr_grad_view
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -145,9 +146,17 @@ class GradBucketReducer:
     backward produces them), ``bucket_mb`` MiB each (DDP default 25), except the bucket of
     the first parameters: backward finishes those last, so their all-reduce cannot overlap
     any compute, and it is capped at ``last_bucket_mb`` (1 MiB, DDP's first-bucket size)
-    so that only a short collective is exposed before the optimizer.  A bucket's
-    ``all_reduce`` is issued (async) from the post-accumulate-grad hook of the last of its
-    parameters to finish; ``wait()`` joins them before the optimizer.  The 1/world average is
+    so that only a short collective is exposed before the optimizer.
+
+    A parameter is "ready" when the HIP kernel that accumulates its gradient straight into
+    the flat buffer has been queued (``ops.conv.grad_ready``: conv / linear wgrads, LayerNorm,
+    attention-table and channel-attention backwards) or, for gradients that still go through
+    autograd, when its post-accumulate-grad hook runs -- whichever comes first, once per step.
+    When the last parameter of a bucket is ready the bucket's ``all_reduce`` is issued (async,
+    RCCL stream ordered after the producing kernels) while backward continues; ``wait()`` joins
+    them before the optimizer.  ``issue_log`` records, per step, which buckets were issued
+    during backward ('backward') and which only at the join ('wait'); ``last_issue_log`` keeps
+    the log of the step joined last.  The 1/world average is
     left to the optimizer (FusedAdam.grad_scale) so no extra pass over the gradients runs.
     """
 
@@ -180,37 +189,46 @@ class GradBucketReducer:
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
-        self.pending = [0] * len(self.buckets)
-        self.handles = []
         self.hooks = []
         for i, p in enumerate(flat.params):
-            self.hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            fn = self._make_hook(i)
+            self.hooks.append(p.register_post_accumulate_grad_hook(fn))
+            on_grad_ready(p, fn)
+        self.issue_log, self.last_issue_log = [], []
         self.reset()
 
     def reset(self):
         self.pending = [len(idx) for (_, _, idx) in self.buckets]
+        self.ready = [False] * len(self.flat.params)
         self.handles = []
+
+    def _issue(self, b, when):
+        lo, hi, _ = self.buckets[b]
+        self.handles.append(dist.all_reduce(self.flat.grad[lo:hi], group=self.group, async_op=True))
+        self.issue_log.append((b, when))
 
     def _make_hook(self, i):
 
         def hook(_p):
+            if self.ready[i]:
+                return
+            self.ready[i] = True
             b = self.bucket_of[i]
             self.pending[b] -= 1
             if self.pending[b] == 0:
-                lo, hi, _ = self.buckets[b]
-                self.handles.append(dist.all_reduce(self.flat.grad[lo:hi], group=self.group, async_op=True))
+                self._issue(b, 'backward')
 
         return hook
 
     def wait(self):
-        """Join outstanding bucket reductions; reduce any bucket whose hooks did not fire
-        (parameters unused in this step) so every rank issues the same collectives."""
+        """Join outstanding bucket reductions; reduce any bucket whose parameters did not all
+        report ready (unused in this step) so every rank issues the same collectives."""
         for b, n in enumerate(self.pending):
             if n > 0:
-                lo, hi, _ = self.buckets[b]
-                self.handles.append(dist.all_reduce(self.flat.grad[lo:hi], group=self.group, async_op=True))
+                self._issue(b, 'wait')
         for h in self.handles:
             h.wait()
+        self.last_issue_log, self.issue_log = self.issue_log, []
         self.reset()
 
     def broadcast_params(self, src=0):

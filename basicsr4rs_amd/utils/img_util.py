@@ -3,6 +3,7 @@
 OpenCV is not available in this image: RGB->BGR is a channel flip and ``imwrite`` writes
 PNG with the standard library (zlib) so validation images can still be saved.
 """
+import math
 import os
 import struct
 import zlib
@@ -11,8 +12,31 @@ import numpy as np
 import torch
 
 
+def make_grid(t, nrow=8, padding=2, pad_value=0.0):
+    """torchvision.utils.make_grid(normalize=False) for a [B, C, H, W] batch (the 4-D branch of
+    tensor2img, img_util.py:72-76): tiles on a pad_value canvas, 1-channel maps repeated to 3."""
+    if t.size(0) == 1:
+        return t.squeeze(0)
+    if t.size(1) == 1:
+        t = torch.cat((t, t, t), 1)
+    nmaps = t.size(0)
+    xmaps = min(nrow, nmaps)
+    ymaps = int(math.ceil(float(nmaps) / xmaps))
+    height, width = int(t.size(2) + padding), int(t.size(3) + padding)
+    grid = t.new_full((t.size(1), height * ymaps + padding, width * xmaps + padding), pad_value)
+    k = 0
+    for y in range(ymaps):
+        for x in range(xmaps):
+            if k >= nmaps:
+                break
+            grid[:, y * height + padding:(y + 1) * height, x * width + padding:(x + 1) * width] = t[k]
+            k += 1
+    return grid
+
+
 def tensor2img(tensor, rgb2bgr=True, out_type=np.uint8, min_max=(0, 1)):
-    """Clamp to min_max, scale to [0,1], CHW->HWC, RGB->BGR, *255 and round for uint8."""
+    """Clamp to min_max, scale to [0,1], CHW->HWC, RGB->BGR, *255 and round for uint8
+    (basicsr/utils/img_util.py:40-96; a 4-D batch is tiled with make_grid first)."""
     if not (torch.is_tensor(tensor) or (isinstance(tensor, list) and all(torch.is_tensor(t) for t in tensor))):
         raise TypeError(f'tensor or list of tensors expected, got {type(tensor)}')
     if torch.is_tensor(tensor):
@@ -21,7 +45,11 @@ def tensor2img(tensor, rgb2bgr=True, out_type=np.uint8, min_max=(0, 1)):
     for t in tensor:
         t = t.squeeze(0).float().detach().cpu().clamp_(*min_max)
         t = (t - min_max[0]) / (min_max[1] - min_max[0])
-        if t.dim() == 3:
+        if t.dim() == 4:
+            img = make_grid(t, nrow=int(math.sqrt(t.size(0)))).numpy().transpose(1, 2, 0)
+            if rgb2bgr:
+                img = img[..., ::-1]
+        elif t.dim() == 3:
             img = t.numpy().transpose(1, 2, 0)
             if img.shape[2] == 1:
                 img = np.squeeze(img, axis=2)
@@ -30,7 +58,7 @@ def tensor2img(tensor, rgb2bgr=True, out_type=np.uint8, min_max=(0, 1)):
         elif t.dim() == 2:
             img = t.numpy()
         else:
-            raise TypeError(f'Only support 3D or 2D tensor. But received with dimension: {t.dim()}')
+            raise TypeError(f'Only support 4D, 3D or 2D tensor. But received with dimension: {t.dim()}')
         if out_type == np.uint8:
             img = (img * 255.0).round()
         result.append(np.ascontiguousarray(img).astype(out_type))

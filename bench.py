@@ -9,12 +9,15 @@ are synthetic U[0,1) tiles already resident in HBM (seed 0 / 1, + rank).
 Run: python bench.py --gpus N --steps K --warmup W   (N>1 under torch.distributed.run).
 `--workload` selects another BASELINE.json config in the same HR-pixels/s unit (rcan = C3,
 swinir = C4, rrdb = C5); the default (edsr = C2) is the north-star line.
-Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events over
-the timed region) and the CPU baseline (oracle restatement on the host cores, bounded
-sample, rank 0 at N=1).
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on an
+untimed warm-up step; bound chosen from its arithmetic intensity against the 312 FLOP/B
+ridge), the CPU baseline (oracle restatement of the same workload's train step on the host
+cores, bounded sample, rank 0 at N=1) and the parity of the benchmarked net against the CPU
+oracle on one LR tile (fp32 max-abs, bf16 PSNR; rank 0 at N=1, outside the timed region).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -65,38 +68,92 @@ def make_opt(world, batch, workload='edsr'):
         path={})
 
 
-def cpu_baseline(seconds=20.0):
-    """Oracle EDSR_Lx4 train step (fwd + L1 + bwd + Adam) in torch-CPU fp32 at batch 1."""
+def _oracle_fn(net_cfg):
+    """CPU oracle forward (oracle/nets.py) of a workload's net: fn(state_dict, x) -> y."""
+    from oracle import nets as O
+    t = net_cfg['type']
+    if t == 'EDSR':
+        return lambda sd, x: O.edsr(sd, x, num_block=net_cfg['num_block'], upscale=net_cfg['upscale'],
+                                    res_scale=net_cfg['res_scale'], img_range=net_cfg['img_range'],
+                                    rgb_mean=net_cfg['rgb_mean'])
+    if t == 'RCAN':
+        return lambda sd, x: O.rcan(sd, x, num_group=net_cfg['num_group'], num_block=net_cfg['num_block'],
+                                    upscale=net_cfg['upscale'], res_scale=net_cfg['res_scale'],
+                                    img_range=net_cfg['img_range'], rgb_mean=net_cfg['rgb_mean'])
+    if t == 'RRDBNet':
+        return lambda sd, x: O.rrdbnet(sd, x, scale=net_cfg['scale'], num_block=net_cfg['num_block'])
+    if t == 'SwinIR':
+        return lambda sd, x: O.swinir(sd, x, net_cfg)
+    raise ValueError(t)
+
+
+def cpu_baseline(workload, seconds=20.0):
+    """The oracle train step of ``workload`` (fwd + L1 + bwd + torch Adam) in torch-CPU fp32 at
+    batch 1 on the host's cores: ONE image of the benchmarked tile, timed as the median of as
+    many steps as fit in ~``seconds`` (at least 1 after a warm-up).  SwinIR runs eval-mode
+    attention (no stochastic depth: its draws only change which samples a branch skips)."""
     from basicsr4rs_amd.archs import build_network
     from oracle import nets as O
+    net_cfg, _, lr, _, lr_px = WORKLOADS[workload][:5]
     torch.manual_seed(42)
-    net = build_network(dict(EDSR_L))
-    params = {k: v.detach().clone().requires_grad_(True) for k, v in net.state_dict().items()}
-    opt = torch.optim.Adam(list(params.values()), lr=1e-4, betas=(0.9, 0.99))
+    net = build_network(dict(net_cfg))
+    params = {k: v.detach().clone().requires_grad_(v.is_floating_point()) for k, v in net.state_dict().items()}
+    opt = torch.optim.Adam([v for v in params.values() if v.requires_grad], lr=lr, betas=(0.9, 0.99))
     g0, g1 = torch.Generator().manual_seed(0), torch.Generator().manual_seed(1)
-    lq = torch.rand(1, 3, 64, 64, generator=g0)
-    gt = torch.rand(1, 3, 256, 256, generator=g1)
+    lq = torch.rand(1, 3, lr_px, lr_px, generator=g0)
+    gt = torch.rand(1, 3, 4 * lr_px, 4 * lr_px, generator=g1)
+    fwd = _oracle_fn(net_cfg)
 
     def step():
         opt.zero_grad()
-        out = O.edsr(params, lq, num_block=32, upscale=4, res_scale=0.1)
-        O.l1_loss(out, gt).backward()
+        O.l1_loss(fwd(params, lq), gt).backward()
         opt.step()
 
+    t = time.time()
     step()  # warm-up
+    warm = time.time() - t
     times = []
     t_all = time.time()
-    while len(times) < 3 or (time.time() - t_all < seconds and len(times) < 10):
+    while not times or (time.time() - t_all + warm < seconds and len(times) < 10):
         t = time.time()
         step()
         times.append(time.time() - t)
-        if time.time() - t_all > seconds and len(times) >= 1:
-            break
     times.sort()
     t_med = times[len(times) // 2]
-    return {'value': 256 * 256 / t_med, 'unit': 'HR-pixels/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-            'sample': f'oracle EDSR_Lx4 fp32 train step, batch 1 (64x64 LR -> 256x256 HR), median of {len(times)} '
-                      f'steps after 1 warm-up, torch CPU threads={torch.get_num_threads()}'}
+    return {'value': (4 * lr_px)**2 / t_med, 'unit': 'HR-pixels/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'sample': f'oracle {net_cfg["type"]} fp32 train step (fwd + L1 + bwd + Adam), batch 1 '
+                      f'({lr_px}x{lr_px} LR -> {4 * lr_px}x{4 * lr_px} HR), median of {len(times)} steps after '
+                      f'1 warm-up, torch CPU threads={torch.get_num_threads()}'}
+
+
+def parity_check(workload, dev):
+    """Parity of the benchmarked net against the CPU oracle on ONE LR tile of the bench size
+    (outside the timed region; same random-init weights and input): fp32 max |GPU - CPU| (the
+    north_star bar is 1e-3) and the PSNR of the bf16 (autocast) GPU output against the fp32 CPU
+    output, with the [0,1] image range as peak."""
+    import copy
+
+    from basicsr4rs_amd.archs import build_network
+    net_cfg, lr_px = WORKLOADS[workload][0], WORKLOADS[workload][4]
+    torch.manual_seed(7)
+    net = build_network(dict(net_cfg)).eval()
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    x = torch.rand(1, 3, lr_px, lr_px, generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        ref = _oracle_fn(net_cfg)(sd, x)
+        g = copy.deepcopy(net).to(dev)
+        out32 = g(x.to(dev)).float().cpu()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out16 = g(x.to(dev)).float().cpu()
+
+    def psnr(a):
+        mse = ((a - ref)**2).mean().item()
+        return round(10 * math.log10(1.0 / mse), 2) if mse > 0 else float('inf')
+
+    return {'max_abs_fp32': float((out32 - ref).abs().max()), 'psnr_fp32_db': psnr(out32),
+            'max_abs_bf16': float((out16 - ref).abs().max()), 'psnr_bf16_db': psnr(out16),
+            'tile': f'1x3x{lr_px}x{lr_px} LR, eval mode, oracle = oracle/nets.py CPU fp32',
+            'bar': 'fp32 max-abs <= 1e-3 (north_star)'}
 
 
 def _pmc_traffic(workload, kernel):
@@ -120,6 +177,7 @@ def main():
     ap.add_argument('--workload', default='edsr', choices=sorted(WORKLOADS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-trace', action='store_true')
+    ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--graph', type=int, default=-1,
                     help='capture the train step in a HIP graph (1/0; default: on for a single process)')
     args = ap.parse_args()
@@ -206,18 +264,24 @@ def main():
     value = hr_px / dt
     roof = None
     if kstats:
+        # dominant kernel; its roof from its algorithmic arithmetic intensity against the ridge
+        # (frac = achieved / min(P, AI * BW))
         name, st = max(kstats.items(), key=lambda kv: kv[1]['ms'])
         avg_ms = st['ms'] / st['count']
-        if st['flops'] > 0:
+        ai = st['flops'] / st['bytes'] if st['bytes'] > 0 else float('inf')
+        ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+        if st['flops'] > 0 and ai >= ridge:
             achieved = st['flops'] / (st['ms'] * 1e-3) / 1e12
             roof = {'bound': 'mfma', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS,
-                    'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None,
-                    'flops_per_launch': st['flops'] / st['count']}
+                    'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None}
         else:
             achieved = st['bytes'] / (st['ms'] * 1e-3) / 1e9
             roof = {'bound': 'hbm', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS,
-                    'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None,
-                    'bytes_per_launch': st['bytes'] / st['count']}
+                    'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None}
+            if st['flops'] > 0:
+                roof['mfma_tflops'] = round(st['flops'] / (st['ms'] * 1e-3) / 1e12, 1)
+        roof.update({'flops_per_launch': st['flops'] / st['count'], 'bytes_per_launch': st['bytes'] / st['count'],
+                     'arith_intensity': round(ai, 1), 'ridge': round(ridge, 1)})
         roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // traced_steps,
                      'share_of_step': round(st['ms'] / traced_steps * 1e-3 / (dt / args.steps), 3),
                      'timing': 'HIP events on the stream of each launch, ' +
@@ -235,19 +299,21 @@ def main():
                 'ms_per_step': round(v['ms'] / traced_steps, 3)}
             for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]['ms'])
         }
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == 'edsr':
-        cpu = cpu_baseline()
+    cpu = parity = None
+    if rank == 0 and world == 1 and not args.no_parity:
+        parity = parity_check(args.workload, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.workload)
     if rank == 0:
         line = {
-            'metric': 'HR-pixels/sec/node (x4 SR train step)', 'value': round(value, 1), 'unit': 'HR-pixels/s',
+            'metric': 'HR-pixels/sec/node (x4 SR train step) + PSNR parity vs CPU ref', 'value': round(value, 1), 'unit': 'HR-pixels/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
             'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
             'config': {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
                        'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph},
             'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
-            'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu,
+            'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu, 'parity': parity,
         }
         print(json.dumps(line))
     if world > 1:

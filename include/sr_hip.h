@@ -80,6 +80,9 @@ typedef struct sr_conv3x3_desc {
                   gcol0 <= n < gcol1 only (activation backward of a dense-block slice whose
                   gradient this call completes) */
   int gcol0, gcol1;
+  const float* row_scale; /* optional fp32 [N]: alpha of every output pixel of image n is multiplied by
+                             row_scale[n] (per-sample stochastic depth, swinir_arch.py:14-40, fused into
+                             the proj / fc2 residual epilogues); NULL = 1 */
 } sr_conv3x3_desc;
 
 /* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.
@@ -184,6 +187,9 @@ size_t sr_l1_loss_workspace(int64_t n);
  * SR_ACT_LRELU, 1 for SR_ACT_NONE; y is the activation OUTPUT (same sign as its input). */
 int sr_act_backward(int dtype, const void* dy, const void* y, int64_t n, int act, float slope, float alpha,
                     void* out, void* stream);
+/* out[m][c] = x[m][c] * scale[m / HW] on a dense [M][C] map (C a multiple of 8 bf16 / 4 f32):
+ * the per-sample DropPath factor (swinir_arch.py:14-40) on a residual-branch gradient. */
+int sr_row_scale(int dtype, const void* x, int64_t M, int C, int HW, const float* scale, void* out, void* stream);
 /* Fused Adam (torch.optim.Adam semantics, no amsgrad/weight decay) + EMA of a flat fp32
  * parameter vector: g is scaled by grad_scale (DDP 1/world_size averaging), p, exp_avg,
  * exp_avg_sq updated in place; if ema != NULL, ema = ema*decay + p*(1-decay) after the step

@@ -260,8 +260,19 @@ def window_attention_core(qkv, nH, ws, shift, scale, table):
     return t
 
 
-def swin_block(x, sd, p, hw, nH, ws, shift, res=None):
-    """SwinTransformerBlock.forward in eval mode (swinir_arch.py:283-323), DropPath = identity.
+def drop_path(x, drop_prob, rand):
+    """drop_path in training (swinir_arch.py:14-26) with the U[0,1) draws ``rand`` [B] given."""
+    if drop_prob == 0.:
+        return x
+    keep_prob = 1 - drop_prob
+    random_tensor = keep_prob + rand.view((x.shape[0], ) + (1, ) * (x.ndim - 1)).to(x.dtype)
+    random_tensor.floor_()
+    return x.div(keep_prob) * random_tensor
+
+
+def swin_block(x, sd, p, hw, nH, ws, shift, res=None, dp=None):
+    """SwinTransformerBlock.forward (swinir_arch.py:283-323); DropPath = identity (eval) unless
+    ``dp`` = (drop_prob, rand [2, B]) gives the training draws of its two branches (:320-321).
     ``res``: the block's constructor input_resolution (img_size / patch_size); the no-shift /
     shrunken-window rule (swinir_arch.py:234-237) is decided on it, not on the runtime size
     ``hw`` (which only sets the shapes and the shift mask, :315-318)."""
@@ -279,13 +290,19 @@ def swin_block(x, sd, p, hw, nH, ws, shift, res=None):
     t = window_reverse(aw.view(-1, ws, ws, c), ws, h, w)
     if shift > 0:
         t = torch.roll(t, shifts=(shift, shift), dims=(1, 2))
-    x = sc + t.reshape(b, h * w, c)
-    m = _linear(F.gelu(_linear(_ln(x, sd, f'{p}.norm2'), sd, f'{p}.mlp.fc1')), sd, f'{p}.mlp.fc2')
-    return x + m
+    t = t.reshape(b, h * w, c)
+    m_fn = lambda v: _linear(F.gelu(_linear(_ln(v, sd, f'{p}.norm2'), sd, f'{p}.mlp.fc1')), sd, f'{p}.mlp.fc2')  # noqa: E731
+    if dp is not None:
+        x = sc + drop_path(t, dp[0], dp[1][0])
+        return x + drop_path(m_fn(x), dp[0], dp[1][1])
+    x = sc + t
+    return x + m_fn(x)
 
 
-def swinir(sd, x, cfg):
-    """SwinIR.forward (swinir_arch.py:868-922), 1conv residual, ape False, eval mode."""
+def swinir(sd, x, cfg, dp_rand=None):
+    """SwinIR.forward (swinir_arch.py:868-922), 1conv residual, ape False; eval mode, or training
+    stochastic depth when ``dp_rand`` [blocks, 2, B] holds the U[0,1) draws (rates: the linear
+    schedule torch.linspace(0, drop_path_rate, sum(depths)), swinir_arch.py:796)."""
     in_ch = cfg.get('in_chans', 3)
     img_range = cfg.get('img_range', 1.)
     ws = cfg.get('window_size', 7)
@@ -298,15 +315,20 @@ def swinir(sd, x, cfg):
     img = (img, img) if isinstance(img, int) else tuple(img)
     res = (img[0] // cfg.get('patch_size', 1), img[1] // cfg.get('patch_size', 1))
 
+    dpr = [v.item() for v in torch.linspace(0, cfg.get('drop_path_rate', 0.1), sum(depths))]
+
     def features(f):
         t = f.flatten(2).transpose(1, 2)
         if cfg.get('patch_norm', True):
             t = _ln(t, sd, 'patch_embed.norm')
+        k = 0
         for i, d in enumerate(depths):
             g = t
             for j in range(d):
+                dp = (dpr[k], dp_rand[k]) if dp_rand is not None else None
                 g = swin_block(g, sd, f'layers.{i}.residual_group.blocks.{j}', (h, w), heads[i], ws,
-                               0 if j % 2 == 0 else ws // 2, res=res)
+                               0 if j % 2 == 0 else ws // 2, res=res, dp=dp)
+                k += 1
             g = g.transpose(1, 2).reshape(b, -1, h, w)
             t = conv(g, sd, f'layers.{i}.conv').flatten(2).transpose(1, 2) + t
         t = _ln(t, sd, 'norm')

@@ -67,17 +67,24 @@ def test_cpu_tensors_refused():
 
 
 def test_struct_layouts_match_header():
-    # field order/size of the ctypes mirrors vs the C structs (all 4-byte members)
+    # field order / kind / size of the ctypes mirrors vs the C structs (4-byte scalars, 8-byte pointers)
     src = re.sub(r'/\*.*?\*/', '', open(os.path.join(ROOT, 'include', 'sr_hip.h')).read(), flags=re.S)
     for cls, tag in ((_lib.ConvDesc, 'sr_conv3x3_desc'), (_lib.WgradDesc, 'sr_conv3x3_wgrad_desc'),
                      (_lib.DcnDesc, 'sr_dcn_desc')):
         body = re.search(r'typedef struct ' + tag + r' \{(.*?)\}', src, re.S).group(1)
-        fields = []
+        fields, size, align = [], 0, 4
         for decl in body.split(';'):
             decl = decl.strip()
             if not decl:
                 continue
-            names = decl.split(None, 1)[1]
-            fields += [n.strip() for n in names.split(',')]
-        assert [f[0] for f in cls._fields_] == fields
-        assert ctypes.sizeof(cls) == 4 * len(fields)
+            ptr = '*' in decl
+            names = decl.replace('*', ' ').split()[-1] if ptr else decl.split(None, 1)[1]
+            for n in names.split(','):
+                fields.append((n.strip(), ptr))
+                w = 8 if ptr else 4
+                size = (size + w - 1) // w * w + w
+                align = max(align, w)
+        size = (size + align - 1) // align * align
+        assert [f[0] for f in cls._fields_] == [n for n, _ in fields]
+        assert [f[1] is ctypes.c_void_p for f in cls._fields_] == [p for _, p in fields]
+        assert ctypes.sizeof(cls) == size

@@ -49,6 +49,9 @@ def _worker(rank, world, port, bucket_mb, q):
         assert spans[0][0] == 0 and spans[-1][1] == flat.offsets[-1]
         assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
         assert 0 in red.buckets[-1][2] and red.buckets[-1][0] == 0
+        # every bucket issued from the post-accumulate hooks while backward ran, not at the join
+        assert sorted(b for b, _ in red.last_issue_log) == list(range(len(red.buckets)))
+        assert all(when == 'backward' for _, when in red.last_issue_log), red.last_issue_log
         q.put((grads, len(red.buckets)))
     dist.barrier()
     dist.destroy_process_group()

@@ -55,7 +55,8 @@ def _worker(rank, world, port, bucket_mb, q):
         model.optimize_parameters(step)
     net = model.get_bare_model(model.net_g)
     sd = {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()}  # by value, not fd-shared
-    q.put((rank, sd, len(model.net_g.reducer.buckets)))
+    red = model.net_g.reducer
+    q.put((rank, sd, len(red.buckets), list(red.last_issue_log)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -72,13 +73,20 @@ def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb):
         p.start()
     res = {}
     for _ in range(2):
-        rank, sd, nb = q.get(timeout=180)
-        res[rank] = (sd, nb)
+        rank, sd, nb, log = q.get(timeout=180)
+        res[rank] = (sd, nb, log)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     if bucket_mb < 1:
-        assert res[0][1] > 1  # several buckets launched while backward runs
+        assert res[0][1] > 1  # several buckets
+    # every bucket's all-reduce was issued from a gradient-ready callback while backward was
+    # still running (overlap), none only at the join before the optimizer; same order on both ranks
+    for r in (0, 1):
+        log = res[r][2]
+        assert sorted(b for b, _ in log) == list(range(res[r][1])), log
+        assert all(when == 'backward' for _, when in log), log
+    assert res[0][2] == res[1][2]
     # both ranks hold identical parameters
     for k in res[0][0]:
         assert (res[0][0][k] == res[1][0][k]).all(), k

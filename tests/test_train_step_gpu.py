@@ -110,3 +110,63 @@ def test_sr_model_hip_graph_matches_eager(cuda, amp):
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
         assert torch.equal(e0[k], e1[k]), k
+
+
+def test_validation_between_graph_replays(cuda, tmp_path):
+    """SRModel.nondist_validation (sr_model.py:183-248 semantics) on PNG pairs of another shape,
+    run between HIP-graph replays (train.cuda_graph): the metrics equal PSNR / SSIM of the
+    oracle's EMA-net outputs (tensor2img -> calculate_*), the SR images are written, and the
+    training that follows is bitwise the eager run's (validation never touches the captured
+    step's static inputs)."""
+    import numpy as np
+
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.data import build_dataloader, build_dataset
+    from basicsr4rs_amd.metrics import calculate_psnr, calculate_ssim
+    from basicsr4rs_amd.models import build_model
+    from basicsr4rs_amd.utils.img_util import tensor2img
+    from tests.test_data import _make_pairs
+    _make_pairs(tmp_path, 3, 12, 12, 4)
+    vopt = dict(name='val', type='PairedImageDataset', dataroot_gt=str(tmp_path / 'gt'),
+                dataroot_lq=str(tmp_path / 'lq'), io_backend=dict(type='disk'), scale=4, phase='val')
+    vds = build_dataset(vopt)
+    vloader = build_dataloader(vds, vopt)
+    metrics = dict(psnr=dict(type='calculate_psnr', crop_border=4, test_y_channel=False),
+                   ssim=dict(type='calculate_ssim', crop_border=4, test_y_channel=False))
+    runs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        o = _opt()
+        o['train']['cuda_graph'] = graph
+        o['val'] = dict(metrics=metrics)
+        o['path'] = dict(visualization=str(tmp_path / f'vis{int(graph)}'))
+        model = build_model(o)
+        losses = []
+        for it in range(1, 7):
+            g0 = torch.Generator().manual_seed(it)
+            model.feed_data({'lq': torch.rand(2, 3, 16, 16, generator=g0), 'gt': torch.rand(2, 3, 64, 64, generator=g0)})
+            model.update_learning_rate(it)
+            model.optimize_parameters(it)
+            losses.append(model.get_current_log()['l_pix'])
+            if graph and it == 4:
+                assert model._graph is not None
+                ema_sd = {k: v.detach().cpu().clone() for k, v in model.net_g_ema.state_dict().items()}
+                model.validation(vloader, it, None, save_img=True)
+                got = dict(model.metric_results)
+                exp = {'psnr': [], 'ssim': []}
+                for i in range(len(vds)):
+                    d = vds[i]
+                    sr = tensor2img([O.edsr(ema_sd, d['lq'][None], num_block=2, upscale=4)])
+                    hr = tensor2img([d['gt'][None]])
+                    exp['psnr'].append(calculate_psnr(sr, hr, 4))
+                    exp['ssim'].append(calculate_ssim(sr, hr, 4))
+                assert abs(got['psnr'] - np.mean(exp['psnr'])) < 0.05, (got, exp)
+                assert abs(got['ssim'] - np.mean(exp['ssim'])) < 1e-3, (got, exp)
+                assert model.best_metric_results['val']['psnr']['iter'] == it
+                assert len(list((tmp_path / 'vis1').rglob('*_4.png'))) == 3
+        net = model.get_bare_model(model.net_g)
+        runs.append((losses, {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}))
+    (l0, p0), (l1, p1) = runs
+    assert l0 == l1
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
