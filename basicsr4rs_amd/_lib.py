@@ -96,6 +96,12 @@ SIGNATURES = {
     'sr_dcn_im2col': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp]),
     'sr_dcn_col2im_workspace': (_sz, [ctypes.POINTER(DcnDesc)]),
     'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    'sr_deform_conv_workspace': (_sz, [_i] * 16),
+    'sr_deform_conv_forward': (_i, [_vp] * 6 + [_i] * 16 + [_vp, _sz, _vp]),
+    'sr_deform_conv_backward_input': (_i, [_vp] * 7 + [_i] * 16 + [_vp, _sz, _vp]),
+    'sr_deform_conv_backward_parameters': (_i, [_vp] * 6 + [_i] * 15 + [_f, _i, _vp, _sz, _vp]),
+    'sr_modulated_deform_conv_forward': (_i, [_vp] * 8 + [_i] * 16 + [_vp, _sz, _vp]),
+    'sr_modulated_deform_conv_backward': (_i, [_vp] * 13 + [_i] * 16 + [_vp, _sz, _vp]),
     'sr_fused_bias_act': (_i, [_i, _vp, _vp, _vp, _vp, _i64, _i, _i, _i, _i, _f, _f, _vp]),
     'sr_fused_lrelu_bwd_workspace': (_sz, [_i, _i, _i64]),
     'sr_fused_lrelu_bwd': (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i64, _f, _f, _vp, _sz, _vp]),

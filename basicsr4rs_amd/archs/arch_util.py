@@ -15,7 +15,9 @@ from torch.nn import init as init
 from torch.nn.modules.batchnorm import _BatchNorm
 
 from ..ops import conv as C
+from ..ops.dcn import ModulatedDeformConvPack, modulated_deform_conv, offset_conv, split_offset_mask
 from ..ops.layout import pixel_unshuffle  # noqa: F401  (re-export, arch_util.py:217-234)
+from ..utils.logger import get_root_logger
 
 
 @torch.no_grad()
@@ -99,3 +101,22 @@ to_ntuple = _ntuple
 def trunc_normal_(tensor, mean=0., std=1., a=-2., b=2.):
     """Truncated normal init (same distribution as arch_util.py:266-327)."""
     return init.trunc_normal_(tensor, mean=mean, std=std, a=a, b=b)
+
+
+class DCNv2Pack(ModulatedDeformConvPack):
+    """Modulated deformable conv whose offsets and masks come from a second feature map
+    (arch_util.py:237-263; EDVR / BasicVSR deformable alignment).
+
+    ``conv_offset(feat)`` -> chunk(3) -> offset = cat(o1, o2), mask = sigmoid(o3); a mean
+    absolute offset above 50 is logged as a warning (the reference's divergence check, a host
+    read per call as there).  The reference prefers torchvision.ops.deform_conv2d, whose
+    sampling (bilinear, zero outside -1 < h < H, offsets interleaved (h, w) per tap) is the
+    same arithmetic as modulated_deform_conv: here both are the HIP DCNv2 path."""
+
+    def forward(self, x, feat):
+        offset, mask = split_offset_mask(offset_conv(self.conv_offset, feat))
+        offset_absmean = torch.mean(torch.abs(offset))
+        if offset_absmean > 50:
+            get_root_logger().warning(f'Offset abs mean is {offset_absmean}, larger than 50.')
+        return modulated_deform_conv(x, offset, mask, self.weight, self.bias, self.stride, self.padding, self.dilation,
+                                     self.groups, self.deformable_groups)

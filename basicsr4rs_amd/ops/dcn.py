@@ -31,7 +31,7 @@ from . import conv as C
 from .swin import LinearSpec
 
 __all__ = ['DeformConvFunction', 'ModulatedDeformConvFunction', 'deform_conv', 'modulated_deform_conv', 'DeformConv',
-           'DeformConvPack', 'ModulatedDeformConv', 'ModulatedDeformConvPack']
+           'DeformConvPack', 'ModulatedDeformConv', 'ModulatedDeformConvPack', 'offset_conv', 'split_offset_mask']
 
 
 def _require_gpu(*tensors):
@@ -243,13 +243,22 @@ modulated_deform_conv = ModulatedDeformConvFunction.apply
 
 
 def _offset_conv(conv, x):
-    """Offset/mask branch (an nn.Conv2d): HIP implicit-GEMM conv for 3x3 / stride 1 / pad 1."""
+    """Offset/mask branch (an nn.Conv2d) on HIP: the implicit-GEMM 3x3 conv for 3x3 / stride 1 /
+    pad 1, any other geometry as a deformable conv with zero offsets and unit masks (bilinear
+    sampling at integer tap positions is exact, and the reference's validity rule
+    -1 < h < H gives exactly the zero padding)."""
     std = (conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
            and conv.dilation == (1, 1) and conv.groups == 1)
-    if not std:
-        return conv(x)
-    xh = C.to_nhwc(x, C.pad8(conv.in_channels), C.feature_dtype())
-    return C.to_nchw(C.conv3x3(xh, conv), conv.out_channels)
+    if std:
+        xh = C.to_nhwc(x, C.pad8(conv.in_channels), C.feature_dtype())
+        return C.to_nchw(C.conv3x3(xh, conv), conv.out_channels)
+    if conv.padding_mode != 'zeros' or isinstance(conv.padding, str):
+        raise NotImplementedError('offset conv: only numeric zero padding is on the HIP path')
+    g = _Geom(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, 1)
+    off = torch.zeros(g.N, 2 * g.K, g.Ho, g.Wo, device=x.device, dtype=torch.float32)
+    msk = torch.ones(g.N, g.K, g.Ho, g.Wo, device=x.device, dtype=torch.float32)
+    return modulated_deform_conv(x, off, msk, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation,
+                                 conv.groups, 1)
 
 
 class _DeformBase(nn.Module):
@@ -380,3 +389,6 @@ class ModulatedDeformConvPack(ModulatedDeformConv):
         offset, mask = split_offset_mask(_offset_conv(self.conv_offset, x))
         return modulated_deform_conv(x, offset, mask, self.weight, self.bias, self.stride, self.padding,
                                      self.dilation, self.groups, self.deformable_groups)
+
+
+offset_conv = _offset_conv

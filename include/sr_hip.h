@@ -303,6 +303,47 @@ int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const 
                   float* grad_x, float* grad_offset, float* grad_mask, void* workspace, size_t ws_bytes,
                   void* stream);
 
+/* deform_conv_ext-compatible entries (basicsr/ops/dcn/src/deform_conv_ext.cpp:52-163; argument order
+ * of :52-57, :70-76, :89-94, :107-113, :127-134): the reference's tensors in its order as fp32 NCHW
+ * contiguous device pointers, then the sizes they carried (input N, C, H, W; Cout = weight.size(0)),
+ * then the reference's integer arguments in its order, then a workspace of
+ * sr_deform_conv_workspace(...) bytes (the same query serves all five; the modulated entries use
+ * im2col_step = N) and the stream.  Buffer semantics as deform_conv_cuda.cpp: output written;
+ * gradInput / grad_input += (the reference scatters into it atomically); gradOffset / grad_offset /
+ * grad_mask written; gradWeight += scale * dW; grad_weight / grad_bias +=.  columns / ones are
+ * accepted and ignored (the reference re-allocates columns itself, deform_conv_cuda.cpp:198, 303, 419,
+ * 532, 610; the bias rides in the GEMM epilogue).  with_bias: 0 / 1. */
+size_t sr_deform_conv_workspace(int N, int C, int H, int W, int Cout, int kW, int kH, int dW, int dH, int padW,
+                                int padH, int dilationW, int dilationH, int group, int deformable_group,
+                                int im2col_step);
+int sr_deform_conv_forward(const float* input, const float* weight, const float* offset, float* output,
+                           float* columns, float* ones, int N, int C, int H, int W, int Cout, int kW, int kH, int dW,
+                           int dH, int padW, int padH, int dilationW, int dilationH, int group, int deformable_group,
+                           int im2col_step, void* workspace, size_t ws_bytes, void* stream);
+int sr_deform_conv_backward_input(const float* input, const float* offset, const float* gradOutput, float* gradInput,
+                                  float* gradOffset, const float* weight, float* columns, int N, int C, int H, int W,
+                                  int Cout, int kW, int kH, int dW, int dH, int padW, int padH, int dilationW,
+                                  int dilationH, int group, int deformable_group, int im2col_step, void* workspace,
+                                  size_t ws_bytes, void* stream);
+int sr_deform_conv_backward_parameters(const float* input, const float* offset, const float* gradOutput,
+                                       float* gradWeight, float* columns, float* ones, int N, int C, int H, int W,
+                                       int Cout, int kW, int kH, int dW, int dH, int padW, int padH, int dilationW,
+                                       int dilationH, int group, int deformable_group, float scale, int im2col_step,
+                                       void* workspace, size_t ws_bytes, void* stream);
+int sr_modulated_deform_conv_forward(const float* input, const float* weight, const float* bias, float* ones,
+                                     const float* offset, const float* mask, float* output, float* columns, int N,
+                                     int C, int H, int W, int Cout, int kernel_h, int kernel_w, int stride_h,
+                                     int stride_w, int pad_h, int pad_w, int dilation_h, int dilation_w, int group,
+                                     int deformable_group, int with_bias, void* workspace, size_t ws_bytes,
+                                     void* stream);
+int sr_modulated_deform_conv_backward(const float* input, const float* weight, const float* bias, float* ones,
+                                      const float* offset, const float* mask, float* columns, float* grad_input,
+                                      float* grad_weight, float* grad_bias, float* grad_offset, float* grad_mask,
+                                      const float* grad_output, int N, int C, int H, int W, int Cout, int kernel_h,
+                                      int kernel_w, int stride_h, int stride_w, int pad_h, int pad_w, int dilation_h,
+                                      int dilation_w, int group, int deformable_group, int with_bias,
+                                      void* workspace, size_t ws_bytes, void* stream);
+
 /* fused_bias_act_op (basicsr/ops/fused_act/src/fused_bias_act_kernel.cu): out = scale *
  * act(x + bias[(i / step_b) % size_b]) with act 1 linear / 3 leaky-relu(alpha), grad 0/1/2
  * (grad 1 gates by ref > 0).  bias / ref may be NULL.  size_x < 2^31 (as the reference). */
