@@ -13,6 +13,7 @@ epilogues (and to the branch gradients in backward).
 import math
 
 import torch
+import torch.utils.checkpoint
 from torch import nn as nn
 
 from .. import _lib
@@ -174,7 +175,14 @@ class BasicLayer(nn.Module):
 
     def forward(self, x):
         for blk in self.blocks:
-            x = blk(x)
+            if self.use_checkpoint and torch.is_grad_enabled():
+                # activation checkpointing per block (swinir_arch.py:460-461); the block's DropPath
+                # factors of this forward are bound here so the recomputation sees the same ones
+                dp = getattr(blk, '_dp', None)
+                x = torch.utils.checkpoint.checkpoint(
+                    lambda t, b=blk, d=dp: S.swin_block(t, b, b._geom, b._fc1, b._fc2, dp=d), x, use_reentrant=False)
+            else:
+                x = blk(x)
         return x
 
 
@@ -362,10 +370,10 @@ class SwinIR(nn.Module):
             blk._dp = (fac[i, 0], fac[i, 1]) if p > 0 else None
 
     def forward_features(self, x):
-        if self.ape:
-            raise NotImplementedError('absolute position embedding (ape=True) is not on the HIP path yet')
         self._set_drop_path(x.shape[0], x.device)
         x = self.patch_embed(x)
+        if self.ape:
+            x = S.add_pos_embed(x, self.absolute_pos_embed, self.embed_dim)
         for layer in self.layers:
             x = layer(x)
         for blk in self._blocks():

@@ -946,6 +946,33 @@ constexpr int LN_BWD_BLOCKS = 512;
 bool ln_vec8(int Cp, int ld1, int ld2) { return Cp <= 256 && Cp % 8 == 0 && ld1 % 8 == 0 && ld2 % 8 == 0; }
 }  // namespace
 
+// Absolute position embedding (swinir_arch.py:789-791, :879-880): y[n][p][c] = x[n][p][c] + pos[p][c]
+// over dense token rows [N][P][Cp] (padded channels c >= C copied), and its parameter gradient
+// dpos[p][c] (+)= sum_n dy[n][p][c] (fixed order over n: deterministic).
+template <typename T>
+__global__ void add_pos_kernel(const T* __restrict__ x, const float* __restrict__ pos, int64_t total, int P, int C,
+                               int Cp, T* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const int p = (int)((i / Cp) % P);
+    float v = Elt<T>::to_f(x[i]);
+    if (c < C) v += pos[(int64_t)p * C + c];
+    y[i] = Elt<T>::from_f(v);
+  }
+}
+
+template <typename T>
+__global__ void pos_grad_kernel(const T* __restrict__ dy, int N, int P, int C, int Cp, float* __restrict__ dpos,
+                                int accumulate) {
+  const int64_t total = (int64_t)P * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int p = (int)(i / C), c = (int)(i - (int64_t)p * C);
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += Elt<T>::to_f(dy[((int64_t)n * P + p) * Cp + c]);
+    dpos[i] = accumulate ? dpos[i] + acc : acc;
+  }
+}
+
 extern "C" {
 
 int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, const float* beta, int64_t M, int C, int Cp,
@@ -1045,6 +1072,36 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
   hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((a.nbins + 63) / 64)), dim3(1024), 0, s,
                      (const float*)workspace, parts, nH, a.nbins, dbias_table, accumulate);
   return sr_check(hipGetLastError(), "window_attn_bwd launch");
+}
+
+int sr_add_pos_embed(int dtype, const void* x, int N, int P, int C, int Cp, const float* pos, void* y, void* stream) {
+  if (!x || !pos || !y || N <= 0 || P <= 0 || C <= 0 || Cp < C) return sr_fail(SR_EINVAL, "add_pos_embed: bad arguments");
+  const int64_t total = (int64_t)N * P * Cp;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(add_pos_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, (const bf16_t*)x, pos, total, P, C,
+                       Cp, (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(add_pos_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)x, pos, total, P, C,
+                       Cp, (float*)y);
+  return sr_check(hipGetLastError(), "add_pos_embed launch");
+}
+
+int sr_pos_embed_grad(int dtype, const void* dy, int N, int P, int C, int Cp, float* dpos, int accumulate, void* stream) {
+  if (!dy || !dpos || N <= 0 || P <= 0 || C <= 0 || Cp < C) return sr_fail(SR_EINVAL, "pos_embed_grad: bad arguments");
+  const int64_t total = (int64_t)P * C;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(pos_grad_kernel<bf16_t>, dim3((unsigned)blocks), dim3(256), 0, s, (const bf16_t*)dy, N, P, C, Cp,
+                       dpos, accumulate);
+  else
+    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)dy, N, P, C, Cp,
+                       dpos, accumulate);
+  return sr_check(hipGetLastError(), "pos_embed_grad launch");
 }
 
 }  // extern "C"

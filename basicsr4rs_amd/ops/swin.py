@@ -297,3 +297,40 @@ def swin_block(x, blk, geom, fc1s, fc2s, dp=None):
     return _STB.apply(x, geom, fc1s, fc2s, float(at.scale), dp, blk.norm1.weight, blk.norm1.bias, at.qkv.weight,
                       at.qkv.bias, at.relative_position_bias_table, at.proj.weight, at.proj.bias, blk.norm2.weight,
                       blk.norm2.bias, blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias)
+
+
+class _AddPos(torch.autograd.Function):
+    """x + absolute_pos_embed over the token map (swinir_arch.py:879-880); the embedding's gradient
+    is the batch sum, accumulated straight into its flat .grad view when it has one."""
+
+    @staticmethod
+    def forward(ctx, x, pos, Creal):
+        N, H, W, Cp = x.shape
+        y = torch.empty_like(x)
+        lib = _lib.load()
+        _lib.check(lib.sr_add_pos_embed(_lib.dtype_code(x.dtype), _lib.ptr(x), N, H * W, Creal, Cp,
+                                        _lib.ptr(pos.detach().contiguous()), _lib.ptr(y), _lib.stream()))
+        ctx.geo = (N, H * W, Creal, Cp)
+        ctx.pos = pos
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, P, Creal, Cp = ctx.geo
+        dy = dy.contiguous()
+        direct = _direct((ctx.pos, ))
+        dpos = direct[0] if direct is not None else torch.empty(ctx.pos.shape, device=dy.device, dtype=torch.float32)
+        lib = _lib.load()
+        _lib.check(lib.sr_pos_embed_grad(_lib.dtype_code(dy.dtype), _lib.ptr(dy), N, P, Creal, Cp, _lib.ptr(dpos),
+                                         int(direct is not None), _lib.stream()))
+        if direct is not None:
+            C.grad_ready(ctx.pos)
+            return dy, None, None
+        return dy, dpos, None
+
+
+def add_pos_embed(x, pos, Creal):
+    if x.shape[1] * x.shape[2] != pos.shape[1]:
+        raise ValueError(f'absolute_pos_embed covers {pos.shape[1]} tokens, the input has {x.shape[1] * x.shape[2]} '
+                         '(ape needs the runtime size to equal img_size, as in the reference)')
+    return _AddPos.apply(x, pos, Creal)

@@ -274,6 +274,12 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
                        float scale, const float* bias_table, void* dqkv, float* dbias_table, void* workspace,
                        size_t ws_bytes, int accumulate, void* stream);
 
+/* SwinIR absolute position embedding (ape=True, swinir_arch.py:789-791, :879-880) on dense token rows
+ * [N][P][Cp]: y = x + pos[p][c] for c < C (pos fp32 [P][C]); its gradient dpos[p][c] (+)= sum_n dy. */
+int sr_add_pos_embed(int dtype, const void* x, int N, int P, int C, int Cp, const float* pos, void* y, void* stream);
+int sr_pos_embed_grad(int dtype, const void* dy, int N, int P, int C, int Cp, float* dpos, int accumulate,
+                      void* stream);
+
 /* ---------------------------------------------------------------------------------
  * basicsr/ops native extensions (replacements of deform_conv_ext, fused_act_ext,
  * upfirdn2d_ext).

@@ -300,7 +300,7 @@ def swin_block(x, sd, p, hw, nH, ws, shift, res=None, dp=None):
 
 
 def swinir(sd, x, cfg, dp_rand=None):
-    """SwinIR.forward (swinir_arch.py:868-922), 1conv residual, ape False; eval mode, or training
+    """SwinIR.forward (swinir_arch.py:868-922), 1conv residual (ape optional); eval mode, or training
     stochastic depth when ``dp_rand`` [blocks, 2, B] holds the U[0,1) draws (rates: the linear
     schedule torch.linspace(0, drop_path_rate, sum(depths)), swinir_arch.py:796)."""
     in_ch = cfg.get('in_chans', 3)
@@ -321,6 +321,8 @@ def swinir(sd, x, cfg, dp_rand=None):
         t = f.flatten(2).transpose(1, 2)
         if cfg.get('patch_norm', True):
             t = _ln(t, sd, 'patch_embed.norm')
+        if cfg.get('ape', False):  # swinir_arch.py:879-880
+            t = t + sd['absolute_pos_embed']
         k = 0
         for i, d in enumerate(depths):
             g = t

@@ -171,3 +171,34 @@ def test_swinir_drop_path_train_matches_oracle(cuda, dtype):
     with torch.no_grad():
         oe = gn(x.to(cuda))
     assert (oe.float().cpu() - ref_eval).abs().max().item() < (1e-3 if dtype == 'fp32' else 5e-2)
+
+
+def test_swinir_ape_and_checkpoint_fp32(cuda):
+    """ape=True (absolute position embedding, swinir_arch.py:789-791, :879-880) with
+    use_checkpoint=True (per-block activation checkpointing, :460-461) and stochastic depth on:
+    output and every gradient (incl. absolute_pos_embed) match the oracle under the same draws."""
+    from basicsr4rs_amd.archs import build_network
+    cfg = dict(type='SwinIR', upscale=2, in_chans=3, img_size=16, window_size=8, img_range=1., depths=[2, 2],
+               embed_dim=60, num_heads=[6, 6], mlp_ratio=2, upsampler='pixelshuffledirect', drop_path_rate=0.3,
+               ape=True, use_checkpoint=True)
+    torch.manual_seed(0)
+    net = build_network(cfg)
+    assert 'absolute_pos_embed' in dict(net.named_parameters())
+    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    x = torch.rand(2, 3, 16, 16)
+    rand = torch.rand(4, 2, 2, generator=torch.Generator().manual_seed(5))
+    gn = copy.deepcopy(net).to(cuda).train()
+    gn.drop_path_draws = lambda nb, b, dev: rand[:nb, :, :b].to(dev)
+    sdg = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    ref = O.swinir(sdg, x, cfg, dp_rand=rand)
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    out = gn(x.to(cuda))
+    assert (out.detach().cpu() - ref.detach()).abs().max().item() < 1e-3
+    (out * g.to(cuda)).sum().backward()
+    for n, p in gn.named_parameters():
+        r = sdg[n].grad
+        e = (p.grad.cpu() - r).abs().max().item() / max(1e-3, r.abs().max().item())
+        assert e < 2e-3, (n, e)
+    with pytest.raises(ValueError, match='absolute_pos_embed'):
+        gn.eval()(torch.rand(1, 3, 24, 24, device=cuda))
