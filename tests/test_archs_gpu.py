@@ -107,20 +107,43 @@ def test_swinir_upsamplers_fp32(cuda, ups):
 
 
 def test_swinir_bf16_c4_shape(cuda):
-    """SwinIR-M geometry (embed 180, 6 heads, window 8) in bf16 on a 32x32 tile."""
+    """SwinIR-M geometry (embed 180, 6 heads, window 8) in bf16 on a 32x32 tile, against the float64
+    oracle on the same bf16-rounded weights and input: output within 5e-3 of its range; every
+    parameter gradient with cosine >= 0.995 to the oracle's and max error <= 0.15 of its max
+    magnitude.  Observed: cosine 0.9979-0.9990 for all 60 tensors, max error 0.05-0.11: the
+    expected size of bf16 (8-bit mantissa) rounding of every stored activation and gradient along a
+    4-STB + upsampler backward under a random HR output gradient (the fp32 path of the same net
+    agrees to 2e-3, test_swinir_upsamplers_fp32)."""
     from basicsr4rs_amd.archs import build_network
     cfg = dict(type='SwinIR', upscale=4, in_chans=3, img_size=32, window_size=8, img_range=1., depths=[2, 2],
                embed_dim=180, num_heads=[6, 6], mlp_ratio=2, upsampler='pixelshuffle', drop_path_rate=0.)
     torch.manual_seed(0)
     net = build_network(cfg)
-    sd = {k: v.detach().clone() for k, v in net.state_dict().items()}
-    x = torch.rand(1, 3, 32, 32)
-    ref = O.swinir(sd, x, cfg)
+    sd = {k: (v.detach().to(torch.bfloat16).float() if v.is_floating_point() else v) for k, v in net.state_dict().items()}
+    net.load_state_dict(sd)
+    x = torch.rand(1, 3, 32, 32).to(torch.bfloat16).float()
+    sdg = {k: (v.double().requires_grad_(True) if v.is_floating_point() else v) for k, v in sd.items()}
+    ref = O.swinir(sdg, x.double(), cfg)
+    g = torch.randn(ref.shape, generator=torch.Generator().manual_seed(1), dtype=torch.float64)
+    (ref * g).sum().backward()
     gn = copy.deepcopy(net).to(cuda)
     with torch.autocast('cuda', dtype=torch.bfloat16):
         out = gn(x.to(cuda))
-    assert (out.float().cpu() - ref).abs().max().item() < 5e-2 * max(1.0, ref.abs().max().item())
-    out.float().mean().backward()
+    rng = max(1.0, ref.abs().max().item())
+    err = (out.float().detach().cpu().double() - ref.detach()).abs().max().item() / rng
+    (out.float() * g.float().to(cuda)).sum().backward()
+    worst, worst_cos = (0.0, ''), (1.0, '')
+    for n, p in gn.named_parameters():
+        r = sdg[n].grad
+        a = p.grad.cpu().double()
+        e = (a - r).abs().max().item() / max(1e-6, r.abs().max().item())
+        cos = torch.nn.functional.cosine_similarity(a.flatten(), r.flatten(), dim=0).item()
+        worst, worst_cos = max(worst, (e, n)), min(worst_cos, (cos, n))
+    print(f'SwinIR-M bf16: out err {err:.3e} of range, worst param-grad err {worst[0]:.3e} ({worst[1]}), '
+          f'lowest cosine {worst_cos[0]:.5f} ({worst_cos[1]})')
+    assert err < 5e-3, err  # observed 1.1e-3
+    assert worst_cos[0] >= 0.995, worst_cos
+    assert worst[0] <= 0.15, worst
 
 
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
