@@ -23,6 +23,7 @@ namespace {
 // set by sr_conv3x3_set_variant (tests / A-B timing): 0 auto (phase-interleaved 256x256),
 // 1 never a 256x256 kernel, 2 the two-barrier 256x256 kernel (previous schedule)
 int g_variant = 0;
+unsigned long long* g_stamps = nullptr;
 #define g_disable_big (g_variant == 1)
 
 struct FwdArgs {
@@ -58,6 +59,7 @@ struct FwdArgs {
   int tiles_n, tiles;
   FastDiv fd_cpt, fd_W, fd_H, fd_cps;  // fd_cps: divide by C' (channels per shuffle slot)
   FastDiv fd_r;                        // divide by in_ps (1 when none)
+  unsigned long long* stamps;  // diagnostics: per-row clock stamps of the band kernel (null = off)
   const float* row_scale;  // optional per-image factor on alpha (SwinIR stochastic depth)
   FastDiv fd_hw;           // divide by H*W (pixel -> image)
 };
@@ -187,8 +189,7 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
         *(f32x4*)((float*)a.aux + da + 4) = f32x4{v[4], v[5], v[6], v[7]};
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+    act_apply_n(v, a.act, a.slope);
     if (a.gate && a.gate_mode != 2) {
       float g[8];
       unpack(gv[it], g);
@@ -1191,8 +1192,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
         for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
         *(u32x4*)((bf16_t*)a.aux + (size_t)m * a.ldy + a.ycoff + n) = o;
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+      act_apply_n(v, a.act, a.slope);
       if (a.gate && a.gate_mode != 2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1408,13 +1408,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
         for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
         *(u32x4*)((bf16_t*)a.aux + (size_t)m * a.ldy + a.ycoff + nn) = o;
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_apply(v[j], a.act, a.slope);
+      act_apply_n(v, a.act, a.slope);
       float gf[8];
       if (a.gate) unpack8(gv, gf);
-      if (a.gate && a.gate_mode != 2) {
+      if (a.gate && a.gate_mode == 1) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= a.gate_mode == 1 ? gelu_grad(gf[j]) : (gf[j] > 0.f ? 1.f : a.gate_slope);
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
+      } else if (a.gate && a.gate_mode == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
       }
       const float al = row_alpha(a, m);
 #pragma unroll
@@ -1460,6 +1462,368 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
     __syncthreads();
     if (DBG != 3) epilogue_tile<bf16_t, 128, BN, 256>(a, Cs, CSTR, m0 + h * 128, n0, tid);
   }
+}
+
+// ------------------------------------------------------------------------------------
+// Narrow-conv forward / dgrad, row-streaming persistent form (bf16 3x3, Cin 32 or 64,
+// Cout 32 or 64, W 64 or 128: RCAN / SRResNet bodies, RRDB conv1 and dgrads into 64 ch).
+//
+// The tile kernel above loads a halo, computes and stores in one pass per block, so with one
+// wave of blocks the chip runs the three phases one after the other (RCAN conv at B 32:
+// 24 us, of which 8 us store tail and ~5 us load burst; the MFMA work is ~4.6 us per SIMD).
+// Here a block owns a band of consecutive output rows (one row = W pixels of one image; the
+// NHWC rows of all images are one contiguous sequence) and streams it: input rows live in an
+// (LA + 2)-slot LDS ring (slot = global row % S, W + 2 swizzled 128-B pixel rows, zero border
+// columns written once); row s + LA is DMA'd while row s is computed, the residual / gate
+// operands of row s are DMA'd into per-wave staging before its MFMAs (each lane reads back its
+// own 16 B), and its stores drain while later rows compute.  Rows outside an image (the 3x3
+// zero padding in y) are never read: the taps that would read them are skipped (wave-uniform
+// test per row).  Each wave keeps ALL its weights (32 output channels x 9 taps x Cin) in
+// registers for the whole band, loaded once.
+// MFMA as the DIRECT halo epilogue: C = W x X^T with row-permuted weight tiles, so each lane
+// ends with 8 consecutive channels of one pixel and stores 16 B; colsum (RCAN avg-pool)
+// partial rows per (image row, pixel wave).
+// vmcnt bookkeeping per wave: per row [NG staging pieces] [PPW row pieces] .. MFMAs ..
+// vmcnt(PPW) (staging landed) [PT stores] [NC colsum stores]; before row s the count of vector
+// memory ops younger than row s + 1's pieces is known in closed form (prologue rows, then the
+// steady state (PT + NC) + (LA - 2) * ops-per-row) and waited with a run-time vmcnt.
+// ------------------------------------------------------------------------------------
+// s_waitcnt vmcnt(n) for a run-time n (wave-uniform): the immediate comes from a jump table;
+// n > 63 waits for vmcnt(63), which only waits longer.
+template <int K>
+SR_DEV void vm_wait_ge(int n) {
+  if constexpr (K >= 63) {
+    asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+  } else {
+    if (n <= K) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
+    else vm_wait_ge<K + 1>(n);
+  }
+}
+SR_DEV void vm_wait_dyn(int n) { vm_wait_ge<0>(n < 0 ? 0 : n); }
+
+template <int CO, int W, int LA, int KH>
+__global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
+  constexpr int WC = CO / 32;       // waves along output channels (32 each = 2 co tiles)
+  constexpr int WP = 4 / WC;        // waves along the row's pixels
+  constexpr int PT = W / 16 / WP;   // 16-pixel tiles per wave
+  constexpr int WPAD = W + 2;
+  constexpr int SLOT = WPAD * 128;
+  constexpr int S = LA + 2;         // ring slots: rows s-1 .. s+1 read, s+2 .. s+LA in flight
+  constexpr int PPW = W / 8 / 4;    // 1-KB DMA pieces per wave per row
+  constexpr int EPI = 3 * PT * 1024;  // per wave: gate / res / res2 staging of its row pixels
+  // + one all-zero slot: the rows above / below an image (3x3 zero padding in y) read it, so
+  // the MFMA sequence has no branches and the compiler can run the fragment reads ahead
+  __shared__ __attribute__((aligned(16))) char smem[(S + 1) * SLOT + 4 * EPI];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = w % WC, wp = w / WC;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int H = a.H;
+  const int T = a.N * H;  // output rows
+  const bool stamp = a.stamps && tid == 0;
+  unsigned long long* st = a.stamps ? a.stamps + (size_t)blockIdx.x * 16 : nullptr;
+  const unsigned long long t_start = __builtin_readcyclecounter();
+  const int G = gridDim.x;
+  const int bb = blockIdx.x;
+  const int s0 = (int)((int64_t)bb * T / G), s1 = (int)((int64_t)(bb + 1) * T / G);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+  constexpr bool khi = KH == 2;  // Cin 64 (two 32-channel K halves) or 32
+  const int NG = PT * ((a.gate ? 1 : 0) + (a.res ? 1 : 0) + (a.res2 ? 1 : 0));
+  const bool cs_on = a.colsum != nullptr;
+  const int NC = (cs_on ? 2 : 0) + (a.aux ? PT : 0);  // stores after the PT output stores
+  const int KROW = NG + PPW + PT + NC;  // vector memory ops per row
+
+  // zero border columns (pixel rows 0 and W + 1) of every slot, and the zero slot S, once
+  for (int i = tid; i < S * 2 * 8; i += 256) {
+    const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
+    *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
+  }
+  for (int i = tid; i < SLOT / 16; i += 256) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
+  const unsigned long long t_zeroed = __builtin_readcyclecounter();
+  // this wave's weights: co = wc*32 + 8*(c16>>2) + 4*c + (c16&3) (DIRECT row permutation),
+  // K chunk kk*32 + 8*g of every tap
+  u32x4 bw[9][2][2];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int co = wc * 32 + 8 * (c16 >> 2) + 4 * c + (c16 & 3);
+        const int ci = kk * 32 + 8 * g;
+        const bool v = co < a.Cout && ci < a.Cin;
+        bw[tap][kk][c] = (kk == 0 || khi) ? buf_load16(wr, v ? (uint32_t)((co * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB)
+                                          : u32x4{0u, 0u, 0u, 0u};
+      }
+  const unsigned long long t_wissued = __builtin_readcyclecounter();
+  const int nn = wc * 32 + 8 * g;  // this lane's 8 output channels
+  float bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bv[j] = 0.f;
+  if (a.bias) {
+    const f32x4 b0 = *(const f32x4*)(a.bias + nn), b1 = *(const f32x4*)(a.bias + nn + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { bv[j] = b0[j]; bv[4 + j] = b1[j]; }
+  }
+  // weights / bias must be complete before the DMA stream starts, AND the compiler must know it:
+  // a use of every value here makes it wait now instead of emitting vmcnt waits (which would
+  // also drain the in-flight row DMA it cannot see) inside the row loop
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) asm volatile("" ::"v"(bw[tap][kk][c]));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // border zeros written
+  const unsigned long long t_loaded = __builtin_readcyclecounter();
+  unsigned long long ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: wait / barrier / MFMA / epilogue
+
+  // DMA of global row q (pixels 1..W of slot q % S); rows outside [0, T) read zeros
+  const int lc_lane = lane & 7;
+  auto issue_row = [&](int q) {
+    char* slot = smem + (q % S) * SLOT;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int k = w * PPW + j;            // piece: pixel rows 1 + 8k .. 8 + 8k
+      const int px = 1 + 8 * k + (lane >> 3);
+      const int lc = lc_lane ^ (px & 7);    // logical 16-B chunk landing in physical slot lane & 7
+      const bool v = q >= 0 && q < T && lc * 8 < a.Cin;
+      const uint32_t off = (uint32_t)((((size_t)q * W + (px - 1)) * a.ldx + a.xcoff + lc * 8) * 2);
+      glds16(xr, slot + (1 + 8 * k) * 128, v ? off : SR_OOB);
+    }
+  };
+  const bool gok = a.gate_mode != 2 || (nn >= a.gcol0 && nn < a.gcol1);
+  const bool rok = nn < a.rcols;
+  auto unpack8 = [](const u32x4& q, float* o) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[2 * j] = bf16_to_f32(q[j] & 0xffff);
+      o[2 * j + 1] = bf16_to_f32(q[j] >> 16);
+    }
+  };
+  char* epi = smem + (S + 1) * SLOT + w * EPI;
+  // gate / res / res2 of this wave's pixels of output row q into its staging buffer (NG ops)
+  auto issue_staging = [&](int q) {
+    const bool qv = q < T;
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const size_t m = (size_t)q * W + wp * PT * 16 + i * 16 + c16;
+      if (a.gate) glds16(gr, epi + (0 * PT + i) * 1024, qv && gok ? (uint32_t)((m * a.ldg + a.gcoff + nn) * 2) : SR_OOB);
+      if (a.res) glds16(rr, epi + (1 * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr + a.rcoff + nn) * 2) : SR_OOB);
+      if (a.res2) glds16(rr2, epi + (2 * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr2 + a.r2coff + nn) * 2) : SR_OOB);
+    }
+  };
+  // prologue: rows s0 - 1 .. s0 + LA - 1 (s0 - 1 first: the oldest), then row s0's staging
+  if (s0 < s1) {
+    for (int q = s0 - 1; q < s0 + LA; ++q) issue_row(q);
+    issue_staging(s0);
+  }
+
+  // Per row, in issue order: [MFMAs] [epilogue] [staging of row s + 1: NG] [pieces of row
+  // s + LA: PPW] [stores: PT + NC].  Vector memory ops complete in issue order, so a wait for
+  // one op is a wait for every older one: the row pieces and the staging are issued after the
+  // epilogue, so neither wait below ever covers the stores or the DMA of the row just issued.
+#pragma unroll 1
+  for (int s = s0; s < s1; ++s) {
+    // rows <= s + 1 landed: the ops issued after row s + 1's pieces may stay in flight
+    const int younger = (s + 1 < s0 + LA) ? (s0 + LA - 2 - s) * PPW + NG + (s - s0) * KROW
+                                          : (PT + NC) + (LA - 2) * KROW;
+    const unsigned long long t0 = __builtin_readcyclecounter();
+    vm_wait_dyn(younger);
+    const unsigned long long t1 = __builtin_readcyclecounter();
+    // every wave's pieces of row s + 1 are in LDS, and every wave is done with row s - 2,
+    // whose slot row s + LA reuses (S = LA + 2)
+    pp_barrier();
+    const unsigned long long t2 = __builtin_readcyclecounter();
+    const int n_img = s / H, y = s - n_img * H;
+    const float rs = a.row_scale ? a.alpha * a.row_scale[n_img] : a.alpha;  // scalar load
+
+    f32x4 acc[PT][2];
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int sl1 = s % S;
+    const int sl0 = y == 0 ? S : (sl1 == 0 ? S - 1 : sl1 - 1);      // zero slot above an image
+    const int sl2 = y == H - 1 ? S : (sl1 == S - 1 ? 0 : sl1 + 1);  // ... and below it
+    const char* srows[3] = {smem + sl0 * SLOT, smem + sl1 * SLOT, smem + sl2 * SLOT};
+    // K steps (tap, K half) in order; the fragments of step k + 1 are read while step k's
+    // MFMAs run (double-buffered registers)
+    constexpr int NK = 9 * KH;
+    // Fragment reads run FD - 1 K steps ahead of the MFMAs.  They are inline-asm ds_reads with
+    // hand-counted lgkmcnt waits that pass the fragments through (so no MFMA can be scheduled
+    // before its wait): the compiler otherwise sinks every read to just before its use and
+    // exposes the full LDS latency per 2 MFMAs (one wave per SIMD has nothing else to run).
+    constexpr int FD = 5;
+    u32x4 fa[FD][PT];
+    uint32_t rbase[3];
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty)
+      rbase[ty] = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)srows[ty];
+    auto read_k = [&](int k, u32x4 (&dst)[PT]) {
+      const int tap = k / KH, kk = k % KH, ty = tap / 3, tx = tap % 3;
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        const uint32_t ad = rbase[ty] + swz128(wp * PT * 16 + i * 16 + c16 + tx, kk * 4 + g);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(dst[i]) : "v"(ad));
+      }
+    };
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (!(a.tiles_n & 1)) {  // ablation 1: no MFMA section (A/B timing only)
+#pragma unroll
+    for (int k = 0; k < FD - 1; ++k) read_k(k, fa[k]);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      if (k + FD - 1 < NK) read_k(k + FD - 1, fa[(k + FD - 1) % FD]);
+      const int ahead = (NK - 1 - k < FD - 1 ? NK - 1 - k : FD - 1) * PT;  // reads issued after step k's
+      u32x4* f = fa[k % FD];
+      if constexpr (PT == 1) {
+        switch (ahead) {
+          case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0])); break;
+          case 1: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(f[0])); break;
+          case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(f[0])); break;
+          case 3: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(f[0])); break;
+          default: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0])); break;
+        }
+      } else if constexpr (PT == 2) {
+        switch (ahead) {
+          case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1])); break;
+          case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(f[0]), "+v"(f[1])); break;
+          case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1])); break;
+          case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(f[0]), "+v"(f[1])); break;
+          default: asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1])); break;
+        }
+      } else {
+        switch (ahead) {
+          case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])); break;
+          case 4: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])); break;
+          case 8: asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])); break;
+          case 12: asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])); break;
+          default: asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])); break;
+        }
+      }
+      const int tap = k / KH, kk = k % KH;
+#pragma unroll
+      for (int i = 0; i < PT; ++i)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) mfma_chunk<bf16_t>(bw[tap][kk][c], f[i], acc[i][c]);
+    }
+    }
+    // The compiler interleaves the epilogue's accumulator reads with the last MFMAs and, on the
+    // path around the optional aux store, left too few wait states between the final MFMA and the
+    // read of its result (acc[PT-1][1][3] came out stale).  Fence the MFMA block and pad it.
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    const unsigned long long t3 = __builtin_readcyclecounter();
+    // this row's staging landed (issued before row s + LA - 1's pieces and row s - 1's stores)
+    if (NG) vm_wait_dyn(s == s0 ? 0 : PPW + PT + NC);
+    if (a.tiles_n & 2) {  // ablation 2: no epilogue; keep the op count (dummy stores)
+      issue_staging(s + 1);
+      issue_row(s + LA);
+#pragma unroll
+      for (int i = 0; i < PT + NC; ++i) glds16(xr, epi, SR_OOB);  // (NC dummies: any count works)
+      continue;
+    }
+    float cs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs[j] = 0.f;
+    u32x4 ov[PT], avx[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
+      if (a.aux) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) avx[i][j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      }
+      act_apply_n(v, a.act, a.slope);
+      float gf[8];
+      if (a.gate) unpack8(*(const u32x4*)(epi + (0 * PT + i) * 1024 + lane * 16), gf);
+      if (a.gate && a.gate_mode == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
+      } else if (a.gate && a.gate_mode == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= rs;
+      if (a.res && rok) {
+        float rf[8];
+        unpack8(*(const u32x4*)(epi + (1 * PT + i) * 1024 + lane * 16), rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a.beta * rf[j] + v[j];
+      }
+      if (a.res2 && rok) {
+        float rf[8];
+        unpack8(*(const u32x4*)(epi + (2 * PT + i) * 1024 + lane * 16), rf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rf[j] + v[j];
+      }
+      if (a.gate && a.gate_mode == 2 && gok) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+      }
+      u32x4& o = ov[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      if (cs_on) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cs[2 * j] += bf16_to_f32(o[j] & 0xffff);
+          cs[2 * j + 1] += bf16_to_f32(o[j] >> 16);
+        }
+      }
+    }
+    // the staging buffer's reads above are consumed (values in registers) before the DMA refills it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    issue_staging(s + 1);
+    issue_row(s + LA);
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const size_t m = (size_t)s * W + wp * PT * 16 + i * 16 + c16;
+      *(u32x4*)((bf16_t*)a.y + m * a.ldy + a.ycoff + nn) = ov[i];
+    }
+    if (a.aux) {
+#pragma unroll
+      for (int i = 0; i < PT; ++i) {
+        const size_t m = (size_t)s * W + wp * PT * 16 + i * 16 + c16;
+        *(u32x4*)((bf16_t*)a.aux + m * a.ldy + a.ycoff + nn) = avx[i];
+      }
+    }
+    if (cs_on) {
+      // the 16 lanes of a g group hold the same 8 channels: fixed-order butterfly, then lane
+      // c16 == 0 writes partial row s * WP + wp (P = H * WP rows per image)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
+      float* dstp = a.colsum + ((size_t)s * WP + wp) * a.Cout + nn;
+      // exactly two vector store instructions per wave (lanes masked): the NC of the count above
+      if (c16 == 0) *(f32x4*)dstp = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      if (c16 == 0) *(f32x4*)(dstp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+    }
+    if (a.stamps) {
+      const unsigned long long t4 = __builtin_readcyclecounter();
+      ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
+    }
+  }
+  if (stamp) {
+    st[0] = t_start; st[1] = t_loaded; st[2] = __builtin_readcyclecounter(); st[3] = s1 - s0;
+    st[4] = ph[0]; st[5] = ph[1]; st[6] = ph[2]; st[7] = ph[3];
+    st[8] = t_zeroed; st[9] = t_wissued;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing row pieces (zeros past T) land before exit
 }
 
 // ------------------------------------------------------------------------------------
@@ -2637,7 +3001,14 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
 
 // Kernel family sr_conv3x3_fwd launches for a call (dispatch, kernel names and the
 // epilogue geometry behind colsum all follow this one choice).
-enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN };
+enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN, FK_BAND };
+// row-streaming narrow conv: bf16 3x3, Cin 32 / 64, Cout 32 / 64 exactly, W 64 / 128, plain or
+// channel-slice NHWC in and out (variant 34: the tile kernel instead, for A/B)
+bool fwd_use_band(const FwdArgs& a, bool bf) {
+  return bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
+         (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && (a.Cout == 32 || a.Cout == 64) &&
+         a.Cout_real == a.Cout && g_variant >= 35 && g_variant <= 39;  // opt-in: slower than the tile kernel so far
+}
 // short-K 1x1 convs (linears): token tile staged once, all output channels swept
 bool fwd_use_lin(const FwdArgs& a, bool bf) {
   return bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && a.Cin <= 192 &&
@@ -2645,6 +3016,7 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
 }
 FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_lin(a, bf)) return FK_LIN;
+  if (fwd_use_band(a, bf)) return FK_BAND;
   if (fwd_use_halo(a, bf)) return FK_HALO;
   // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
   // kernel with a partial N tile: x read once (vs twice by 128x128 tiles); 68 -> 57 us and 82 -> 65 us
@@ -2669,6 +3041,26 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
       FwdArgs b = a;
       b.tiles = (a.M + 127) / 128;
       hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3>), dim3(b.tiles), dim3(256), 0, s, b);
+      return hipGetLastError();
+    }
+    case FK_BAND: {
+      // 2 blocks per CU (1 for W 128: its ring + staging take 91-116 KB of LDS); variant 35 forces
+      // 64 blocks (long bands: ring wrap-around and image crossings inside a band, for tests)
+      const int rows = a.N * a.H;
+      const int gmax = (g_variant == 35 || g_variant >= 37) ? 64 : 256;  // one block per CU (1 wave / SIMD)
+      FwdArgs ab = a;
+      ab.tiles_n = g_variant >= 36 ? g_variant - 36 : 0;  // band ablations (36 + code, 37+ on 64 blocks)
+      ab.stamps = g_stamps;
+      const dim3 grid(rows < gmax ? rows : gmax);
+#define SR_BAND(CO_, W_, LA_, KH_) \
+  if (a.Cout == CO_ && a.W == W_ && a.Cin == 32 * KH_) { \
+    hipLaunchKernelGGL((conv3x3_fwd_band_kernel<CO_, W_, LA_, KH_>), grid, dim3(256), 0, s, ab); \
+    return hipGetLastError(); \
+  }
+      SR_BAND(64, 64, 5, 2) SR_BAND(64, 64, 5, 1) SR_BAND(32, 64, 5, 2) SR_BAND(32, 64, 5, 1)
+      SR_BAND(64, 128, 3, 2) SR_BAND(64, 128, 3, 1) SR_BAND(32, 128, 4, 2) SR_BAND(32, 128, 4, 1)
+#undef SR_BAND
+      return hipErrorInvalidValue;
       return hipGetLastError();
     }
     case FK_HALO: return launch_fwd_halo(a, s);
@@ -2827,6 +3219,7 @@ FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
 // Partial rows per image of the colsum output, or 0 when the call cannot produce it.
 int colsum_parts(const sr_conv3x3_desc* d, const FwdArgs& a) {
   if (d->out_ps || d->out_nchw || fwd_kind(a, d->dtype == SR_BF16) == FK_LIN) return 0;
+  if (fwd_kind(a, d->dtype == SR_BF16) == FK_BAND) return d->H * (4 / (d->Cout / 32));  // rows x pixel waves
   int rows, nt;
   fwd_epi_geom(fwd_kind(a, d->dtype == SR_BF16), &rows, &nt);
   const int HW = d->H * d->W;
@@ -2890,6 +3283,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   switch (fwd_kind(fwd_shape(d), bf)) {
     case FK_LIN: return "conv3x3_lin_kernel";
     case FK_HALO: return "conv3x3_fwd_halo_kernel";
+    case FK_BAND: return "conv3x3_fwd_band_kernel";
     case FK_BIG: {
       if (g_variant == 2) return "conv3x3_fwd_big_kernel";
       return fwd_use_pph(fwd_shape(d)) ? "conv3x3_fwd_pph_kernel" : "conv3x3_fwd_pp_kernel";
@@ -2911,9 +3305,17 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 33)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 39)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-33: schedule A/B switches)");
   g_variant = variant;
+  return SR_OK;
+}
+
+// Diagnostics: the band kernel writes 16 clock values per block (wave 0: start, weights loaded,
+// end, rows, cycles summed over rows in the row wait / barrier / MFMA / epilogue phases, then
+// LDS zeroed, weight loads issued) into buf while it is set; null turns it off.
+int sr_conv3x3_set_stamps(void* buf) {
+  g_stamps = (unsigned long long*)buf;
   return SR_OK;
 }
 

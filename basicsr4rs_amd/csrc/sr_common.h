@@ -95,3 +95,18 @@ SR_DEV float act_apply(float v, int act, float slope) {
   if (act == 3) return gelu_exact(v);
   return v;
 }
+// the same over 8 values with one (wave-uniform) branch: a per-value switch costs ~4 scalar
+// branches per value, exposed when a kernel runs one wave per SIMD
+template <int N>
+SR_DEV void act_apply_n(float (&v)[N], int act, float slope) {
+  if (act == 1) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = v[j] > 0.f ? v[j] : 0.f;
+  } else if (act == 2) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * slope;
+  } else if (act == 3) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = gelu_exact(v[j]);
+  }
+}

@@ -206,12 +206,13 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
         if P <= 0:
             raise ValueError(f'conv3x3_fwd: no fused channel sums for this call (N={N} H={H} W={W} cout={cout})')
         parts = torch.empty(N, P, cout, device=y.device, dtype=torch.float32)
+    args = (d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res), _lib.ptr(res2),
+            _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.ptr(aux), _lib.ptr(parts), _lib.stream())
+    keep = (x, wf, bias_g, gate, res, res2, aff_scale, aff_shift, y, aux, parts, kw.get('row_scale'))
     with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * taps * cin * cout_real,
-                     x.element_size() * (M * (cin + cout) + taps * cin * cout)):
-        _lib.check(
-            lib.sr_conv3x3_fwd(d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res),
-                               _lib.ptr(res2), _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.ptr(aux),
-                               _lib.ptr(parts), _lib.stream()))
+                     x.element_size() * (M * (cin + cout) + taps * cin * cout),
+                     relaunch=(lambda a=args, k=keep: lib.sr_conv3x3_fwd(*a)) if ktrace.active() else None):
+        _lib.check(lib.sr_conv3x3_fwd(*args))
     return (y, parts) if colsum else y
 
 
@@ -283,11 +284,18 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
         dw = torch.empty(cout_real, cin_real, kk, kk, device=x.device, dtype=torch.float32)
         db = torch.empty(cout_real, device=x.device, dtype=torch.float32) if need_bias else None
     M = N * H * W
+    args = (d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(dw), _lib.ptr(db), _lib.ptr(kw.get('co_map')),
+            _lib.ptr(kw.get('ci_map')), _lib.stream())
+    if ktrace.active():  # the relaunch closure must not accumulate into the live gradients
+        scratch = (torch.empty_like(dw), torch.empty_like(db) if db is not None else None)
+        rargs = args[:5] + (_lib.ptr(scratch[0]), _lib.ptr(scratch[1])) + args[7:]
+        keep = (dy, x, ws, scratch, kw.get('co_map'), kw.get('ci_map'))
+        relaunch = lambda a=rargs, k=keep: lib.sr_conv3x3_wgrad(*a)  # noqa: E731
+    else:
+        relaunch = None
     with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * kk * kk * cin_real * cout_real,
-                     x.element_size() * M * (cin + cout) + 4 * kk * kk * cin * cout):
-        _lib.check(
-            lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(dw), _lib.ptr(db),
-                                 _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')), _lib.stream()))
+                     x.element_size() * M * (cin + cout) + 4 * kk * kk * cin * cout, relaunch=relaunch):
+        _lib.check(lib.sr_conv3x3_wgrad(*args))
     if tw is not None:
         grad_ready(params[0])
         if need_bias:

@@ -4,17 +4,28 @@ When active, every conv launch records a start/end torch.cuda.Event on the strea
 launched on, with its kernel instantiation name and algorithmic FLOPs / bytes; after a
 synchronize the records give per-kernel average duration and achieved TFLOP/s or GB/s,
 directly comparable with ``rocprofv3 --kernel-trace --stats`` averages for the same names.
+
+A span may also carry a ``relaunch`` closure that re-issues exactly that launch (same
+arguments, buffers kept alive by the closure).  ``time_relaunch(name)`` replays every launch
+of a kernel name recorded by the last trace back to back between two events -- the kernel's
+steady-state average duration without per-launch event packets in between, which is what
+rocprofv3 reports for the same kernel inside the timed graph replays.
 """
 import contextlib
 
 import torch
 
-_STATE = {'active': False, 'records': [], 'pool': []}
+_STATE = {'active': False, 'records': [], 'pool': [], 'relaunch': {}}
+
+
+def active():
+    return _STATE['active']
 
 
 def start():
     _STATE['active'] = True
     _STATE['records'] = []
+    _STATE['relaunch'] = {}
 
 
 def stop():
@@ -39,7 +50,7 @@ def _event():
 
 
 @contextlib.contextmanager
-def span(name, flops=0.0, nbytes=0.0):
+def span(name, flops=0.0, nbytes=0.0, relaunch=None):
     if not _STATE['active']:
         yield
         return
@@ -48,3 +59,31 @@ def span(name, flops=0.0, nbytes=0.0):
     yield
     e.record()
     _STATE['records'].append((name, float(flops), float(nbytes), s, e))
+    if relaunch is not None:
+        _STATE['relaunch'].setdefault(name, []).append(relaunch)
+
+
+def relaunch_count(name):
+    return len(_STATE['relaunch'].get(name, ()))
+
+
+def time_relaunch(name, reps=3):
+    """Average ms per launch of ``name`` re-issued back to back (all launches of the last trace,
+    ``reps`` passes after one warm-up pass), or None when its launches carry no closure."""
+    fns = _STATE['relaunch'].get(name)
+    if not fns:
+        return None
+    for f in fns:
+        f()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        for f in fns:
+            f()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / (reps * len(fns))
+
+
+def clear_relaunch():
+    _STATE['relaunch'] = {}

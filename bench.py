@@ -267,7 +267,14 @@ def main():
         # dominant kernel; its roof from its algorithmic arithmetic intensity against the ridge
         # (frac = achieved / min(P, AI * BW))
         name, st = max(kstats.items(), key=lambda kv: kv[1]['ms'])
-        avg_ms = st['ms'] / st['count']
+        traced_ms = st['ms'] / st['count']
+        # the kernel's steady-state duration: every launch of it from the traced step re-issued back to
+        # back between two events (no per-launch event packets in between; rocprof's view of the same
+        # kernel in the timed replays); falls back to the per-launch events when it has no closure
+        relaunch_ms = ktrace.time_relaunch(name)
+        avg_ms = relaunch_ms if relaunch_ms is not None else traced_ms
+        ktrace.clear_relaunch()
+        st = dict(st, ms=avg_ms * st['count'])
         ai = st['flops'] / st['bytes'] if st['bytes'] > 0 else float('inf')
         ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
         if st['flops'] > 0 and ai >= ridge:
@@ -282,9 +289,13 @@ def main():
                 roof['mfma_tflops'] = round(st['flops'] / (st['ms'] * 1e-3) / 1e12, 1)
         roof.update({'flops_per_launch': st['flops'] / st['count'], 'bytes_per_launch': st['bytes'] / st['count'],
                      'arith_intensity': round(ai, 1), 'ridge': round(ridge, 1)})
-        roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'launches_per_step': st['count'] // traced_steps,
+        roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'avg_launch_us_per_launch_events': round(traced_ms * 1e3, 2),
+                     'launches_per_step': st['count'] // traced_steps,
                      'share_of_step': round(st['ms'] / traced_steps * 1e-3 / (dt / args.steps), 3),
-                     'timing': 'HIP events on the stream of each launch, ' +
+                     'timing': ('HIP events around all launches of this kernel from the traced step re-issued back to '
+                                'back (same arguments and buffers, 3 passes after a warm-up pass, after the timed region); '
+                                if relaunch_ms is not None else 'HIP events on the stream of each launch; ') +
+                               'per-kernel table: events around each launch of ' +
                                ('one eager step before capture (replays run the same kernels)' if use_graph
                                 else 'the last (untimed) warm-up step')})
         tr = _pmc_traffic(args.workload, name)

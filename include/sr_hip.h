@@ -105,6 +105,9 @@ const char* sr_conv3x3_wgrad_kernel_name(const struct sr_conv3x3_wgrad_desc* d);
 /* Kernel-variant selection for A/B tests: 0 = automatic (default), 1 = never use the
  * 256x256 LDS-DMA kernel (all shapes on the 128-row register-staged kernels). */
 int sr_conv3x3_set_variant(int variant);
+/* Diagnostics (not part of the reference interface): per-block clock stamps of the row-band
+ * forward kernel into a device buffer of 16 uint64 per block; NULL turns them off. */
+int sr_conv3x3_set_stamps(void* buf);
 
 /* Weight gradient: dw[co][ci][ky][kx] = scale * sum_pixels dy[p][co'] * x[p + tap][ci]
  * (param layout, fp32, co = perm(co') undoing out_ps), db[co] = scale * sum_p dy[p][co'].

@@ -514,3 +514,77 @@ def test_wgrad_rgb_head_reduce_vs_fp64(cuda, shape, variant):
     dw = dw.cpu().double().reshape(w.shape)
     assert (dw - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize('shape', [(16, 64, 64, 64, 64), (5, 13, 64, 64, 64), (1, 1, 64, 64, 64), (3, 2, 64, 32, 32),
+                                   (2, 24, 128, 64, 32), (2, 9, 128, 32, 64), (4, 7, 64, 32, 64)])
+@pytest.mark.parametrize('epi', ['relu', 'gate_alpha_res', 'gelu_gate_aux', 'res2_rowscale', 'colsum', 'slices'])
+@pytest.mark.parametrize('grid', [36, 35])
+def test_fwd_band_bitwise_equals_halo(cuda, shape, epi, grid):
+    """Row-streaming narrow conv (conv3x3_fwd_band_kernel: persistent bands of image rows, 4-slot
+    LDS row ring, epilogue operands staged by LDS-DMA) against the tile kernel it replaces
+    (variant 34) -- same K order, so bitwise equal -- on every epilogue the nets use, with bands
+    of one row (variant 36: 256 blocks, one row each on small shapes) and long bands crossing image
+    boundaries (variant 35: 64 blocks); colsum partial rows sum to the stored output's channel
+    sums.  The band kernel is opt-in (variants 35-39) until it beats the tile kernel."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(6)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    wf, _, bg = C.prepared(conv.weight, conv.bias, C.ConvSpec(cin, cout), dt)
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    gate = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    res2 = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    kw, ldy, ycoff, xin = {}, cout, 0, x
+    if epi == 'relu':
+        kw = dict(act=_lib.ACT_RELU)
+    elif epi == 'gate_alpha_res':
+        kw = dict(gate=gate, gate_slope=0.2, alpha=0.3, res=res, beta=0.7)
+    elif epi == 'gelu_gate_aux':
+        kw = dict(gate=gate, gate_mode=1, aux=torch.empty(N, H, W, cout, device=cuda, dtype=dt))
+    elif epi == 'res2_rowscale':
+        kw = dict(res=res, res2=res2, beta2=-0.5, row_scale=torch.rand(N, device=cuda) * 2)
+    elif epi == 'slices':
+        xin = torch.randn(N, H, W, cin + 32, device=cuda).to(dt)
+        ldy, ycoff = cout + 24, 16
+        kw = dict(ldx=cin + 32, xcoff=16, act=_lib.ACT_LRELU, slope=0.2)
+    outs = []
+    try:
+        for variant in (grid, 34):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.zeros(N, H, W, ldy, device=cuda, dtype=dt)
+            if variant == grid:
+                name = lib.sr_conv3x3_fwd_kernel_name(C._desc(dt, N, H, W, cin, cin, cout, cout, cout)).decode()
+                assert name == 'conv3x3_fwd_band_kernel', name
+            if epi == 'colsum':
+                has = lib.sr_conv3x3_fwd_colsum_parts(C._desc(dt, N, H, W, cin, cin, cout, cout, cout)) > 0
+                if has:
+                    y, parts = C.conv_fwd_raw(xin, wf, bg, y, N, H, W, cin, cout, cout, colsum=True)
+                else:  # the tile kernel has no fused sums at this H * W
+                    assert variant == 34
+                    y, parts = C.conv_fwd_raw(xin, wf, bg, y, N, H, W, cin, cout, cout), None
+                outs.append((y, parts))
+            else:
+                kk = dict(kw)
+                if 'aux' in kk:
+                    kk['aux'] = torch.zeros_like(kk['aux'])
+                C.conv_fwd_raw(xin, wf, bg, y, N, H, W, cin, cout, cout, ycoff=ycoff, **kk)
+                outs.append((y, kk.get('aux')))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    (y0, e0), (y1, e1) = outs
+    assert torch.equal(y0, y1)
+    if epi == 'gelu_gate_aux':
+        assert torch.equal(e0, e1)
+    if epi == 'colsum':
+        ref = y0.double().sum((1, 2))
+        for parts in (e0, e1):
+            if parts is None:
+                continue
+            got = parts.double().sum(1)
+            assert (got - ref).abs().max().item() <= 1e-5 * y0.double().abs().sum((1, 2)).max().item() + 1e-6
+    if epi == 'slices':
+        assert y0[..., :16].abs().max().item() == 0 and y0[..., 16 + cout:].abs().max().item() == 0
