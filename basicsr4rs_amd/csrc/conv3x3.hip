@@ -1501,8 +1501,16 @@ SR_DEV void vm_wait_ge(int n) {
 }
 SR_DEV void vm_wait_dyn(int n) { vm_wait_ge<0>(n < 0 ? 0 : n); }
 
-template <int CO, int W, int LA, int KH>
+// E (the epilogue, fixed at compile time: at one wave per SIMD every run-time branch of a
+// per-row epilogue is exposed): bits 0-1 act, 2-3 gate (0 none, 1 pre-residual (g > 0 ? 1 :
+// gate_slope), 2 pre-residual GELU'(g), 3 post-residual (g > 0 ? 1 : gate_slope) on output
+// channels gcol0..gcol1), 4 res, 5 res2, 6 aux, 7 colsum, 8 row_scale.
+template <int CO, int W, int LA, int KH, int E>
 __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
+  constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
+  constexpr bool RES = (E & 16) != 0, RES2 = (E & 32) != 0, AUX = (E & 64) != 0, CS = (E & 128) != 0,
+                 RSC = (E & 256) != 0;
+  constexpr int IR = GATE ? 1 : 0, IR2 = IR + (RES ? 1 : 0), NSTG = IR2 + (RES2 ? 1 : 0);
   constexpr int WC = CO / 32;       // waves along output channels (32 each = 2 co tiles)
   constexpr int WP = 4 / WC;        // waves along the row's pixels
   constexpr int PT = W / 16 / WP;   // 16-pixel tiles per wave
@@ -1510,19 +1518,27 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
   constexpr int SLOT = WPAD * 128;
   constexpr int S = LA + 2;         // ring slots: rows s-1 .. s+1 read, s+2 .. s+LA in flight
   constexpr int PPW = W / 8 / 4;    // 1-KB DMA pieces per wave per row
-  constexpr int EPI = 3 * PT * 1024;  // per wave: gate / res / res2 staging of its row pixels
-  // + one all-zero slot: the rows above / below an image (3x3 zero padding in y) read it, so
-  // the MFMA sequence has no branches and the compiler can run the fragment reads ahead
-  __shared__ __attribute__((aligned(16))) char smem[(S + 1) * SLOT + 4 * EPI];
+  constexpr int NG = NSTG * PT;     // staging pieces per wave per row (gate / res / res2)
+  constexpr int NC = (CS ? 2 : 0) + (AUX ? PT : 0);  // stores after the PT output stores
+  constexpr int KROW = NG + PPW + PT + NC;            // vector memory ops per wave per row
+  constexpr int EPI = (NSTG ? NSTG : 1) * PT * 1024;  // per-wave staging
+  constexpr int CIN = 32 * KH;
+  constexpr int WROW = 9 * CIN * 2;  // bytes of one output channel's weights [tap][ci]
+  constexpr int WBYTES = CO * WROW;
+  constexpr int RING = (S + 1) * SLOT + 4 * EPI;
+  // ring + one all-zero slot (the rows above / below an image read it, so the MFMA sequence has
+  // no branches) + staging; the weight image is staged in the same space before the ring starts
+  __shared__ __attribute__((aligned(16))) char smem[RING > WBYTES ? RING : WBYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = w % WC, wp = w / WC;
   const int g = lane >> 4, c16 = lane & 15;
   const int H = a.H;
   const int T = a.N * H;  // output rows
-  const bool stamp = a.stamps && tid == 0;
-  unsigned long long* st = a.stamps ? a.stamps + (size_t)blockIdx.x * 16 : nullptr;
+#ifdef SR_BAND_STAMPS
   const unsigned long long t_start = __builtin_readcyclecounter();
+  unsigned long long ph[4] = {0ull, 0ull, 0ull, 0ull};  // row wait / barrier / MFMA / epilogue
+#endif
   const int G = gridDim.x;
   const int bb = blockIdx.x;
   const int s0 = (int)((int64_t)bb * T / G), s1 = (int)((int64_t)(bb + 1) * T / G);
@@ -1531,35 +1547,15 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
   const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
-  constexpr bool khi = KH == 2;  // Cin 64 (two 32-channel K halves) or 32
-  const int NG = PT * ((a.gate ? 1 : 0) + (a.res ? 1 : 0) + (a.res2 ? 1 : 0));
-  const bool cs_on = a.colsum != nullptr;
-  const int NC = (cs_on ? 2 : 0) + (a.aux ? PT : 0);  // stores after the PT output stores
-  const int KROW = NG + PPW + PT + NC;  // vector memory ops per row
 
-  // zero border columns (pixel rows 0 and W + 1) of every slot, and the zero slot S, once
-  for (int i = tid; i < S * 2 * 8; i += 256) {
-    const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
-    *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
+  // weights: one coalesced LDS-DMA image [co][tap][ci] (1 KB contiguous per wave instruction),
+  // then each wave reads its MFMA fragments from it: co = wc*32 + 8*(c16>>2) + 4*c + (c16&3)
+  // (DIRECT row permutation), K chunk kk*32 + 8*g of every tap
+  for (int p = w; p < WBYTES / 1024; p += 4) {
+    const int e = p * 1024 + lane * 16;
+    const int co = e / WROW, off = e - co * WROW;
+    glds16(wr, smem + p * 1024, (uint32_t)(co * a.ldw * 2 + off));
   }
-  for (int i = tid; i < SLOT / 16; i += 256) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
-  const unsigned long long t_zeroed = __builtin_readcyclecounter();
-  // this wave's weights: co = wc*32 + 8*(c16>>2) + 4*c + (c16&3) (DIRECT row permutation),
-  // K chunk kk*32 + 8*g of every tap
-  u32x4 bw[9][2][2];
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int co = wc * 32 + 8 * (c16 >> 2) + 4 * c + (c16 & 3);
-        const int ci = kk * 32 + 8 * g;
-        const bool v = co < a.Cout && ci < a.Cin;
-        bw[tap][kk][c] = (kk == 0 || khi) ? buf_load16(wr, v ? (uint32_t)((co * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB)
-                                          : u32x4{0u, 0u, 0u, 0u};
-      }
-  const unsigned long long t_wissued = __builtin_readcyclecounter();
   const int nn = wc * 32 + 8 * g;  // this lane's 8 output channels
   float bv[8];
 #pragma unroll
@@ -1569,21 +1565,47 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) { bv[j] = b0[j]; bv[4 + j] = b1[j]; }
   }
-  // weights / bias must be complete before the DMA stream starts, AND the compiler must know it:
-  // a use of every value here makes it wait now instead of emitting vmcnt waits (which would
-  // also drain the in-flight row DMA it cannot see) inside the row loop
+  float rsv = a.alpha;  // RSC: alpha * row_scale of image s0 / H + lane (a band spans < 64 images)
+  if constexpr (RSC) {
+    const int ni = s0 / H + lane;
+    rsv = ni < a.N ? a.alpha * a.row_scale[ni] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
+  asm volatile("" ::"v"(rsv));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  u32x4 bw[9][2][2];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int co = wc * 32 + 8 * (c16 >> 2) + 4 * c + (c16 & 3);
+        bw[tap][kk][c] = kk < KH ? *(const u32x4*)(smem + co * WROW + (tap * CIN + kk * 32 + 8 * g) * 2)
+                                 : u32x4{0u, 0u, 0u, 0u};
+      }
+  // every fragment in registers (and the compiler knows it) before the ring overwrites the image
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int c = 0; c < 2; ++c) asm volatile("" ::"v"(bw[tap][kk][c]));
-#pragma unroll
-  for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // border zeros written
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // zero border columns (pixel rows 0 and W + 1) of every slot, and the zero slot S
+  for (int i = tid; i < S * 2 * 8; i += 256) {
+    const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
+    *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
+  }
+  for (int i = tid; i < SLOT / 16; i += 256) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+#ifdef SR_BAND_STAMPS
   const unsigned long long t_loaded = __builtin_readcyclecounter();
-  unsigned long long ph[4] = {0ull, 0ull, 0ull, 0ull};  // diagnostics: wait / barrier / MFMA / epilogue
+#endif
 
   // DMA of global row q (pixels 1..W of slot q % S); rows outside [0, T) read zeros
   const int lc_lane = lane & 7;
@@ -1599,7 +1621,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
       glds16(xr, slot + (1 + 8 * k) * 128, v ? off : SR_OOB);
     }
   };
-  const bool gok = a.gate_mode != 2 || (nn >= a.gcol0 && nn < a.gcol1);
+  const bool gok = GATE != 3 || (nn >= a.gcol0 && nn < a.gcol1);
   const bool rok = nn < a.rcols;
   auto unpack8 = [](const u32x4& q, float* o) {
 #pragma unroll
@@ -1615,9 +1637,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
       const size_t m = (size_t)q * W + wp * PT * 16 + i * 16 + c16;
-      if (a.gate) glds16(gr, epi + (0 * PT + i) * 1024, qv && gok ? (uint32_t)((m * a.ldg + a.gcoff + nn) * 2) : SR_OOB);
-      if (a.res) glds16(rr, epi + (1 * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr + a.rcoff + nn) * 2) : SR_OOB);
-      if (a.res2) glds16(rr2, epi + (2 * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr2 + a.r2coff + nn) * 2) : SR_OOB);
+      if constexpr (GATE != 0)
+        glds16(gr, epi + i * 1024, qv && gok ? (uint32_t)((m * a.ldg + a.gcoff + nn) * 2) : SR_OOB);
+      if constexpr (RES)
+        glds16(rr, epi + (IR * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr + a.rcoff + nn) * 2) : SR_OOB);
+      if constexpr (RES2)
+        glds16(rr2, epi + (IR2 * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr2 + a.r2coff + nn) * 2) : SR_OOB);
     }
   };
   // prologue: rows s0 - 1 .. s0 + LA - 1 (s0 - 1 first: the oldest), then row s0's staging
@@ -1625,6 +1650,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
     for (int q = s0 - 1; q < s0 + LA; ++q) issue_row(q);
     issue_staging(s0);
   }
+  const int n0 = s0 / H;
 
   // Per row, in issue order: [MFMAs] [epilogue] [staging of row s + 1: NG] [pieces of row
   // s + LA: PPW] [stores: PT + NC].  Vector memory ops complete in issue order, so a wait for
@@ -1632,18 +1658,23 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
   // epilogue, so neither wait below ever covers the stores or the DMA of the row just issued.
 #pragma unroll 1
   for (int s = s0; s < s1; ++s) {
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t0 = __builtin_readcyclecounter();
+#endif
     // rows <= s + 1 landed: the ops issued after row s + 1's pieces may stay in flight
     const int younger = (s + 1 < s0 + LA) ? (s0 + LA - 2 - s) * PPW + NG + (s - s0) * KROW
                                           : (PT + NC) + (LA - 2) * KROW;
-    const unsigned long long t0 = __builtin_readcyclecounter();
     vm_wait_dyn(younger);
+#ifdef SR_BAND_STAMPS
     const unsigned long long t1 = __builtin_readcyclecounter();
+#endif
     // every wave's pieces of row s + 1 are in LDS, and every wave is done with row s - 2,
     // whose slot row s + LA reuses (S = LA + 2)
     pp_barrier();
+#ifdef SR_BAND_STAMPS
     const unsigned long long t2 = __builtin_readcyclecounter();
+#endif
     const int n_img = s / H, y = s - n_img * H;
-    const float rs = a.row_scale ? a.alpha * a.row_scale[n_img] : a.alpha;  // scalar load
 
     f32x4 acc[PT][2];
 #pragma unroll
@@ -1654,13 +1685,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
     const int sl0 = y == 0 ? S : (sl1 == 0 ? S - 1 : sl1 - 1);      // zero slot above an image
     const int sl2 = y == H - 1 ? S : (sl1 == S - 1 ? 0 : sl1 + 1);  // ... and below it
     const char* srows[3] = {smem + sl0 * SLOT, smem + sl1 * SLOT, smem + sl2 * SLOT};
-    // K steps (tap, K half) in order; the fragments of step k + 1 are read while step k's
-    // MFMAs run (double-buffered registers)
+    // K steps (tap, K half) in order.  Fragment reads run FD - 1 K steps ahead of the MFMAs.  They
+    // are inline-asm ds_reads with hand-counted lgkmcnt waits that pass the fragments through (so
+    // no MFMA can be scheduled before its wait): the compiler otherwise sinks every read to just
+    // before its use and exposes the full LDS latency per 2 MFMAs (one wave per SIMD has nothing
+    // else to run).
     constexpr int NK = 9 * KH;
-    // Fragment reads run FD - 1 K steps ahead of the MFMAs.  They are inline-asm ds_reads with
-    // hand-counted lgkmcnt waits that pass the fragments through (so no MFMA can be scheduled
-    // before its wait): the compiler otherwise sinks every read to just before its use and
-    // exposes the full LDS latency per 2 MFMAs (one wave per SIMD has nothing else to run).
     constexpr int FD = 5;
     u32x4 fa[FD][PT];
     uint32_t rbase[3];
@@ -1676,7 +1706,6 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
       }
     };
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(a.tiles_n & 1)) {  // ablation 1: no MFMA section (A/B timing only)
 #pragma unroll
     for (int k = 0; k < FD - 1; ++k) read_k(k, fa[k]);
 #pragma unroll
@@ -1715,24 +1744,23 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) mfma_chunk<bf16_t>(bw[tap][kk][c], f[i], acc[i][c]);
     }
-    }
-    // The compiler interleaves the epilogue's accumulator reads with the last MFMAs and, on the
-    // path around the optional aux store, left too few wait states between the final MFMA and the
-    // read of its result (acc[PT-1][1][3] came out stale).  Fence the MFMA block and pad it.
+    // The compiler interleaves the epilogue's accumulator reads with the last MFMAs and, on a
+    // branchy path, once left too few wait states between the final MFMA and the read of its
+    // result (acc[PT-1][1][3] came out stale).  Fence the MFMA block and pad it.
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-
+#ifdef SR_BAND_STAMPS
     const unsigned long long t3 = __builtin_readcyclecounter();
+#endif
+
     // this row's staging landed (issued before row s + LA - 1's pieces and row s - 1's stores)
-    if (NG) vm_wait_dyn(s == s0 ? 0 : PPW + PT + NC);
-    if (a.tiles_n & 2) {  // ablation 2: no epilogue; keep the op count (dummy stores)
-      issue_staging(s + 1);
-      issue_row(s + LA);
-#pragma unroll
-      for (int i = 0; i < PT + NC; ++i) glds16(xr, epi, SR_OOB);  // (NC dummies: any count works)
-      continue;
+    if constexpr (NG > 0) {
+      if (s == s0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + PT + NC) : "memory");
     }
+    float rs = a.alpha;
+    if constexpr (RSC) rs = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, rsv), n_img - n0));
     float cs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) cs[j] = 0.f;
@@ -1742,51 +1770,64 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
-      if (a.aux) {
+      if constexpr (AUX) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) avx[i][j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
       }
-      act_apply_n(v, a.act, a.slope);
-      float gf[8];
-      if (a.gate) unpack8(*(const u32x4*)(epi + (0 * PT + i) * 1024 + lane * 16), gf);
-      if (a.gate && a.gate_mode == 1) {
+      if constexpr (ACT == 1) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
-      } else if (a.gate && a.gate_mode == 0) {
+        for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : 0.f;
+      } else if constexpr (ACT == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.slope;
+      } else if constexpr (ACT == 3) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = gelu_exact(v[j]);
+      }
+      float gf[8];
+      if constexpr (GATE != 0) unpack8(*(const u32x4*)(epi + i * 1024 + lane * 16), gf);
+      if constexpr (GATE == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+      } else if constexpr (GATE == 2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= rs;
-      if (a.res && rok) {
+      if constexpr (RES) {
         float rf[8];
-        unpack8(*(const u32x4*)(epi + (1 * PT + i) * 1024 + lane * 16), rf);
+        unpack8(*(const u32x4*)(epi + (IR * PT + i) * 1024 + lane * 16), rf);
+        if (rok) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = a.beta * rf[j] + v[j];
+          for (int j = 0; j < 8; ++j) v[j] = a.beta * rf[j] + v[j];
+        }
       }
-      if (a.res2 && rok) {
+      if constexpr (RES2) {
         float rf[8];
-        unpack8(*(const u32x4*)(epi + (2 * PT + i) * 1024 + lane * 16), rf);
+        unpack8(*(const u32x4*)(epi + (IR2 * PT + i) * 1024 + lane * 16), rf);
+        if (rok) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rf[j] + v[j];
+          for (int j = 0; j < 8; ++j) v[j] = a.beta2 * rf[j] + v[j];
+        }
       }
-      if (a.gate && a.gate_mode == 2 && gok) {
+      if constexpr (GATE == 3) {
+        if (gok) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+          for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+        }
       }
-      u32x4& o = ov[i];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
-      if (cs_on) {
+      for (int j = 0; j < 4; ++j) ov[i][j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+      if constexpr (CS) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          cs[2 * j] += bf16_to_f32(o[j] & 0xffff);
-          cs[2 * j + 1] += bf16_to_f32(o[j] >> 16);
+          cs[2 * j] += bf16_to_f32(ov[i][j] & 0xffff);
+          cs[2 * j + 1] += bf16_to_f32(ov[i][j] >> 16);
         }
       }
     }
-    // the staging buffer's reads above are consumed (values in registers) before the DMA refills it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (NG > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read before refill
     issue_staging(s + 1);
     issue_row(s + LA);
 #pragma unroll
@@ -1794,14 +1835,14 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
       const size_t m = (size_t)s * W + wp * PT * 16 + i * 16 + c16;
       *(u32x4*)((bf16_t*)a.y + m * a.ldy + a.ycoff + nn) = ov[i];
     }
-    if (a.aux) {
+    if constexpr (AUX) {
 #pragma unroll
       for (int i = 0; i < PT; ++i) {
         const size_t m = (size_t)s * W + wp * PT * 16 + i * 16 + c16;
         *(u32x4*)((bf16_t*)a.aux + m * a.ldy + a.ycoff + nn) = avx[i];
       }
     }
-    if (cs_on) {
+    if constexpr (CS) {
       // the 16 lanes of a g group hold the same 8 channels: fixed-order butterfly, then lane
       // c16 == 0 writes partial row s * WP + wp (P = H * WP rows per image)
 #pragma unroll
@@ -1809,20 +1850,22 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
       float* dstp = a.colsum + ((size_t)s * WP + wp) * a.Cout + nn;
-      // exactly two vector store instructions per wave (lanes masked): the NC of the count above
+      // exactly two vector store instructions per wave (lanes masked): counted in NC
       if (c16 == 0) *(f32x4*)dstp = f32x4{cs[0], cs[1], cs[2], cs[3]};
       if (c16 == 0) *(f32x4*)(dstp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
     }
-    if (a.stamps) {
-      const unsigned long long t4 = __builtin_readcyclecounter();
-      ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
-    }
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t4 = __builtin_readcyclecounter();
+    ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
+#endif
   }
-  if (stamp) {
+#ifdef SR_BAND_STAMPS
+  if (a.stamps && tid == 0) {
+    unsigned long long* st = a.stamps + (size_t)blockIdx.x * 16;
     st[0] = t_start; st[1] = t_loaded; st[2] = __builtin_readcyclecounter(); st[3] = s1 - s0;
     st[4] = ph[0]; st[5] = ph[1]; st[6] = ph[2]; st[7] = ph[3];
-    st[8] = t_zeroed; st[9] = t_wissued;
   }
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing row pieces (zeros past T) land before exit
 }
 
@@ -3004,10 +3047,29 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
 enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN, FK_BAND };
 // row-streaming narrow conv: bf16 3x3, Cin 32 / 64, Cout 32 / 64 exactly, W 64 / 128, plain or
 // channel-slice NHWC in and out (variant 34: the tile kernel instead, for A/B)
+// the band kernel's compile-time epilogue code (see conv3x3_fwd_band_kernel) for these arguments,
+// -1 when it is not one of the instantiated ones
+int band_epi(const FwdArgs& a, int grid) {
+  int gate = 0;
+  if (a.gate) gate = a.gate_mode == 2 ? 3 : (a.gate_mode == 1 ? 2 : 1);
+  const int e = a.act | (gate << 2) | (a.res ? 16 : 0) | (a.res2 ? 32 : 0) | (a.aux ? 64 : 0) |
+                (a.colsum ? 128 : 0) | (a.row_scale ? 256 : 0);
+  if (a.row_scale) {  // the images of one band fit one wave's lanes
+    const int rows = (a.N * a.H + grid - 1) / grid;
+    if ((rows + a.H - 1) / a.H + 1 > 64) return -1;
+  }
+  switch (e) {
+    case 0: case 1: case 2: case 4: case 16: case 20: case 48: case 72: case 128: case 304: return e;
+    default: return -1;
+  }
+}
 bool fwd_use_band(const FwdArgs& a, bool bf) {
-  return bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
-         (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && (a.Cout == 32 || a.Cout == 64) &&
-         a.Cout_real == a.Cout && g_variant >= 35 && g_variant <= 39;  // opt-in: slower than the tile kernel so far
+  if (!(bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
+        (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && (a.Cout == 32 || a.Cout == 64) &&
+        a.Cout_real == a.Cout && g_variant != 1 && g_variant != 34))  // 34: the tile kernel (A/B, tests)
+    return false;
+  const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
+  return band_epi(a, rows < gmax ? rows : gmax) >= 0;
 }
 // short-K 1x1 convs (linears): token tile staged once, all output channels swept
 bool fwd_use_lin(const FwdArgs& a, bool bf) {
@@ -3044,24 +3106,32 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
       return hipGetLastError();
     }
     case FK_BAND: {
-      // 2 blocks per CU (1 for W 128: its ring + staging take 91-116 KB of LDS); variant 35 forces
-      // 64 blocks (long bands: ring wrap-around and image crossings inside a band, for tests)
+      // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64
+      // blocks (long bands: ring wrap-around and image crossings inside a band, for tests)
       const int rows = a.N * a.H;
-      const int gmax = (g_variant == 35 || g_variant >= 37) ? 64 : 256;  // one block per CU (1 wave / SIMD)
+      const int gmax = g_variant == 35 ? 64 : 256;
       FwdArgs ab = a;
-      ab.tiles_n = g_variant >= 36 ? g_variant - 36 : 0;  // band ablations (36 + code, 37+ on 64 blocks)
       ab.stamps = g_stamps;
       const dim3 grid(rows < gmax ? rows : gmax);
+      const int e = band_epi(a, grid.x);
+#define SR_BAND_E(CO_, W_, LA_, KH_, E_) \
+  case E_: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<CO_, W_, LA_, KH_, E_>), grid, dim3(256), 0, s, ab); break;
 #define SR_BAND(CO_, W_, LA_, KH_) \
   if (a.Cout == CO_ && a.W == W_ && a.Cin == 32 * KH_) { \
-    hipLaunchKernelGGL((conv3x3_fwd_band_kernel<CO_, W_, LA_, KH_>), grid, dim3(256), 0, s, ab); \
+    switch (e) { \
+      SR_BAND_E(CO_, W_, LA_, KH_, 0) SR_BAND_E(CO_, W_, LA_, KH_, 1) SR_BAND_E(CO_, W_, LA_, KH_, 2) \
+      SR_BAND_E(CO_, W_, LA_, KH_, 4) SR_BAND_E(CO_, W_, LA_, KH_, 16) SR_BAND_E(CO_, W_, LA_, KH_, 20) \
+      SR_BAND_E(CO_, W_, LA_, KH_, 48) SR_BAND_E(CO_, W_, LA_, KH_, 72) SR_BAND_E(CO_, W_, LA_, KH_, 128) \
+      SR_BAND_E(CO_, W_, LA_, KH_, 304) \
+      default: return hipErrorInvalidValue; \
+    } \
     return hipGetLastError(); \
   }
       SR_BAND(64, 64, 5, 2) SR_BAND(64, 64, 5, 1) SR_BAND(32, 64, 5, 2) SR_BAND(32, 64, 5, 1)
       SR_BAND(64, 128, 3, 2) SR_BAND(64, 128, 3, 1) SR_BAND(32, 128, 4, 2) SR_BAND(32, 128, 4, 1)
 #undef SR_BAND
+#undef SR_BAND_E
       return hipErrorInvalidValue;
-      return hipGetLastError();
     }
     case FK_HALO: return launch_fwd_halo(a, s);
     case FK_BIG: return launch_fwd_big(a, s);
@@ -3305,7 +3375,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 39)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 36)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-33: schedule A/B switches)");
   g_variant = variant;
   return SR_OK;

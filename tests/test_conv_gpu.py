@@ -526,7 +526,7 @@ def test_fwd_band_bitwise_equals_halo(cuda, shape, epi, grid):
     (variant 34) -- same K order, so bitwise equal -- on every epilogue the nets use, with bands
     of one row (variant 36: 256 blocks, one row each on small shapes) and long bands crossing image
     boundaries (variant 35: 64 blocks); colsum partial rows sum to the stored output's channel
-    sums.  The band kernel is opt-in (variants 35-39) until it beats the tile kernel."""
+    sums."""
     N, H, W, cin, cout = shape
     torch.manual_seed(6)
     dt = torch.bfloat16

@@ -41,7 +41,7 @@ def main():
         out = dict(v=v, blocks=int(s.shape[0]), rows_per_block=float(rows.mean()),
                    load_cyc=float((s[:, 1] - s[:, 0]).mean()), zero_cyc=float((s[:, 8] - s[:, 0]).mean()),
                    wissue_cyc=float((s[:, 9] - s[:, 8]).mean()), wwait_cyc=float((s[:, 1] - s[:, 9]).mean()), loop_cyc=float((s[:, 2] - s[:, 1]).mean()),
-                   start_spread_cyc=float(s[:, 0].max() - s[:, 0].min()),
+                   loop_per_row=float(((s[:, 2] - s[:, 1]) / rows).mean()),
                    per_row=dict(wait=float((s[:, 4] / rows).mean()), barrier=float((s[:, 5] / rows).mean()),
                                 mfma=float((s[:, 6] / rows).mean()), epilogue=float((s[:, 7] / rows).mean())))
         print(json.dumps(out), flush=True)
