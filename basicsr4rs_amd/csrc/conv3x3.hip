@@ -1488,18 +1488,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
 // memory ops younger than row s + 1's pieces is known in closed form (prologue rows, then the
 // steady state (PT + NC) + (LA - 2) * ops-per-row) and waited with a run-time vmcnt.
 // ------------------------------------------------------------------------------------
-// s_waitcnt vmcnt(n) for a run-time n (wave-uniform): the immediate comes from a jump table;
-// n > 63 waits for vmcnt(63), which only waits longer.
-template <int K>
-SR_DEV void vm_wait_ge(int n) {
-  if constexpr (K >= 63) {
-    asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+// s_waitcnt vmcnt(n) for a run-time n (wave-uniform): the immediate is chosen by a binary
+// search over 0..63 (6 scalar branches; a linear compare chain cost ~40 cycles per step at one
+// wave per SIMD); n > 63 waits for vmcnt(63), which only waits longer.
+template <int LO, int HI>
+SR_DEV void vm_wait_bs(int n) {
+  if constexpr (LO == HI) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LO) : "memory");
   } else {
-    if (n <= K) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
-    else vm_wait_ge<K + 1>(n);
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= MID) vm_wait_bs<LO, MID>(n);
+    else vm_wait_bs<MID + 1, HI>(n);
   }
 }
-SR_DEV void vm_wait_dyn(int n) { vm_wait_ge<0>(n < 0 ? 0 : n); }
+SR_DEV void vm_wait_dyn(int n) { vm_wait_bs<0, 63>(n < 0 ? 0 : (n > 63 ? 63 : n)); }
 
 // E (the epilogue, fixed at compile time: at one wave per SIMD every run-time branch of a
 // per-row epilogue is exposed): bits 0-1 act, 2-3 gate (0 none, 1 pre-residual (g > 0 ? 1 :
@@ -1662,9 +1664,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
     const unsigned long long t0 = __builtin_readcyclecounter();
 #endif
     // rows <= s + 1 landed: the ops issued after row s + 1's pieces may stay in flight
-    const int younger = (s + 1 < s0 + LA) ? (s0 + LA - 2 - s) * PPW + NG + (s - s0) * KROW
-                                          : (PT + NC) + (LA - 2) * KROW;
-    vm_wait_dyn(younger);
+    if (s + 1 >= s0 + LA) {
+      constexpr int STEADY = (PT + NC) + (LA - 2) * KROW;
+      static_assert(STEADY <= 63, "band: too many vector memory ops in flight for vmcnt");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEADY) : "memory");
+    } else {
+      vm_wait_dyn((s0 + LA - 2 - s) * PPW + NG + (s - s0) * KROW);
+    }
 #ifdef SR_BAND_STAMPS
     const unsigned long long t1 = __builtin_readcyclecounter();
 #endif
@@ -1889,6 +1895,7 @@ struct WgArgs {
   int taps, tap0;  // 9 / 0 for 3x3, 1 / 4 for 1x1 (linear)
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   FastDiv fd_W, fd_H, fd_cps;
+  unsigned long long* stamps;  // diagnostics (SR_BAND_STAMPS builds): per-block phase cycles
 };
 
 // 32-byte-block XOR swizzle for the [K rows][256 B] tr-read image (tools/lds_banks.py):
@@ -2748,6 +2755,246 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
   }
 }
 
+// Row-streaming form of the halo wgrad (whole image rows per split, W % 64 == 0): the block walks
+// each 64-px column segment of its rows top to bottom, so a K-step loads ONE new x halo row (66 px
+// of a 16-ci tile) into a ring instead of three rows; the rows above / below an image read a zero
+// slot (x read ~once per pass instead of ~3x).  Wave w owns ci tile w and all co tiles (9 x CO_T
+// accumulator tiles, pinned to AGPRs).  (An 8-wave form, two waves per SIMD over halves of the co
+// tiles, ran its two groups in lock-step between the per-step barriers and was slower.)  The
+// first step of a segment loads its three rows itself, after the previous segment's last step
+// (its slots may still be read), so a block has nseg - 1 one-step bubbles.
+template <int CO_T>
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
+  constexpr int D = 2;              // steps in flight
+  constexpr int CW = CO_T;  // co tiles per wave
+  constexpr int RS = 3 * 1024;      // one halo row of one 16-ci tile: 96 rows x 32 B (66 used)
+  constexpr int RSL = D + 2;        // ring slots: rows q-1 .. q+1 read, D - 1 more in flight
+  constexpr int RING = (RSL + 1) * RS;  // + the zero slot, per ci tile
+  constexpr int DYB = CO_T * 2048;  // dy image: CO_T tiles x 64 rows x 32 B
+  constexpr int DYS = DYB + 1024;   // + 1 KB target for padding DMAs
+  constexpr int DYI = (CO_T * 2 + 3) / 4;  // dy DMAs per wave
+  __shared__ __attribute__((aligned(16))) char smem[4 * RING + D * DYS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = w;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = (int)b / a.tiles_ci;
+  const int chunk = (int)b - split * a.tiles_ci;
+  const int ci0 = chunk * 64;
+  const int rows_total = a.N * a.H;
+  const int rps = a.kper / a.W;  // image rows per split
+  const int r0 = split * rps, r1 = min(rows_total, r0 + rps);
+  const int nrows = r1 - r0, nseg = a.W >> 6, nk = nrows * nseg;
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const int sh = a.in_up > 1 ? 1 : 0;  // in_up is 1 or 2 here
+  const int Hs = a.H >> sh, Ws = a.W >> sh;
+  char* ring = smem + wl * RING;
+  char* dys = smem + 4 * RING;
+  auto slot = [](int q) { return (q + RSL) % RSL; };  // q >= -1
+  constexpr bool xdma = true;  // every wave loads its ci tile's x rows and some dy
+
+  // this lane's halo pixels of its 3 DMAs per row: physical row 32i + (lane >> 1) holds pixel
+  // hrow(.) (x0 - 1 + that), channel half lane & 1
+  int hpx[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int hr = hrow(32 * i + (lane >> 1));
+    hpx[i] = hr < 66 ? hr : -100000;
+  }
+  const int cil = ci0 + wl * 16 + (lane & 1) * 8;
+  const bool civ = cil < a.Cin;
+  if (xdma)
+    for (int i = lane; i < RS / 16; i += 64) *(u32x4*)(ring + RSL * RS + i * 16) = u32x4{0u, 0u, 0u, 0u};
+
+  f32x4 acc[9][CW], accb[CW];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < CW; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < CW; ++c) accb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int ct0 = 0, ncw = CW;
+  const bool do_bias = a.wsb != nullptr && chunk == 0 && wl == 0;
+
+  // x halo row q (global image row; outside [0, rows_total) -> zeros), column segment seg
+  auto issue_row = [&](int q, int seg) {
+    const bool qv = q >= 0 && q < rows_total;
+    const int n = qv ? (int)fdiv((uint32_t)q, a.fd_H) : 0;
+    const int yy = q - n * a.H;
+    char* dst = ring + slot(q) * RS;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int xx = seg * 64 - 1 + hpx[i];
+      const bool v = qv && civ && (unsigned)xx < (unsigned)a.W;
+      const uint32_t off = (uint32_t)((((n * Hs + (yy >> sh)) * Ws + (xx >> sh)) * a.ldx + a.xcoff + cil) * 2);
+      glds16(xr, dst + i * 1024, v ? off : SR_OOB);
+    }
+  };
+  // step j = (segment j / nrows, row r0 + j % nrows); the first step of a segment loads its
+  // three rows and is issued after the previous segment's last step (whose slots it reuses)
+  auto first = [&](int j) { return j % nrows == 0; };
+  auto nops = [&](int j) { return DYI + (xdma ? (first(j) ? 9 : 3) : 0); };
+  auto issue_iter = [&](int j) { const int f = j - j % nrows - 1, e = j - D; return f > e ? f : e; };
+  auto issue = [&](int j) {
+    const int seg = j / nrows, q = r0 + (j - seg * nrows);
+    if (xdma) {
+      if (first(j)) {
+        issue_row(q - 1, seg);
+        issue_row(q, seg);
+      }
+      issue_row(q + 1, seg);
+    }
+    const int p0s = q * a.W + seg * 64;
+    char* st = dys + (j % D) * DYS;
+#pragma unroll
+    for (int i = 0; i < DYI; ++i) {
+      const int k = w + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
+      char* dst = st + DYB;
+      uint32_t off = SR_OOB;
+      if (k < CO_T * 2) {
+        const int pr = hrow((k & 1) * 32 + (lane >> 1));
+        const int co = (k >> 1) * 16 + (lane & 1) * 8;
+        dst = st + k * 1024;
+        if (co < a.Cout) off = (uint32_t)(((p0s + pr) * a.ldy + a.ycoff + co) * 2);
+      }
+      glds16(dyr, dst, off);
+    }
+  };
+
+  const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  auto tr2 = [&](const char* img, int r0_) -> s16x8 {  // rows r0 + tq (K 0..3), r0 + 4 + tq (K 4..7)
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0_ + tq) * 32 + tp * 8));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0_ + 4 + tq) * 32 + tp * 8));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  auto compute = [&](int j) {
+    const int q = r0 + j % nrows;
+    const int y = q - (int)fdiv((uint32_t)q, a.fd_H) * a.H;
+    const char* rows3[3] = {ring + (y == 0 ? RSL : slot(q - 1)) * RS, ring + slot(q) * RS,
+                            ring + (y == a.H - 1 ? RSL : slot(q + 1)) * RS};
+    const char* ds = dys + (j % D) * DYS + ct0 * 2048;
+    // Fragment reads (per K half: this wave's dy tiles, then the 9 taps' x tiles) run LA reads
+    // ahead of the MFMA group (one tap x CW co tiles) that needs them, in program order fixed by
+    // scheduling barriers (the compiler otherwise sinks each read to just before its MFMAs); at
+    // most ~2 (LA + 1) reads are in flight, within what lgkmcnt counts, so its waits stay exact.
+    constexpr int NR = CW + 9, LA = 3;
+    s16x8 fr[2 * NR];
+    auto rd = [&](int r) {
+      const int kk = r / NR, i = r - kk * NR;
+      fr[r] = i < CW ? tr2(ds + i * 2048, kk * 32 + 8 * g) : tr2(rows3[(i - CW) / 3], ((i - CW) % 3) + kk * 32 + 8 * g);
+    };
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int need = kk * NR + CW + t;
+        // reads not yet issued up to need + LA (the previous group issued up to its need + LA)
+        const int lo = (kk == 0 && t == 0) ? 0 : (t > 0 ? need + LA : NR + LA);
+#pragma unroll
+        for (int r = 0; r < 2 * NR; ++r)
+          if (r >= lo && r <= need + LA) rd(r);
+        // accumulators pinned to AGPRs (inline asm): with this many of them the compiler
+        // otherwise moves every one between AGPRs and VGPRs once per step
+#pragma unroll
+        for (int c = 0; c < CW; ++c)
+          if (CW == 1 || c < ncw)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[t][c]) : "v"(fr[kk * NR + c]), "v"(fr[need]));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (do_bias) {  // builtin: the compiler pads the VALU write of `ones` before its read
+#pragma unroll
+        for (int c = 0; c < CW; ++c)
+          if (c < ncw) accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kk * NR + c], ones, accb[c], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+#ifdef SR_BAND_STAMPS
+  unsigned long long ph[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
+  const unsigned long long t_start = __builtin_readcyclecounter();
+#endif
+  __syncthreads();  // zero slots written
+  int next = 0;  // steps issued so far, in step order (issue_iter is non-decreasing)
+  while (next < nk && issue_iter(next) < 0) issue(next++);
+  for (int ks = 0; ks < nk; ++ks) {
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t0 = __builtin_readcyclecounter();
+#endif
+    // step ks's DMAs landed; the steps issued after it may stay in flight
+    if (next == ks + D && (ks + 1) % nrows != 0 && (ks + 1) / nrows == (next - 1) / nrows) {
+      // steady state: the D - 1 steps after ks, none of them a segment's first
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (DYI + 3)) : "memory");
+    } else {
+      int younger = 0;
+      for (int j = ks + 1; j < next; ++j) younger += nops(j);
+      vm_wait_dyn(younger);
+    }
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t1 = __builtin_readcyclecounter();
+#endif
+    __builtin_amdgcn_s_barrier();
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t2 = __builtin_readcyclecounter();
+#endif
+    compute(ks);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t3 = __builtin_readcyclecounter();
+#endif
+    __builtin_amdgcn_s_barrier();
+    while (next < nk && issue_iter(next) <= ks) issue(next++);
+#ifdef SR_BAND_STAMPS
+    const unsigned long long t4 = __builtin_readcyclecounter();
+    ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
+#endif
+  }
+#ifdef SR_BAND_STAMPS
+  const unsigned long long t_loop = __builtin_readcyclecounter();
+#endif
+
+  // the last MFMAs' results are read below (inline-asm MFMAs: the hazard wait is ours)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  // slab [split][tap][ci][co] (co fastest): a lane's 4 accumulator rows are 4 consecutive co,
+  // so one 16-B store per (tap, co tile) per lane (a [co][ci] slab takes four 4-B ones)
+  const int c16 = lane & 15;
+  const int ci = ci0 + wl * 16 + c16;
+  if (ci < a.Cin) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float* ws = a.ws + (((size_t)split * 9 + t) * a.Cin + ci) * a.Cout;
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        const int co = (ct0 + c) * 16 + g * 4;
+        if (c < ncw && co < a.Cout) *(f32x4*)(ws + co) = acc[t][c];
+      }
+    }
+  }
+#ifdef SR_BAND_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.stamps && tid == 0) {
+    unsigned long long* st = a.stamps + (size_t)blockIdx.x * 16;
+    st[0] = t_start; st[1] = t_loop; st[2] = __builtin_readcyclecounter(); st[3] = nk;
+    st[4] = ph[0]; st[5] = ph[1]; st[6] = ph[2]; st[7] = ph[3];
+  }
+#endif
+  if (do_bias && c16 == 0) {
+#pragma unroll
+    for (int c = 0; c < CW; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = (ct0 + c) * 16 + g * 4 + r;
+        if (c < ncw && co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
+      }
+  }
+}
+
 // dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co' = GEMM column of co (out_ps
 // permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
@@ -2914,6 +3161,83 @@ __global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, co
     float* d = dw + ((size_t)co * Cin_real + ci4 * 4) * taps + tap;
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = sm[e] * scale + (accumulate ? d[(size_t)e * taps] : 0.f);
+  }
+}
+
+// Slab reduction for the row-streaming wgrad's [S][taps][Cin][Cout] slab: 64 (tap, ci, 4 co)
+// groups per 1024-thread block, 16-B loads coalesced along co, the 16 waves take splits
+// k = wave (mod 16), fixed-order LDS combine (deterministic); bias blocks as wgrad_reduce4_kernel.
+__global__ __launch_bounds__(1024) void wgrad_reduce_tr_kernel(const float* ws, const float* wsb, float* dw, float* db,
+                                                               int S, int Cout, int Cin, int Cout_real, int Cin_real,
+                                                               int taps, const int* co_map, const int* ci_map,
+                                                               float scale, int wblocks, int accumulate) {
+  __shared__ f32x4 red[16][64];
+  const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if ((int)blockIdx.x >= wblocks) {  // bias
+    const int c = ((int)blockIdx.x - wblocks) * 64 + t;
+    float sb = 0.f;
+    if (c < Cout_real) {
+      const int cop = co_map ? co_map[c] : c;
+      for (int k = wv; k < S; k += 16) sb += wsb[(size_t)k * Cout + cop];
+    }
+    red[wv][t] = f32x4{sb, 0.f, 0.f, 0.f};
+    __syncthreads();
+    if (wv == 0 && c < Cout_real) {
+      float sm = red[0][t][0];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) sm += red[k][t][0];
+      db[c] = sm * scale + (accumulate ? db[c] : 0.f);
+    }
+    return;
+  }
+  const int64_t i = (int64_t)blockIdx.x * 64 + t;
+  const int c4n = (Cout_real + 3) >> 2;
+  const int64_t total = (int64_t)taps * Cin_real * c4n;
+  int co4 = 0, ci = 0, tap = 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < total) {
+    co4 = (int)(i % c4n);
+    const int64_t t2 = i / c4n;
+    ci = (int)(t2 % Cin_real);
+    tap = (int)(t2 / Cin_real);
+    const int cip = ci_map ? ci_map[ci] : ci;
+    const size_t stride = (size_t)taps * Cin * Cout;
+    const float* row = ws + ((size_t)tap * Cin + cip) * Cout;
+    if (co_map) {  // GEMM columns of the 4 parameter channels: gathered loads
+      int cop[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cop[e] = co4 * 4 + e < Cout_real ? co_map[co4 * 4 + e] : 0;
+      for (int k = wv; k < S; k += 16) {
+        const float* sk = row + (size_t)k * stride;
+        acc += f32x4{sk[cop[0]], sk[cop[1]], sk[cop[2]], sk[cop[3]]};
+      }
+    } else {
+      const float* src = row + co4 * 4;
+      int k = wv;
+      for (; k + 48 < S; k += 64) {
+        const f32x4 v0 = *(const f32x4*)(src + (size_t)k * stride);
+        const f32x4 v1 = *(const f32x4*)(src + (size_t)(k + 16) * stride);
+        const f32x4 v2 = *(const f32x4*)(src + (size_t)(k + 32) * stride);
+        const f32x4 v3 = *(const f32x4*)(src + (size_t)(k + 48) * stride);
+        acc += v0; acc += v1; acc += v2; acc += v3;
+      }
+      for (; k < S; k += 16) acc += *(const f32x4*)(src + (size_t)k * stride);
+    }
+  }
+  red[wv][t] = acc;
+  __syncthreads();
+  if (wv == 0 && i < total) {
+    f32x4 sm = red[0][t];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) sm += red[k][t];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = co4 * 4 + e;
+      if (co < Cout_real) {
+        float* d = dw + ((size_t)co * Cin_real + ci) * taps + tap;
+        *d = sm[e] * scale + (accumulate ? *d : 0.f);
+      }
+    }
   }
 }
 
@@ -3206,6 +3530,8 @@ bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
 
+// the row-streaming form of it (variant 37: the tile-row form, for A/B)
+bool wg_use_ring() { return g_variant != 37; }
 // All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2.
 bool wg_use_halo(const sr_conv3x3_wgrad_desc* d) {
   return d->dtype == SR_BF16 && d->ksize != 1 && d->Cout <= 64 && d->W % 64 == 0 && d->in_up <= 2 && d->out_ps == 0 &&
@@ -3226,6 +3552,13 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     const int maxS = M / 512 > 1 ? M / 512 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
+    if (wg_use_ring()) {  // whole image rows per split
+      const int rows = d->N * d->H;
+      const int rps = (rows + S - 1) / S;
+      *splits = (rows + rps - 1) / rps;
+      *kper = rps * d->W;
+      return;
+    }
     int kp = (M + S - 1) / S;
     kp = (kp + 63) / 64 * 64;
     *splits = (M + kp - 1) / kp;
@@ -3366,7 +3699,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
 }
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
-  if (wg_use_halo(d)) return "conv3x3_wgrad_halo_kernel";
+  if (wg_use_halo(d)) return wg_use_ring() ? "conv3x3_wgrad_ring_kernel" : "conv3x3_wgrad_halo_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
@@ -3375,7 +3708,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 36)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 37)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-33: schedule A/B switches)");
   g_variant = variant;
   return SR_OK;
@@ -3434,12 +3767,18 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   a.fd_cps = make_fastdiv(cps);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
+  a.stamps = g_stamps;
   if (wg_use_halo(d)) {
     a.tiles_co = 1;
     a.tiles_ci = (a.Cin + 63) / 64;
     const int ct = (a.Cout + 15) / 16;
     const dim3 grid(S * a.tiles_ci);
-    if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<1>, grid, dim3(256), 0, s, a);
+    if (wg_use_ring()) {
+      if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<1>, grid, dim3(256), 0, s, a);
+      else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<2>, grid, dim3(256), 0, s, a);
+      else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<3>, grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<4>, grid, dim3(256), 0, s, a);
+    } else if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<1>, grid, dim3(256), 0, s, a);
     else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<2>, grid, dim3(256), 0, s, a);
     else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<3>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<4>, grid, dim3(256), 0, s, a);
@@ -3461,7 +3800,14 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t work = total > Cout_real ? total : Cout_real;
-  if (Cin_real % 4 == 0) {
+  if (wg_use_halo(d) && wg_use_ring()) {
+    const int64_t work4 = (int64_t)taps * Cin_real * ((Cout_real + 3) / 4);
+    const int wblocks = (int)((work4 + 63) / 64);
+    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_reduce_tr_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s,
+                       (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, taps,
+                       co_map, ci_map, d->scale, wblocks, d->accumulate);
+  } else if (Cin_real % 4 == 0) {
     const int64_t work4 = (int64_t)taps * Cout_real * (Cin_real / 4);
     const int wblocks = (int)((work4 + 63) / 64);
     const int bblocks = db ? (Cout_real + 63) / 64 : 0;

@@ -244,11 +244,14 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
 
 
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
-                                   (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1)])
+                                   (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
+                                   (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
 def test_wgrad_halo_vs_fp64(cuda, shape):
-    """All-taps halo wgrad (Cout <= 64, W % 64 == 0): channel slices of wider buffers (ldx,
-    xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather (in_up = 2), ragged
-    last split, against an fp64 CPU reference on the same bf16 operands."""
+    """All-taps halo wgrad (Cout <= 64, W % 64 == 0), row-streaming form: channel slices of
+    wider buffers (ldx, xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather
+    (in_up = 2), splits that cross image boundaries (rows per split not dividing H), several
+    64-px column segments per row, ragged last split, against an fp64 CPU reference on the same
+    bf16 operands."""
     N, H, W, cin, cout, up = shape
     torch.manual_seed(9)
     dt = torch.bfloat16
@@ -263,6 +266,12 @@ def test_wgrad_halo_vs_fp64(cuda, shape):
     w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
     b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
     F.conv2d(xd, w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W, d.ksize, d.in_up = _lib.dtype_code(dt), N, H, W, 3, up
+    d.Cin = d.Cin_real = cin
+    d.Cout = d.Cout_real = cout
+    d.ldx, d.xcoff, d.ldy, d.ycoff = cin + 24, 8, cout + 16, 16
+    assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_ring_kernel'
     dw, db = C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
                               xcoff=8, ldy=cout + 16, ycoff=16, in_up=up)
     torch.cuda.synchronize()
