@@ -1087,9 +1087,17 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // channel 8(r/4) + 4t + r%4) and stores 16 B directly, with the fused epilogue (bias,
 // activation, pre-activation side output, gate, alpha, residuals) in registers.
 // ------------------------------------------------------------------------------------
-template <int MT, int MAXCG>
+// E >= 0: the epilogue fixed at compile time (bits 0-1 act, 2-3 gate 0 none / 1 pre-residual
+// (g > 0 ? 1 : gate_slope) / 2 pre-residual GELU'(g) / 3 post-residual on gcol0..gcol1, 4 res,
+// 5 res2, 6 aux, 7 row_scale, uniform per block: H*W % MT == 0): its operand loads for a pass are
+// issued before the pass's MFMAs, so they land under them; E = -1: run-time flags, loads next to
+// their use (every combination).
+template <int MT, int MAXCG, int NPASS, int E>
 __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
   constexpr int NMT = MT / 16;  // token tiles per wave (every wave covers all MT tokens)
+  constexpr bool CE = E >= 0;
+  constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
+  constexpr bool RES = (E & 16) != 0, RES2 = (E & 32) != 0, AUX = (E & 64) != 0, RSC = (E & 128) != 0;
   __shared__ __attribute__((aligned(16))) char smem[MAXCG * MT * 128];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1118,8 +1126,19 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
   const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+  // output descriptors sized to the output (a lane past it stores at SR_OOB = 2^31, which must
+  // fall outside the descriptor to be dropped)
+  const size_t ybytes = (size_t)a.M * a.ldy * 2;
+  const uint32_t yb = ybytes < 0x80000000ull ? (uint32_t)ybytes : 0x7fffffffu;
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, yb);
+  const __amdgpu_buffer_rsrc_t ar = make_rsrc(a.aux, a.aux ? yb : 0u);
+  // compile-time epilogue: the block's row scale (all MT tokens in one image)
+  float alpha_blk = a.alpha;
+  if constexpr (CE && RSC) alpha_blk = a.alpha * a.row_scale[fdiv((uint32_t)m0, a.fd_hw)];
   const int nkk = (K + 31) >> 5;
-  const int npass = (a.Cout + 127) >> 7;
+  constexpr int npass = NPASS;  // (Cout + 127) / 128, fixed so the pass loop unrolls: the
+  // compiler's own vmcnt waits are then exact (a rolled loop waited vmcnt(0) for the W loads,
+  // i.e. for the previous pass's output stores too)
   constexpr int MAXKK = MAXCG * 2;
   // W fragments of a whole pass (all K) in registers, the next pass's loads in flight while the
   // current pass computes: an L2 round trip per K-step would otherwise set the pace
@@ -1135,27 +1154,62 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       wb[kk][1] = buf_load16(wr, (wv1 && kv) ? (uint32_t)(((r0 + 4) * a.ldw + k) * 2) : SR_OOB);
     }
   };
+  // the bias of every pass up front: a load in the epilogue would queue behind the next pass's
+  // W loads (vector memory completes in order), exposing their latency per pass
+  // (buffer loads, no branch: a missing bias or channels past Cout read zeros)
+  const __amdgpu_buffer_rsrc_t br = make_rsrc(a.bias, a.bias ? (uint32_t)a.Cout * 4u : 0u);
+  float bva[NPASS][8];
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
+    const uint32_t n = (uint32_t)(pass * 128 + w * 32 + 8 * g);
+    const u32x4 b0 = buf_load16(br, n * 4u), b1 = buf_load16(br, n * 4u + 16u);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { bva[pass][j] = __uint_as_float(b0[j]); bva[pass][4 + j] = __uint_as_float(b1[j]); }
+  }
   wload_pass(0);
-#pragma unroll 1
+#pragma unroll
   for (int pass = 0; pass < npass; ++pass) {
     const int nb = pass * 128 + w * 32;  // this wave's 32 channels (tile t row r -> nb + 8(r/4) + 4t + r%4)
+    const int n = nb + 8 * g;
+    const bool nok = n < a.Cout;
+    // compile-time epilogue operands of this pass, issued now so they land under the MFMAs
+    // (out-of-range lanes read zeros: buffer offsets past the descriptor)
+    u32x4 gv[NMT], rv[NMT], rv2[NMT];
+    if constexpr (CE) {
+      const bool gok = nok && (GATE != 3 || (n >= a.gcol0 && n < a.gcol1));
+      const bool rok = nok && n < a.rcols;
+#pragma unroll
+      for (int i = 0; i < NMT; ++i) {
+        const int m = m0 + i * 16 + c16;
+        const bool mok = m < a.M;
+        if constexpr (GATE != 0)
+          gv[i] = buf_load16(gr, (mok && gok) ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2) : SR_OOB);
+        if constexpr (RES)
+          rv[i] = buf_load16(rr, (mok && rok) ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
+        if constexpr (RES2)
+          rv2[i] = buf_load16(rr2, (mok && rok) ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * 2) : SR_OOB);
+      }
+    }
     f32x4 acc[NMT][2];
 #pragma unroll
     for (int i = 0; i < NMT; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int kk = 0; kk < MAXKK; ++kk) {
       if (kk >= nkk) break;
       const int ch = kk * 4 + g;  // logical 16-B chunk of the X^T fragment
       // [cg][row][128 B], physical chunk = logical ^ (row & 7); row & 7 == c16 & 7 for all i
       const char* base = smem + (ch >> 3) * MT * 128 + c16 * 128 + ((((ch & 7) ^ (c16 & 7))) << 4);
+      // all NMT fragments of the K step first (in flight together), then the MFMAs
+      u32x4 xf[NMT];
+#pragma unroll
+      for (int i = 0; i < NMT; ++i) xf[i] = *(const u32x4*)(base + i * 16 * 128);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < NMT; ++i) {
-        const u32x4 xf = *(const u32x4*)(base + i * 16 * 128);
         acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, wb[kk][0]),
-                                                            __builtin_bit_cast(s16x8, xf), acc[i][0], 0, 0, 0);
+                                                            __builtin_bit_cast(s16x8, xf[i]), acc[i][0], 0, 0, 0);
         acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, wb[kk][1]),
-                                                            __builtin_bit_cast(s16x8, xf), acc[i][1], 0, 0, 0);
+                                                            __builtin_bit_cast(s16x8, xf[i]), acc[i][1], 0, 0, 0);
       }
     }
     // the next pass's W fragments load while this pass's epilogue runs
@@ -1163,26 +1217,89 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
     // ---- epilogue: lane (g, c16) holds channels nb + 8g .. +7 of token m0 + 16i + c16 and
     // stores them as one 16-B vector (4 lanes cover 64 contiguous bytes of a token row;
     // staging whole rows through LDS measured slower: 78 -> 95 us on the qkv shape)
-    const int n = nb + 8 * g;
-    if (n >= a.Cout) continue;
-    float bv[8];
+    const float* bv = bva[pass];
+    if constexpr (CE) {
+      // branch-free over lanes: stores of out-of-range lanes go past the buffer descriptor
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bv[j] = 0.f;
-    if (a.bias) {
-      const f32x4 b0 = *(const f32x4*)(a.bias + n), b1 = *(const f32x4*)(a.bias + n + 4);
+      for (int i = 0; i < NMT; ++i) {
+        const int m = m0 + i * 16 + c16;
+        const bool ok = nok && m < a.M;
+        float v[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { bv[j] = b0[j]; bv[4 + j] = b1[j]; }
+        for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
+        if constexpr (AUX) {
+          u32x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+          __builtin_amdgcn_raw_buffer_store_b128(o, ar,
+                                                 ok ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB, 0, 0);
+        }
+        if constexpr (ACT == 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : 0.f;
+        } else if constexpr (ACT == 2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * a.slope;
+        } else if constexpr (ACT == 3) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = gelu_exact(v[j]);
+        }
+        float gf[8];
+        if constexpr (GATE != 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            gf[2 * j] = bf16_to_f32(gv[i][j] & 0xffff);
+            gf[2 * j + 1] = bf16_to_f32(gv[i][j] >> 16);
+          }
+        }
+        if constexpr (GATE == 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+        } else if constexpr (GATE == 2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= alpha_blk;
+        if constexpr (RES) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[2 * j] += a.beta * bf16_to_f32(rv[i][j] & 0xffff);
+            v[2 * j + 1] += a.beta * bf16_to_f32(rv[i][j] >> 16);
+          }
+        }
+        if constexpr (RES2) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[2 * j] += a.beta2 * bf16_to_f32(rv2[i][j] & 0xffff);
+            v[2 * j + 1] += a.beta2 * bf16_to_f32(rv2[i][j] >> 16);
+          }
+        }
+        if constexpr (GATE == 3) {
+          if (n >= a.gcol0 && n < a.gcol1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
+          }
+        }
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        __builtin_amdgcn_raw_buffer_store_b128(o, yr,
+                                               ok ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB, 0, 0);
+      }
+      continue;
     }
+    if (!nok) continue;
 #pragma unroll
     for (int i = 0; i < NMT; ++i) {  // fully unrolled: acc must stay register-indexed (no scratch)
       const int m = m0 + i * 16 + c16;
       if (m >= a.M) continue;
-      u32x4 gv, rv, rv2;
+      u32x4 gv1, rv1, rv21;
       const bool rok = n < a.rcols;
-      if (a.gate) gv = buf_load16(gr, (a.gate_mode != 2 || (n >= a.gcol0 && n < a.gcol1))
-                                          ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2) : SR_OOB);
-      if (a.res) rv = buf_load16(rr, rok ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
-      if (a.res2) rv2 = buf_load16(rr2, rok ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * 2) : SR_OOB);
+      if (a.gate) gv1 = buf_load16(gr, (a.gate_mode != 2 || (n >= a.gcol0 && n < a.gcol1))
+                                           ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2) : SR_OOB);
+      if (a.res) rv1 = buf_load16(rr, rok ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
+      if (a.res2) rv21 = buf_load16(rr2, rok ? (uint32_t)(((size_t)m * a.ldr2 + a.r2coff + n) * 2) : SR_OOB);
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
@@ -1196,7 +1313,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       if (a.gate && a.gate_mode != 2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float g0 = bf16_to_f32(gv[j] & 0xffff), g1 = bf16_to_f32(gv[j] >> 16);
+          const float g0 = bf16_to_f32(gv1[j] & 0xffff), g1 = bf16_to_f32(gv1[j] >> 16);
           if (a.gate_mode == 1) {
             v[2 * j] *= gelu_grad(g0);
             v[2 * j + 1] *= gelu_grad(g1);
@@ -1212,22 +1329,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       if (a.res) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[2 * j] += a.beta * bf16_to_f32(rv[j] & 0xffff);
-          v[2 * j + 1] += a.beta * bf16_to_f32(rv[j] >> 16);
+          v[2 * j] += a.beta * bf16_to_f32(rv1[j] & 0xffff);
+          v[2 * j + 1] += a.beta * bf16_to_f32(rv1[j] >> 16);
         }
       }
       if (a.res2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[2 * j] += a.beta2 * bf16_to_f32(rv2[j] & 0xffff);
-          v[2 * j + 1] += a.beta2 * bf16_to_f32(rv2[j] >> 16);
+          v[2 * j] += a.beta2 * bf16_to_f32(rv21[j] & 0xffff);
+          v[2 * j + 1] += a.beta2 * bf16_to_f32(rv21[j] >> 16);
         }
       }
       if (a.gate && a.gate_mode == 2 && n >= a.gcol0 && n < a.gcol1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[2 * j] *= bf16_to_f32(gv[j] & 0xffff) > 0.f ? 1.f : a.gate_slope;
-          v[2 * j + 1] *= bf16_to_f32(gv[j] >> 16) > 0.f ? 1.f : a.gate_slope;
+          v[2 * j] *= bf16_to_f32(gv1[j] & 0xffff) > 0.f ? 1.f : a.gate_slope;
+          v[2 * j + 1] *= bf16_to_f32(gv1[j] >> 16) > 0.f ? 1.f : a.gate_slope;
         }
       }
       u32x4 o;
@@ -3395,10 +3512,26 @@ bool fwd_use_band(const FwdArgs& a, bool bf) {
   const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
   return band_epi(a, rows < gmax ? rows : gmax) >= 0;
 }
+// the lin kernel's compile-time epilogue code for these arguments (see conv3x3_lin_kernel), -1
+// for the run-time-flag form; instantiated: plain (qkv fwd, proj dgrad), GELU' gate (fc2
+// dgrad), residual (proj fwd), GELU + pre-activation (fc1 fwd), residual + row scale (proj
+// fwd with stochastic depth)
+int lin_epi(const FwdArgs& a) {
+  int gate = 0;
+  if (a.gate) gate = a.gate_mode == 2 ? 3 : (a.gate_mode == 1 ? 2 : 1);
+  const int e = a.act | (gate << 2) | (a.res ? 16 : 0) | (a.res2 ? 32 : 0) | (a.aux ? 64 : 0) |
+                (a.row_scale ? 128 : 0);
+  if (a.row_scale && (a.H * a.W) % 128) return -1;  // row scale uniform per 128-token block
+  if ((size_t)a.M * a.ldy * 2 >= 0x80000000ull) return -1;  // buffer-store offsets are 31-bit
+  switch (e) {
+    case 0: case 8: case 16: case 67: case 144: return e;
+    default: return -1;
+  }
+}
 // short-K 1x1 convs (linears): token tile staged once, all output channels swept
 bool fwd_use_lin(const FwdArgs& a, bool bf) {
   return bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && a.Cin <= 192 &&
-         g_variant != 1 && g_variant != 27;
+         a.Cout <= 640 && g_variant != 1 && g_variant != 27;
 }
 FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_lin(a, bf)) return FK_LIN;
@@ -3426,7 +3559,22 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
     case FK_LIN: {
       FwdArgs b = a;
       b.tiles = (a.M + 127) / 128;
-      hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3>), dim3(b.tiles), dim3(256), 0, s, b);
+      const int e = lin_epi(a);
+#define SR_LIN_E(NP_, E_) \
+  case E_: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, E_>), dim3(b.tiles), dim3(256), 0, s, b); break;
+#define SR_LIN(NP_) \
+  case NP_: \
+    switch (e) { \
+      SR_LIN_E(NP_, 0) SR_LIN_E(NP_, 8) SR_LIN_E(NP_, 16) SR_LIN_E(NP_, 67) SR_LIN_E(NP_, 144) \
+      default: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, -1>), dim3(b.tiles), dim3(256), 0, s, b); \
+    } \
+    break;
+      switch ((a.Cout + 127) / 128) {
+        SR_LIN(1) SR_LIN(2) SR_LIN(3) SR_LIN(4) SR_LIN(5)
+        default: return hipErrorInvalidValue;
+      }
+#undef SR_LIN
+#undef SR_LIN_E
       return hipGetLastError();
     }
     case FK_BAND: {
