@@ -1993,6 +1993,143 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// HR tail convs (conv_last: Cout <= 16, NCHW fp32 store, W >= 256, Cin 64..256): row streaming
+// over 32-px column strips.  A block owns (image, strip, band of RB rows); per output row ONE new
+// input row (34 px x Cin, per 64-ch chunk a [40 px][128 B] swizzled image) is DMA'd into a ring
+// of LA + 2 slots, LA rows ahead, so x crosses HBM ~once (the one-row halo tiles read it three
+// times).  The waves split K by 64-channel chunk (NW = Cin / 64 chunks; with fewer chunks they
+// split the two 16-px tiles), keep their chunk's weights in registers, and combine their partial
+// sums through LDS; the fused tail epilogue (bias, activation, alpha, NCHW affine) stores 4
+// consecutive pixels of one channel per lane.
+// ------------------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(256, 1) void conv3x3_fwd_tail_kernel(FwdArgs a) {
+  constexpr int LA = 3, S = LA + 2;
+  constexpr int CHB = 40 * 128;         // one 64-ch chunk of a ring row (34 px used)
+  constexpr int SLOT = NW * CHB;
+  constexpr int PPR = NW * 5;           // 1-KB pieces per row
+  constexpr int PPW = (PPR + 3) / 4;    // per wave (padded with dummies: uniform vmcnt counts)
+  constexpr int G = 4 / NW;             // wave groups over the two px tiles
+  constexpr int NT = G == 1 ? 2 : 1;    // px tiles per wave
+  constexpr int PART = 4 * NT * 64 * 16;  // one partial-sum buffer
+  __shared__ __attribute__((aligned(16))) char smem[S * SLOT + 2 * PART + 1024];
+  char* part = smem + S * SLOT;
+  char* dummy = part + 2 * PART;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int H = a.H, W = a.W;
+  const int strips = W >> 5, RB = a.tiles;
+  const int bands = (H + RB - 1) / RB;
+  int b = (int)blockIdx.x;
+  const int band = b % bands; b /= bands;
+  const int strip = b % strips;
+  const int n = b / strips;
+  const int x0 = strip * 32, y0 = band * RB, y1 = min(H, y0 + RB);
+  const int chunk = w % NW, grp = w / NW;
+  const bool mma_on = G < 4 || grp < 2;  // Cin 64: waves 2, 3 only move data
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+  const int STO = w < 2 ? 1 : 0;        // waves 0, 1 store one vector per row (tiles 0, 1)
+
+  // this wave's weights: co = c16, K chunk kk*32 + 8g of its 64-ch chunk, all taps
+  u32x4 bw[9][2];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ci = chunk * 64 + kk * 32 + 8 * g;
+      bw[tap][kk] = buf_load16(wr, c16 < a.Cout ? (uint32_t)((c16 * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB);
+    }
+  // the epilogue's per-channel constants (loads here, not in the row loop: they would count in
+  // the row loop's vmcnt bookkeeping)
+  const int co = c16;
+  const bool cok = co < a.Cout_real;
+  const float ebias = (a.bias && cok) ? a.bias[co] : 0.f;
+  const float escale = (a.aff_scale && cok) ? a.aff_scale[co] : 1.f;
+  const float eshift = (a.aff_shift && cok) ? a.aff_shift[co] : 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) asm volatile("" ::"v"(bw[tap][kk]));
+  asm volatile("" ::"v"(ebias), "v"(escale), "v"(eshift));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // DMA of input row yy (outside [0, H): zeros) into its ring slot: piece p = (chunk p / 5,
+  // px rows 8 (p % 5) ..); physical 16-B slot lane & 7 of px row r holds logical chunk
+  // (lane & 7) ^ (r & 7)
+  auto issue_row = [&](int yy) {
+    char* slot = smem + ((yy - (y0 - 1)) % S) * SLOT;
+    const bool yv = (unsigned)yy < (unsigned)H;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int p = w + 4 * j;
+      const int c = p / 5, q = p - c * 5;
+      const int px = 8 * q + (lane >> 3);
+      const int lc = (lane & 7) ^ (px & 7);
+      const int xx = x0 - 1 + px;
+      const bool v = p < PPR && yv && px < 34 && (unsigned)xx < (unsigned)W;
+      const uint32_t off = (uint32_t)(((((size_t)n * H + yy) * W + xx) * a.ldx + a.xcoff + c * 64 + lc * 8) * 2);
+      glds16(xr, p < PPR ? slot + c * CHB + q * 1024 : dummy, v ? off : SR_OOB);
+    }
+  };
+  for (int yy = y0 - 1; yy < y0 + LA; ++yy) issue_row(yy);
+
+#pragma unroll 1
+  for (int y = y0; y < y1; ++y) {
+    const int s = y - y0;
+    // rows <= y + 1 landed (ops issued after row y + 1's pieces may stay in flight)
+    if (s + 1 >= LA) {
+      if (STO) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + (LA - 2) * (PPW + 1)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 2) * PPW) : "memory");
+    } else {
+      vm_wait_dyn((LA - 1 - s) * PPW + s * (PPW + STO));
+    }
+    __syncthreads();
+    issue_row(y + LA);  // its slot held row y - 2, done by every wave (barrier above)
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (mma_on) {
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty) {
+        const char* row = smem + ((y - 1 + ty - (y0 - 1)) % S) * SLOT + chunk * CHB;
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+              const int tile = G == 1 ? t : grp;
+              const u32x4 fa = *(const u32x4*)(row + swz128(tile * 16 + c16 + tx, kk * 4 + g));
+              mfma_chunk<bf16_t>(fa, bw[ty * 3 + tx][kk], acc[t]);
+            }
+      }
+    }
+    f32x4* pb = (f32x4*)(part + (s & 1) * PART);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) pb[(w * NT + t) * 64 + lane] = acc[t];
+    __syncthreads();
+    if (tid < 128) {  // (tile, lane): px tile * 16 + 4g + r, channel c16
+      const int t = tid >> 6;
+      f32x4 v;
+      if constexpr (G == 1) v = pb[(0 * 2 + t) * 64 + lane] + pb[(1 * 2 + t) * 64 + lane] +
+                                pb[(2 * 2 + t) * 64 + lane] + pb[(3 * 2 + t) * 64 + lane];
+      else if constexpr (G == 2) v = pb[(t * 2 + 0) * 64 + lane] + pb[(t * 2 + 1) * 64 + lane];
+      else v = pb[t * 64 + lane];
+      if (cok) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = act_apply(v[r] + ebias, a.act, a.slope) * a.alpha * escale + eshift;
+        float* yp = (float*)a.y + (((size_t)n * a.Cout_real + co) * H + y) * W + x0 + t * 16 + 4 * g;
+        *(f32x4*)yp = f32x4{o[0], o[1], o[2], o[3]};
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // trailing row pieces land before exit
+}
+
+// ------------------------------------------------------------------------------------
 // Weight gradient.  GEMM per tap: C[co][ci] = sum_p dy[p][co] * x[p + tap][ci] over a
 // K-range of pixels (split-K).  LDS images are [pixels][cols] (rows = K); MFMA operands
 // need 8 consecutive K per lane, read with ds_read_b64_tr_b16 (bf16) or ds_read_b32
@@ -3485,7 +3622,7 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
 
 // Kernel family sr_conv3x3_fwd launches for a call (dispatch, kernel names and the
 // epilogue geometry behind colsum all follow this one choice).
-enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN, FK_BAND };
+enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN, FK_BAND, FK_TAIL };
 // row-streaming narrow conv: bf16 3x3, Cin 32 / 64, Cout 32 / 64 exactly, W 64 / 128, plain or
 // channel-slice NHWC in and out (variant 34: the tile kernel instead, for A/B)
 // the band kernel's compile-time epilogue code (see conv3x3_fwd_band_kernel) for these arguments,
@@ -3533,7 +3670,14 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
   return bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && a.Cin <= 192 &&
          a.Cout <= 640 && g_variant != 1 && g_variant != 27;
 }
+// HR tail convs: Cout <= 16 with the NCHW fp32 store, W >= 256 (32-px strips), Cin 64 / 128 / 256
+bool fwd_use_tail(const FwdArgs& a, bool bf) {
+  return bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && a.out_ps == 0 && a.out_nchw && a.Cout <= 16 &&
+         a.W >= 256 && a.W % 32 == 0 && (a.Cin == 64 || a.Cin == 128 || a.Cin == 256) && !a.gate && !a.res && !a.res2 &&
+         !a.aux && !a.colsum && !a.row_scale && g_variant != 1 && g_variant != 29;
+}
 FwdKind fwd_kind(const FwdArgs& a, bool bf) {
+  if (fwd_use_tail(a, bf)) return FK_TAIL;
   if (fwd_use_lin(a, bf)) return FK_LIN;
   if (fwd_use_band(a, bf)) return FK_BAND;
   if (fwd_use_halo(a, bf)) return FK_HALO;
@@ -3604,6 +3748,18 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
 #undef SR_BAND
 #undef SR_BAND_E
       return hipErrorInvalidValue;
+    }
+    case FK_TAIL: {
+      FwdArgs b = a;
+      b.tiles = a.H < 32 ? a.H : 32;  // rows per band
+      const dim3 grid((unsigned)(a.N * (a.W / 32) * ((a.H + b.tiles - 1) / b.tiles)));
+      switch (a.Cin / 64) {
+        case 1: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<1>, grid, dim3(256), 0, s, b); break;
+        case 2: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<2>, grid, dim3(256), 0, s, b); break;
+        case 3: return hipErrorInvalidValue;
+        default: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<4>, grid, dim3(256), 0, s, b); break;
+      }
+      return hipGetLastError();
     }
     case FK_HALO: return launch_fwd_halo(a, s);
     case FK_BIG: return launch_fwd_big(a, s);
@@ -3835,6 +3991,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
     case FK_LIN: return "conv3x3_lin_kernel";
     case FK_HALO: return "conv3x3_fwd_halo_kernel";
     case FK_BAND: return "conv3x3_fwd_band_kernel";
+    case FK_TAIL: return "conv3x3_fwd_tail_kernel";
     case FK_BIG: {
       if (g_variant == 2) return "conv3x3_fwd_big_kernel";
       return fwd_use_pph(fwd_shape(d)) ? "conv3x3_fwd_pph_kernel" : "conv3x3_fwd_pp_kernel";

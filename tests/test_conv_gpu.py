@@ -460,11 +460,13 @@ def test_wgrad_1x1_partial_tiles_vs_fp64(cuda, shape):
         assert (db - ref_b).abs().max().item() <= 1e-3 * ref_b.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize('shape', [(2, 3, 256, 256, 3), (1, 2, 256, 64, 3), (1, 2, 256, 96, 16)])
+@pytest.mark.parametrize('shape', [(2, 3, 256, 256, 3), (1, 2, 256, 64, 3), (1, 2, 256, 96, 16), (2, 40, 512, 128, 3),
+                                   (1, 33, 256, 256, 16), (3, 35, 256, 64, 8)])
 def test_fwd_halo_w256_nchw_tail(cuda, shape):
-    """HR-resolution tail conv (conv_last: Cout <= 16, W 256, fp32 NCHW store with the mean
-    shift / range affine) on the one-row halo tiles, against fp64 and the 256x16 kernel
-    (variant 29)."""
+    """HR-resolution tail conv (conv_last: Cout <= 16, W >= 256, fp32 NCHW store with the mean
+    shift / range affine): the row-streaming tail kernel (Cin 64 / 128 / 256; bands of 32 rows,
+    ragged last band) or the one-row halo tiles (other Cin, W 256), against fp64 and the 256x16
+    kernel (variant 29)."""
     N, H, W, cin, cout = shape
     torch.manual_seed(11)
     dt = torch.bfloat16
@@ -476,7 +478,8 @@ def test_fwd_halo_w256_nchw_tail(cuda, shape):
     wf, _, bg = C.prepared(conv.weight, conv.bias, spec, dt)
     x = torch.randn(N, H, W, cin, device=cuda).to(dt)
     d = C._desc(dt, N, H, W, cin, cin, spec.cout_p, cout, 0, out_nchw=1)
-    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_halo_kernel'
+    want = b'conv3x3_fwd_tail_kernel' if cin in (64, 128, 256) else b'conv3x3_fwd_halo_kernel'
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == want
     outs = []
     try:
         for variant in (0, 29):
