@@ -3622,7 +3622,7 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
 
 // Kernel family sr_conv3x3_fwd launches for a call (dispatch, kernel names and the
 // epilogue geometry behind colsum all follow this one choice).
-enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN, FK_BAND, FK_TAIL };
+enum FwdKind { FK_HALO, FK_BIG, FK_256_16, FK_256_32, FK_128_64, FK_128_128, FK_LIN, FK_BAND, FK_TAIL, FK_BANDS };
 // row-streaming narrow conv: bf16 3x3, Cin 32 / 64, Cout 32 / 64 exactly, W 64 / 128, plain or
 // channel-slice NHWC in and out (variant 34: the tile kernel instead, for A/B)
 // the band kernel's compile-time epilogue code (see conv3x3_fwd_band_kernel) for these arguments,
@@ -3637,7 +3637,7 @@ int band_epi(const FwdArgs& a, int grid) {
     if ((rows + a.H - 1) / a.H + 1 > 64) return -1;
   }
   switch (e) {
-    case 0: case 1: case 2: case 4: case 16: case 20: case 48: case 72: case 128: case 304: return e;
+    case 0: case 1: case 2: case 4: case 16: case 20: case 28: case 48: case 72: case 128: case 304: return e;
     default: return -1;
   }
 }
@@ -3645,6 +3645,17 @@ bool fwd_use_band(const FwdArgs& a, bool bf) {
   if (!(bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
         (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && (a.Cout == 32 || a.Cout == 64) &&
         a.Cout_real == a.Cout && g_variant != 1 && g_variant != 34))  // 34: the tile kernel (A/B, tests)
+    return false;
+  const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
+  return band_epi(a, rows < gmax ? rows : gmax) >= 0;
+}
+// wider outputs (RRDB dense-block dgrads: Cout 96..192 from a 32- or 64-channel input) as
+// band launches over 64-channel output column slices: the narrow input is re-read per slice
+bool fwd_use_band_sliced(const FwdArgs& a, bool bf) {
+  if (!(bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
+        (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && a.Cout > 64 && a.Cout <= 256 &&
+        a.Cout % 32 == 0 && a.Cout_real == a.Cout && !a.colsum && g_variant != 1 && g_variant != 34 &&
+        g_variant != 39))  // 39: the halo kernel for these (A/B)
     return false;
   const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
   return band_epi(a, rows < gmax ? rows : gmax) >= 0;
@@ -3680,6 +3691,7 @@ FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_tail(a, bf)) return FK_TAIL;
   if (fwd_use_lin(a, bf)) return FK_LIN;
   if (fwd_use_band(a, bf)) return FK_BAND;
+  if (fwd_use_band_sliced(a, bf)) return FK_BANDS;
   if (fwd_use_halo(a, bf)) return FK_HALO;
   // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
   // kernel with a partial N tile: x read once (vs twice by 128x128 tiles); 68 -> 57 us and 82 -> 65 us
@@ -3697,76 +3709,102 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
   *nt = k == FK_BIG ? 512 : 256;
 }
 
-template <typename T>
-hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
-  switch (fwd_kind(a, sizeof(T) == 2)) {
-    case FK_LIN: {
-      FwdArgs b = a;
-      b.tiles = (a.M + 127) / 128;
-      const int e = lin_epi(a);
-#define SR_LIN_E(NP_, E_) \
-  case E_: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, E_>), dim3(b.tiles), dim3(256), 0, s, b); break;
-#define SR_LIN(NP_) \
-  case NP_: \
-    switch (e) { \
-      SR_LIN_E(NP_, 0) SR_LIN_E(NP_, 8) SR_LIN_E(NP_, 16) SR_LIN_E(NP_, 67) SR_LIN_E(NP_, 144) \
-      default: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, -1>), dim3(b.tiles), dim3(256), 0, s, b); \
-    } \
-    break;
-      switch ((a.Cout + 127) / 128) {
-        SR_LIN(1) SR_LIN(2) SR_LIN(3) SR_LIN(4) SR_LIN(5)
-        default: return hipErrorInvalidValue;
-      }
-#undef SR_LIN
-#undef SR_LIN_E
-      return hipGetLastError();
-    }
-    case FK_BAND: {
-      // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64
-      // blocks (long bands: ring wrap-around and image crossings inside a band, for tests)
-      const int rows = a.N * a.H;
-      const int gmax = g_variant == 35 ? 64 : 256;
-      FwdArgs ab = a;
-      ab.stamps = g_stamps;
-      const dim3 grid(rows < gmax ? rows : gmax);
-      const int e = band_epi(a, grid.x);
+hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
+  // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64
+  // blocks (long bands: ring wrap-around and image crossings inside a band, for tests)
+  const int rows = a.N * a.H;
+  const int gmax = g_variant == 35 ? 64 : 256;
+  FwdArgs ab = a;
+  ab.stamps = g_stamps;
+  const dim3 grid(rows < gmax ? rows : gmax);
+  const int e = band_epi(a, grid.x);
 #define SR_BAND_E(CO_, W_, LA_, KH_, E_) \
   case E_: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<CO_, W_, LA_, KH_, E_>), grid, dim3(256), 0, s, ab); break;
 #define SR_BAND(CO_, W_, LA_, KH_) \
   if (a.Cout == CO_ && a.W == W_ && a.Cin == 32 * KH_) { \
-    switch (e) { \
-      SR_BAND_E(CO_, W_, LA_, KH_, 0) SR_BAND_E(CO_, W_, LA_, KH_, 1) SR_BAND_E(CO_, W_, LA_, KH_, 2) \
-      SR_BAND_E(CO_, W_, LA_, KH_, 4) SR_BAND_E(CO_, W_, LA_, KH_, 16) SR_BAND_E(CO_, W_, LA_, KH_, 20) \
-      SR_BAND_E(CO_, W_, LA_, KH_, 48) SR_BAND_E(CO_, W_, LA_, KH_, 72) SR_BAND_E(CO_, W_, LA_, KH_, 128) \
-      SR_BAND_E(CO_, W_, LA_, KH_, 304) \
-      default: return hipErrorInvalidValue; \
-    } \
-    return hipGetLastError(); \
+switch (e) { \
+  SR_BAND_E(CO_, W_, LA_, KH_, 0) SR_BAND_E(CO_, W_, LA_, KH_, 1) SR_BAND_E(CO_, W_, LA_, KH_, 2) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 4) SR_BAND_E(CO_, W_, LA_, KH_, 16) SR_BAND_E(CO_, W_, LA_, KH_, 20) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 28) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 48) SR_BAND_E(CO_, W_, LA_, KH_, 72) SR_BAND_E(CO_, W_, LA_, KH_, 128) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 304) \
+  default: return hipErrorInvalidValue; \
+} \
+return hipGetLastError(); \
   }
-      SR_BAND(64, 64, 5, 2) SR_BAND(64, 64, 5, 1) SR_BAND(32, 64, 5, 2) SR_BAND(32, 64, 5, 1)
-      SR_BAND(64, 128, 3, 2) SR_BAND(64, 128, 3, 1) SR_BAND(32, 128, 4, 2) SR_BAND(32, 128, 4, 1)
+  SR_BAND(64, 64, 5, 2) SR_BAND(64, 64, 5, 1) SR_BAND(32, 64, 5, 2) SR_BAND(32, 64, 5, 1)
+  SR_BAND(64, 128, 3, 2) SR_BAND(64, 128, 3, 1) SR_BAND(32, 128, 4, 2) SR_BAND(32, 128, 4, 1)
 #undef SR_BAND
 #undef SR_BAND_E
-      return hipErrorInvalidValue;
-    }
-    case FK_TAIL: {
-      FwdArgs b = a;
-      b.tiles = a.H < 32 ? a.H : 32;  // rows per band
-      const dim3 grid((unsigned)(a.N * (a.W / 32) * ((a.H + b.tiles - 1) / b.tiles)));
-      switch (a.Cin / 64) {
-        case 1: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<1>, grid, dim3(256), 0, s, b); break;
-        case 2: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<2>, grid, dim3(256), 0, s, b); break;
-        case 3: return hipErrorInvalidValue;
-        default: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<4>, grid, dim3(256), 0, s, b); break;
-      }
-      return hipGetLastError();
-    }
-    case FK_HALO: return launch_fwd_halo(a, s);
-    case FK_BIG: return launch_fwd_big(a, s);
-    case FK_256_16: return launch_fwd<T, 256, 16, 4, 1>(a, s);
-    case FK_256_32: return launch_fwd<T, 256, 32, 4, 1>(a, s);
-    case FK_128_64: return launch_fwd<T, 128, 64, 2, 2>(a, s);
-    default: return launch_fwd<T, 128, 128, 2, 2>(a, s);
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
+  switch (fwd_kind(a, sizeof(T) == 2)) {
+case FK_LIN: {
+  FwdArgs b = a;
+  b.tiles = (a.M + 127) / 128;
+  const int e = lin_epi(a);
+#define SR_LIN_E(NP_, E_) \
+  case E_: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, E_>), dim3(b.tiles), dim3(256), 0, s, b); break;
+#define SR_LIN(NP_) \
+  case NP_: \
+switch (e) { \
+  SR_LIN_E(NP_, 0) SR_LIN_E(NP_, 8) SR_LIN_E(NP_, 16) SR_LIN_E(NP_, 67) SR_LIN_E(NP_, 144) \
+  default: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, -1>), dim3(b.tiles), dim3(256), 0, s, b); \
+} \
+break;
+  switch ((a.Cout + 127) / 128) {
+    SR_LIN(1) SR_LIN(2) SR_LIN(3) SR_LIN(4) SR_LIN(5)
+    default: return hipErrorInvalidValue;
+  }
+#undef SR_LIN
+#undef SR_LIN_E
+  return hipGetLastError();
+}
+case FK_BAND: return launch_band(a, s);
+case FK_BANDS: {
+  // 64-channel output column slices (the last may be 32 wide), each a band launch with the
+  // weight rows, bias, output / residual / gate columns and the gate / residual column
+  // ranges shifted to the slice
+  for (int n0 = 0; n0 < a.Cout; n0 += 64) {
+    FwdArgs b = a;
+    const int cw = a.Cout - n0 < 64 ? a.Cout - n0 : 64;
+    b.Cout = b.Cout_real = cw;
+    b.w = (const bf16_t*)a.w + (size_t)n0 * a.ldw;
+    b.w_bytes = a.w_bytes - (uint32_t)((size_t)n0 * a.ldw * 2);
+    if (a.bias) b.bias = a.bias + n0;
+    b.ycoff = a.ycoff + n0;
+    b.gcoff = a.gcoff + n0;
+    b.rcoff = a.rcoff + n0;
+    b.r2coff = a.r2coff + n0;
+    b.gcol0 = a.gcol0 - n0;
+    b.gcol1 = a.gcol1 - n0;
+    b.rcols = a.rcols - n0;
+    const hipError_t e = launch_band(b, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+case FK_TAIL: {
+  FwdArgs b = a;
+  b.tiles = a.H < 32 ? a.H : 32;  // rows per band
+  const dim3 grid((unsigned)(a.N * (a.W / 32) * ((a.H + b.tiles - 1) / b.tiles)));
+  switch (a.Cin / 64) {
+    case 1: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<1>, grid, dim3(256), 0, s, b); break;
+    case 2: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<2>, grid, dim3(256), 0, s, b); break;
+    case 3: return hipErrorInvalidValue;
+    default: hipLaunchKernelGGL(conv3x3_fwd_tail_kernel<4>, grid, dim3(256), 0, s, b); break;
+  }
+  return hipGetLastError();
+}
+case FK_HALO: return launch_fwd_halo(a, s);
+case FK_BIG: return launch_fwd_big(a, s);
+case FK_256_16: return launch_fwd<T, 256, 16, 4, 1>(a, s);
+case FK_256_32: return launch_fwd<T, 256, 32, 4, 1>(a, s);
+case FK_128_64: return launch_fwd<T, 128, 64, 2, 2>(a, s);
+default: return launch_fwd<T, 128, 128, 2, 2>(a, s);
   }
 }
 
@@ -3992,6 +4030,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
     case FK_HALO: return "conv3x3_fwd_halo_kernel";
     case FK_BAND: return "conv3x3_fwd_band_kernel";
     case FK_TAIL: return "conv3x3_fwd_tail_kernel";
+    case FK_BANDS: return "conv3x3_fwd_band_kernel";
     case FK_BIG: {
       if (g_variant == 2) return "conv3x3_fwd_big_kernel";
       return fwd_use_pph(fwd_shape(d)) ? "conv3x3_fwd_pph_kernel" : "conv3x3_fwd_pp_kernel";
@@ -4013,7 +4052,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 37)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 39)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-33: schedule A/B switches)");
   g_variant = variant;
   return SR_OK;
