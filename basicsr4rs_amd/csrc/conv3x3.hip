@@ -2083,7 +2083,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_tail_kernel(FwdArgs a) {
       if (STO) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + (LA - 2) * (PPW + 1)) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 2) * PPW) : "memory");
     } else {
-      vm_wait_dyn((LA - 1 - s) * PPW + s * (PPW + STO));
+      vm_wait_dyn((LA - 2 - s) * PPW + s * (PPW + STO));  // issued after row y + 1: rows y + 2 .. y0 + LA, stores
     }
     __syncthreads();
     issue_row(y + LA);  // its slot held row y - 2, done by every wave (barrier above)
@@ -3653,7 +3653,7 @@ bool fwd_use_band(const FwdArgs& a, bool bf) {
 // band launches over 64-channel output column slices: the narrow input is re-read per slice
 bool fwd_use_band_sliced(const FwdArgs& a, bool bf) {
   if (!(bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
-        (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && a.Cout > 64 && a.Cout <= 256 &&
+        (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && a.Cout > 64 && a.Cout < 256 &&
         a.Cout % 32 == 0 && a.Cout_real == a.Cout && !a.colsum && g_variant != 1 && g_variant != 34 &&
         g_variant != 39))  // 39: the halo kernel for these (A/B)
     return false;

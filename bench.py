@@ -327,6 +327,9 @@ def main():
             'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu, 'parity': parity,
         }
         print(json.dumps(line))
+        if not math.isfinite(loss):  # a step that trains on NaNs is not a measurement
+            print(f'bench: non-finite training loss {loss}', file=sys.stderr)
+            sys.exit(1)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

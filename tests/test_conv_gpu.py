@@ -461,7 +461,8 @@ def test_wgrad_1x1_partial_tiles_vs_fp64(cuda, shape):
 
 
 @pytest.mark.parametrize('shape', [(2, 3, 256, 256, 3), (1, 2, 256, 64, 3), (1, 2, 256, 96, 16), (2, 40, 512, 128, 3),
-                                   (1, 33, 256, 256, 16), (3, 35, 256, 64, 8)])
+                                   (1, 33, 256, 256, 16), (3, 35, 256, 64, 8), (32, 256, 256, 256, 3),
+                                   (32, 256, 256, 64, 3)])
 def test_fwd_halo_w256_nchw_tail(cuda, shape):
     """HR-resolution tail conv (conv_last: Cout <= 16, W >= 256, fp32 NCHW store with the mean
     shift / range affine): the row-streaming tail kernel (Cin 64 / 128 / 256; bands of 32 rows,
@@ -491,11 +492,15 @@ def test_fwd_halo_w256_nchw_tail(cuda, shape):
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
     torch.cuda.synchronize()
-    ref = F.conv2d(x.permute(0, 3, 1, 2).double().cpu(), bf(conv.weight.detach().cpu()).double(),
+    # full-size cases (the EDSR_Lx4 / RCAN / SwinIR conv_last at B 32: 8 blocks per CU, each block's
+    # ring prologue racing the previous block's LDS contents): fp64 on the first and last image
+    im = [0, N - 1] if N > 4 else list(range(N))
+    ref = F.conv2d(x[im].permute(0, 3, 1, 2).double().cpu(), bf(conv.weight.detach().cpu()).double(),
                    conv.bias.detach().cpu().double(), padding=1)
     ref = ref * scale.cpu().double().view(1, -1, 1, 1) + shift.cpu().double().view(1, -1, 1, 1)
     tol = 1e-3 * max(1.0, ref.abs().max().item())
-    assert (outs[0].cpu().double() - ref).abs().max().item() <= tol
+    assert torch.isfinite(outs[0]).all()
+    assert (outs[0][im].cpu().double() - ref).abs().max().item() <= tol
     assert (outs[0] - outs[1]).abs().max().item() <= tol
 
 
