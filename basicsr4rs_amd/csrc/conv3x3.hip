@@ -3341,6 +3341,91 @@ __global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(const float* w
   }
 }
 
+// Slab reduction, one kernel for both slab layouts (TR false: [S][taps][Cout][Cin], groups (tap,
+// co, 4 ci); TR true: the row-streaming wgrad's [S][taps][Cin][Cout], groups (tap, ci, 4 co)), no
+// gathered loads (ci_map with TR false / co_map with TR true go to the kernels below).  A block
+// of nw waves holds GPW groups x P = nw * 64 / GPW split phases: lane -> (phase, group), one 16-B
+// load per split, GPW * 16 B contiguous per phase and wave instruction, phases k = ph (mod P)
+// with 4 independent loads in flight, then a fixed-order LDS combine -- deterministic.  The host
+// sizes P to ~8 slabs per thread and GPW so that the grid covers the chip (RCAN: S 256 over 9216
+// groups = 288 blocks of 32 groups x 32 phases instead of 144 of 64 x 16).
+template <int GPW, bool TR>
+__global__ __launch_bounds__(1024) void wgrad_reduce_g_kernel(const float* ws, const float* wsb, float* dw, float* db,
+                                                              int S, int Cout, int Cin, int Cout_real, int Cin_real,
+                                                              int out_ps, int taps, const int* co_map,
+                                                              const int* ci_map, float scale, int wblocks,
+                                                              int accumulate) {
+  __shared__ f32x4 red[1024];
+  const int nw = (int)(blockDim.x >> 6);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
+  const int cps = Cout_real / r2;
+  if ((int)blockIdx.x >= wblocks) {  // bias: 64 co per block, nw phases
+    const int c = ((int)blockIdx.x - wblocks) * 64 + lane;
+    float sb = 0.f;
+    if (c < Cout_real) {
+      const int cop = co_map ? co_map[c] : (out_ps > 0 ? (c % r2) * cps + c / r2 : c);
+      for (int k = wv; k < S; k += nw) sb += wsb[(size_t)k * Cout + cop];
+    }
+    red[wv * 64 + lane] = f32x4{sb, 0.f, 0.f, 0.f};
+    __syncthreads();
+    if (wv == 0 && c < Cout_real) {
+      float sm = red[lane][0];
+      for (int k = 1; k < nw; ++k) sm += red[k * 64 + lane][0];
+      db[c] = sm * scale + (accumulate ? db[c] : 0.f);
+    }
+    return;
+  }
+  const int P = nw * (64 / GPW);
+  const int ph = wv * (64 / GPW) + lane / GPW, gl = lane % GPW;
+  const int64_t i = (int64_t)blockIdx.x * GPW + gl;
+  const int c4n = TR ? (Cout_real + 3) >> 2 : Cin_real >> 2;
+  const int rows = TR ? Cin_real : Cout_real;
+  const int64_t total = (int64_t)taps * rows * c4n;
+  int q4 = 0, rw = 0, tap = 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < total) {
+    q4 = (int)(i % c4n);
+    const int64_t t2 = i / c4n;
+    rw = (int)(t2 % rows);
+    tap = (int)(t2 / rows);
+    int rp;
+    if (TR) rp = ci_map ? ci_map[rw] : rw;
+    else rp = co_map ? co_map[rw] : (out_ps > 0 ? (rw % r2) * cps + rw / r2 : rw);
+    const size_t stride = (size_t)taps * Cout * Cin;
+    const float* src = ws + ((size_t)tap * (TR ? Cin : Cout) + rp) * (TR ? Cout : Cin) + q4 * 4;
+    int k = ph;
+    for (; k + 3 * P < S; k += 4 * P) {
+      const f32x4 v0 = *(const f32x4*)(src + (size_t)k * stride);
+      const f32x4 v1 = *(const f32x4*)(src + (size_t)(k + P) * stride);
+      const f32x4 v2 = *(const f32x4*)(src + (size_t)(k + 2 * P) * stride);
+      const f32x4 v3 = *(const f32x4*)(src + (size_t)(k + 3 * P) * stride);
+      acc += v0; acc += v1; acc += v2; acc += v3;
+    }
+    for (; k < S; k += P) acc += *(const f32x4*)(src + (size_t)k * stride);
+  }
+  red[ph * GPW + gl] = acc;
+  __syncthreads();
+  if (ph == 0 && i < total) {
+    f32x4 sm = red[gl];
+    for (int k = 1; k < P; ++k) sm += red[k * GPW + gl];
+    if (TR) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = q4 * 4 + e;
+        if (co < Cout_real) {
+          float* d = dw + ((size_t)co * Cin_real + rw) * taps + tap;
+          *d = sm[e] * scale + (accumulate ? *d : 0.f);
+        }
+      }
+    } else {
+      float* d = dw + ((size_t)rw * Cin_real + q4 * 4) * taps + tap;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[(size_t)e * taps] = sm[e] * scale + (accumulate ? d[(size_t)e * taps] : 0.f);
+    }
+  }
+}
+
 // Slab reduction for Cin_real % 4 == 0 (16-B loads, or gathered through ci_map): 64 (tap, co, 4 ci) groups per
 // 1024-thread block; the 16 waves take splits k = wave (mod 16) with independent 16-B loads
 // (coalesced along ci), then a fixed-order LDS combine -- deterministic, and S / 16 loads
@@ -4144,7 +4229,28 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t work = total > Cout_real ? total : Cout_real;
-  if (wg_use_halo(d) && wg_use_ring()) {
+  const bool tr = wg_use_halo(d) && wg_use_ring();
+  // (the row-streaming slab keeps wgrad_reduce_tr_kernel: 32-group blocks measured slower on RCAN / RRDB)
+  if (g_variant != 40 && !tr && Cin_real % 4 == 0 && !ci_map) {
+    // split phases P ~ S / 8 (pow2 <= 32), group width GPW so that the grid covers the chip
+    const int64_t groups = tr ? (int64_t)taps * Cin_real * ((Cout_real + 3) / 4) : (int64_t)taps * Cout_real * (Cin_real / 4);
+    int P = 1;
+    while (P * 8 < S && P < 32) P <<= 1;
+    int gpw = 64;
+    while (gpw > 16 && P * gpw / 64 > 16) gpw >>= 1;  // <= 16 waves
+    while (gpw > 16 && (groups + gpw - 1) / gpw < 256 && P * gpw / 64 >= 2) gpw >>= 1;
+    const int nw = P * gpw / 64 > 0 ? P * gpw / 64 : 1;
+    const int wblocks = (int)((groups + gpw - 1) / gpw);
+    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
+    const dim3 grid((unsigned)(wblocks + bblocks)), blk((unsigned)(nw * 64));
+#define SR_RG(G, T)                                                                                             \
+  hipLaunchKernelGGL((wgrad_reduce_g_kernel<G, T>), grid, blk, 0, s, (const float*)a.ws, (const float*)a.wsb, dw, db, \
+                     S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, wblocks,  \
+                     d->accumulate)
+    if (tr) { if (gpw == 64) SR_RG(64, true); else if (gpw == 32) SR_RG(32, true); else SR_RG(16, true); }
+    else { if (gpw == 64) SR_RG(64, false); else if (gpw == 32) SR_RG(32, false); else SR_RG(16, false); }
+#undef SR_RG
+  } else if (tr) {
     const int64_t work4 = (int64_t)taps * Cin_real * ((Cout_real + 3) / 4);
     const int wblocks = (int)((work4 + 63) / 64);
     const int bblocks = db ? (Cout_real + 63) / 64 : 0;

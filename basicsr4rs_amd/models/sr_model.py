@@ -18,7 +18,9 @@ import torch
 from ..archs import build_network
 from ..losses import build_loss
 from ..metrics import calculate_metric
-from ..ops.conv import bump_param_epoch
+import os
+
+from ..ops.conv import async_wgrad, bump_param_epoch
 from ..utils.flat import FlatParams
 from ..utils.img_util import imwrite, tensor2img
 from ..utils.registry import MODEL_REGISTRY
@@ -55,6 +57,10 @@ class SRModel(BaseModel):
         self._eager_steps = 0
         # HIP-graph capture of the train step (after 2 eager warm-up steps); single process
         self.use_graph = bool(train_opt.get('cuda_graph', False)) and not self.opt.get('dist', False)
+        # weight gradients on a side stream during backward (train.async_wgrad, ops.conv.async_wgrad);
+        # the environment variable SR_ASYNC_WGRAD=0/1 overrides the option (A/B)
+        env = os.environ.get('SR_ASYNC_WGRAD')
+        self.async_wgrad = env == '1' if env in ('0', '1') else bool(train_opt.get('async_wgrad', False))
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)
@@ -101,7 +107,8 @@ class SRModel(BaseModel):
             l_pix = self.cri_pix(self.output, self.gt)
             l_total += l_pix
             loss_dict['l_pix'] = l_pix
-        l_total.backward()
+        with async_wgrad(self.async_wgrad):  # weight gradients on a side stream, joined here
+            l_total.backward()
         # drop the autograd graph now: a graph kept alive by self.output would pin this step's
         # AccumulateGrad nodes (and their stream) into the next step / a HIP-graph capture
         self.output = self.output.detach()

@@ -9,6 +9,7 @@ from collections import OrderedDict
 
 import torch
 
+from ..ops.conv import async_wgrad
 from ..utils.registry import MODEL_REGISTRY
 from .sr_model import SRModel
 
@@ -37,7 +38,8 @@ class SRRSModel(SRModel):
             self.log_nan_inf_loss(current_iter, l_total)
             self.optimizer_g.zero_grad()
             return
-        l_total.backward()
+        with async_wgrad(self.async_wgrad):
+            l_total.backward()
         self.sync_gradients()
         if hasattr(self.optimizer_g, 'fp') and self.ema_decay > 0 and self.flat_ema is not None:
             self.optimizer_g.step(ema=self.flat_ema, ema_decay=self.ema_decay)

@@ -27,6 +27,50 @@ def bump_param_epoch():
     _PARAM_EPOCH[0] += 1
 
 
+# Weight gradients on a side stream.  Inside ``async_wgrad()`` (the model's backward), every
+# conv / linear weight gradient that accumulates straight into a FlatParams .grad is launched on a
+# per-device side stream forked from the current stream: its split-K kernel and slab reduce then
+# overlap the dgrad chain of the main stream (dgrad i and wgrad i only share their inputs), filling
+# kernel tails and the memory-bound reduce under MFMA-bound dgrads.  Operands are record_stream'ed
+# to the side stream; leaving the context joins it (the current stream waits on it), so the
+# optimizer, the bucketed all-reduce and any reader of .grad see finished gradients.  Results are
+# the same kernels on the same inputs: bitwise equal to the single-stream order.
+_ASYNC = {'depth': 0, 'streams': {}, 'used': False}
+
+
+def _side_stream(device):
+    st = _ASYNC['streams'].get(device)
+    if st is None:
+        st = _ASYNC['streams'][device] = torch.cuda.Stream(device)
+    return st
+
+
+def async_side_stream(device=None):
+    """The side stream weight gradients are queued on right now (None outside async_wgrad)."""
+    if _ASYNC['depth'] == 0:
+        return None
+    return _side_stream(device if device is not None else torch.device('cuda', torch.cuda.current_device()))
+
+
+class async_wgrad:
+    """Context: weight gradients on the side stream, joined into the current stream on exit."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        if self.enabled:
+            _ASYNC['depth'] += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            _ASYNC['depth'] -= 1
+            for st in _ASYNC['streams'].values():
+                torch.cuda.current_stream(st.device).wait_stream(st)
+        return False
+
+
 def pad8(c):
     return (c + 7) // 8 * 8
 
@@ -275,6 +319,24 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
     d.ksize = kw.get('ksize', 3)
     lib = _lib.load()
     ws_bytes = lib.sr_conv3x3_wgrad_workspace(d)
+    # (a traced step stays single-stream: its per-kernel event spans then time each kernel alone)
+    side = async_side_stream(x.device) if tw is not None and not ktrace.active() else None
+    if side is not None:  # fork: dy / x are ready on the current stream
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        for t in (dy, x, kw.get('co_map'), kw.get('ci_map')):
+            if t is not None:
+                t.record_stream(side)
+        with torch.cuda.stream(side):
+            _wgrad_launch(lib, d, dy, x, ws_bytes, tw, tb, cin_real, cout_real, need_bias, kw)
+        grad_ready(params[0])
+        if need_bias:
+            grad_ready(params[1])
+        return None, None
+    return _wgrad_launch(lib, d, dy, x, ws_bytes, tw, tb, cin_real, cout_real, need_bias, kw, params)
+
+
+def _wgrad_launch(lib, d, dy, x, ws_bytes, tw, tb, cin_real, cout_real, need_bias, kw, params=None):
+    N, H, W, cin, cout = d.N, d.H, d.W, d.Cin, d.Cout
     ws = torch.empty(ws_bytes // 4 + 1, device=x.device, dtype=torch.float32)
     kk = 3 if d.ksize == 3 else 1
     if tw is not None:
@@ -290,13 +352,14 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
         scratch = (torch.empty_like(dw), torch.empty_like(db) if db is not None else None)
         rargs = args[:5] + (_lib.ptr(scratch[0]), _lib.ptr(scratch[1])) + args[7:]
         keep = (dy, x, ws, scratch, kw.get('co_map'), kw.get('ci_map'))
-        relaunch = lambda a=rargs, k=keep: lib.sr_conv3x3_wgrad(*a)  # noqa: E731
+        # on the stream current at relaunch time (a side-stream launch is re-timed on the timing stream)
+        relaunch = lambda a=rargs, k=keep: lib.sr_conv3x3_wgrad(*a[:-1], _lib.stream())  # noqa: E731
     else:
         relaunch = None
     with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * kk * kk * cin_real * cout_real,
                      x.element_size() * M * (cin + cout) + 4 * kk * kk * cin * cout, relaunch=relaunch):
         _lib.check(lib.sr_conv3x3_wgrad(*args))
-    if tw is not None:
+    if tw is not None and params is not None:
         grad_ready(params[0])
         if need_bias:
             grad_ready(params[1])

@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _lib
-from ..ops.conv import bump_param_epoch, on_grad_ready, refresh_prepared
+from ..ops.conv import async_side_stream, bump_param_epoch, on_grad_ready, refresh_prepared
 
 
 def _params(module):
@@ -204,7 +204,16 @@ class GradBucketReducer:
 
     def _issue(self, b, when):
         lo, hi, _ = self.buckets[b]
-        self.handles.append(dist.all_reduce(self.flat.grad[lo:hi], group=self.group, async_op=True))
+        g = self.flat.grad[lo:hi]
+        side = async_side_stream(g.device) if g.is_cuda else None
+        if side is not None:
+            # weight gradients are being accumulated on the side stream (ops.conv.async_wgrad):
+            # issue from it, after the main stream's gradient kernels so far
+            side.wait_stream(torch.cuda.current_stream(g.device))
+            with torch.cuda.stream(side):
+                self.handles.append(dist.all_reduce(g, group=self.group, async_op=True))
+        else:
+            self.handles.append(dist.all_reduce(g, group=self.group, async_op=True))
         self.issue_log.append((b, when))
 
     def _make_hook(self, i):

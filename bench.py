@@ -56,12 +56,18 @@ WORKLOADS = {
 }
 
 
+# train.async_wgrad per workload (weight gradients on a side stream, ops.conv.async_wgrad), from A/B
+# runs in one GPU call: RCAN 38.9 -> 37.4 ms, SwinIR 49.8 -> 49.5 ms; EDSR 40.4 -> 41.4 and RRDB
+# 65.6 -> 66.9 ms (two full-chip MFMA kernels interfering), so those stay single-stream
+ASYNC_WGRAD = {'rcan': True, 'swinir': True}
+
+
 def make_opt(world, batch, workload='edsr'):
     net, mtype, lr = WORKLOADS[workload][:3]
     return dict(
         model_type=mtype, is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
         network_g=dict(net),
-        train=dict(ema_decay=0.999, use_amp=True, cuda_graph=False,
+        train=dict(ema_decay=0.999, use_amp=True, cuda_graph=False, async_wgrad=ASYNC_WGRAD.get(workload, False),
                    optim_g=dict(type='Adam', lr=lr, weight_decay=0, betas=[0.9, 0.99]),
                    scheduler=dict(type='MultiStepLR', milestones=[200000], gamma=0.5),
                    pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')),

@@ -21,12 +21,12 @@ def _free_port():
     return p
 
 
-def _opt(dist_, world, rank, bucket_mb):
+def _opt(dist_, world, rank, bucket_mb, async_wgrad=False):
     return dict(model_type='SRModel', is_train=True, dist=dist_, num_gpu=1, world_size=world, rank=rank, path={},
                 bucket_cap_mb=bucket_mb,
                 network_g=dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=2, upscale=4,
                                res_scale=1),
-                train=dict(ema_decay=0.999, use_amp=False, optim_g=dict(type='Adam', lr=1e-3, weight_decay=0,
+                train=dict(ema_decay=0.999, use_amp=False, async_wgrad=async_wgrad, optim_g=dict(type='Adam', lr=1e-3, weight_decay=0,
                                                                         betas=[0.9, 0.99]),
                            scheduler=dict(type='MultiStepLR', milestones=[100], gamma=0.5),
                            pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')))
@@ -37,7 +37,7 @@ def _batch(step):
     return torch.rand(4, 3, 16, 16, generator=g), torch.rand(4, 3, 64, 64, generator=g)
 
 
-def _worker(rank, world, port, bucket_mb, q):
+def _worker(rank, world, port, bucket_mb, async_wgrad, q):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
@@ -46,7 +46,7 @@ def _worker(rank, world, port, bucket_mb, q):
     import basicsr4rs_amd.archs  # noqa: F401
     from basicsr4rs_amd.models import build_model
     torch.manual_seed(0 + rank)  # different init per rank: the reducer broadcasts rank 0's
-    model = build_model(_opt(True, world, rank, bucket_mb))
+    model = build_model(_opt(True, world, rank, bucket_mb, async_wgrad))
     for step in (1, 2):
         lq, gt = _batch(step)
         sl = slice(rank * 2, rank * 2 + 2)
@@ -61,14 +61,16 @@ def _worker(rank, world, port, bucket_mb, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('async_wgrad', [False, True])
 @pytest.mark.parametrize('bucket_mb', [25.0, 0.05])
-def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb):
+def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb, async_wgrad):
+    """async_wgrad: weight gradients on the side stream, buckets issued from it (utils/flat.py)."""
     import basicsr4rs_amd.archs  # noqa: F401
     from basicsr4rs_amd.models import build_model
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket_mb, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, bucket_mb, async_wgrad, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
