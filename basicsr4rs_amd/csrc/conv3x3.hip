@@ -2645,6 +2645,8 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
 // shuffle slot width) multiples of 128.  Output: fp32 slab tile staged through LDS and
 // written with 16-B row-contiguous stores.
 // ------------------------------------------------------------------------------------
+// DBG (timing ablations, wrong results): 1 no operand DMA, 2 no MFMA, 3 no slab store
+template <int DBG = 0>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   constexpr int STAGE = 65536;
   constexpr int CSTR = 256 + 4;
@@ -2721,12 +2723,14 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   };
   constexpr uint32_t SLOT_A0 = 0, SLOT_A1 = 16384, SLOT_B0 = 32768, SLOT_B1 = 49152;
   auto issue_a = [&](int ks, int h) {
+    if constexpr (DBG == 1) if (ks > 0) return;
     char* dst = smem + (ks & 1) * STAGE + (h ? SLOT_A1 : SLOT_A0) + w * 2048;
     const uint32_t ua = (uint32_t)(h ? s_ua1 : s_ua0);
 #pragma unroll
     for (int j = 0; j < 2; ++j) glds16(dyr, dst + j * 1024, Rj[j] < s_left ? ua + la[j] : SR_OOB);
   };
   auto issue_b = [&](int ks, int g) {
+    if constexpr (DBG == 1) if (ks > 0) return;
     char* dst = smem + (ks & 1) * STAGE + (g ? SLOT_B1 : SLOT_B0) + w * 2048;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -2768,6 +2772,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](int h, int g) {
+    if constexpr (DBG == 2) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -2847,7 +2852,226 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
     for (int idx = tid; idx < 128 * 64; idx += 512) {
       const int row = idx >> 6, c4 = (idx & 63) * 4;
       const int co = co0 + h * 128 + row, ci = ci0 + c4;
-      if (co < a.Cout && ci < a.Cin) *(f32x4*)(ws + (size_t)co * a.Cin + ci) = *(const f32x4*)(Cs + row * CSTR + c4);
+      if (DBG != 3 && co < a.Cout && ci < a.Cin)
+        *(f32x4*)(ws + (size_t)co * a.Cin + ci) = *(const f32x4*)(Cs + row * CSTR + c4);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Weight gradient, tap-row form (bf16, Cout and Cin multiples of 128, W % 64 == 0): a block owns
+// one kernel row ty and a 128 (co) x 128 (ci) tile of all THREE taps of that row over a pixel
+// K-range.  A 64-pixel K-step is one image-row segment; per step it DMA's the dy tile [64 px][128
+// co] (16 KB) once for the three taps and ONE x halo row [66 px][128 ci] (17 KB: pixels x0-1 ..
+// x0+64 of input row y+ty-1) whose rows t .. t+63 are tap t's B operand -- 33 KB per 3.1 M MACs
+// against the per-tap pp kernel's 64 KB per 4.2 M (ablation on the EDSR-L body shape: that
+// kernel's MFMA-only and DMA-only runs take 117 / 122 us and 192 us together).  Waves (wr, wc)
+// own co wr*64 .. +64 x ci wc*32 .. +32 of every tap (24 accumulator tiles); a K-step is three
+// phases, one per tap (16 MFMAs each, the A fragments read once in the first), waves 4-7 one
+// barrier behind waves 0-3 as in the pp kernels.  Stages are triple-buffered: step t+2's dy
+// (phase 0) and halo row (phase 1) are issued during step t and a counted wait at phase 2 retires
+// step t+1.  Fragment reads finish (lgkmcnt) before each barrier, so a stage refilled after that
+// barrier has no reader left.  Output: the [S][9][Cout][Cin] slab of the pp kernel (same reduce).
+// ------------------------------------------------------------------------------------
+template <int DBG = 0>  // timing ablations (wrong results): 1 no DMA, 2 no MFMA, 3 no lgkmcnt waits
+__global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
+  constexpr int DYB = 64 * 256;          // dy image [64 px][256 B]
+  constexpr int XB = 68 * 256;           // x halo image [66 (68) px][256 B]
+  constexpr int STG = DYB + XB;
+  constexpr int DUMMY = 3 * STG;         // target of the padding DMAs
+  constexpr int CSTR = 128 + 4;
+  constexpr int EPI = 128 * CSTR * 4;    // one tap's 128 x 128 fp32 tile
+  constexpr int SMEM = (DUMMY + 1024 > EPI ? DUMMY + 1024 : EPI);
+  static_assert(SMEM >= 2 * 64 * 512, "bias role LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = 3 * a.tiles_co * a.tiles_ci;
+  const int per_split = ntile + (a.wsb ? (a.Cout + 255) / 256 : 0);
+  const int split = (int)b / per_split;
+  int rem = (int)b - split * per_split;
+  if (rem >= ntile) {
+    wgrad_bias_role(a, smem, split, (rem - ntile) * 256);
+    return;
+  }
+  const int ty = rem / (a.tiles_co * a.tiles_ci);
+  rem -= ty * a.tiles_co * a.tiles_ci;
+  const int co0 = (rem / a.tiles_ci) * 128;
+  const int ci0 = (rem % a.tiles_ci) * 128;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const int rps = a.out_ps > 0 ? a.out_ps : 1;
+
+  // DMA lanes: instruction q of an image covers rows 4q .. 4q+3, lane -> row 4q + (lane >> 4),
+  // 16-B slot lane & 15 holding the logical chunk lc of the swizzled 256-B row
+  auto lchunk = [&](int R) {
+    const int f = (R & 3) | (((R >> 3) & 1) << 2);
+    const int sl = lane & 15;
+    return (((sl >> 1) ^ f) << 1) | (sl & 1);
+  };
+  uint32_t la[2];  // dy rows 8w + 4j + (lane >> 4)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int R = 8 * w + 4 * j + (lane >> 4);
+    la[j] = (uint32_t)(R * rps * a.ldy) * 2u + (uint32_t)lchunk(R) * 16u;
+  }
+  int xR[3];       // halo rows of this wave's 3 instructions (q = w, w + 8, w + 16; q > 16: padding)
+  uint32_t lx[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int q = w + 8 * j;
+    const int R = 4 * q + (lane >> 4);
+    xR[j] = q <= 16 && R < 66 ? R : -1000000;
+    lx[j] = (uint32_t)(R * a.ldx) * 2u + (uint32_t)lchunk(R) * 16u;
+  }
+
+  // scalar state of the step being issued
+  int s_ua = 0, s_ub = 0, s_xm1 = 0, s_yv = 0;
+  auto k_eval = [&](int ks) {
+    const int p0s = p_begin + ks * 64;
+    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
+    const int x0 = p0s - q * a.W;
+    const int n = (int)fdiv((uint32_t)q, a.fd_H);
+    const int y = q - n * a.H;
+    int ua;
+    if (a.out_ps == 0) {
+      ua = (p0s * a.ldy + a.ycoff + co0) * 2;
+    } else {
+      const int r = a.out_ps;
+      const int sl = (int)fdiv((uint32_t)co0, a.fd_cps);
+      const int cch = co0 - sl * a.fd_cps.d;
+      const int si = sl / r, sj = sl - si * r;
+      ua = (((q * r + si) * (a.W * r) + x0 * r + sj) * a.ldy + a.ycoff + cch) * 2;
+    }
+    const int yy = y + ty - 1;
+    s_ua = __builtin_amdgcn_readfirstlane(ua);
+    s_ub = __builtin_amdgcn_readfirstlane((((n * a.H + yy) * a.W + x0 - 1) * a.ldx + a.xcoff + ci0) * 2);
+    s_xm1 = __builtin_amdgcn_readfirstlane(x0 - 1);
+    s_yv = __builtin_amdgcn_readfirstlane((unsigned)yy < (unsigned)a.H ? 1 : 0);
+  };
+  auto issue_dy = [&](int ks, bool real) {
+    if (DBG == 1 && ks > 1) real = false;
+    char* dst = smem + (ks % 3) * STG + w * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(dyr, real ? dst + j * 1024 : smem + DUMMY, real ? (uint32_t)s_ua + la[j] : SR_OOB);
+  };
+  auto issue_x = [&](int ks, bool real) {
+    if (DBG == 1 && ks > 1) real = false;
+    char* img = smem + (ks % 3) * STG + DYB;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int q = w + 8 * j;
+      const bool v = real && s_yv && (unsigned)(s_xm1 + xR[j]) < (unsigned)a.W;
+      glds16(xr, (real && q <= 16) ? img + q * 1024 : smem + DUMMY, v ? (uint32_t)s_ub + lx[j] : SR_OOB);
+    }
+  };
+
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  auto tr8 = [&](const char* base, int r0, int col) -> s16x8 {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0, col * 2, 256)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0 + 4, col * 2, 256)));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  s16x8 fa[2][4], fb[2][2];
+  auto read_a = [&](int st) {
+    const char* As = smem + st * STG;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[kk][i] = tr8(As, kk * 32 + 8 * tg + tq, wr * 64 + i * 16 + 4 * tp);
+  };
+  auto read_b = [&](int st, int t) {
+    const char* Xs = smem + st * STG + DYB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[kk][j] = tr8(Xs, t + kk * 32 + 8 * tg + tq, wc * 32 + j * 16 + 4 * tp);
+  };
+  f32x4 acc[3][4][2];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int t) {
+    if constexpr (DBG == 2) return;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[t][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = (p_end - p_begin) / 64;  // >= 1 (whole 64-px row segments)
+  k_eval(0);
+  issue_dy(0, true);
+  issue_x(0, true);
+  if (nk > 1) k_eval(1);
+  issue_dy(1, nk > 1);
+  issue_x(1, nk > 1);
+  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // step 0 landed (step 1's 5 in flight)
+  pp_barrier();
+  if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const int st = t % 3;
+    const bool more = t + 2 < nk;
+    // phase 0: tap 0, A fragments; issue dy(t + 2)
+    read_a(st);
+    read_b(st, 0);
+    if (more) k_eval(t + 2);
+    issue_dy(t + 2, more);
+    if (DBG != 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    mma(0);
+    pp_barrier();
+    // phase 1: tap 1; issue the halo row of step t + 2
+    read_b(st, 1);
+    issue_x(t + 2, more);
+    if (DBG != 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    mma(1);
+    pp_barrier();
+    // phase 2: tap 2; retire step t + 1 (step t + 2's 5 DMAs stay in flight)
+    read_b(st, 2);
+    if (DBG != 3) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    pp_barrier();
+    mma(2);
+    pp_barrier();
+  }
+  if (!wr) pp_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CSTR + wc * 32 + j * 16 + (lane & 15)] = acc[t][i][j][r];
+    __syncthreads();
+    float* ws = a.ws + ((size_t)split * 9 + ty * 3 + t) * a.Cout * a.Cin;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = tid + k * 512;
+      const int row = idx >> 5, c4 = (idx & 31) * 4;
+      *(f32x4*)(ws + (size_t)(co0 + row) * a.Cin + ci0 + c4) = *(const f32x4*)(Cs + row * CSTR + c4);
     }
   }
 }
@@ -3957,6 +4181,16 @@ bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
 
+// Tap-row wgrad (three taps of a kernel row per block, one x halo row per K-step): bf16 3x3,
+// Cout / Cin (and the shuffle slot width) multiples of 128, W % 64 == 0.  Opt-in (variant 46; 47-49
+// its ablations): on the EDSR-L body shape it measured 236 us against the pp kernel's 184 us --
+// its DMA-only run is faster (99 vs 121 us) but its MFMA + fragment-read run is not (172 vs 116 us).
+bool wg_use_tr3(const sr_conv3x3_wgrad_desc* d) {
+  if (d->dtype != SR_BF16 || d->ksize == 1 || d->in_up > 1 || g_variant < 46 || g_variant > 49) return false;
+  const int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 128;
+  return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
+}
+
 // the row-streaming form of it (variant 37: the tile-row form, for A/B)
 bool wg_use_ring() { return g_variant != 37; }
 // All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2.
@@ -3992,9 +4226,21 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     *kper = kp;
     return;
   }
+  if (wg_use_tr3(d)) {
+    const int tiles = 3 * (d->Cout / 128) * (d->Cin / 128) + (d->Cout + 255) / 256;
+    int S = 256 / tiles;
+    const int maxS = M / 256 > 1 ? M / 256 : 1;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
   if (wg_use_big(d)) {
     bm = bn = 256;
-    target = 256;
+    target = g_variant == 44 ? 512 : (g_variant == 45 ? 128 : 256);  // 44 / 45: split-count A/B
     extra = (d->Cout + 255) / 256;
   } else {
     wg_tiles(d->Cout, d->Cin, &bm, &bn);
@@ -4129,6 +4375,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
   if (wg_use_halo(d)) return wg_use_ring() ? "conv3x3_wgrad_ring_kernel" : "conv3x3_wgrad_halo_kernel";
+  if (wg_use_tr3(d)) return "conv3x3_wgrad_tr3_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
@@ -4137,8 +4384,8 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 39)
-    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-33: schedule A/B switches)");
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 49)
+    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
 }
@@ -4212,12 +4459,25 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<3>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<4>, grid, dim3(256), 0, s, a);
     e = hipGetLastError();
+  } else if (wg_use_tr3(d)) {
+    a.tiles_co = a.Cout / 128;
+    a.tiles_ci = a.Cin / 128;
+    const int per_split = 3 * a.tiles_co * a.tiles_ci + (a.wsb ? (a.Cout + 255) / 256 : 0);
+    if (g_variant == 47) hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<1>, dim3(S * per_split), dim3(512), 0, s, a);
+    else if (g_variant == 48) hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<2>, dim3(S * per_split), dim3(512), 0, s, a);
+    else if (g_variant == 49) hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<3>, dim3(S * per_split), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<0>, dim3(S * per_split), dim3(512), 0, s, a);
+    e = hipGetLastError();
   } else if (wg_use_big(d)) {
     a.tiles_co = (a.Cout + 255) / 256;
     a.tiles_ci = (a.Cin + 255) / 256;
     const int per_split = taps * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
-    if (wg_use_pp(d))
-      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel, dim3(S * per_split), dim3(512), 0, s, a);
+    if (wg_use_pp(d) && g_variant >= 41 && g_variant <= 43) {  // timing ablations (wrong results)
+      if (g_variant == 41) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<1>, dim3(S * per_split), dim3(512), 0, s, a);
+      else if (g_variant == 42) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<2>, dim3(S * per_split), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<3>, dim3(S * per_split), dim3(512), 0, s, a);
+    } else if (wg_use_pp(d))
+      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * per_split), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
     e = hipGetLastError();

@@ -243,6 +243,46 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize('shape', [(2, 6, 64, 128, 128, 0), (1, 4, 192, 256, 128, 0), (32, 8, 64, 256, 256, 0),
+                                   (2, 2, 128, 128, 512, 2), (1, 5, 64, 384, 256, 0), (3, 3, 128, 256, 1024, 2),
+                                   (1, 1, 64, 128, 256, 0)])
+def test_wgrad_tr3_vs_fp64(cuda, shape):
+    """Tap-row wgrad kernel (three taps of a kernel row per block from one x halo row per K-step;
+    image top / bottom rows, the left / right halo columns, multi-image splits, pixel-shuffled dy)
+    against fp64 on the same bf16 operands and against the per-tap pp kernel (variant 0); opt-in (variant 46)."""
+    N, H, W, cin, cout, ps = shape
+    torch.manual_seed(12)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin).to(dt)
+    if ps:
+        dy = torch.randn(N, H * ps, W * ps, cout // (ps * ps)).to(dt)
+        dy_gemm = O.pixel_unshuffle(dy.permute(0, 3, 1, 2).double(), ps)
+    else:
+        dy = torch.randn(N, H, W, cout).to(dt)
+        dy_gemm = dy.permute(0, 3, 1, 2).double()
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, dy.shape[-1], ps, 3
+    outs = []
+    try:
+        _lib.check(lib.sr_conv3x3_set_variant(46))  # the tap-row kernel is opt-in
+        assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_tr3_kernel'
+        for variant in (46, 0):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy_gemm).sum().backward()
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
+    assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+
+
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
                                    (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
