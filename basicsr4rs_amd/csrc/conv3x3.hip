@@ -3846,19 +3846,71 @@ __global__ void prep_kernel(const float* w, const float* bias, int Cout_real, in
 }
 
 // All of a net's cached GEMM images in one launch (after an optimizer step): block b belongs
-// to the item whose [block_start[k], block_start[k+1]) range holds it.
+// to the item whose [block_start[k], block_start[k+1]) range holds it, and owns a 32 (GEMM row n)
+// x 32 (channel ci) tile of it, all taps.  The tile is read coalesced along (ci, tap) -- the
+// fp32 [Cout][Cin][taps] layout -- into LDS, then written as 64-B runs along ci (wf rows) and
+// along n (wd rows), instead of one scattered 2-B store per element per image.
+constexpr int PREP_T = 32;
 template <typename T>
-__global__ void prep_batch_kernel(const sr_prep_item* __restrict__ items, const int* __restrict__ block_start, int n) {
-  const int b = blockIdx.x;
+__global__ __launch_bounds__(256) void prep_batch_kernel(const sr_prep_item* __restrict__ items,
+                                                         const int* __restrict__ block_start, int n) {
+  __shared__ float tile[PREP_T][9][PREP_T + 1];
+  const int b = blockIdx.x, tid = threadIdx.x;
   int lo = 0, hi = n - 1;  // last k with block_start[k] <= b
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (block_start[mid] <= b) lo = mid; else hi = mid - 1;
   }
   const sr_prep_item it = items[lo];
-  prep_elem<T>(it.w, it.bias, it.Cout_real, it.Cin_real, it.Cout, it.Cin, it.out_ps, it.ksize == 1 ? 1 : 9,
-               it.row_map, it.col_map, (T*)it.wf, (T*)it.wd, it.bias_g,
-               (int64_t)(b - block_start[lo]) * blockDim.x + threadIdx.x);
+  const int taps = it.ksize == 1 ? 1 : 9;
+  const int tci = (it.Cin + PREP_T - 1) / PREP_T;
+  const int t = b - block_start[lo];
+  const int n0 = (t / tci) * PREP_T, c0 = (t % tci) * PREP_T;
+  const int r2 = it.out_ps > 0 ? it.out_ps * it.out_ps : 1;
+  const int cps = it.Cout_real / r2;
+  auto row_of = [&](int nn) -> int {
+    if (it.row_map) return it.row_map[nn];
+    if (nn >= it.Cout_real) return -1;
+    return it.out_ps > 0 ? (nn % cps) * r2 + nn / cps : nn;
+  };
+  const int per = PREP_T * taps;  // elements per GEMM row of the tile
+  for (int idx = tid; idx < PREP_T * per; idx += 256) {
+    const int nl = idx / per, rem = idx - nl * per;
+    const int cil = rem / taps, tap = rem - cil * taps;
+    const int nn = n0 + nl, ci = c0 + cil;
+    float v = 0.f;
+    if (nn < it.Cout && ci < it.Cin) {
+      const int co = row_of(nn);
+      const int cs = it.col_map ? it.col_map[ci] : (ci < it.Cin_real ? ci : -1);
+      if (co >= 0 && cs >= 0) v = it.w[((size_t)co * it.Cin_real + cs) * taps + tap];
+    }
+    tile[nl][tap][cil] = v;
+  }
+  if (it.bias_g && c0 == 0 && tid < PREP_T) {
+    const int nn = n0 + tid;
+    if (nn < it.Cout) {
+      const int co = row_of(nn);
+      it.bias_g[nn] = (co >= 0 && it.bias) ? it.bias[co] : 0.f;
+    }
+  }
+  __syncthreads();
+  T* wf = (T*)it.wf;
+  T* wd = (T*)it.wd;
+  for (int idx = tid; idx < PREP_T * per; idx += 256) {
+    if (wf) {  // wf[n][tap][ci]: runs along ci
+      const int nl = idx / per, rem = idx - nl * per;
+      const int tap = rem / PREP_T, cil = rem - tap * PREP_T;
+      const int nn = n0 + nl, ci = c0 + cil;
+      if (nn < it.Cout && ci < it.Cin) wf[(size_t)nn * taps * it.Cin + (size_t)tap * it.Cin + ci] = Elt<T>::from_f(tile[nl][tap][cil]);
+    }
+    if (wd) {  // wd[ci][taps - 1 - tap][n]: runs along n
+      const int cil = idx / per, rem = idx - cil * per;
+      const int tap = rem / PREP_T, nl = rem - tap * PREP_T;
+      const int nn = n0 + nl, ci = c0 + cil;
+      if (nn < it.Cout && ci < it.Cin)
+        wd[(size_t)ci * taps * it.Cout + (size_t)(taps - 1 - tap) * it.Cout + nn] = Elt<T>::from_f(tile[nl][tap][cil]);
+    }
+  }
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -4240,7 +4292,7 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
   }
   if (wg_use_big(d)) {
     bm = bn = 256;
-    target = g_variant == 44 ? 512 : (g_variant == 45 ? 128 : 256);  // 44 / 45: split-count A/B
+    target = g_variant == 44 ? 512 : (g_variant == 45 ? 128 : 256);  // 44 / 45: split-count A/B (512: 40.2 -> 41.7 ms EDSR step)
     extra = (d->Cout + 255) / 256;
   } else {
     wg_tiles(d->Cout, d->Cin, &bm, &bn);
@@ -4558,9 +4610,7 @@ int sr_conv_prep_mapped(int dtype, int ksize, const float* w, const float* bias,
 }
 
 int sr_conv_prep_blocks(const sr_prep_item* it) {
-  const int64_t total = (int64_t)it->Cout * it->Cin * (it->ksize == 1 ? 1 : 9);
-  const int64_t work = total > it->Cout ? total : it->Cout;
-  return (int)((work + 255) / 256);
+  return ((it->Cout + PREP_T - 1) / PREP_T) * ((it->Cin + PREP_T - 1) / PREP_T);
 }
 
 int sr_conv_prep_batch(int dtype, const sr_prep_item* items, const int* block_start, int n, int total_blocks,

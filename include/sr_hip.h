@@ -152,7 +152,7 @@ typedef struct {
   void* wd;
   float* bias_g;
 } sr_prep_item;
-/* 256-thread blocks item needs (host helper for building block_start). */
+/* Blocks (32 x 32 GEMM-row x channel tiles) item needs (host helper for building block_start). */
 int sr_conv_prep_blocks(const sr_prep_item* item);
 /* sr_conv_prep_mapped for n items in ONE launch: items and block_start (n + 1 prefix sums of
  * sr_conv_prep_blocks, block_start[n] = total_blocks) in device memory, all items of dtype.
