@@ -726,40 +726,51 @@ __global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
   for (int d = 0; d < 7; ++d)
 #pragma unroll
     for (int r = 0; r < 4; ++r) dbs[d][r] = 0.f;
-  for (int k = lane; k < 225; k += 64) sBin[k] = 0.f;
   const bf16_t* qkv = (const bf16_t*)a.qkv;
+  // the head's bias table once per wave (the same for its ATT_UPW windows)
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (lane + 64 * k < 225) {
+      sT[lane + 64 * k] = a.bias_table[(lane + 64 * k) * a.nH + h];
+      sBin[lane + 64 * k] = 0.f;
+    }
+  // global loads of window uw: issued one window ahead (wave occupancy is 1 per SIMD: nothing
+  // else hides their latency), consumed by the next iteration
+  int64_t pix[4];
+  u32x4 qu[4], ku[4], vu[4], du[4], ou[4];
+  f32x4 l4[4];
+  auto fetch = [&](int uw, int64_t* px, u32x4* q_, u32x4* k_, u32x4* v_, u32x4* d_, u32x4* o_, f32x4* l_) {
+    const int wg = win0 + uw;
+    if (uw >= ATT_UPW || wg >= a.N * a.nwin) return;
+    const int unit = wg * a.nH + h;
+    const int n = wg / a.nwin, win = wg - n * a.nwin;
+    const int wy = win / a.nwx, wx = win - (win / a.nwx) * a.nwx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      px[i] = token_pixel(a, n, wy, wx, 16 * i + c);
+      const bf16_t* row = qkv + px[i] * a.ldq + g * 8;
+      q_[i] = *(const u32x4*)(row + h * 32);
+      k_[i] = *(const u32x4*)(row + (a.nH + h) * 32);
+      v_[i] = *(const u32x4*)(row + (2 * a.nH + h) * 32);
+      const int64_t orow = px[i] * a.ldo + h * 32 + g * 8;
+      d_[i] = *(const u32x4*)((const bf16_t*)a.dout + orow);
+      o_[i] = *(const u32x4*)((const bf16_t*)a.out + orow);
+      l_[i] = *(const f32x4*)(a.lse + (int64_t)unit * 64 + 16 * i + 4 * g);
+    }
+  };
+  fetch(0, pix, qu, ku, vu, du, ou, l4);
   for (int uw = 0; uw < ATT_UPW; ++uw) {
   const int wg = win0 + uw;  // global window index n * nwin + win
   if (wg >= a.N * a.nwin) break;
-  const int unit = wg * a.nH + h;
   const int n = wg / a.nwin, win = wg - n * a.nwin;
   const int wy = win / a.nwx, wx = win - (win / a.nwx) * a.nwx;
-  int64_t pix[4];
   s16x8 qf[4], kf[4], vf[4], df[4];
-  u32x4 qu[4], ku[4], du[4], ou[4];
-  f32x4 l4[4];
-  // every global load of the unit first (one round trip), then the LDS images
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    pix[i] = token_pixel(a, n, wy, wx, 16 * i + c);
-    const bf16_t* row = qkv + pix[i] * a.ldq + g * 8;
-    qu[i] = *(const u32x4*)(row + h * 32);
-    ku[i] = *(const u32x4*)(row + (a.nH + h) * 32);
-    vf[i] = __builtin_bit_cast(s16x8, *(const u32x4*)(row + (2 * a.nH + h) * 32));
-    const int64_t orow = pix[i] * a.ldo + h * 32 + g * 8;
-    du[i] = *(const u32x4*)((const bf16_t*)a.dout + orow);
-    ou[i] = *(const u32x4*)((const bf16_t*)a.out + orow);
-    l4[i] = *(const f32x4*)(a.lse + (int64_t)unit * 64 + 16 * i + 4 * g);
-  }
-  float tv[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) tv[k] = lane + 64 * k < 225 ? a.bias_table[(lane + 64 * k) * a.nH + h] : 0.f;
-  __builtin_amdgcn_sched_barrier(0);  // keep all 28 loads ahead of their first use
   float dd[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     qf[i] = __builtin_bit_cast(s16x8, qu[i]);
     kf[i] = __builtin_bit_cast(s16x8, ku[i]);
+    vf[i] = __builtin_bit_cast(s16x8, vu[i]);
     df[i] = __builtin_bit_cast(s16x8, du[i]);
     *(u32x4*)(sQ + sx_off(16 * i + c, g)) = qu[i];
     *(u32x4*)(sK + sx_off(16 * i + c, g)) = ku[i];
@@ -771,15 +782,21 @@ __global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
            bf16_to_f32(du[i][e] >> 16) * bf16_to_f32(ou[i][e] >> 16);
     dd[i] = t;
   }
+  f32x4 lc4[4];
+  int64_t pxc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    lc4[i] = l4[i];
+    pxc[i] = pix[i];
+  }
+  // the next window's loads, in flight under this window's work
+  fetch(uw + 1, pix, qu, ku, vu, du, ou, l4);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     dd[i] += __shfl_xor(dd[i], 16);
     dd[i] += __shfl_xor(dd[i], 32);
     if (g == 0) sD[16 * i + c] = dd[i];
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (lane + 64 * k < 225) sT[lane + 64 * k] = tv[k];
   __syncthreads();
 
   // S = Q K^T and dP = dO V^T: [query 16i + 4g + r][key 16j + c]
@@ -820,7 +837,7 @@ __global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         float v = pa[i][j][r] * a.scale + bt[i - j + 3][r];
         if (a.shift && rq[i][r] != rk[j]) v -= 100.f;
-        const float p = __expf(v - l4[i][r]);
+        const float p = __expf(v - lc4[i][r]);
         const float dsv = p * (ds[i][j][r] - Dq[i][r]);
         pa[i][j][r] = p;
         ds[i][j][r] = dsv;
@@ -879,7 +896,7 @@ __global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
   bf16_t* gq = (bf16_t*)a.y;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    bf16_t* row = gq + pix[j] * a.ldq + 4 * g;
+    bf16_t* row = gq + pxc[j] * a.ldq + 4 * g;
 #pragma unroll
     for (int d = 0; d < 2; ++d) {
       uint2 w;
