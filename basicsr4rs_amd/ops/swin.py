@@ -46,6 +46,11 @@ class LinearSpec:
             for k, c in enumerate(col_map):
                 if c >= 0:
                     ci_map[c] = k
+        # identity maps are dropped: the slab reduce then reads 16-B rows instead of gathering
+        if co_map is not None and co_map == list(range(cout)):
+            co_map = None
+        if ci_map is not None and ci_map == list(range(cin)):
+            ci_map = None
         self.co_map, self.ci_map = co_map, ci_map
         self._dev = {}
 

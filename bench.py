@@ -57,9 +57,14 @@ WORKLOADS = {
 
 
 # train.async_wgrad per workload (weight gradients on a side stream, ops.conv.async_wgrad), from A/B
-# runs in one GPU call: RCAN 38.9 -> 37.4 ms, SwinIR 49.8 -> 49.5 ms; EDSR 40.4 -> 41.4 and RRDB
+# runs in one GPU call: RCAN graph 38.9 -> 37.4 ms but eager 54.5 -> 71.5 ms (its eager step is
+# host-bound: 2.7k launches, and the fork / record_stream per weight gradient add host time), so
+# RCAN takes it only with the HIP graph; SwinIR eager 49.1 -> 46.8 ms; EDSR 40.4 -> 41.4 and RRDB
 # 65.6 -> 66.9 ms (two full-chip MFMA kernels interfering), so those stay single-stream
-ASYNC_WGRAD = {'rcan': True, 'swinir': True}
+ASYNC_WGRAD = {'rcan': 'graph', 'swinir': True}
+# single-process step mode: HIP-graph replay except SwinIR, whose eager step with side-stream weight
+# gradients runs 46.7-47.2 ms against 49.0 ms replayed (the replay overlaps the two streams less)
+GRAPH_DEFAULT = {'swinir': False}
 
 
 def make_opt(world, batch, workload='edsr'):
@@ -67,7 +72,7 @@ def make_opt(world, batch, workload='edsr'):
     return dict(
         model_type=mtype, is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
         network_g=dict(net),
-        train=dict(ema_decay=0.999, use_amp=True, cuda_graph=False, async_wgrad=ASYNC_WGRAD.get(workload, False),
+        train=dict(ema_decay=0.999, use_amp=True, cuda_graph=False, async_wgrad=bool(ASYNC_WGRAD.get(workload, False)),
                    optim_g=dict(type='Adam', lr=lr, weight_decay=0, betas=[0.9, 0.99]),
                    scheduler=dict(type='MultiStepLR', milestones=[200000], gamma=0.5),
                    pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')),
@@ -212,8 +217,10 @@ def main():
     hr_px_tile = (4 * lr_px) ** 2
     opt = make_opt(world, B, args.workload)
     opt['rank'] = rank
-    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    use_graph = (world == 1 and GRAPH_DEFAULT.get(args.workload, True)) if args.graph < 0 else bool(args.graph)
     opt['train']['cuda_graph'] = use_graph
+    if ASYNC_WGRAD.get(args.workload) == 'graph':
+        opt['train']['async_wgrad'] = use_graph
     model = build_model(opt)
     g0 = torch.Generator(device=dev).manual_seed(0 + rank)
     g1 = torch.Generator(device=dev).manual_seed(1 + rank)
@@ -328,7 +335,8 @@ def main():
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
             'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
             'config': {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
-                       'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph},
+                       'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph,
+                       'async_wgrad': bool(opt['train']['async_wgrad'])},
             'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
             'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu, 'parity': parity,
         }
