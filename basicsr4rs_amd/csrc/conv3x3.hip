@@ -2875,10 +2875,10 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
 // ------------------------------------------------------------------------------------
 template <int DBG = 0>  // timing ablations (wrong results): 1 no DMA, 2 no MFMA, 3 no lgkmcnt waits
 __global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
-  constexpr int DYB = 64 * 256;          // dy image [64 px][256 B]
-  constexpr int XB = 68 * 256;           // x halo image [66 (68) px][256 B]
-  constexpr int STG = DYB + XB;
-  constexpr int DUMMY = 3 * STG;         // target of the padding DMAs
+  constexpr int DYB = 64 * 256;          // dy image [64 px][256 B], stage s at s * DYB
+  constexpr int XB = 68 * 256;           // x halo image [66 (68) px][256 B], stage s at XOFF + s * XB
+  constexpr int XOFF = 3 * DYB;
+  constexpr int DUMMY = XOFF + 3 * XB;   // target of the padding DMAs
   constexpr int CSTR = 128 + 4;
   constexpr int EPI = 128 * CSTR * 4;    // one tap's 128 x 128 fp32 tile
   constexpr int SMEM = (DUMMY + 1024 > EPI ? DUMMY + 1024 : EPI);
@@ -2955,13 +2955,13 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
   };
   auto issue_dy = [&](int ks, bool real) {
     if (DBG == 1 && ks > 1) real = false;
-    char* dst = smem + (ks % 3) * STG + w * 2048;
+    char* dst = smem + (ks % 3) * DYB + w * 2048;
 #pragma unroll
     for (int j = 0; j < 2; ++j) glds16(dyr, real ? dst + j * 1024 : smem + DUMMY, real ? (uint32_t)s_ua + la[j] : SR_OOB);
   };
   auto issue_x = [&](int ks, bool real) {
     if (DBG == 1 && ks > 1) real = false;
-    char* img = smem + (ks % 3) * STG + DYB;
+    char* img = smem + XOFF + (ks % 3) * XB;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int q = w + 8 * j;
@@ -2970,28 +2970,40 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
     }
   };
 
+  // Fragment reads: per-lane swizzled offsets computed once (kk = 0 rows; kk = 1 is +8192 B, the
+  // stage a compile-time offset), so a read costs no VALU (the per-read swz_tr math doubled the
+  // kernel's VALU count against the pp kernel's)
   const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-  auto tr8 = [&](const char* base, int r0, int col) -> s16x8 {
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0, col * 2, 256)));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0 + 4, col * 2, 256)));
-    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  uint32_t offA[4][2], offX[3][2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) offA[i][hl] = swz_tr(8 * tg + tq + 4 * hl, (wr * 64 + i * 16 + 4 * tp) * 2, 256);
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl)
+        offX[t][j][hl] = XOFF + swz_tr(t + 8 * tg + tq + 4 * hl, (wc * 32 + j * 16 + 4 * tp) * 2, 256);
+  auto lds_tr = [&](uint32_t off) -> s16x4 {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(smem + off));
   };
+  auto cat8 = [](s16x4 lo, s16x4 hi) { return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}; };
   s16x8 fa[2][4], fb[2][2];
   auto read_a = [&](int st) {
-    const char* As = smem + st * STG;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[kk][i] = tr8(As, kk * 32 + 8 * tg + tq, wr * 64 + i * 16 + 4 * tp);
+      for (int i = 0; i < 4; ++i)
+        fa[kk][i] = cat8(lds_tr(offA[i][0] + st * DYB + kk * 8192), lds_tr(offA[i][1] + st * DYB + kk * 8192));
   };
   auto read_b = [&](int st, int t) {
-    const char* Xs = smem + st * STG + DYB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[kk][j] = tr8(Xs, t + kk * 32 + 8 * tg + tq, wc * 32 + j * 16 + 4 * tp);
+      for (int j = 0; j < 2; ++j)
+        fb[kk][j] = cat8(lds_tr(offX[t][j][0] + st * XB + kk * 8192), lds_tr(offX[t][j][1] + st * XB + kk * 8192));
   };
   f32x4 acc[3][4][2];
 #pragma unroll
@@ -3023,9 +3035,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
   asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // step 0 landed (step 1's 5 in flight)
   pp_barrier();
   if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
-#pragma unroll 1
-  for (int t = 0; t < nk; ++t) {
-    const int st = t % 3;
+  auto step = [&](int t, const int st) {
     const bool more = t + 2 < nk;
     // phase 0: tap 0, A fragments; issue dy(t + 2)
     read_a(st);
@@ -3050,7 +3060,9 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
     pp_barrier();
     mma(2);
     pp_barrier();
-  }
+  };
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) step(t, t % 3);  // (a 3-way unrolled stage loop spilled)
   if (!wr) pp_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
