@@ -55,6 +55,7 @@ SIGNATURES = {
     'sr_version': (ctypes.c_char_p, []),
     'sr_last_error': (ctypes.c_char_p, []),
     'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_linear_ln_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_conv3x3_fwd_colsum_parts': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_set_variant': (_i, [_i]),
     'sr_conv3x3_set_stamps': (_i, [_vp]),

@@ -62,6 +62,14 @@ struct FwdArgs {
   unsigned long long* stamps;  // diagnostics: per-row clock stamps of the band kernel (null = off)
   const float* row_scale;  // optional per-image factor on alpha (SwinIR stochastic depth)
   FastDiv fd_hw;           // divide by H*W (pixel -> image)
+  // LayerNorm of the input rows fused into the lin kernel's prologue (sr_linear_ln_fwd)
+  const float* ln_g;
+  const float* ln_b;
+  void* ln_out;  // the normalised rows [M][Cin] (bf16), for the weight gradient and backward
+  float* ln_mean;
+  float* ln_rstd;
+  int ln_C;      // channels normalised (the rest of the Cin padded columns are written as zeros)
+  float ln_eps;
 };
 
 // alpha of output row m: a.alpha, times the per-image row_scale when given
@@ -1092,7 +1100,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // 5 res2, 6 aux, 7 row_scale, uniform per block: H*W % MT == 0): its operand loads for a pass are
 // issued before the pass's MFMAs, so they land under them; E = -1: run-time flags, loads next to
 // their use (every combination).
-template <int MT, int MAXCG, int NPASS, int E>
+template <int MT, int MAXCG, int NPASS, int E, bool LN = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
   constexpr int NMT = MT / 16;  // token tiles per wave (every wave covers all MT tokens)
   constexpr bool CE = E >= 0;
@@ -1108,6 +1116,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, a.w_bytes);
 
+  __shared__ float sgb[LN ? 2 * 192 : 1];  // LN: gamma, beta (channels < 192)
+  if constexpr (LN) {
+    for (int c = tid; c < 192; c += 256) {
+      sgb[c] = c < a.ln_C ? a.ln_g[c] : 0.f;
+      sgb[192 + c] = c < a.ln_C ? a.ln_b[c] : 0.f;
+    }
+  }
   // ---- stage the MT x K token tile: piece p = (chunk group cg, 8-row group rg)
   {
     const int npieces = CG * (MT / 8);
@@ -1120,6 +1135,68 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       glds16(xr, smem + (cg * MT + rg * 8) * 128, v ? (uint32_t)(((size_t)m * a.ldx + a.xcoff + ch * 8) * 2) : SR_OOB);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if constexpr (LN) {
+    // LayerNorm of the staged rows in place (fp32 statistics, two lanes per row over alternate
+    // 16-B chunks held in registers: one LDS read per chunk), gamma / beta from LDS, the
+    // normalised rows also stored to ln_out with the row mean / rstd: the standalone LN kernel's
+    // read of x and this kernel's read of its output become one read
+    constexpr int MAXQ = MAXCG * 4;  // chunks per lane (2 lanes per row, MAXCG * 8 chunks)
+    const int row = tid >> 1, half = tid & 1, m = m0 + row;
+    auto chunk_ptr = [&](int ch) -> u32x4* {
+      return (u32x4*)(smem + (ch >> 3) * MT * 128 + row * 128 + (((ch & 7) ^ (row & 7)) << 4));
+    };
+    u32x4 raw[MAXQ];
+    float sm = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      const int ch = half + 2 * q;
+      raw[q] = ch < KC ? *chunk_ptr(ch) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 8 + 2 * j;
+        sm += (c < a.ln_C ? bf16_to_f32(raw[q][j] & 0xffff) : 0.f) + (c + 1 < a.ln_C ? bf16_to_f32(raw[q][j] >> 16) : 0.f);
+      }
+    }
+    sm += __shfl_xor(sm, 1);
+    const float mu = sm / a.ln_C;
+    float sq = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      const int ch = half + 2 * q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 8 + 2 * j;
+        const float d0 = c < a.ln_C ? bf16_to_f32(raw[q][j] & 0xffff) - mu : 0.f;
+        const float d1 = c + 1 < a.ln_C ? bf16_to_f32(raw[q][j] >> 16) - mu : 0.f;
+        sq += d0 * d0 + d1 * d1;
+      }
+    }
+    sq += __shfl_xor(sq, 1);
+    const float rs = rsqrtf(sq / a.ln_C + a.ln_eps);
+    __syncthreads();  // gamma / beta staged (below the token DMA wait) by every wave
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+      const int ch = half + 2 * q;
+      if (ch >= KC) break;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = ch * 8 + j;
+        const float xv = bf16_to_f32((raw[q][j >> 1] >> (16 * (j & 1))) & 0xffff);
+        o[j] = c < a.ln_C ? (xv - mu) * rs * sgb[c] + sgb[192 + c] : 0.f;
+      }
+      u32x4 r;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
+      *chunk_ptr(ch) = r;
+      if (m < a.M) *(u32x4*)((bf16_t*)a.ln_out + (size_t)m * K + ch * 8) = r;
+    }
+    if (half == 0 && m < a.M) {
+      a.ln_mean[m] = mu;
+      a.ln_rstd[m] = rs;
+    }
     __syncthreads();
   }
 
@@ -4409,6 +4486,40 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = d->dtype == SR_BF16 ? dispatch_fwd<bf16_t>(a, s) : dispatch_fwd<float>(a, s);
   return sr_check(e, "conv3x3_fwd launch");
+}
+
+int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_gamma, const float* ln_beta, int ln_C,
+                     float eps, void* ln_out, float* ln_mean, float* ln_rstd, const void* w, const float* bias, void* y,
+                     void* aux, void* stream) {
+  if (!d || !x || !ln_gamma || !ln_beta || !ln_out || !ln_mean || !ln_rstd || !w || !y)
+    return sr_fail(SR_EINVAL, "linear_ln_fwd: null pointer");
+  if (d->dtype != SR_BF16 || d->ksize != 1 || d->Cin % 8 || d->Cout % 8 || d->ldx != d->Cin || d->xcoff != 0 ||
+      ln_C <= 0 || ln_C > d->Cin || d->ldw < d->Cin)
+    return sr_fail(SR_EINVAL, "linear_ln_fwd: bf16 1x1 conv over dense rows (ldx == Cin) with ln_C <= Cin");
+  FwdArgs a = fwd_shape(d);
+  if (!fwd_use_lin(a, true)) return sr_fail(SR_EINVAL, "linear_ln_fwd: shape not on the lin kernel (Cin <= 192, Cout <= 640)");
+  a.aux = aux;
+  const int e = lin_epi(a);
+  if (e != 0 && e != 67) return sr_fail(SR_EINVAL, "linear_ln_fwd: epilogue must be plain or GELU + pre-activation aux");
+  const size_t xb = (size_t)a.M * d->ldx * 2, wb = (size_t)d->Cout * d->ldw * 2;
+  if (xb >= 0x80000000ull || wb >= 0x80000000ull) return sr_fail(SR_ETOOBIG, "linear_ln_fwd: tensor >= 2 GiB");
+  a.x = x; a.w = w; a.bias = bias; a.y = y;
+  a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
+  a.ln_g = ln_gamma; a.ln_b = ln_beta; a.ln_out = ln_out; a.ln_mean = ln_mean; a.ln_rstd = ln_rstd;
+  a.ln_C = ln_C; a.ln_eps = eps;
+  a.tiles = (a.M + 127) / 128;
+  hipStream_t s = (hipStream_t)stream;
+#define SR_LNL(NP_)                                                                                       \
+  case NP_:                                                                                               \
+    if (e == 0) hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, 0, true>), dim3(a.tiles), dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, 67, true>), dim3(a.tiles), dim3(256), 0, s, a); \
+    break;
+  switch ((a.Cout + 127) / 128) {
+    SR_LNL(1) SR_LNL(2) SR_LNL(3) SR_LNL(4) SR_LNL(5)
+    default: return sr_fail(SR_EINVAL, "linear_ln_fwd: Cout > 640");
+  }
+#undef SR_LNL
+  return sr_check(hipGetLastError(), "linear_ln_fwd launch");
 }
 
 int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d) {

@@ -20,6 +20,8 @@ s = floor(keep + U[0,1)) / keep drawn per forward (archs/swinir_arch.py).  The f
 the proj / fc2 GEMM epilogues (sr_conv3x3_desc.row_scale); the backward scales the branch
 gradients once (sr_row_scale) and feeds them to both the dgrad and the wgrad.
 """
+import os
+
 import torch
 
 from .. import _lib
@@ -131,6 +133,32 @@ def layernorm(x, weight, bias, Creal, eps=1e-5):
                                  _lib.ptr(bias.detach()), M, Creal, Cp, float(eps), _lib.ptr(y), Cp, _lib.ptr(mean),
                                  _lib.ptr(rstd), _lib.stream()))
     return y, mean, rstd
+
+
+def linear_ln_fwd(x, weight, bias, Creal, wf, bg, spec, N, H, W, act=0, aux=None, eps=1e-5):
+    """Linear(LayerNorm(x)) in one launch (sr_linear_ln_fwd: the LayerNorm runs in the lin
+    kernel's prologue on the staged token rows), or None when the call is not on that path
+    (fp32 parity mode, shapes past the lin kernel) -- the caller then runs the two ops.
+    Returns (y, ln, mean, rstd): ln / mean / rstd are what ``layernorm`` returns."""
+    Cp = x.shape[-1]
+    if x.dtype != torch.bfloat16 or Cp != spec.cin_p or spec.cin_p > 192 or spec.cout_p > 640:
+        return None
+    if os.environ.get('SR_LN_UNFUSED') == '1':  # A/B: the standalone LayerNorm kernel + linear
+        return None
+    M = N * H * W
+    ln = torch.empty_like(x)
+    mean = torch.empty(M, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(M, device=x.device, dtype=torch.float32)
+    y = torch.empty(N, H, W, spec.cout_p, device=x.device, dtype=x.dtype)
+    d = C._desc(x.dtype, N, H, W, spec.cin_p, Cp, spec.cout_p, spec.cout_p, spec.cout_p, ksize=1, act=act)
+    lib = _lib.load()
+    with ktrace.span('conv3x3_lin_kernel+ln', 2.0 * M * spec.cin_p * spec.cout_p,
+                     x.element_size() * M * (2 * Cp + spec.cout_p * (2 if aux is not None else 1))):
+        _lib.check(
+            lib.sr_linear_ln_fwd(d, _lib.ptr(x), _lib.ptr(weight.detach()), _lib.ptr(bias.detach()), Creal, float(eps),
+                                 _lib.ptr(ln), _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(wf), _lib.ptr(bg), _lib.ptr(y),
+                                 _lib.ptr(aux), _lib.stream()))
+    return y, ln, mean, rstd
 
 
 def _direct(params):
@@ -247,18 +275,26 @@ class _STB(torch.autograd.Function):
         dtype = x.dtype
         N, H, W, Cp = x.shape
         Cr = geom.dim
-        ln1, m1, r1 = layernorm(x, n1w, n1b, Cr)
         qwf, _, qbg = prepared_linear(qw, qb, geom.qkv, dtype)
-        qkv = linear_fwd(ln1, qwf, qbg, geom.qkv, N, H, W)
+        fused = linear_ln_fwd(x, n1w, n1b, Cr, qwf, qbg, geom.qkv, N, H, W)  # norm1 -> qkv in one launch
+        if fused is not None:
+            qkv, ln1, m1, r1 = fused
+        else:
+            ln1, m1, r1 = layernorm(x, n1w, n1b, Cr)
+            qkv = linear_fwd(ln1, qwf, qbg, geom.qkv, N, H, W)
         tab = table.detach().float().contiguous()
         a, lse = window_attn(qkv, geom, N, H, W, scale, tab)
         pwf, _, pbg = prepared_linear(pw, pb, geom.proj, dtype)
         s1, s2 = dp if dp is not None else (None, None)  # per-sample DropPath factors (fp32 [N])
         x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0, row_scale=s1)
-        ln2, m2, r2 = layernorm(x2, n2w, n2b, Cr)
         f1wf, _, f1bg = prepared_linear(f1w, f1b, fc1s, dtype)
         z = torch.empty(N, H, W, fc1s.cout_p, device=x.device, dtype=dtype)
-        h = linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)
+        fused = linear_ln_fwd(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)  # norm2 -> fc1
+        if fused is not None:
+            h, ln2, m2, r2 = fused
+        else:
+            ln2, m2, r2 = layernorm(x2, n2w, n2b, Cr)
+            h = linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)
         f2wf, _, f2bg = prepared_linear(f2w, f2b, fc2s, dtype)
         out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0, row_scale=s2)
         ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale, ctx.dp = geom, fc1s, fc2s, scale, dp

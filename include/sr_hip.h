@@ -85,6 +85,18 @@ typedef struct sr_conv3x3_desc {
                              the proj / fc2 residual epilogues); NULL = 1 */
 } sr_conv3x3_desc;
 
+/* A SwinIR block's LayerNorm fused into the following linear (norm1 -> attn.qkv, norm2 -> mlp.fc1:
+ * basicsr/archs/swinir_arch.py:240, 251, 289-291, 320-323): y = Linear(LayerNorm(x)) on bf16
+ * token rows [M][Cin] (dense, ldx == Cin), LayerNorm over the first ln_C channels (fp32 statistics,
+ * eps), the normalised rows also written to ln_out [M][Cin] (padded columns zero) with the per-row
+ * mean / rstd, as sr_layernorm_fwd would (they feed the weight gradient and the LayerNorm
+ * backward).  The linear is sr_conv3x3_fwd's ksize-1 path with a plain (act 0) or GELU +
+ * pre-activation aux epilogue and Cin <= 192, Cout <= 640. */
+int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_gamma, const float* ln_beta, int ln_C,
+                     float eps, void* ln_out, float* ln_mean, float* ln_rstd, const void* w, const float* bias, void* y,
+                     void* aux, void* stream);
+
+
 /* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.
  * act: SR_ACT_* or 3 = GELU (exact erf).  aux (may be NULL): also store the pre-activation
  * value conv(x, w) + bias in y's layout (GELU backward).  colsum (may be NULL): fp32

@@ -80,3 +80,43 @@ def test_window_attention_fwd_bwd(cuda, shift, dtype, geom):
     gref = qd.grad
     assert (dq - gref).abs().max().item() < tol * max(1.0, gref.abs().max().item())
     assert (dtab.double().cpu() - td.grad).abs().max().item() < tol * max(1.0, td.grad.abs().max().item())
+
+
+@pytest.mark.parametrize('which', ['qkv', 'fc1'])
+@pytest.mark.parametrize('shape', [(2, 16, 16, 180, 6), (1, 8, 24, 60, 6), (3, 5, 13, 96, 3)])
+def test_linear_ln_fused_vs_separate(cuda, which, shape):
+    """sr_linear_ln_fwd (LayerNorm in the lin kernel's prologue) against the standalone LayerNorm
+    kernel followed by the linear: the normalised rows, mean / rstd, the GELU pre-activation and
+    the output; ragged last token tile (M % 128 != 0) included."""
+    from basicsr4rs_amd.ops import swin as S
+    N, H, W, C_, nH = shape
+    torch.manual_seed(3)
+    dt = torch.bfloat16
+    Cp = (C_ + 7) // 8 * 8
+    x = torch.zeros(N, H, W, Cp, device=cuda)
+    x[..., :C_] = torch.randn(N, H, W, C_, device=cuda) * 2 + 0.5
+    x = x.to(dt)
+    g = torch.nn.Parameter(torch.rand(C_, device=cuda) + 0.5)
+    b = torch.nn.Parameter(torch.randn(C_, device=cuda) * 0.1)
+    if which == 'qkv':
+        spec = S.qkv_spec(C_, nH, 32)
+        lin = torch.nn.Linear(C_, 3 * C_).to(cuda)
+        act, aux = 0, None
+    else:
+        spec = S.plain_spec(C_, 2 * C_)
+        lin = torch.nn.Linear(C_, 2 * C_).to(cuda)
+        act = S.GELU
+        aux = torch.empty(N, H, W, spec.cout_p, device=cuda, dtype=dt)
+    wf, _, bg = S.prepared_linear(lin.weight, lin.bias, spec, dt)
+    y, ln, mean, rstd = S.linear_ln_fwd(x, g, b, C_, wf, bg, spec, N, H, W, act=act, aux=aux)
+    ln_r, mean_r, rstd_r = S.layernorm(x, g, b, C_)
+    aux_r = torch.empty_like(aux) if aux is not None else None
+    y_r = S.linear_fwd(ln_r, wf, bg, spec, N, H, W, act=act, aux=aux_r)
+    torch.cuda.synchronize()
+    assert (mean - mean_r).abs().max().item() <= 1e-5 * max(1.0, mean_r.abs().max().item())
+    assert (rstd - rstd_r).abs().max().item() <= 1e-4 * rstd_r.abs().max().item()
+    assert (ln.float() - ln_r.float()).abs().max().item() <= 2e-2 * ln_r.float().abs().max().item()
+    assert torch.equal(ln[..., C_:], torch.zeros_like(ln[..., C_:]))
+    assert (y.float() - y_r.float()).abs().max().item() <= 2e-2 * max(1.0, y_r.float().abs().max().item())
+    if aux is not None:
+        assert (aux.float() - aux_r.float()).abs().max().item() <= 2e-2 * max(1.0, aux_r.float().abs().max().item())
