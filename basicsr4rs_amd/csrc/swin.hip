@@ -1010,6 +1010,22 @@ int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, cons
   return sr_check(hipGetLastError(), "layernorm_fwd launch");
 }
 
+// dgamma / dbeta partial rows sr_layernorm_bwd leaves in the workspace on its vectorised path
+// (bf16, Cp <= 256), 0 when that path does not apply (the reduce then always runs inside)
+int sr_layernorm_bwd_parts(int dtype, int64_t M, int Cp, int ldx, int lddx, int lddy, int ldr) {
+  if (!(dtype == SR_BF16 && ln_vec8(Cp, ldx, lddx) && lddy % 8 == 0 && ldr % 8 == 0)) return 0;
+  return (int)((M + 15) / 16 < LN_BWD_BLOCKS ? (M + 15) / 16 : LN_BWD_BLOCKS);
+}
+
+int sr_layernorm_bwd_reduce(const float* workspace, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
+                            void* stream) {
+  if (!workspace || !dgamma || !dbeta || nparts <= 0 || C <= 0 || C > 512)
+    return sr_fail(SR_EINVAL, "layernorm_bwd_reduce: bad arguments");
+  hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 15) / 16), dim3(1024), 0, (hipStream_t)stream, workspace, nparts, C,
+                     dgamma, dbeta, accumulate & 1);
+  return sr_check(hipGetLastError(), "layernorm_bwd_reduce launch");
+}
+
 size_t sr_layernorm_bwd_workspace(int64_t M, int C) {
   (void)M;
   return (size_t)2048 * 4 * 2 * C * sizeof(float);
@@ -1029,10 +1045,12 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
     const unsigned g8 = (unsigned)((M + 15) / 16 < LN_BWD_BLOCKS ? (M + 15) / 16 : LN_BWD_BLOCKS);
     hipLaunchKernelGGL(ln_bwd8_kernel<16>, dim3(g8), dim3(512), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
                        rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
-    hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
-                       dgamma, dbeta, accumulate);
+    if (!(accumulate & 2))  // bit 1: partials only (sr_layernorm_bwd_reduce later, e.g. on another stream)
+      hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
+                         dgamma, dbeta, accumulate & 1);
     return sr_check(hipGetLastError(), "layernorm_bwd launch");
   }
+  accumulate &= 1;
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx,
                        mean, rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
@@ -1086,9 +1104,28 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
   } else {
     hipLaunchKernelGGL(wattn_bwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
   }
-  hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((a.nbins + 63) / 64)), dim3(1024), 0, s,
-                     (const float*)workspace, parts, nH, a.nbins, dbias_table, accumulate);
+  if (!(accumulate & 2))  // bit 1: partials only (sr_window_attn_dbias_reduce later)
+    hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((a.nbins + 63) / 64)), dim3(1024), 0, s,
+                       (const float*)workspace, parts, nH, a.nbins, dbias_table, accumulate & 1);
   return sr_check(hipGetLastError(), "window_attn_bwd launch");
+}
+
+// relative-bias gradient partial rows sr_window_attn_bwd leaves in its workspace
+int sr_window_attn_bwd_parts(int dtype, int N, int H, int W, int ws, int nH, int hd, int hdp, int ldq, int ldo) {
+  AttnArgs a{};
+  if (!attn_setup(a, N, H, W, ws, 0, nH, hd, hdp, 1.f)) return 0;
+  a.ldq = ldq; a.ldo = ldo;
+  return attn_mfma_ok(a, dtype) ? nH * ((N * a.nwin + ATT_UPW - 1) / ATT_UPW) : a.units;
+}
+
+int sr_window_attn_dbias_reduce(const float* workspace, int parts, int nH, int ws, float* dbias_table, int accumulate,
+                                void* stream) {
+  const int nbins = (2 * ws - 1) * (2 * ws - 1);
+  if (!workspace || !dbias_table || parts <= 0 || nH <= 0 || ws <= 0)
+    return sr_fail(SR_EINVAL, "window_attn_dbias_reduce: bad arguments");
+  hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((nbins + 63) / 64)), dim3(1024), 0, (hipStream_t)stream, workspace,
+                     parts, nH, nbins, dbias_table, accumulate & 1);
+  return sr_check(hipGetLastError(), "window_attn_dbias_reduce launch");
 }
 
 int sr_add_pos_embed(int dtype, const void* x, int N, int P, int C, int Cp, const float* pos, void* y, void* stream) {

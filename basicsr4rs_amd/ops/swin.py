@@ -29,6 +29,9 @@ from ..utils import ktrace
 from . import conv as C
 
 GELU = 3
+# SR_PARAM_REDUCE_MAIN=1 keeps the LayerNorm / attention-table gradient reduces on the main stream
+# under async_wgrad (A/B)
+_PARAM_REDUCE_SIDE = os.environ.get('SR_PARAM_REDUCE_MAIN') != '1'
 
 
 class LinearSpec:
@@ -185,12 +188,24 @@ def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None):
     lib = _lib.load()
     wsb = lib.sr_layernorm_bwd_workspace(M, Creal)
     ws = torch.empty(wsb // 4 + 1, device=x.device, dtype=torch.float32)
+    ldr = res.shape[-1] if res is not None else 0
+    # side-stream weight gradients (ops.conv.async_wgrad): the dgamma / dbeta reduce goes there too
+    side = C.async_side_stream(x.device) if direct is not None and not ktrace.active() and _PARAM_REDUCE_SIDE else None
+    nparts = lib.sr_layernorm_bwd_parts(_lib.dtype_code(x.dtype), M, Cp, Cp, Cp, dy.shape[-1], ldr) if side else 0
+    if nparts <= 0:
+        side = None
     with ktrace.span('ln_bwd_kernel', 0.0, (4.0 if res is not None else 3.0) * M * Creal * x.element_size()):
         _lib.check(
             lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
-                                 _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res),
-                                 res.shape[-1] if res is not None else 0, _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db),
-                                 _lib.ptr(ws), wsb, int(direct is not None), _lib.stream()))
+                                 _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res), ldr,
+                                 _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(ws), wsb,
+                                 int(direct is not None) | (2 if side is not None else 0), _lib.stream()))
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        ws.record_stream(side)
+        with torch.cuda.stream(side):
+            _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg), _lib.ptr(db), 1,
+                                                   _lib.stream()))
     if direct is not None:
         for p in params:
             C.grad_ready(p)
@@ -256,12 +271,22 @@ def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table, table_param=N
     lib = _lib.load()
     wsb = lib.sr_window_attn_bwd_workspace(N, H, W, g.ws, g.nH)
     ws = torch.empty(wsb // 4 + 1, device=qkv.device, dtype=torch.float32)
+    # side-stream weight gradients (ops.conv.async_wgrad): the table-gradient reduce goes there too
+    side = C.async_side_stream(qkv.device) if direct is not None and not ktrace.active() and _PARAM_REDUCE_SIDE else None
     with ktrace.span('wattn_bwd_kernel', 2.5 * attn_flops(g, N, H, W), 9.0 * N * H * W * g.dim * qkv.element_size()):
         _lib.check(
             lib.sr_window_attn_bwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], _lib.ptr(out), _lib.ptr(dout),
                                    out.shape[-1], _lib.ptr(lse), N, H, W, g.ws, g.shift, g.nH, g.hd, g.hdp, float(scale),
                                    _lib.ptr(table), _lib.ptr(dqkv), _lib.ptr(dtable), _lib.ptr(ws), wsb,
-                                   int(direct is not None), _lib.stream()))
+                                   int(direct is not None) | (2 if side is not None else 0), _lib.stream()))
+    if side is not None:
+        parts = lib.sr_window_attn_bwd_parts(_lib.dtype_code(qkv.dtype), N, H, W, g.ws, g.nH, g.hd, g.hdp, qkv.shape[-1],
+                                             out.shape[-1])
+        side.wait_stream(torch.cuda.current_stream(qkv.device))
+        ws.record_stream(side)
+        with torch.cuda.stream(side):
+            _lib.check(lib.sr_window_attn_dbias_reduce(_lib.ptr(ws), parts, g.nH, g.ws, _lib.ptr(dtable), 1,
+                                                       _lib.stream()))
     if direct is not None:
         C.grad_ready(table_param)
         return dqkv, None

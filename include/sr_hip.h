@@ -271,11 +271,16 @@ int sr_layernorm_fwd(int dtype, const void* x, int ldx, const float* gamma, cons
                      int C, int Cp, float eps, void* y, int ldy, float* mean, float* rstd, void* stream);
 size_t sr_layernorm_bwd_workspace(int64_t M, int C);
 /* dx = LN backward (+ res if not NULL), dgamma / dbeta over all rows (deterministic);
- * accumulate = 1 adds them to dgamma / dbeta (the optimizer's gradient views). */
+ * accumulate bit 0 adds them to dgamma / dbeta (the optimizer's gradient views); bit 1 leaves
+ * the dgamma / dbeta partial rows in the workspace for sr_layernorm_bwd_reduce (when
+ * sr_layernorm_bwd_parts > 0), so that reduction can run on another stream. */
 int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean,
                      const float* rstd, const float* gamma, int64_t M, int C, int Cp, const void* res,
                      int ldr, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
                      size_t ws_bytes, int accumulate, void* stream);
+int sr_layernorm_bwd_parts(int dtype, int64_t M, int Cp, int ldx, int lddx, int lddy, int ldr);
+int sr_layernorm_bwd_reduce(const float* workspace, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
+                            void* stream);
 /* Shifted-window multi-head attention on [N*H*W][ldq] qkv rows laid out [3][nH][hdp]
  * (head_dim hd <= hdp, zero padded): cyclic shift by `shift`, ws x ws windows, scale,
  * relative-position bias table [(2ws-1)^2][nH], -100 shift mask; out rows [nH][hdp];
@@ -288,6 +293,11 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
                        const float* lse, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp,
                        float scale, const float* bias_table, void* dqkv, float* dbias_table, void* workspace,
                        size_t ws_bytes, int accumulate, void* stream);
+/* accumulate bit 1 of sr_window_attn_bwd: the relative-bias gradient partial rows (count:
+ * sr_window_attn_bwd_parts) stay in the workspace for sr_window_attn_dbias_reduce. */
+int sr_window_attn_bwd_parts(int dtype, int N, int H, int W, int ws, int nH, int hd, int hdp, int ldq, int ldo);
+int sr_window_attn_dbias_reduce(const float* workspace, int parts, int nH, int ws, float* dbias_table, int accumulate,
+                                void* stream);
 
 /* SwinIR absolute position embedding (ape=True, swinir_arch.py:789-791, :879-880) on dense token rows
  * [N][P][Cp]: y = x + pos[p][c] for c < C (pos fp32 [P][C]); its gradient dpos[p][c] (+)= sum_n dy. */
