@@ -92,6 +92,8 @@ SIGNATURES = {
     'sr_layernorm_bwd': (_i, [_i, _vp, _i, _vp, _i, _vp, _vp, _vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _sz,
                              _i, _vp]),
     'sr_window_attn_fwd': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp, _vp]),
+    'sr_layernorm_bwd_scaled': (_i, [_i, _vp, _i, _vp, _i, _vp, _vp, _vp, _i64, _i, _i, _vp, _i, _vp, _i, _vp, _vp, _vp, _sz,
+                                     _i, _vp, _i, _vp, _vp]),
     'sr_layernorm_bwd_parts': (_i, [_i, _i64, _i, _i, _i, _i, _i]),
     'sr_layernorm_bwd_reduce': (_i, [_vp, _i, _i, _vp, _vp, _i, _vp]),
     'sr_window_attn_bwd_parts': (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i]),

@@ -229,7 +229,8 @@ __global__ __launch_bounds__(SLOTS * 32) void ln_bwd8_kernel(const bf16_t* __res
                                                       int ldx, const float* __restrict__ mean,
                                                       const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                       int64_t M, int C, int Cp, const bf16_t* __restrict__ res, int ldr,
-                                                      bf16_t* __restrict__ dx, int lddx, float* __restrict__ partial) {
+                                                      bf16_t* __restrict__ dx, int lddx, float* __restrict__ partial,
+                                                      const float* __restrict__ rscale, int HW, bf16_t* __restrict__ dxs) {
   __shared__ float red[SLOTS][2][256];
   const int lane = threadIdx.x & 63, hl = lane & 31, slot = threadIdx.x >> 5;
   const int c0 = hl * 8;
@@ -270,7 +271,15 @@ __global__ __launch_bounds__(SLOTS * 32) void ln_bwd8_kernel(const bf16_t* __res
       o[j] = c0 + j < C ? rs * (g[j] - s1 - xh[j] * s2) : 0.f;
       if (res && c0 + j < C) o[j] += rv[j];
     }
-    if (c0 < Cp) *(u32x4*)(dx + row * lddx + c0) = pack8(o);
+    if (c0 < Cp) {
+      *(u32x4*)(dx + row * lddx + c0) = pack8(o);
+      if (dxs) {  // also dx * rscale[image] (a stochastic-depth branch gradient), same layout
+        const float sc = rscale[row / HW];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= sc;
+        *(u32x4*)(dxs + row * lddx + c0) = pack8(o);
+      }
+    }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -1031,9 +1040,13 @@ size_t sr_layernorm_bwd_workspace(int64_t M, int C) {
   return (size_t)2048 * 4 * 2 * C * sizeof(float);
 }
 
-int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean, const float* rstd,
-                     const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr, void* dx, int lddx,
-                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes, int accumulate, void* stream) {
+}  // extern "C"
+
+namespace {
+int ln_bwd_impl(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean, const float* rstd,
+                const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr, void* dx, int lddx,
+                float* dgamma, float* dbeta, void* workspace, size_t ws_bytes, int accumulate, void* stream,
+                const float* rscale, int HW, void* dx_scaled) {
   if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || C > 512)
     return sr_fail(SR_EINVAL, "layernorm_bwd: bad arguments");
   if (ws_bytes < sr_layernorm_bwd_workspace(M, C)) return sr_fail(SR_EINVAL, "layernorm_bwd: workspace too small");
@@ -1044,12 +1057,14 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
     // number of dgamma / dbeta partials (more blocks instead moves the cost into the reduce)
     const unsigned g8 = (unsigned)((M + 15) / 16 < LN_BWD_BLOCKS ? (M + 15) / 16 : LN_BWD_BLOCKS);
     hipLaunchKernelGGL(ln_bwd8_kernel<16>, dim3(g8), dim3(512), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, mean,
-                       rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace);
+                       rstd, gamma, M, C, Cp, (const bf16_t*)res, ldr, (bf16_t*)dx, lddx, (float*)workspace, rscale, HW,
+                       (bf16_t*)dx_scaled);
     if (!(accumulate & 2))  // bit 1: partials only (sr_layernorm_bwd_reduce later, e.g. on another stream)
       hipLaunchKernelGGL(ln_bwd_reduce8, dim3((2 * C + 15) / 16), dim3(1024), 0, s, (const float*)workspace, (int)g8, C,
                          dgamma, dbeta, accumulate & 1);
     return sr_check(hipGetLastError(), "layernorm_bwd launch");
   }
+  if (dx_scaled) return sr_fail(SR_EINVAL, "layernorm_bwd_scaled: bf16, Cp <= 256, 16-B aligned rows only");
   accumulate &= 1;
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(grid), dim3(256), 0, s, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx,
@@ -1060,6 +1075,25 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
   hipLaunchKernelGGL(ln_bwd_reduce, dim3((2 * C + 255) / 256), dim3(256), 0, s, (const float*)workspace, (int)grid * 4,
                      C, dgamma, dbeta, accumulate);
   return sr_check(hipGetLastError(), "layernorm_bwd launch");
+}
+}  // namespace
+
+extern "C" {
+
+int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean, const float* rstd,
+                     const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr, void* dx, int lddx,
+                     float* dgamma, float* dbeta, void* workspace, size_t ws_bytes, int accumulate, void* stream) {
+  return ln_bwd_impl(dtype, dy, lddy, x, ldx, mean, rstd, gamma, M, C, Cp, res, ldr, dx, lddx, dgamma, dbeta, workspace,
+                     ws_bytes, accumulate, stream, nullptr, 1, nullptr);
+}
+
+int sr_layernorm_bwd_scaled(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean,
+                            const float* rstd, const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr,
+                            void* dx, int lddx, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
+                            int accumulate, const float* row_scale, int HW, void* dx_scaled, void* stream) {
+  if (!row_scale || !dx_scaled || HW <= 0 || M % HW) return sr_fail(SR_EINVAL, "layernorm_bwd_scaled: bad row scale");
+  return ln_bwd_impl(dtype, dy, lddy, x, ldx, mean, rstd, gamma, M, C, Cp, res, ldr, dx, lddx, dgamma, dbeta, workspace,
+                     ws_bytes, accumulate, stream, row_scale, HW, dx_scaled);
 }
 
 int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W, int ws, int shift, int nH, int hd,

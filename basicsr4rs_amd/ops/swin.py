@@ -32,6 +32,8 @@ GELU = 3
 # SR_PARAM_REDUCE_MAIN=1 keeps the LayerNorm / attention-table gradient reduces on the main stream
 # under async_wgrad (A/B)
 _PARAM_REDUCE_SIDE = os.environ.get('SR_PARAM_REDUCE_MAIN') != '1'
+# SR_ROWSCALE_UNFUSED=1: the proj-branch stochastic-depth gradient by a separate row-scale pass (A/B)
+_ROWSCALE_FUSED = os.environ.get('SR_ROWSCALE_UNFUSED') != '1'
 
 
 class LinearSpec:
@@ -116,6 +118,9 @@ def row_scale(x, scale, HW):
     return out
 
 
+row_scale_ = row_scale  # for layernorm_bwd, whose row_scale parameter shadows the function
+
+
 def linear_wgrad(dy, x, spec, N, H, W, need_bias=True, params=None):
     _, _, co, ci = spec.maps(dy.device)
     dw, db = C.conv_wgrad_raw(dy, x, N, H, W, spec.cin_p, spec.cin, spec.cout_p, spec.cout, ksize=1, co_map=co,
@@ -173,9 +178,11 @@ def _direct(params):
     return tg if all(g is not None for g in tg) else None
 
 
-def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None):
+def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None, row_scale=None):
     """dx, dgamma, dbeta; with ``params=(weight, bias)`` held in a FlatParams buffer the
-    parameter gradients are accumulated in place and (dx, None, None) is returned."""
+    parameter gradients are accumulated in place and (dx, None, None) is returned.  With
+    ``row_scale`` (fp32 [N]) dx is returned as the pair (dx, dx * row_scale[image]) when the
+    kernel writes both in one pass (sr_layernorm_bwd_scaled), else the caller scales."""
     N, H, W, Cp = x.shape
     M = N * H * W
     dx = torch.empty_like(x)
@@ -194,12 +201,26 @@ def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None):
     nparts = lib.sr_layernorm_bwd_parts(_lib.dtype_code(x.dtype), M, Cp, Cp, Cp, dy.shape[-1], ldr) if side else 0
     if nparts <= 0:
         side = None
+    acc = int(direct is not None) | (2 if side is not None else 0)
+    scaled = None
+    if row_scale is not None and _ROWSCALE_FUSED and x.dtype == torch.bfloat16 and lib.sr_layernorm_bwd_parts(
+            _lib.dtype_code(x.dtype), M, Cp, Cp, Cp, dy.shape[-1], ldr) > 0:
+        scaled = torch.empty_like(x)
     with ktrace.span('ln_bwd_kernel', 0.0, (4.0 if res is not None else 3.0) * M * Creal * x.element_size()):
-        _lib.check(
-            lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
-                                 _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res), ldr,
-                                 _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(ws), wsb,
-                                 int(direct is not None) | (2 if side is not None else 0), _lib.stream()))
+        if scaled is not None:  # the stochastic-depth branch gradient in the same pass
+            _lib.check(
+                lib.sr_layernorm_bwd_scaled(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp,
+                                            _lib.ptr(mean), _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp,
+                                            _lib.ptr(res), ldr, _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(ws),
+                                            wsb, acc, _lib.ptr(row_scale), H * W, _lib.ptr(scaled), _lib.stream()))
+        else:
+            _lib.check(
+                lib.sr_layernorm_bwd(_lib.dtype_code(x.dtype), _lib.ptr(dy), dy.shape[-1], _lib.ptr(x), Cp, _lib.ptr(mean),
+                                     _lib.ptr(rstd), _lib.ptr(weight.detach()), M, Creal, Cp, _lib.ptr(res), ldr,
+                                     _lib.ptr(dx), Cp, _lib.ptr(dg), _lib.ptr(db), _lib.ptr(ws), wsb, acc,
+                                     _lib.stream()))
+    if row_scale is not None:
+        dx = (dx, scaled if scaled is not None else row_scale_(dx, row_scale, H * W))
     if side is not None:
         side.wait_stream(torch.cuda.current_stream(x.device))
         ws.record_stream(side)
@@ -344,8 +365,11 @@ class _STB(torch.autograd.Function):
         _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
         dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
         df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W, params=(f1w, f1b))
-        dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b))
-        g1 = row_scale(dx2, s1, H * W) if s1 is not None else dx2  # proj-branch gradient
+        dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b), row_scale=s1)
+        if s1 is not None:
+            dx2, g1 = dx2  # g1 = the proj-branch gradient s1 * dx2, written by the same kernel
+        else:
+            g1 = dx2
         _, pwd, _ = prepared_linear(pw, pb, g.proj, dtype)
         da = linear_dgrad(g1, pwd, g.proj, N, H, W)
         dpw, dpb = linear_wgrad(g1, a, g.proj, N, H, W, params=(pw, pb))

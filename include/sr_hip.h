@@ -278,6 +278,13 @@ int sr_layernorm_bwd(int dtype, const void* dy, int lddy, const void* x, int ldx
                      const float* rstd, const float* gamma, int64_t M, int C, int Cp, const void* res,
                      int ldr, void* dx, int lddx, float* dgamma, float* dbeta, void* workspace,
                      size_t ws_bytes, int accumulate, void* stream);
+/* sr_layernorm_bwd that also writes dx_scaled[m] = dx[m] * row_scale[m / HW] (same layout as dx):
+ * the SwinIR proj-branch gradient under stochastic depth (swinir_arch.py:14-40, 320) in the same
+ * pass (bf16, Cp <= 256 path only). */
+int sr_layernorm_bwd_scaled(int dtype, const void* dy, int lddy, const void* x, int ldx, const float* mean,
+                            const float* rstd, const float* gamma, int64_t M, int C, int Cp, const void* res, int ldr,
+                            void* dx, int lddx, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
+                            int accumulate, const float* row_scale, int HW, void* dx_scaled, void* stream);
 int sr_layernorm_bwd_parts(int dtype, int64_t M, int Cp, int ldx, int lddx, int lddy, int ldr);
 int sr_layernorm_bwd_reduce(const float* workspace, int nparts, int C, float* dgamma, float* dbeta, int accumulate,
                             void* stream);
