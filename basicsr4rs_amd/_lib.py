@@ -63,6 +63,7 @@ SIGNATURES = {
     'sr_conv3x3_wgrad_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad_workspace': (_sz, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad': (_i, [ctypes.POINTER(WgradDesc), _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
+    'sr_conv3x3_wgrad_reduce': (_i, [ctypes.POINTER(WgradDesc), _vp, _sz, _vp, _vp, _vp, _vp, _vp]),
     'sr_conv_prep_blocks': (_i, [ctypes.POINTER(PrepItem)]),
     'sr_conv_prep_batch': (_i, [_i, _vp, _vp, _i, _i, _vp]),
     'sr_conv3x3_prep': (_i, [_i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),

@@ -3668,7 +3668,8 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_g_kernel(const float* ws, c
                                                               int out_ps, int taps, const int* co_map,
                                                               const int* ci_map, float scale, int wblocks,
                                                               int accumulate) {
-  __shared__ f32x4 red[1024];
+  extern __shared__ f32x4 red[];  // nw * 64 entries (dynamic: a 4-wave block needs 4 KB, so it can
+                                  // share a CU with the 158 KB pph kernel when it runs on a side stream)
   const int nw = (int)(blockDim.x >> 6);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r2 = out_ps > 0 ? out_ps * out_ps : 1;
@@ -4580,6 +4581,67 @@ size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d) {
   return ((size_t)S * taps * d->Cout * d->Cin + (size_t)S * d->Cout) * sizeof(float) + 256;
 }
 
+}  // extern "C"
+
+namespace {
+// The slab reduce of a sr_conv3x3_wgrad call (S splits of its plan, slab ws, bias slab wsb)
+int wgrad_reduce_launch(const sr_conv3x3_wgrad_desc* d, int S, int taps, const float* ws, const float* wsb, float* dw,
+                        float* db, const int* co_map, const int* ci_map, hipStream_t s) {
+  const int acc1 = d->accumulate & 1;
+  const int Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout;
+  const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
+  const int64_t total = (int64_t)Cout_real * Cin_real;
+  const int64_t work = total > Cout_real ? total : Cout_real;
+  const bool tr = wg_use_halo(d) && wg_use_ring();
+  // (the row-streaming slab keeps wgrad_reduce_tr_kernel: 32-group blocks measured slower on RCAN / RRDB)
+  if (g_variant != 40 && !tr && Cin_real % 4 == 0 && !ci_map) {
+    // split phases P ~ S / 8 (pow2 <= 32), group width GPW so that the grid covers the chip
+    const int64_t groups = tr ? (int64_t)taps * Cin_real * ((Cout_real + 3) / 4) : (int64_t)taps * Cout_real * (Cin_real / 4);
+    int P = 1;
+    while (P * 8 < S && P < 32) P <<= 1;
+    int gpw = 64;
+    while (gpw > 16 && P * gpw / 64 > 16) gpw >>= 1;  // <= 16 waves
+    while (gpw > 16 && (groups + gpw - 1) / gpw < 256 && P * gpw / 64 >= 2) gpw >>= 1;
+    const int nw = P * gpw / 64 > 0 ? P * gpw / 64 : 1;
+    const int wblocks = (int)((groups + gpw - 1) / gpw);
+    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
+    const dim3 grid((unsigned)(wblocks + bblocks)), blk((unsigned)(nw * 64));
+#define SR_RG(G, T)                                                                                             \
+  hipLaunchKernelGGL((wgrad_reduce_g_kernel<G, T>), grid, blk, (size_t)nw * 64 * 16, s, (const float*)ws, (const float*)wsb, dw, db, \
+                     S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, wblocks,  \
+                     acc1)
+    if (tr) { if (gpw == 64) SR_RG(64, true); else if (gpw == 32) SR_RG(32, true); else SR_RG(16, true); }
+    else { if (gpw == 64) SR_RG(64, false); else if (gpw == 32) SR_RG(32, false); else SR_RG(16, false); }
+#undef SR_RG
+  } else if (tr) {
+    const int64_t work4 = (int64_t)taps * Cin_real * ((Cout_real + 3) / 4);
+    const int wblocks = (int)((work4 + 63) / 64);
+    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_reduce_tr_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s,
+                       (const float*)ws, (const float*)wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, taps,
+                       co_map, ci_map, d->scale, wblocks, acc1);
+  } else if (Cin_real % 4 == 0) {
+    const int64_t work4 = (int64_t)taps * Cout_real * (Cin_real / 4);
+    const int wblocks = (int)((work4 + 63) / 64);
+    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
+    hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s, (const float*)ws,
+                       (const float*)wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map,
+                       ci_map, d->scale, wblocks, acc1);
+  } else if (Cin_real <= 8 && g_variant != 33) {
+    hipLaunchKernelGGL(wgrad_reduce_narrow_kernel, dim3((unsigned)Cout_real), dim3(256), 0, s, (const float*)ws,
+                       (const float*)wsb, dw, db, S, d->Cout, d->Cin, Cin_real, d->out_ps, taps, co_map, ci_map,
+                       d->scale, acc1);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                       (const float*)ws, (const float*)wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
+                       Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, acc1);
+  }
+  return sr_check(hipGetLastError(), "conv3x3_wgrad reduce launch");
+}
+}  // namespace
+
+extern "C" {
+
 int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void* x, void* workspace,
                      size_t ws_bytes, float* dw, float* db, const int* co_map, const int* ci_map, void* stream) {
   if (!d || !dy || !x || !workspace || !dw) return sr_fail(SR_EINVAL, "conv3x3_wgrad: null pointer");
@@ -4660,55 +4722,20 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     e = d->dtype == SR_BF16 ? dispatch_wg<bf16_t>(a, s) : dispatch_wg<float>(a, s);
   }
   if (e != hipSuccess) return sr_check(e, "conv3x3_wgrad launch");
-  const int Cout_real = d->Cout_real > 0 ? d->Cout_real : d->Cout;
-  const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
-  const int64_t total = (int64_t)Cout_real * Cin_real;
-  const int64_t work = total > Cout_real ? total : Cout_real;
-  const bool tr = wg_use_halo(d) && wg_use_ring();
-  // (the row-streaming slab keeps wgrad_reduce_tr_kernel: 32-group blocks measured slower on RCAN / RRDB)
-  if (g_variant != 40 && !tr && Cin_real % 4 == 0 && !ci_map) {
-    // split phases P ~ S / 8 (pow2 <= 32), group width GPW so that the grid covers the chip
-    const int64_t groups = tr ? (int64_t)taps * Cin_real * ((Cout_real + 3) / 4) : (int64_t)taps * Cout_real * (Cin_real / 4);
-    int P = 1;
-    while (P * 8 < S && P < 32) P <<= 1;
-    int gpw = 64;
-    while (gpw > 16 && P * gpw / 64 > 16) gpw >>= 1;  // <= 16 waves
-    while (gpw > 16 && (groups + gpw - 1) / gpw < 256 && P * gpw / 64 >= 2) gpw >>= 1;
-    const int nw = P * gpw / 64 > 0 ? P * gpw / 64 : 1;
-    const int wblocks = (int)((groups + gpw - 1) / gpw);
-    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
-    const dim3 grid((unsigned)(wblocks + bblocks)), blk((unsigned)(nw * 64));
-#define SR_RG(G, T)                                                                                             \
-  hipLaunchKernelGGL((wgrad_reduce_g_kernel<G, T>), grid, blk, 0, s, (const float*)a.ws, (const float*)a.wsb, dw, db, \
-                     S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, wblocks,  \
-                     d->accumulate)
-    if (tr) { if (gpw == 64) SR_RG(64, true); else if (gpw == 32) SR_RG(32, true); else SR_RG(16, true); }
-    else { if (gpw == 64) SR_RG(64, false); else if (gpw == 32) SR_RG(32, false); else SR_RG(16, false); }
-#undef SR_RG
-  } else if (tr) {
-    const int64_t work4 = (int64_t)taps * Cin_real * ((Cout_real + 3) / 4);
-    const int wblocks = (int)((work4 + 63) / 64);
-    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
-    hipLaunchKernelGGL(wgrad_reduce_tr_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s,
-                       (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, taps,
-                       co_map, ci_map, d->scale, wblocks, d->accumulate);
-  } else if (Cin_real % 4 == 0) {
-    const int64_t work4 = (int64_t)taps * Cout_real * (Cin_real / 4);
-    const int wblocks = (int)((work4 + 63) / 64);
-    const int bblocks = db ? (Cout_real + 63) / 64 : 0;
-    hipLaunchKernelGGL(wgrad_reduce4_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s, (const float*)a.ws,
-                       (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map,
-                       ci_map, d->scale, wblocks, d->accumulate);
-  } else if (Cin_real <= 8 && g_variant != 33) {
-    hipLaunchKernelGGL(wgrad_reduce_narrow_kernel, dim3((unsigned)Cout_real), dim3(256), 0, s, (const float*)a.ws,
-                       (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cin_real, d->out_ps, taps, co_map, ci_map,
-                       d->scale, d->accumulate);
-  } else {
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
-                       (const float*)a.ws, (const float*)a.wsb, dw, db, S, d->Cout, d->Cin, Cout_real,
-                       Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, d->accumulate);
-  }
-  return sr_check(hipGetLastError(), "conv3x3_wgrad reduce launch");
+  if (d->accumulate & 2) return SR_OK;  // bit 1: slab only (sr_conv3x3_wgrad_reduce later, e.g. on another stream)
+  return wgrad_reduce_launch(d, S, taps, a.ws, a.wsb, dw, db, co_map, ci_map, s);
+}
+
+int sr_conv3x3_wgrad_reduce(const sr_conv3x3_wgrad_desc* d, void* workspace, size_t ws_bytes, float* dw, float* db,
+                            const int* co_map, const int* ci_map, void* stream) {
+  if (!d || !workspace || !dw) return sr_fail(SR_EINVAL, "conv3x3_wgrad_reduce: null pointer");
+  if (ws_bytes < sr_conv3x3_wgrad_workspace(d)) return sr_fail(SR_EINVAL, "conv3x3_wgrad_reduce: workspace too small");
+  int S, kp;
+  wgrad_plan(d, &S, &kp);
+  const int taps = d->ksize == 1 ? 1 : 9;
+  float* ws = (float*)workspace;
+  float* wsb = db ? ws + (size_t)S * taps * d->Cout * d->Cin : nullptr;
+  return wgrad_reduce_launch(d, S, taps, ws, wsb, dw, db, co_map, ci_map, (hipStream_t)stream);
 }
 
 int sr_conv_prep_mapped(int dtype, int ksize, const float* w, const float* bias, int Cout_real, int Cin_real,

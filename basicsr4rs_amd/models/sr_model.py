@@ -60,7 +60,8 @@ class SRModel(BaseModel):
         # weight gradients on a side stream during backward (train.async_wgrad, ops.conv.async_wgrad);
         # the environment variable SR_ASYNC_WGRAD=0/1 overrides the option (A/B)
         env = os.environ.get('SR_ASYNC_WGRAD')
-        self.async_wgrad = env == '1' if env in ('0', '1') else bool(train_opt.get('async_wgrad', False))
+        mode = train_opt.get('async_wgrad', False)
+        self.async_wgrad = {'0': False, '1': True, 'reduce': 'reduce'}.get(env, mode if mode == 'reduce' else bool(mode))
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)

@@ -35,7 +35,7 @@ def bump_param_epoch():
 # to the side stream; leaving the context joins it (the current stream waits on it), so the
 # optimizer, the bucketed all-reduce and any reader of .grad see finished gradients.  Results are
 # the same kernels on the same inputs: bitwise equal to the single-stream order.
-_ASYNC = {'depth': 0, 'streams': {}, 'used': False}
+_ASYNC = {'depth': 0, 'streams': {}, 'used': False, 'mode': True}
 
 
 def _side_stream(device):
@@ -52,8 +52,16 @@ def async_side_stream(device=None):
     return _side_stream(device if device is not None else torch.device('cuda', torch.cuda.current_device()))
 
 
+def async_mode():
+    """True (whole weight gradients on the side stream), 'reduce' (only their slab reduces), or
+    None outside async_wgrad."""
+    return _ASYNC['mode'] if _ASYNC['depth'] > 0 else None
+
+
 class async_wgrad:
-    """Context: weight gradients on the side stream, joined into the current stream on exit."""
+    """Context: weight gradients on the side stream, joined into the current stream on exit.
+    ``enabled='reduce'`` moves only the split-K slab reduces there (the slab kernel stays on the
+    main stream): a memory-bound reduce then fills the CUs beside the next MFMA-bound conv."""
 
     def __init__(self, enabled=True):
         self.enabled = enabled
@@ -61,6 +69,7 @@ class async_wgrad:
     def __enter__(self):
         if self.enabled:
             _ASYNC['depth'] += 1
+            _ASYNC['mode'] = self.enabled
         return self
 
     def __exit__(self, *exc):
@@ -321,6 +330,25 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
     ws_bytes = lib.sr_conv3x3_wgrad_workspace(d)
     # (a traced step stays single-stream: its per-kernel event spans then time each kernel alone)
     side = async_side_stream(x.device) if tw is not None and not ktrace.active() else None
+    if side is not None and async_mode() == 'reduce':  # slab here, its reduce on the side stream
+        ws = torch.empty(ws_bytes // 4 + 1, device=x.device, dtype=torch.float32)
+        d.accumulate = 1 | 2
+        _lib.check(lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(tw), _lib.ptr(tb),
+                                        _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')), _lib.stream()))
+        d.accumulate = 1
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        ws.record_stream(side)
+        for t in (kw.get('co_map'), kw.get('ci_map')):
+            if t is not None:
+                t.record_stream(side)
+        with torch.cuda.stream(side):
+            _lib.check(lib.sr_conv3x3_wgrad_reduce(d, _lib.ptr(ws), ws_bytes, _lib.ptr(tw), _lib.ptr(tb),
+                                                   _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')),
+                                                   _lib.stream()))
+        grad_ready(params[0])
+        if need_bias:
+            grad_ready(params[1])
+        return None, None
     if side is not None:  # fork: dy / x are ready on the current stream
         side.wait_stream(torch.cuda.current_stream(x.device))
         for t in (dy, x, kw.get('co_map'), kw.get('ci_map')):

@@ -143,6 +143,11 @@ size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d);
 int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void* x,
                      void* workspace, size_t ws_bytes, float* dw, float* db, const int* co_map,
                      const int* ci_map, void* stream);
+/* accumulate bit 1 of the descriptor: sr_conv3x3_wgrad writes only the split-K slab into the
+ * workspace; sr_conv3x3_wgrad_reduce (same descriptor and workspace, e.g. on another stream)
+ * then reduces it into dw / db (bit 0 of accumulate as for sr_conv3x3_wgrad). */
+int sr_conv3x3_wgrad_reduce(const sr_conv3x3_wgrad_desc* d, void* workspace, size_t ws_bytes, float* dw, float* db,
+                            const int* co_map, const int* ci_map, void* stream);
 
 /* Weight preparation from the nn.Conv2d parameter w[Cout_real][Cin_real][3][3] (fp32):
  *   wf[n][tap*Cin + ci]       forward GEMM rows (n = GEMM column, permuted by out_ps)
