@@ -902,10 +902,21 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
     bval[k] = n < a.Cout;
     boff[k] = (uint32_t)(n * a.ldw) * 2u + (uint32_t)c * 16u;
   }
-  // halo piece p of wave w: pixels 64p + 8w .. +7 of a row
-  const uint32_t hlane = (uint32_t)((8 * w + (lane >> 3)) * a.ldx + a.xcoff) * 2u + (uint32_t)ch_h * 16u;
-  const uint32_t rowb = (uint32_t)(W * a.ldx) * 2u;
-  const uint32_t pieceb = (uint32_t)(64 * a.ldx) * 2u;
+  // halo piece p of wave w: pixels 64p + 8w .. +7 of a row.  With in_ps = r (pixel-shuffled
+  // input, the upsample convs' dgrads) LR pixel (y, x) of LR channel sl * C' + cch is HR pixel
+  // (y r + si, x r + sj) (sl = si r + sj) channel cch: rows r HR rows apart, pixels r apart, and a
+  // per-chunk (si, sj, cch) offset instead of cc * 128
+  const int rps = a.in_ps > 0 ? a.in_ps : 1;
+  const uint32_t hlane = (uint32_t)((8 * w + (lane >> 3)) * rps * a.ldx + a.xcoff) * 2u + (uint32_t)ch_h * 16u;
+  const uint32_t rowb = (uint32_t)(W * rps * rps * a.ldx) * 2u;
+  const uint32_t pieceb = (uint32_t)(64 * rps * a.ldx) * 2u;
+  auto chunk_off = [&](int cc) -> uint32_t {
+    if (a.in_ps == 0) return (uint32_t)cc * 128u;
+    const int c0 = cc * 64;
+    const int sl = (int)fdiv((uint32_t)c0, a.fd_cps), cch = c0 - sl * a.fd_cps.d;
+    const int si = sl / rps, sj = sl - si * rps;
+    return (uint32_t)((si * W * rps + sj) * a.ldx + cch) * 2u;
+  };
 
   if (tid < 64) *(u32x4*)(smem + G::ZERO + tid * 16) = u32x4{0u, 0u, 0u, 0u};
   if (tid < G::NSLOT * 16) {  // border columns (slot px index 0 and W + 1) of every slot
@@ -931,7 +942,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
     const int slot = (RH * cc + rr) % G::NSLOT;
     glds16(xr, smem + PPH_SLOT0 + slot * G::ROWB + 128 + p * 8192 + w * 1024,
            (unsigned)y < (unsigned)a.H
-               ? (uint32_t)(img * a.H + y) * rowb + (uint32_t)p * pieceb + hlane + (uint32_t)cc * 128u
+               ? (uint32_t)(img * a.H + y) * rowb + (uint32_t)p * pieceb + hlane + chunk_off(cc)
                : SR_OOB);
   };
   auto issue_dummy = [&]() { glds16(xr, smem + G::ZERO, SR_OOB); };
@@ -4016,8 +4027,8 @@ hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
 // Halo variant of the 256x256 kernel: whole-row tiles of W = 64 / 128 images, 64-channel chunks.
 bool fwd_use_pph(const FwdArgs& a) {
   return g_variant != 2 && g_variant != 24 && (g_variant < 21 || g_variant > 24) &&
-         ((a.W == 64 && a.H % 4 == 0) || (a.W == 128 && a.H % 2 == 0)) && a.Cin % 64 == 0 && a.in_ps == 0 &&
-         a.in_up == 1 && a.tap0 == 0;
+         ((a.W == 64 && a.H % 4 == 0) || (a.W == 128 && a.H % 2 == 0)) && a.Cin % 64 == 0 &&
+         (a.in_ps == 0 || (a.fd_cps.d % 64 == 0 && g_variant != 50)) && a.in_up == 1 && a.tap0 == 0;
 }
 
 hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
@@ -4560,7 +4571,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 49)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 50)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;

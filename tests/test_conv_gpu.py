@@ -652,3 +652,38 @@ def test_fwd_band_bitwise_equals_halo(cuda, shape, epi, grid):
             assert (got - ref).abs().max().item() <= 1e-5 * y0.double().abs().sum((1, 2)).max().item() + 1e-6
     if epi == 'slices':
         assert y0[..., :16].abs().max().item() == 0 and y0[..., 16 + cout:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize('shape', [(2, 4, 64, 1024, 256, 2), (1, 2, 128, 1024, 256, 2), (1, 4, 64, 2304, 256, 3)])
+def test_fwd_pph_pixel_shuffled_input(cuda, shape):
+    """The halo-row kernel reading a pixel-shuffled input (in_ps: the upsample convs' dgrads read
+    the HR gradient as an LR map of r*r*C' channels, LR channel sl*C' + c = HR pixel (y r + sl / r,
+    x r + sl % r) channel c): against fp64 on the same bf16 operands and against the per-tap pp
+    kernel (variant 50)."""
+    N, H, W, cin, cout, r = shape
+    torch.manual_seed(21)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    cp = cin // (r * r)
+    xh = torch.randn(N, H * r, W * r, cp, device=cuda).to(dt)
+    wt = torch.randn(cout, cin, 3, 3, device=cuda) * 0.03
+    spec = C.ConvSpec(cin, cout)
+    wf, _, bg = C.prepared(torch.nn.Parameter(wt), None, spec, dt)
+    d = C._desc(dt, N, H, W, cin, cp, cout, cout, cout, in_ps=r)
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_pph_kernel'
+    outs = []
+    try:
+        for variant in (0, 50):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+            C.conv_fwd_raw(xh, wf, None, y, N, H, W, cin, cout, cout, in_ps=r, ldx=cp)
+            outs.append(y)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    xl = xh.view(N, H, r, W, r, cp).permute(0, 2, 4, 5, 1, 3).reshape(N, r * r * cp, H, W)
+    ref = F.conv2d(xl.double().cpu(), bf(wt.cpu()).double(), padding=1)
+    got = outs[0].permute(0, 3, 1, 2).double().cpu()
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= tol
+    assert (outs[0].float() - outs[1].float()).abs().max().item() <= tol
