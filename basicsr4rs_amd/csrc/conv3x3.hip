@@ -2236,6 +2236,7 @@ struct WgArgs {
   int in_up;  // nearest upsample factor of the x gather (1 = none)
   int taps, tap0;  // 9 / 0 for 3x3, 1 / 4 for 1x1 (linear)
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
+  int bias_group;  // pp kernel: > 0 = the bias-role blocks come after all tile blocks, each doing this many splits
   FastDiv fd_W, fd_H, fd_cps;
   unsigned long long* stamps;  // diagnostics (SR_BAND_STAMPS builds): per-block phase cycles
 };
@@ -2746,12 +2747,30 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   const int wr = w >> 2, wc = w & 3;
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
   const int ntile = a.taps * a.tiles_co * a.tiles_ci;
-  const int per_split = ntile + (a.wsb ? a.tiles_co : 0);
-  const int split = (int)b / per_split;
-  int rem = (int)b - split * per_split;
-  if (rem >= ntile) {
-    wgrad_bias_role(a, smem, split, (rem - ntile) * 256);
-    return;
+  int split, rem;
+  if (a.bias_group > 0) {
+    // tile blocks first; the bias-role blocks (light: dy only) each take bias_group splits, so
+    // fewer CUs sit on them and the tile blocks get more splits (shorter K ranges)
+    if ((int)b >= a.splits * ntile) {
+      const int bb = (int)b - a.splits * ntile;
+      const int grp = bb / a.tiles_co, co_t = bb - grp * a.tiles_co;
+      const int s1 = min(a.splits, (grp + 1) * a.bias_group);
+      for (int sp = grp * a.bias_group; sp < s1; ++sp) {
+        if (sp > grp * a.bias_group) __syncthreads();  // the previous split's LDS stages are free
+        wgrad_bias_role(a, smem, sp, co_t * 256);
+      }
+      return;
+    }
+    split = (int)b / ntile;
+    rem = (int)b - split * ntile;
+  } else {
+    const int per_split = ntile + (a.wsb ? a.tiles_co : 0);
+    split = (int)b / per_split;
+    rem = (int)b - split * per_split;
+    if (rem >= ntile) {
+      wgrad_bias_role(a, smem, split, (rem - ntile) * 256);
+      return;
+    }
   }
   const int tap = rem / (a.tiles_co * a.tiles_ci);
   rem -= tap * a.tiles_co * a.tiles_ci;
@@ -4344,6 +4363,16 @@ bool wg_use_tr3(const sr_conv3x3_wgrad_desc* d) {
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
 
+// Splits per bias-role block of the pp kernel (0: one bias block per split, interleaved with the
+// tile blocks).  The bias role reads dy only, so a third of the CUs' worth of bias blocks can take
+// three splits each and the tile blocks get more, shorter splits (EDSR-L body wgrad, 247 blocks:
+// 176 -> 170 us).  3x3 convs only (the SwinIR linears' slabs are HBM traffic: more splits cost
+// there); variant 51: groups of 2, 53: the interleaved layout.
+int wg_bias_group(const sr_conv3x3_wgrad_desc* d) {
+  if (g_variant == 53 || d->ksize == 1 || !wg_use_pp(d)) return 0;
+  return g_variant == 51 ? 2 : 3;
+}
+
 // the row-streaming form of it (variant 37: the tile-row form, for A/B)
 bool wg_use_ring() { return g_variant != 37; }
 // All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2.
@@ -4383,6 +4412,20 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     const int tiles = 3 * (d->Cout / 128) * (d->Cin / 128) + (d->Cout + 255) / 256;
     int S = 256 / tiles;
     const int maxS = M / 256 > 1 ? M / 256 : 1;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
+  if (wg_bias_group(d) > 0) {  // pp kernel, bias-role blocks grouped (see conv3x3_wgrad_pp_kernel)
+    const int bg = wg_bias_group(d), tco = (d->Cout + 255) / 256;
+    const int ntile = 9 * tco * ((d->Cin + 255) / 256);
+    int S = (int)(256.0 / (ntile + (double)tco / bg));
+    while (S > 1 && S * ntile + (S + bg - 1) / bg * tco > 256) --S;
+    const int maxS = (M + 255) / 256;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
     int kp = (M + S - 1) / S;
@@ -4571,7 +4614,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 50)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 53)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -4720,7 +4763,11 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.tiles_co = (a.Cout + 255) / 256;
     a.tiles_ci = (a.Cin + 255) / 256;
     const int per_split = taps * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
-    if (wg_use_pp(d) && g_variant >= 41 && g_variant <= 43) {  // timing ablations (wrong results)
+    a.bias_group = wg_bias_group(d);
+    if (a.bias_group > 0) {
+      const int nb = S * taps * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
+      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(nb), dim3(512), 0, s, a);
+    } else if (wg_use_pp(d) && g_variant >= 41 && g_variant <= 43) {  // timing ablations (wrong results)
       if (g_variant == 41) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<1>, dim3(S * per_split), dim3(512), 0, s, a);
       else if (g_variant == 42) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<2>, dim3(S * per_split), dim3(512), 0, s, a);
       else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<3>, dim3(S * per_split), dim3(512), 0, s, a);
