@@ -2237,6 +2237,7 @@ struct WgArgs {
   int taps, tap0;  // 9 / 0 for 3x3, 1 / 4 for 1x1 (linear)
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   int bias_group;  // pp kernel: > 0 = the bias-role blocks come after all tile blocks, each doing this many splits
+  int bias_fused;  // pp kernel: no bias-role blocks; the centre-tap, first-ci-tile blocks sum dy as well
   FastDiv fd_W, fd_H, fd_cps;
   unsigned long long* stamps;  // diagnostics (SR_BAND_STAMPS builds): per-block phase cycles
 };
@@ -2764,7 +2765,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
     split = (int)b / ntile;
     rem = (int)b - split * ntile;
   } else {
-    const int per_split = ntile + (a.wsb ? a.tiles_co : 0);
+    const int per_split = ntile + (a.wsb && !a.bias_fused ? a.tiles_co : 0);
     split = (int)b / per_split;
     rem = (int)b - split * per_split;
     if (rem >= ntile) {
@@ -2878,6 +2879,11 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused bias (a.bias_fused): the centre-tap blocks of the first ci tile also sum dy over their
+  // pixels -- wave (wr, wc) takes A row block i = wc of each half against a ones operand
+  const bool bias_here = a.bias_fused && a.wsb && tap == a.taps / 2 && ci0 == 0;
+  const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mma = [&](int h, int g) {
     if constexpr (DBG == 2) return;
     __builtin_amdgcn_s_setprio(1);
@@ -2888,6 +2894,15 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[h][g][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[g][kk][j], acc[h][g][i][j], 0, 0, 0);
+    if (g == 0 && bias_here) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (wc == 0) accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][0], ones, accb[h], 0, 0, 0);
+        else if (wc == 1) accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][1], ones, accb[h], 0, 0, 0);
+        else if (wc == 2) accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][2], ones, accb[h], 0, 0, 0);
+        else accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][3], ones, accb[h], 0, 0, 0);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -2940,6 +2955,15 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   }
   if (!wr) pp_barrier();
 
+  if (bias_here && (lane & 15) == 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + h * 128 + wr * 64 + wc * 16 + (lane >> 4) * 4 + r;
+        if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[h][r];
+      }
+  }
   float* ws = a.ws + ((size_t)split * a.taps + tap) * a.Cout * a.Cin;
   float* Cs = (float*)smem;
 #pragma unroll
@@ -4373,6 +4397,16 @@ int wg_bias_group(const sr_conv3x3_wgrad_desc* d) {
   return g_variant == 51 ? 2 : 3;
 }
 
+// The pp kernel's bias gradient inside its centre-tap blocks: no bias-role blocks, so one 256-block
+// wave holds floor(256 / tiles) splits.  Taken for Cout > 256 (the EDSR upsample convs, 36 tiles:
+// 6 -> 7 splits, 677 -> 650 us at 64^2, 2614 -> 2517 us at 128^2); at one co tile the centre-tap
+// blocks' extra MFMAs cost more than the split gained (EDSR body 170 -> 177 us, SwinIR 3x3 161 ->
+// 173 us), so those keep the grouped bias blocks.  Variant 54: everywhere, 53: neither.
+bool wg_bias_fused(const sr_conv3x3_wgrad_desc* d) {
+  if (g_variant == 53 || d->ksize == 1 || !wg_use_pp(d)) return false;
+  return g_variant == 54 || d->Cout > 256;
+}
+
 // the row-streaming form of it (variant 37: the tile-row form, for A/B)
 bool wg_use_ring() { return g_variant != 37; }
 // All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2.
@@ -4412,6 +4446,18 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     const int tiles = 3 * (d->Cout / 128) * (d->Cin / 128) + (d->Cout + 255) / 256;
     int S = 256 / tiles;
     const int maxS = M / 256 > 1 ? M / 256 : 1;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
+  if (wg_bias_fused(d)) {
+    const int ntile = 9 * ((d->Cout + 255) / 256) * ((d->Cin + 255) / 256);
+    int S = 256 / ntile;
+    const int maxS = (M + 255) / 256;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
     int kp = (M + S - 1) / S;
@@ -4614,7 +4660,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 53)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 54)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -4764,7 +4810,11 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.tiles_ci = (a.Cin + 255) / 256;
     const int per_split = taps * a.tiles_co * a.tiles_ci + (a.wsb ? a.tiles_co : 0);
     a.bias_group = wg_bias_group(d);
-    if (a.bias_group > 0) {
+    a.bias_fused = wg_bias_fused(d) ? 1 : 0;
+    if (a.bias_fused) {
+      a.bias_group = 0;
+      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+    } else if (a.bias_group > 0) {
       const int nb = S * taps * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
       hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(nb), dim3(512), 0, s, a);
     } else if (wg_use_pp(d) && g_variant >= 41 && g_variant <= 43) {  // timing ablations (wrong results)
