@@ -20,11 +20,13 @@ from ..losses import build_loss
 from ..metrics import calculate_metric
 import os
 
-from ..ops.conv import async_wgrad, bump_param_epoch
+from ..ops.conv import async_wgrad, bump_param_epoch, take_captured_tables
 from ..utils.flat import FlatParams
 from ..utils.img_util import imwrite, tensor2img
+from ..utils.logger import get_root_logger
 from ..utils.registry import MODEL_REGISTRY
-from .base_model import BaseModel
+from ..utils.step_graph import SegmentedStepGraph
+from .base_model import BaseModel, SRDistributed
 
 
 @MODEL_REGISTRY.register()
@@ -55,8 +57,9 @@ class SRModel(BaseModel):
         self.use_amp = bool(train_opt.get('use_amp', False))
         self._graph = None
         self._eager_steps = 0
-        # HIP-graph capture of the train step (after 2 eager warm-up steps); single process
-        self.use_graph = bool(train_opt.get('cuda_graph', False)) and not self.opt.get('dist', False)
+        # HIP-graph capture of the train step (after 2 eager warm-up steps); distributed: a chain of
+        # graphs cut at the gradient buckets, all-reduced between them (utils/step_graph.py)
+        self.use_graph = bool(train_opt.get('cuda_graph', False))
         # weight gradients on a side stream during backward (train.async_wgrad, ops.conv.async_wgrad);
         # the environment variable SR_ASYNC_WGRAD=0/1 overrides the option (A/B)
         env = os.environ.get('SR_ASYNC_WGRAD')
@@ -152,17 +155,28 @@ class SRModel(BaseModel):
         """Capture one whole train step (forward, L1, backward, fused Adam+EMA) in a HIP graph
         and run it; later steps replay it (train.cuda_graph).  Host-side per-step state (step
         count, lr) is kept outside the graph (FusedAdam.host_step + device hyper-parameters),
-        the inputs live in static buffers refilled by feed_data.  Single process only: the
-        gradient all-reduce of the distributed path stays eager."""
+        the inputs live in static buffers refilled by feed_data.  Distributed: the step becomes
+        a chain of graphs cut where the gradient buckets complete, with each bucket's all-reduce
+        launched between them (utils/step_graph.py), so the exchange still overlaps backward."""
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
         ema = self.flat_ema if self.ema_decay > 0 else None
         self.optimizer_g.host_step()
         # the captured step reads these two tensors at replay: keep them under private names
         self._g_lq, self._g_gt = self.lq, self.gt
-        with torch.cuda.graph(g):
-            losses = self._step_body()
+
+        def opt_step():
             self.optimizer_g.device_step(ema=ema, ema_decay=self.ema_decay)
+
+        if isinstance(self.net_g, SRDistributed):
+            g = SegmentedStepGraph(self.net_g.reducer, self.device)
+            losses = g.capture(self._step_body, opt_step)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                losses = self._step_body()
+                opt_step()
+        # the batched weight-image refresh inside the graph launches on these device tables
+        self._graph_keep = take_captured_tables()
         self._graph = g
         self._g_out = self.output
         self._graph_losses = losses
@@ -201,8 +215,7 @@ class SRModel(BaseModel):
             del self.lq
             del self.output
             if save_img:
-                save_img_path = osp.join(self.opt['path']['visualization'], img_name, f'{img_name}_{current_iter}.png')
-                imwrite(sr_img, save_img_path)
+                imwrite(sr_img, self._val_image_path(dataset_name, img_name, current_iter))
             if with_metrics:
                 for name, opt_ in self.opt['val']['metrics'].items():
                     self.metric_results[name] += calculate_metric(metric_data, opt_)
@@ -210,6 +223,31 @@ class SRModel(BaseModel):
             for metric in self.metric_results.keys():
                 self.metric_results[metric] /= (idx + 1)
                 self._update_best_metric_result(dataset_name, metric, self.metric_results[metric], current_iter)
+            self._log_validation_metric_values(current_iter, dataset_name, tb_logger)
+
+    def _val_image_path(self, dataset_name, img_name, current_iter):
+        """Where a validation SR image goes (basicsr/models/sr_model.py:226-235): per image and
+        iteration while training; per dataset with ``val.suffix`` (else the run name) at test time."""
+        root = self.opt['path']['visualization']
+        if self.opt['is_train']:
+            return osp.join(root, img_name, f'{img_name}_{current_iter}.png')
+        tag = self.opt['val'].get('suffix') or self.opt['name']
+        return osp.join(root, dataset_name, f'{img_name}_{tag}.png')
+
+    def _log_validation_metric_values(self, current_iter, dataset_name, tb_logger):
+        """One log record with every metric and its best value / iteration, and a tensorboard
+        scalar per metric (basicsr/models/sr_model.py:252-266)."""
+        best = getattr(self, 'best_metric_results', {}).get(dataset_name, {})
+        lines = [f'Validation {dataset_name}']
+        for metric, value in self.metric_results.items():
+            line = f'\t # {metric}: {value:.4f}'
+            if metric in best:
+                line += f'\tBest: {best[metric]["val"]:.4f} @ {best[metric]["iter"]} iter'
+            lines.append(line)
+        get_root_logger().info('\n'.join(lines) + '\n')
+        if tb_logger:
+            for metric, value in self.metric_results.items():
+                tb_logger.add_scalar(f'metrics/{dataset_name}/{metric}', value, current_iter)
 
     def get_current_visuals(self, current_iter=None):
         out_dict = OrderedDict()

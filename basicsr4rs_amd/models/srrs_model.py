@@ -37,6 +37,8 @@ class SRRSModel(SRModel):
             print('Loss is NaN or Inf. Skipping optimizer step.')
             self.log_nan_inf_loss(current_iter, l_total)
             self.optimizer_g.zero_grad()
+            # drop this batch and its graph like the reference (srrs_model.py:68-77)
+            del self.lq, self.gt, self.output
             return
         with async_wgrad(self.async_wgrad):
             l_total.backward()

@@ -65,16 +65,19 @@ class async_wgrad:
 
     def __init__(self, enabled=True):
         self.enabled = enabled
+        self._prev_mode = None
 
     def __enter__(self):
         if self.enabled:
             _ASYNC['depth'] += 1
+            self._prev_mode = _ASYNC['mode']
             _ASYNC['mode'] = self.enabled
         return self
 
     def __exit__(self, *exc):
         if self.enabled:
             _ASYNC['depth'] -= 1
+            _ASYNC['mode'] = self._prev_mode  # a nested context must not leak its mode outward
             for st in _ASYNC['streams'].values():
                 torch.cuda.current_stream(st.device).wait_stream(st)
         return False
@@ -118,15 +121,24 @@ class _Prep:
 
 _PREP_ALL = {}  # (id(weight), static key) -> _Prep
 _PREP_TABLE = {}  # dtype -> (entries, device item table, device block starts, total blocks)
-# tables replaced since: a captured HIP graph may still launch the batched refresh on one of
-# them, so their device buffers are kept alive instead of returning to the allocator
-_PREP_TABLE_RETIRED = []
+# tables launched by refresh_prepared while a HIP graph was being captured: the graph keeps
+# launching the batched refresh on their device buffers, so whoever owns the graph takes these
+# references (take_captured_tables) and holds them exactly as long as the graph itself
+_CAPTURED_TABLES = []
 
 
 def _retire_table(dtype):
-    tab = _PREP_TABLE.pop(dtype, None)
-    if tab is not None:
-        _PREP_TABLE_RETIRED.append(tab)
+    # a table not referenced by a captured graph is simply released; one that is stays alive
+    # through the graph owner's reference
+    _PREP_TABLE.pop(dtype, None)
+
+
+def take_captured_tables():
+    """Device tables of the batched weight-image refresh launched during the capture that just
+    ended; the caller keeps them alive with its graph (models/sr_model.py)."""
+    out = list(_CAPTURED_TABLES)
+    _CAPTURED_TABLES.clear()
+    return out
 
 
 def prepared_images(weight, bias, dtype, shape, maps=(None, None), tag=''):
@@ -204,6 +216,8 @@ def refresh_prepared():
             _retire_table(dt)
             _PREP_TABLE[dt] = tab
         _, raw, st, total = tab
+        if torch.cuda.is_current_stream_capturing():
+            _CAPTURED_TABLES.append(tab)
         _lib.check(lib.sr_conv_prep_batch(_lib.dtype_code(dt), _lib.ptr(raw), _lib.ptr(st), len(ents), total,
                                           _lib.stream()))
     for e in live:
@@ -277,6 +291,13 @@ def on_grad_ready(p, fn):
     if cbs is None:
         cbs = p._sr_grad_ready = []
     cbs.append(fn)
+
+
+def remove_grad_ready(p, fn):
+    """Unregister a callback added by on_grad_ready (no-op if absent)."""
+    cbs = p.__dict__.get('_sr_grad_ready')
+    if cbs and fn in cbs:
+        cbs.remove(fn)
 
 
 def grad_ready(p):

@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _lib
-from ..ops.conv import async_side_stream, bump_param_epoch, on_grad_ready, refresh_prepared
+from ..ops.conv import async_side_stream, bump_param_epoch, on_grad_ready, refresh_prepared, remove_grad_ready
 
 
 def _params(module):
@@ -148,16 +148,24 @@ class GradBucketReducer:
     any compute, and it is capped at ``last_bucket_mb`` (1 MiB, DDP's first-bucket size)
     so that only a short collective is exposed before the optimizer.
 
-    A parameter is "ready" when the HIP kernel that accumulates its gradient straight into
-    the flat buffer has been queued (``ops.conv.grad_ready``: conv / linear wgrads, LayerNorm,
-    attention-table and channel-attention backwards) or, for gradients that still go through
-    autograd, when its post-accumulate-grad hook runs -- whichever comes first, once per step.
-    When the last parameter of a bucket is ready the bucket's ``all_reduce`` is issued (async,
-    RCCL stream ordered after the producing kernels) while backward continues; ``wait()`` joins
-    them before the optimizer.  ``issue_log`` records, per step, which buckets were issued
-    during backward ('backward') and which only at the join ('wait'); ``last_issue_log`` keeps
-    the log of the step joined last.  The 1/world average is
+    A parameter's gradient arrives as one or more *contributions* per step: a HIP kernel that
+    accumulates straight into the flat buffer reports each launch (``ops.conv.grad_ready``: conv /
+    linear wgrads, LayerNorm, attention-table and channel-attention backwards), and gradients that
+    still go through autograd report through the post-accumulate-grad hook.  A parameter used twice
+    in a step (a module applied twice, weight tying) gets two.  The first step is a learning step:
+    every contribution is counted and all buckets are reduced at the join (``wait``).  From then on
+    a bucket is issued (async, RCCL stream ordered after the producing kernels) as soon as every
+    parameter in it has received the number of contributions counted in the first step, while
+    backward continues.  A parameter receiving MORE contributions than that raises (its bucket
+    may already be on the wire; DDP raises for the same condition unless its graph is static);
+    fewer leaves its bucket to the join.  ``wait()`` joins before the optimizer.  ``issue_log``
+    records, per step, which buckets were issued during backward ('backward') and which only at the
+    join ('wait'); ``last_issue_log`` keeps the log of the step joined last.  The 1/world average is
     left to the optimizer (FusedAdam.grad_scale) so no extra pass over the gradients runs.
+
+    ``on_issue``: when set (HIP-graph capture of a distributed step, models/sr_model.py), a ready
+    bucket is handed to it instead of being all-reduced; the capture cuts its graph there and the
+    replay all-reduces the bucket between graph segments (``all_reduce_bucket``).
     """
 
     def __init__(self, flat, group=None, bucket_mb=25.0, last_bucket_mb=1.0):
@@ -189,20 +197,37 @@ class GradBucketReducer:
         for b, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
-        self.hooks = []
+        self.expected = None  # contributions per parameter and step (learned on the first step)
+        self.on_issue = None
+        self.hooks, self._ready_fns = [], []
         for i, p in enumerate(flat.params):
             fn = self._make_hook(i)
             self.hooks.append(p.register_post_accumulate_grad_hook(fn))
             on_grad_ready(p, fn)
+            self._ready_fns.append((p, fn))
         self.issue_log, self.last_issue_log = [], []
         self.reset()
 
+    def remove(self):
+        """Detach from the parameters (hooks and gradient-ready callbacks); the reducer is dead."""
+        for h in self.hooks:
+            h.remove()
+        for p, fn in self._ready_fns:
+            remove_grad_ready(p, fn)
+        self.hooks, self._ready_fns = [], []
+
     def reset(self):
-        self.pending = [len(idx) for (_, _, idx) in self.buckets]
-        self.ready = [False] * len(self.flat.params)
+        self.counts = [0] * len(self.flat.params)
+        self.issued = [False] * len(self.buckets)
+        if self.expected is None:
+            self.pending = [None] * len(self.buckets)  # learning step: everything at the join
+        else:
+            self.pending = [sum(1 for i in idx if self.expected[i] > 0) for (_, _, idx) in self.buckets]
         self.handles = []
 
-    def _issue(self, b, when):
+    def all_reduce_bucket(self, b):
+        """Launch the async all-reduce of bucket b on the current stream's order (or from the
+        side stream while weight gradients run there)."""
         lo, hi, _ = self.buckets[b]
         g = self.flat.grad[lo:hi]
         side = async_side_stream(g.device) if g.is_cuda else None
@@ -214,27 +239,47 @@ class GradBucketReducer:
                 self.handles.append(dist.all_reduce(g, group=self.group, async_op=True))
         else:
             self.handles.append(dist.all_reduce(g, group=self.group, async_op=True))
+
+    def _issue(self, b, when):
+        self.issued[b] = True
         self.issue_log.append((b, when))
+        if self.on_issue is not None:
+            self.on_issue(b)
+        else:
+            self.all_reduce_bucket(b)
 
     def _make_hook(self, i):
 
         def hook(_p):
-            if self.ready[i]:
+            self.counts[i] += 1
+            if self.expected is None:
                 return
-            self.ready[i] = True
-            b = self.bucket_of[i]
-            self.pending[b] -= 1
-            if self.pending[b] == 0:
-                self._issue(b, 'backward')
+            e = self.expected[i]
+            if self.counts[i] > e:
+                raise RuntimeError(
+                    f'GradBucketReducer: parameter {i} received {self.counts[i]} gradient contributions this step, '
+                    f'more than the {e} of the first step; its bucket may already be reduced. The set of gradient '
+                    f'contributions must be the same every step (DDP static-graph semantics).')
+            if self.counts[i] == e:
+                b = self.bucket_of[i]
+                self.pending[b] -= 1
+                if self.pending[b] == 0:
+                    self._issue(b, 'backward')
 
         return hook
 
-    def wait(self):
-        """Join outstanding bucket reductions; reduce any bucket whose parameters did not all
-        report ready (unused in this step) so every rank issues the same collectives."""
-        for b, n in enumerate(self.pending):
-            if n > 0:
+    def flush(self):
+        """Issue every bucket not issued yet (parameters unused this step, or the learning step) so
+        every rank issues the same collectives in the same order."""
+        if self.expected is None:
+            self.expected = list(self.counts)
+        for b in range(len(self.buckets)):
+            if not self.issued[b]:
                 self._issue(b, 'wait')
+
+    def wait(self):
+        """Issue what is left (flush) and join the outstanding bucket reductions."""
+        self.flush()
         for h in self.handles:
             h.wait()
         self.last_issue_log, self.issue_log = self.issue_log, []

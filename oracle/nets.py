@@ -21,14 +21,38 @@ import torch
 import torch.nn.functional as F
 
 
-def conv(x, sd, name, act=None, slope=0.0):
+# Storage-rounding emulation (diagnostic, tests only): inside ``bf16_storage()`` every tensor the
+# HIP bf16 path stores between kernels (a conv's activated output, a fused residual result) is
+# rounded to bf16 and widened again, so the oracle shows the error budget of bf16 activations
+# alone.  Off by default: the oracle is the exact restatement.
+_STORE_DTYPE = [None]
+
+
+class bf16_storage:
+    def __enter__(self):
+        self._prev = _STORE_DTYPE[0]
+        _STORE_DTYPE[0] = torch.bfloat16
+        return self
+
+    def __exit__(self, *exc):
+        _STORE_DTYPE[0] = self._prev
+        return False
+
+
+def store(t):
+    """A tensor written to HBM between kernels: identity unless bf16_storage() is active."""
+    dt = _STORE_DTYPE[0]
+    return t if dt is None else t.to(dt).to(t.dtype)
+
+
+def conv(x, sd, name, act=None, slope=0.0, stored=True):
     """nn.Conv2d(C, C', 3, 1, 1) (e.g. basicsr/archs/arch_util.py:78-79)."""
     y = F.conv2d(x, sd[f'{name}.weight'], sd.get(f'{name}.bias'), stride=1, padding=1)
     if act == 'relu':
         y = F.relu(y)
     elif act == 'lrelu':
         y = F.leaky_relu(y, slope)
-    return y
+    return store(y) if stored else y
 
 
 def pixel_shuffle(x, r):
@@ -127,8 +151,8 @@ def rdb(x, sd, p):
     x2 = conv(torch.cat((x, x1), 1), sd, f'{p}.conv2', act='lrelu', slope=0.2)
     x3 = conv(torch.cat((x, x1, x2), 1), sd, f'{p}.conv3', act='lrelu', slope=0.2)
     x4 = conv(torch.cat((x, x1, x2, x3), 1), sd, f'{p}.conv4', act='lrelu', slope=0.2)
-    x5 = conv(torch.cat((x, x1, x2, x3, x4), 1), sd, f'{p}.conv5')
-    return x5 * 0.2 + x
+    x5 = conv(torch.cat((x, x1, x2, x3, x4), 1), sd, f'{p}.conv5', stored=False)
+    return store(x5 * 0.2 + x)
 
 
 def rrdbnet(sd, x, scale=4, num_block=23):
@@ -145,8 +169,8 @@ def rrdbnet(sd, x, scale=4, num_block=23):
         out = body
         for k in (1, 2, 3):
             out = rdb(out, sd, f'body.{i}.rdb{k}')
-        body = out * 0.2 + body
-    feat = feat + conv(body, sd, 'conv_body')
+        body = store(out * 0.2 + body)
+    feat = store(feat + conv(body, sd, 'conv_body', stored=False))
     feat = conv(F.interpolate(feat, scale_factor=2, mode='nearest'), sd, 'conv_up1', act='lrelu', slope=0.2)
     feat = conv(F.interpolate(feat, scale_factor=2, mode='nearest'), sd, 'conv_up2', act='lrelu', slope=0.2)
     return conv(conv(feat, sd, 'conv_hr', act='lrelu', slope=0.2), sd, 'conv_last')

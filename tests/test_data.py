@@ -165,3 +165,33 @@ def test_cuda_prefetcher_feeds_model_buffers(cuda, tmp_path):
     assert n == 2
     pf.reset()
     assert pf.next() is not None
+
+
+def test_prefetch_loader_and_cpu_prefetcher():
+    """PrefetchDataLoader yields the DataLoader's batches in order, stays exhausted, and re-raises
+    a loading error in the consumer; CPUPrefetcher returns None at the end of an epoch and
+    restarts on reset() (basicsr/data/prefetch_dataloader.py API, basicsr/train.py:170-209 loop)."""
+    from basicsr4rs_amd.data.prefetch_dataloader import CPUPrefetcher, PrefetchDataLoader
+    data = torch.arange(10.).view(10, 1)
+    loader = PrefetchDataLoader(num_prefetch_queue=2, dataset=data, batch_size=3)
+    it = iter(loader)
+    got = list(it)
+    assert [b.tolist() for b in got] == [b.tolist() for b in torch.utils.data.DataLoader(data, batch_size=3)]
+    with pytest.raises(StopIteration):
+        next(it)
+
+    class Bad(torch.utils.data.Dataset):
+        def __len__(self):
+            return 4
+
+        def __getitem__(self, i):
+            if i == 2:
+                raise ValueError('corrupt sample 2')
+            return torch.tensor([float(i)])
+
+    with pytest.raises(ValueError, match='corrupt sample 2'):
+        list(PrefetchDataLoader(num_prefetch_queue=1, dataset=Bad(), batch_size=1))
+    pf = CPUPrefetcher(torch.utils.data.DataLoader(data, batch_size=5))
+    assert pf.next().shape == (5, 1) and pf.next() is not None and pf.next() is None
+    pf.reset()
+    assert torch.equal(pf.next(), data[:5])

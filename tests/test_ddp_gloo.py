@@ -82,3 +82,122 @@ def test_bucketed_allreduce_matches_full_batch(bucket_mb):
     assert torch.allclose(grads, ref, rtol=1e-5, atol=1e-6)
     if bucket_mb < 0.01:
         assert nb > 1
+
+
+class _DirectLinear(torch.autograd.Function):
+    """y = x W^T whose weight gradient is accumulated straight into the flat .grad view and
+    reported through ops.conv.grad_ready (the path of the HIP wgrad kernels), not autograd."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x)
+        ctx.p = w
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, gy):
+        from basicsr4rs_amd.ops.conv import grad_ready, grad_target
+        (x, ) = ctx.saved_tensors
+        gx, gw = gy @ ctx.p.detach(), gy.t() @ x
+        tgt = grad_target(ctx.p)
+        if tgt is None:  # not in a FlatParams (the single-process reference): plain autograd
+            return gx, gw
+        tgt.add_(gw)
+        grad_ready(ctx.p)
+        return gx, None
+
+
+class _TwiceNet(torch.nn.Module):
+    """w1 applied twice per step (two gradient contributions), w2 once."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(1)
+        self.w1 = torch.nn.Parameter(torch.randn(16, 16) * 0.3)
+        self.w2 = torch.nn.Parameter(torch.randn(4, 16) * 0.3)
+
+    def forward(self, x):
+        h = torch.tanh(_DirectLinear.apply(x, self.w1))
+        h = torch.tanh(_DirectLinear.apply(h, self.w1))
+        return _DirectLinear.apply(h, self.w2)
+
+
+def _twice_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    net = _TwiceNet()
+    flat = FlatParams(net)
+    red = GradBucketReducer(flat, bucket_mb=0.0005, last_bucket_mb=0.0005)  # one parameter per bucket
+    g = torch.Generator().manual_seed(7)
+    x, y = torch.randn(8, 16, generator=g), torch.randn(8, 4, generator=g)
+    sl = slice(rank * 4, rank * 4 + 4)
+    out = []
+    for step in range(3):
+        flat.zero_grad()
+        ((net(x[sl]) - y[sl])**2).mean().backward()
+        red.wait()
+        out.append(((flat.grad / world).clone(), list(red.last_issue_log)))
+    if rank == 0:
+        q.put((out, red.expected))
+    dist.barrier()
+    red.remove()
+    flat.zero_grad()
+    ((net(x[sl]) - y[sl])**2).mean().backward()  # no hooks left: nothing issued, nothing raised
+    assert red.issue_log == []
+    dist.destroy_process_group()
+
+
+def test_reducer_counts_repeated_contributions():
+    """a parameter with two gradient contributions per step must not have its bucket
+    all-reduced after the first one.  The first step learns the counts (w1: 2 direct + the autograd hook, w2: 1 + hook) and joins
+    every bucket; later steps issue each bucket during backward only after its last contribution;
+    the averaged gradient equals the full-batch gradient every step."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_twice_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out, expected = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert expected == [3, 2]  # + autograd's post-accumulate hook (it fires for a None gradient too)
+    net = _TwiceNet()
+    g = torch.Generator().manual_seed(7)
+    x, y = torch.randn(8, 16, generator=g), torch.randn(8, 4, generator=g)
+    ref = []
+    for sl in (slice(0, 4), slice(4, 8)):
+        net.zero_grad()
+        ((net(x[sl]) - y[sl])**2).mean().backward()
+        ref.append(torch.cat([p.grad.reshape(-1) for p in net.parameters()]))
+    ref = (ref[0] + ref[1]) / 2
+    for step, (grads, log) in enumerate(out):
+        assert torch.allclose(grads, ref, rtol=1e-5, atol=1e-6), step
+        assert all(w == ('wait' if step == 0 else 'backward') for _, w in log), (step, log)
+
+
+def test_reducer_raises_on_extra_contribution():
+    """More contributions than learned on the first step: the reducer raises instead of letting a
+    gradient land after its bucket was reduced (world 1, gloo)."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(_free_port())
+    dist.init_process_group('gloo', rank=0, world_size=1)
+    try:
+        net = _TwiceNet()
+        flat = FlatParams(net)
+        red = GradBucketReducer(flat, bucket_mb=0.0005, last_bucket_mb=0.0005)
+        x = torch.randn(2, 16)
+        flat.zero_grad()
+        net(x).sum().backward()
+        red.wait()
+        assert red.expected == [3, 2]
+        flat.zero_grad()
+        h = _DirectLinear.apply(torch.tanh(_DirectLinear.apply(x, net.w1)), net.w1)
+        h = _DirectLinear.apply(torch.tanh(h), net.w1)  # a third use of w1
+        with pytest.raises(RuntimeError, match='more than the 3'):
+            _DirectLinear.apply(h, net.w2).sum().backward()
+        red.remove()
+    finally:
+        dist.destroy_process_group()

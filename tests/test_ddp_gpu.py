@@ -21,13 +21,13 @@ def _free_port():
     return p
 
 
-def _opt(dist_, world, rank, bucket_mb, async_wgrad=False):
+def _opt(dist_, world, rank, bucket_mb, async_wgrad=False, graph=False):
     return dict(model_type='SRModel', is_train=True, dist=dist_, num_gpu=1, world_size=world, rank=rank, path={},
                 bucket_cap_mb=bucket_mb,
                 network_g=dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=2, upscale=4,
                                res_scale=1),
-                train=dict(ema_decay=0.999, use_amp=False, async_wgrad=async_wgrad, optim_g=dict(type='Adam', lr=1e-3, weight_decay=0,
-                                                                        betas=[0.9, 0.99]),
+                train=dict(ema_decay=0.999, use_amp=False, async_wgrad=async_wgrad, cuda_graph=graph,
+                           optim_g=dict(type='Adam', lr=1e-3, weight_decay=0, betas=[0.9, 0.99]),
                            scheduler=dict(type='MultiStepLR', milestones=[100], gamma=0.5),
                            pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')))
 
@@ -37,7 +37,7 @@ def _batch(step):
     return torch.rand(4, 3, 16, 16, generator=g), torch.rand(4, 3, 64, 64, generator=g)
 
 
-def _worker(rank, world, port, bucket_mb, async_wgrad, q):
+def _worker(rank, world, port, bucket_mb, async_wgrad, q, graph=False, steps=2):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
@@ -46,8 +46,8 @@ def _worker(rank, world, port, bucket_mb, async_wgrad, q):
     import basicsr4rs_amd.archs  # noqa: F401
     from basicsr4rs_amd.models import build_model
     torch.manual_seed(0 + rank)  # different init per rank: the reducer broadcasts rank 0's
-    model = build_model(_opt(True, world, rank, bucket_mb, async_wgrad))
-    for step in (1, 2):
+    model = build_model(_opt(True, world, rank, bucket_mb, async_wgrad, graph))
+    for step in range(1, steps + 1):
         lq, gt = _batch(step)
         sl = slice(rank * 2, rank * 2 + 2)
         model.feed_data({'lq': lq[sl], 'gt': gt[sl]})
@@ -56,7 +56,8 @@ def _worker(rank, world, port, bucket_mb, async_wgrad, q):
     net = model.get_bare_model(model.net_g)
     sd = {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()}  # by value, not fd-shared
     red = model.net_g.reducer
-    q.put((rank, sd, len(red.buckets), list(red.last_issue_log)))
+    nseg = model._graph.n_segments if graph else 0
+    q.put((rank, sd, len(red.buckets), list(red.last_issue_log), nseg))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -75,7 +76,7 @@ def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb, async_wgrad):
         p.start()
     res = {}
     for _ in range(2):
-        rank, sd, nb, log = q.get(timeout=180)
+        rank, sd, nb, log, _ = q.get(timeout=180)
         res[rank] = (sd, nb, log)
     for p in procs:
         p.join(timeout=60)
@@ -104,3 +105,93 @@ def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb, async_wgrad):
         got = torch.from_numpy(res[0][0][k])
         err = (got - v.cpu()).abs().max().item() / max(1e-3, v.abs().max().item())
         assert err < 2e-4, (k, err)
+
+
+@pytest.mark.parametrize('async_wgrad', [False, True])
+def test_ddp_graph_segments_match_full_batch(cuda, async_wgrad):
+    """train.cuda_graph with DDP: steps 1-2 eager, step 3 captured as graph segments cut at the ready
+    buckets (utils/step_graph.py), steps 4-5 replayed with the bucket all-reduces launched between
+    segments.  Two gloo ranks on the one card, fp32: both ranks equal, and equal to single-process
+    eager training on the full batch (relative 2e-4); every bucket but the flushed tail goes out
+    between backward segments."""
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 0.05, async_wgrad, q, True, 5)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        rank, sd, nb, log, nseg = q.get(timeout=240)
+        res[rank] = (sd, nb, log, nseg)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nb = res[0][1]
+    assert nb > 1
+    for r in (0, 1):
+        log, nseg = res[r][2], res[r][3]
+        assert sorted(b for b, _ in log) == list(range(nb)), log
+        assert sum(1 for _, w in log if w == 'backward') >= nb - 1, log
+        assert nseg >= 3, nseg
+    assert res[0][2] == res[1][2]
+    for k in res[0][0]:
+        assert (res[0][0][k] == res[1][0][k]).all(), k
+    torch.manual_seed(0)
+    ref = build_model(_opt(False, 1, 0, 0.05))
+    for step in range(1, 6):
+        lq, gt = _batch(step)
+        ref.feed_data({'lq': lq, 'gt': gt})
+        ref.update_learning_rate(step)
+        ref.optimize_parameters(step)
+    for k, v in ref.get_bare_model(ref.net_g).state_dict().items():
+        got = torch.from_numpy(res[0][0][k])
+        err = (got - v.cpu()).abs().max().item() / max(1e-3, v.abs().max().item())
+        assert err < 2e-4, (k, err)
+
+
+def _nccl_worker(port, q):
+    """World 1 over RCCL: the segmented graph's replay issues real RCCL all-reduces."""
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1)
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    out = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        o = _opt(True, 1, 0, 0.05, False, graph)
+        o['train']['use_amp'] = True
+        model = build_model(o)
+        losses = []
+        for step in range(1, 6):
+            lq, gt = _batch(step)
+            model.feed_data({'lq': lq, 'gt': gt})
+            model.update_learning_rate(step)
+            model.optimize_parameters(step)
+            losses.append(model.get_current_log()['l_pix'])
+        net = model.get_bare_model(model.net_g)
+        out.append((losses, {k: v.detach().cpu().numpy().copy() for k, v in net.state_dict().items()},
+                    model._graph.n_segments if graph else 0))
+    dist.destroy_process_group()
+    q.put(out)
+
+
+def test_ddp_graph_segments_rccl_world1_bitwise(cuda):
+    """The segmented-graph DDP step over RCCL (world 1 on the one card, bf16): graph replays are
+    bitwise equal to the eager DDP steps."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    (l0, s0, _), (l1, s1, nseg) = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert nseg >= 3
+    assert l0 == l1
+    for k in s0:
+        assert (s0[k] == s1[k]).all(), k

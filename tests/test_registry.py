@@ -14,7 +14,6 @@ def test_register_get_suffix_duplicate():
     r.register(A, suffix='x')
     assert r.get('A') is A
     assert 'A' in r and 'A_x' in r
-    assert r.get('B', suffix='nope') if False else True
     with pytest.raises(AssertionError):
         r.register(A)
     with pytest.raises(KeyError):

@@ -1,0 +1,127 @@
+"""SRRSModel / SwinIRRSModel (basicsr/models/srrs_model.py:33-88, swinir_model.py:40-42): the AMP
+train step of the fork's remote-sensing configs (options/train/SwinIR/train_SwinIR_S2N256_scratch.yml
+selects SwinIRRSModel).
+
+* fp32 (use_amp false): two steps replayed by the CPU oracle with torch.optim.Adam and the EMA
+  formula, relative 2e-4 (as the SRModel test);
+* bf16 autocast (use_amp true; the reference's fp16 + GradScaler, bf16 here needs no scaler): the
+  step's loss is the oracle's fp32 loss on the same weights within 1e-2 relative, and the parameter
+  update it applies points the same way as the oracle's fp32 Adam update (cosine >= 0.98 over all
+  parameters; Adam's first step is ~lr * sign(g), so bf16 rounding flips only the signs of
+  near-zero gradient entries);
+* the NaN / Inf branch: a non-finite loss skips the optimizer step (parameters, EMA and the Adam
+  step count untouched, gradients zero, the batch dropped) and training continues afterwards.
+"""
+import pytest
+import torch
+
+from oracle import nets as O
+
+pytestmark = pytest.mark.gpu
+
+EDSR = dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=2, upscale=4, res_scale=1)
+SWINIR = dict(type='SwinIR', upscale=4, in_chans=3, img_size=16, window_size=8, img_range=1., depths=[2],
+              embed_dim=60, num_heads=[6], mlp_ratio=2, upsampler='pixelshuffle', resi_connection='1conv',
+              drop_path_rate=0.)
+
+
+def _opt(model_type, net, amp):
+    return dict(model_type=model_type, is_train=True, dist=False, num_gpu=1, path={}, network_g=dict(net), scale=4,
+                train=dict(ema_decay=0.999, use_amp=amp,
+                           optim_g=dict(type='Adam', lr=1e-3, weight_decay=0, betas=[0.9, 0.99]),
+                           scheduler=dict(type='MultiStepLR', milestones=[100], gamma=0.5),
+                           pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')))
+
+
+def _oracle(net, sd, lq):
+    if net['type'] == 'EDSR':
+        return O.edsr(sd, lq, num_block=2, upscale=4)
+    return O.swinir(sd, lq, net)
+
+
+def _replay(net, sd0, lq, gt, steps):
+    params = {k: v.clone().requires_grad_(True) for k, v in sd0.items() if v.is_floating_point()}
+    ema = {k: v.clone() for k, v in params.items()}
+    opt = torch.optim.Adam(list(params.values()), lr=1e-3, betas=(0.9, 0.99))
+    losses = []
+    for _ in range(steps):
+        opt.zero_grad()
+        full = dict(sd0, **params)
+        loss = O.l1_loss(_oracle(net, full, lq), gt)
+        loss.backward()
+        opt.step()
+        with torch.no_grad():
+            for k in ema:
+                ema[k].mul_(0.999).add_(params[k], alpha=0.001)
+        losses.append(loss.item())
+    return params, ema, losses
+
+
+@pytest.mark.parametrize('mtype,net', [('SRRSModel', EDSR), ('SwinIRRSModel', SWINIR)])
+def test_srrs_fp32_steps_match_oracle(cuda, mtype, net):
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    torch.manual_seed(0)
+    model = build_model(_opt(mtype, net, amp=False))
+    assert type(model).__name__ == mtype
+    bare = model.get_bare_model(model.net_g)
+    sd0 = {k: v.detach().cpu().clone() for k, v in bare.state_dict().items()}
+    lq = torch.rand(2, 3, 16, 16, generator=torch.Generator().manual_seed(0))
+    gt = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(1))
+    got = []
+    for it in (1, 2):
+        model.feed_data({'lq': lq, 'gt': gt})
+        model.update_learning_rate(it)
+        model.optimize_parameters(it)
+        got.append(model.get_current_log()['l_pix'])
+    params, ema, losses = _replay(net, sd0, lq, gt, 2)
+    for a, b in zip(got, losses):
+        assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (got, losses)
+    for k, v in bare.state_dict().items():
+        if k in params:
+            err = (v.cpu() - params[k].detach()).abs().max().item() / max(1e-3, params[k].abs().max().item())
+            assert err < 2e-4, (k, err)
+    for k, v in model.net_g_ema.state_dict().items():
+        if k in ema:
+            err = (v.cpu() - ema[k]).abs().max().item() / max(1e-3, ema[k].abs().max().item())
+            assert err < 2e-4, (k, err)
+
+
+@pytest.mark.parametrize('mtype,net', [('SRRSModel', EDSR), ('SwinIRRSModel', SWINIR)])
+def test_srrs_bf16_step_and_nan_skip(cuda, mtype, net):
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    torch.manual_seed(0)
+    model = build_model(_opt(mtype, net, amp=True))
+    bare = model.get_bare_model(model.net_g)
+    sd0 = {k: v.detach().cpu().clone() for k, v in bare.state_dict().items()}
+    lq = torch.rand(2, 3, 16, 16, generator=torch.Generator().manual_seed(0))
+    gt = torch.rand(2, 3, 64, 64, generator=torch.Generator().manual_seed(1))
+
+    # a NaN batch first: skipped, nothing moves
+    bad = lq.clone()
+    bad[0, 0, 3, 3] = float('nan')
+    model.feed_data({'lq': bad, 'gt': gt})
+    model.update_learning_rate(1)
+    model.optimize_parameters(1)
+    assert not hasattr(model, 'lq') and not hasattr(model, 'output')
+    assert model.optimizer_g.nstep == 0
+    assert float(model.flat_g.grad.abs().max()) == 0.0
+    for k, v in bare.state_dict().items():
+        assert torch.equal(v.cpu(), sd0[k]), k
+    for k, v in model.net_g_ema.state_dict().items():
+        assert torch.equal(v.cpu(), sd0[k]), k
+
+    # then a real bf16 step
+    model.feed_data({'lq': lq, 'gt': gt})
+    model.update_learning_rate(2)
+    model.optimize_parameters(2)
+    loss = model.get_current_log()['l_pix']
+    assert model.optimizer_g.nstep == 1
+    params, _, losses = _replay(net, sd0, lq, gt, 1)
+    assert abs(loss - losses[0]) < 1e-2 * abs(losses[0]), (loss, losses)
+    d_gpu = torch.cat([(v.cpu() - sd0[k]).reshape(-1) for k, v in bare.state_dict().items() if k in params])
+    d_ref = torch.cat([(params[k].detach() - sd0[k]).reshape(-1) for k in bare.state_dict() if k in params])
+    cos = torch.nn.functional.cosine_similarity(d_gpu.double(), d_ref.double(), dim=0).item()
+    print(f'{mtype} bf16: loss {loss:.6f} vs oracle fp32 {losses[0]:.6f}, update cosine {cos:.4f}')
+    assert cos >= 0.98, cos

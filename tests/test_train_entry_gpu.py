@@ -110,7 +110,10 @@ def test_train_pipeline_from_yaml_then_auto_resume(cuda, tmp_path):
     ck = torch.load(os.path.join(exp, 'models', 'net_g_2.pth'), map_location='cpu', weights_only=True)
     assert set(ck) == {'params', 'params_ema'}
     logs = [f for f in os.listdir(exp) if f.startswith('train_') and f.endswith('.log')]
-    assert logs and 'l_pix:' in open(os.path.join(exp, logs[0])).read()
+    log_text = open(os.path.join(exp, logs[0])).read()
+    assert logs and 'l_pix:' in log_text
+    # the validation metric record of basicsr/models/sr_model.py:252-266, with the best value
+    assert 'Validation Set5' in log_text and '# psnr: ' in log_text and 'Best: ' in log_text
 
     # auto-resume from the newest state (iter 2) and run on to iteration 5
     reset_root_logger()
