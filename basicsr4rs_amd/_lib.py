@@ -85,6 +85,10 @@ SIGNATURES = {
     'sr_ca_mlp_fwd': (_i, [_vp, _i, _f, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     'sr_ca_mlp_bwd': (_i, [_vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
     'sr_nc_affine': (_i, [_i, _vp, _vp, _vp, _vp, _i, _i, _i, _f, _f, _f, _vp, _vp]),
+    'sr_ca_fwd_apply': (_i, [_i, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp,
+                             _vp]),
+    'sr_ca_bwd_apply': (_i, [_i, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    'sr_ca_param_grad': (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     'sr_act_backward_nhwc': (_i, [_i, _i64, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _f, _f, _vp]),
     'sr_nearest_up_backward': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     'sr_copy_channels': (_i, [_i, _vp, _i, _i, _vp, _i, _i, _i64, _i, _vp]),

@@ -8,8 +8,10 @@
 //   sr_channel_partials  the first pass alone (consumers sum the per-chunk partials)
 //   sr_ca_mlp_fwd/_bwd   the 1x1 conv -> ReLU -> 1x1 conv -> Sigmoid squeeze MLP (rcan_arch.py:19-20),
 //                        summing partial pools (conv colsum / channel partials) on the way in
-//   sr_ca_scale_residual out = x + rs * u * s[n, c]   (RCAB tail, rcan_arch.py:22-24, 44-46)
-//   sr_ca_du             du = rs * dout * s[n, c] + dpool[n, c] / HW   (RCAB backward)
+//   sr_nc_affine         out = beta x + alpha u s[n, c] + gamma t[n, c] (RCAB tail and its du)
+//   sr_ca_fwd_apply      squeeze MLP + RCAB tail y = x + rs * u * s in one launch (rcan_arch.py:22-24, 44-46)
+//   sr_ca_bwd_apply      squeeze-MLP backward + du = rs * dout * s + dpool / HW in one launch
+//   sr_ca_param_grad     the squeeze convs' parameter gradients (off the critical path)
 //   sr_act_backward_nhwc strided (channel-slice) ReLU/LeakyReLU backward (RRDB dense slices)
 //   sr_nearest_up_backward  sum of each 2x2 (s x s) block: backward of F.interpolate(
 //                        scale_factor=s, mode='nearest') (rrdbnet_arch.py:116-117)
@@ -252,6 +254,177 @@ __global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restric
   }
 }
 
+// ---- Fused channel-attention apply kernels (RCAB, rcan_arch.py:8-24, :44-46) -------------------
+// The squeeze MLP of one image is a few hundred FLOPs; as its own launch it costs a dependent
+// kernel (ca_mlp_fwd 5 us, ca_mlp_bwd 17.6 us on one block) ahead of an elementwise pass over the
+// image (nc_affine 8.5 us).  Here every block of the elementwise pass recomputes its image's MLP
+// from the partial sums (fixed summation order, so every block gets bit-identical s / dpool) and
+// then applies it to its pixel range: one launch instead of two, no single-block kernel on the
+// critical path.  Block 0 of each image also writes the MLP state the backward / the parameter
+// gradients need.  Grid (K, N), 256 threads, C % 8 == 0, C <= CA_FMAXC, Cr <= CA_FMAXR.
+constexpr int CA_FMAXC = 256, CA_FMAXR = 64, CA_FNT = 256;
+
+// pool (forward: scale * sum of parts, groups of rows in a fixed order) -> h -> s into LDS
+SR_DEV void ca_block_fwd_mlp(const float* __restrict__ pn, int P, float scale, const float* __restrict__ w1,
+                             const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+                             int C, int Cr, float* red, float* pl, float* hr, float* sl) {
+  const int t = threadIdx.x;
+  const int G = CA_FNT / C > 0 ? CA_FNT / C : 1;
+  for (int i = t; i < C * G; i += CA_FNT) {
+    const int c = i % C, g = i / C;
+    red[g * C + c] = strided_sum(pn + c, g, P, G, C);
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += CA_FNT) {
+    float acc = 0.f;
+    for (int g = 0; g < G; ++g) acc += red[g * C + c];
+    pl[c] = acc * scale;
+  }
+  __syncthreads();
+  for (int r = t; r < Cr; r += CA_FNT) {
+    float acc = b1 ? b1[r] : 0.f;
+    for (int c = 0; c < C; ++c) acc += w1[r * C + c] * pl[c];
+    hr[r] = acc > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += CA_FNT) {
+    float acc = b2 ? b2[c] : 0.f;
+    for (int r = 0; r < Cr; ++r) acc += w2[c * Cr + r] * hr[r];
+    sl[c] = 1.f / (1.f + expf(-acc));
+  }
+  __syncthreads();
+}
+
+// y = x + alpha * u * s[n, c] over pixels [k * ppb, (k + 1) * ppb) of image n
+template <typename T>
+__global__ __launch_bounds__(256) void ca_fwd_apply_kernel(const float* __restrict__ parts, int P, float scale,
+                                                           const float* __restrict__ w1, const float* __restrict__ b1,
+                                                           const float* __restrict__ w2, const float* __restrict__ b2,
+                                                           const T* __restrict__ x, const T* __restrict__ u, int HW,
+                                                           int C, int Cr, int ppb, float alpha, T* __restrict__ y,
+                                                           float* __restrict__ pool, float* __restrict__ h,
+                                                           float* __restrict__ s) {
+  constexpr int PER = Elt<T>::PER16;
+  __shared__ float red[CA_FNT], pl[CA_FMAXC], hr[CA_FMAXR], sl[CA_FMAXC];
+  const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x;
+  ca_block_fwd_mlp(parts + (size_t)n * P * C, P, scale, w1, b1, w2, b2, C, Cr, red, pl, hr, sl);
+  if (k == 0) {
+    for (int c = t; c < C; c += CA_FNT) { pool[n * C + c] = pl[c]; s[n * C + c] = sl[c]; }
+    for (int r = t; r < Cr; r += CA_FNT) h[n * Cr + r] = hr[r];
+  }
+  const int cv = C / PER;
+  const int p0 = k * ppb, p1 = min(HW, p0 + ppb);
+  const size_t base = ((size_t)n * HW) * cv;
+  for (int i = p0 * cv + t; i < p1 * cv; i += CA_FNT) {
+    const int c0 = (i % cv) * PER;
+    const u32x4 vu = ((const u32x4*)u)[base + i];
+    const u32x4 vx = ((const u32x4*)x)[base + i];
+    u32x4 o;
+    if constexpr (PER == 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float u0 = bf16_to_f32(vu[j] & 0xffff), u1 = bf16_to_f32(vu[j] >> 16);
+        const float x0 = bf16_to_f32(vx[j] & 0xffff), x1 = bf16_to_f32(vx[j] >> 16);
+        o[j] = pack_bf16x2(1.f * x0 + alpha * u0 * sl[c0 + 2 * j], 1.f * x1 + alpha * u1 * sl[c0 + 2 * j + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = __float_as_uint(1.f * __uint_as_float(vx[j]) + alpha * __uint_as_float(vu[j]) * sl[c0 + j]);
+    }
+    ((u32x4*)y)[base + i] = o;
+  }
+}
+
+// du = alpha * dy * s[n, c] + dpool[n, c] / HW, with ds = alpha * sum_p parts (dL/ds), dz2 = ds s (1 - s),
+// dz1 = relu'(h) (W2^T dz2), dpool = W1^T dz1 recomputed per block (the order of ca_mlp_bwd_kernel)
+template <typename T>
+__global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restrict__ parts, int P, float alpha,
+                                                           const float* __restrict__ s, const float* __restrict__ h,
+                                                           const float* __restrict__ w1, const float* __restrict__ w2,
+                                                           const T* __restrict__ dy, int HW, int C, int Cr, int ppb,
+                                                           T* __restrict__ du, float* __restrict__ dz2_out,
+                                                           float* __restrict__ dz1_out) {
+  constexpr int PER = Elt<T>::PER16;
+  __shared__ float sl[CA_FMAXC], dz2[CA_FMAXC], dz1[CA_FMAXR], tp[CA_FMAXC];
+  const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x;
+  for (int c = t; c < C; c += CA_FNT) {
+    const float ds = strided_sum(parts + (size_t)n * P * C + c, 0, P, 1, C);
+    const float si = s[n * C + c];
+    sl[c] = si;
+    dz2[c] = ds * alpha * si * (1.f - si);
+  }
+  __syncthreads();
+  for (int r = t; r < Cr; r += CA_FNT) {
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc += w2[c * Cr + r] * dz2[c];
+    dz1[r] = h[n * Cr + r] > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+  const float inv_hw = 1.f / (float)HW;
+  for (int c = t; c < C; c += CA_FNT) {
+    float acc = 0.f;
+    for (int r = 0; r < Cr; ++r) acc += w1[r * C + c] * dz1[r];
+    tp[c] = inv_hw * acc;
+  }
+  if (k == 0) {
+    for (int c = t; c < C; c += CA_FNT) dz2_out[n * C + c] = dz2[c];
+    for (int r = t; r < Cr; r += CA_FNT) dz1_out[n * Cr + r] = dz1[r];
+  }
+  __syncthreads();
+  const int cv = C / PER;
+  const int p0 = k * ppb, p1 = min(HW, p0 + ppb);
+  const size_t base = ((size_t)n * HW) * cv;
+  for (int i = p0 * cv + t; i < p1 * cv; i += CA_FNT) {
+    const int c0 = (i % cv) * PER;
+    const u32x4 vd = ((const u32x4*)dy)[base + i];
+    u32x4 o;
+    if constexpr (PER == 8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d0 = bf16_to_f32(vd[j] & 0xffff), d1 = bf16_to_f32(vd[j] >> 16);
+        o[j] = pack_bf16x2(0.f * 0.f + alpha * d0 * sl[c0 + 2 * j] + tp[c0 + 2 * j],
+                           0.f * 0.f + alpha * d1 * sl[c0 + 2 * j + 1] + tp[c0 + 2 * j + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = __float_as_uint(0.f * 0.f + alpha * __uint_as_float(vd[j]) * sl[c0 + j] + tp[c0 + j]);
+    }
+    ((u32x4*)du)[base + i] = o;
+  }
+}
+
+// squeeze-conv parameter gradients from the per-image dz2 / dz1 (same loop order as ca_mlp_bwd_kernel)
+__global__ __launch_bounds__(256) void ca_param_grad_kernel(const float* __restrict__ dz2, const float* __restrict__ dz1,
+                                                            const float* __restrict__ h, const float* __restrict__ pool,
+                                                            int N, int C, int Cr, float* __restrict__ dw1,
+                                                            float* __restrict__ db1, float* __restrict__ dw2,
+                                                            float* __restrict__ db2, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nt = gridDim.x * blockDim.x;
+  for (int i = t; i < C * Cr; i += nt) {
+    const int c = i / Cr, r = i - c * Cr;
+    float a2 = 0.f, a1 = 0.f;
+    for (int n = 0; n < N; ++n) {
+      a2 += dz2[n * C + c] * h[n * Cr + r];
+      a1 += dz1[n * Cr + r] * pool[n * C + c];
+    }
+    dw2[i] = (accumulate ? dw2[i] : 0.f) + a2;
+    dw1[r * C + c] = (accumulate ? dw1[r * C + c] : 0.f) + a1;
+  }
+  for (int c = t; c < C; c += nt) {
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += dz2[n * C + c];
+    if (db2) db2[c] = (accumulate ? db2[c] : 0.f) + acc;
+  }
+  for (int r = t; r < Cr; r += nt) {
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r];
+    if (db1) db1[r] = (accumulate ? db1[r] : 0.f) + acc;
+  }
+}
+
 // out = beta * x + alpha * u * s[n,c] + gamma * t[n,c]   (all NHWC with the same C, dense)
 // RCAB forward: beta 1, alpha rs, s = sigmoid, t = null.  RCAB du: x = null, u = dout,
 // alpha = rs, s = sigmoid, gamma = 1/HW, t = dpool.
@@ -487,6 +660,63 @@ int sr_ca_mlp_bwd(const float* parts, int P, float scale, const float* s, const 
   hipLaunchKernelGGL(ca_mlp_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, parts, P, scale, s, h, pool, w1,
                      w2, N, C, Cr, dpool, dw1, db1, dw2, db2, accumulate);
   return sr_check(hipGetLastError(), "ca_mlp_bwd launch");
+}
+
+// pixels per block of the fused CA kernels: ~8 16-B vectors per thread, at least 64 pixels
+static int ca_ppb(int HW, int C, int PER) {
+  int ppb = (CA_FNT * 8 * PER) / C;
+  if (ppb < 64) ppb = 64;
+  return ppb > HW ? HW : ppb;
+}
+
+int sr_ca_fwd_apply(int dtype, const float* parts, int P, float scale, const float* w1, const float* b1,
+                    const float* w2, const float* b2, const void* x, const void* u, int N, int HW, int C, int Cr,
+                    float alpha, void* y, float* pool, float* h, float* s_out, void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!parts || P < 1 || !w1 || !w2 || !x || !u || !y || !pool || !h || !s_out || N < 1 || HW < 1 || C % 8 ||
+      C > CA_FMAXC || Cr < 1 || Cr > CA_FMAXR || !aligned16(x) || !aligned16(u) || !aligned16(y))
+    return sr_fail(SR_EINVAL, "ca_fwd_apply: bad arguments (C % 8 == 0, C <= 256, Cr <= 64, 16-B aligned maps)");
+  if ((int64_t)N * HW * C / PER >= 0x7fffffffll) return sr_fail(SR_ETOOBIG, "ca_fwd_apply: tensor too large");
+  const int ppb = ca_ppb(HW, C, PER);
+  const dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)N);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(ca_fwd_apply_kernel<bf16_t>, grid, dim3(CA_FNT), 0, st, parts, P, scale, w1, b1, w2, b2,
+                       (const bf16_t*)x, (const bf16_t*)u, HW, C, Cr, ppb, alpha, (bf16_t*)y, pool, h, s_out);
+  else
+    hipLaunchKernelGGL(ca_fwd_apply_kernel<float>, grid, dim3(CA_FNT), 0, st, parts, P, scale, w1, b1, w2, b2,
+                       (const float*)x, (const float*)u, HW, C, Cr, ppb, alpha, (float*)y, pool, h, s_out);
+  return sr_check(hipGetLastError(), "ca_fwd_apply launch");
+}
+
+int sr_ca_bwd_apply(int dtype, const float* parts, int P, float alpha, const float* s, const float* h, const float* w1,
+                    const float* w2, const void* dy, int N, int HW, int C, int Cr, void* du, float* dz2, float* dz1,
+                    void* stream) {
+  const int PER = dtype == SR_BF16 ? 8 : 4;
+  if (!parts || P < 1 || !s || !h || !w1 || !w2 || !dy || !du || !dz2 || !dz1 || N < 1 || HW < 1 || C % 8 ||
+      C > CA_FMAXC || Cr < 1 || Cr > CA_FMAXR || !aligned16(dy) || !aligned16(du))
+    return sr_fail(SR_EINVAL, "ca_bwd_apply: bad arguments (C % 8 == 0, C <= 256, Cr <= 64, 16-B aligned maps)");
+  if ((int64_t)N * HW * C / PER >= 0x7fffffffll) return sr_fail(SR_ETOOBIG, "ca_bwd_apply: tensor too large");
+  const int ppb = ca_ppb(HW, C, PER);
+  const dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)N);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == SR_BF16)
+    hipLaunchKernelGGL(ca_bwd_apply_kernel<bf16_t>, grid, dim3(CA_FNT), 0, st, parts, P, alpha, s, h, w1, w2,
+                       (const bf16_t*)dy, HW, C, Cr, ppb, (bf16_t*)du, dz2, dz1);
+  else
+    hipLaunchKernelGGL(ca_bwd_apply_kernel<float>, grid, dim3(CA_FNT), 0, st, parts, P, alpha, s, h, w1, w2,
+                       (const float*)dy, HW, C, Cr, ppb, (float*)du, dz2, dz1);
+  return sr_check(hipGetLastError(), "ca_bwd_apply launch");
+}
+
+int sr_ca_param_grad(const float* dz2, const float* dz1, const float* h, const float* pool, int N, int C, int Cr,
+                     float* dw1, float* db1, float* dw2, float* db2, int accumulate, void* stream) {
+  if (!dz2 || !dz1 || !h || !pool || !dw1 || !dw2 || N < 1 || C < 1 || Cr < 1)
+    return sr_fail(SR_EINVAL, "ca_param_grad: bad arguments");
+  const int work = C * Cr > C ? C * Cr : C;
+  hipLaunchKernelGGL(ca_param_grad_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     dz2, dz1, h, pool, N, C, Cr, dw1, db1, dw2, db2, accumulate);
+  return sr_check(hipGetLastError(), "ca_param_grad launch");
 }
 
 int sr_nc_affine(int dtype, const void* x, const void* u, const float* s, const float* t, int N, int HW, int C,

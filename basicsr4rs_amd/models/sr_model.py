@@ -100,8 +100,10 @@ class SRModel(BaseModel):
     def _fused_step(self):
         return hasattr(self.optimizer_g, 'device_step')
 
-    def _step_body(self):
-        """Device work of one train step (everything a captured replay re-executes)."""
+    def _step_body(self, before_backward=None):
+        """Device work of one train step (everything a captured replay re-executes).
+        ``before_backward(loss) -> loss`` runs between the loss and backward (the segmented
+        capture ends its forward segment there, utils/step_graph.py)."""
         self.optimizer_g.zero_grad()
         with torch.autocast('cuda', dtype=torch.bfloat16, enabled=self.use_amp):
             self.output = self.net_g(self.lq)
@@ -111,6 +113,8 @@ class SRModel(BaseModel):
             l_pix = self.cri_pix(self.output, self.gt)
             l_total += l_pix
             loss_dict['l_pix'] = l_pix
+        if before_backward is not None:
+            l_total = before_backward(l_total)
         with async_wgrad(self.async_wgrad):  # weight gradients on a side stream, joined here
             l_total.backward()
         # drop the autograd graph now: a graph kept alive by self.output would pin this step's

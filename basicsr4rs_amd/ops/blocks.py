@@ -78,12 +78,14 @@ class _RCAB(torch.autograd.Function):
         pool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
         h = torch.empty(N, Cr, device=x.device, dtype=torch.float32)
         s = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+        y = torch.empty_like(u)
+        # squeeze MLP + y = x + rs * u * s in one launch (csrc/blocks.hip ca_fwd_apply_kernel)
         _lib.check(
-            lib.sr_ca_mlp_fwd(_lib.ptr(parts), parts.shape[1], 1.0 / (H * W), _lib.ptr(a1),
-                              _lib.ptr(ab1.detach() if ab1 is not None else None), _lib.ptr(a2),
-                              _lib.ptr(ab2.detach() if ab2 is not None else None), N, Cp, Cr, _lib.ptr(pool),
-                              _lib.ptr(h), _lib.ptr(s), _lib.stream()))
-        y = nc_affine(x, u, s, None, 1.0, rs, 0.0)
+            lib.sr_ca_fwd_apply(_lib.dtype_code(dtype), _lib.ptr(parts), parts.shape[1], 1.0 / (H * W), _lib.ptr(a1),
+                                _lib.ptr(ab1.detach() if ab1 is not None else None), _lib.ptr(a2),
+                                _lib.ptr(ab2.detach() if ab2 is not None else None), _lib.ptr(x), _lib.ptr(u), N,
+                                H * W, Cp, Cr, float(rs), _lib.ptr(y), _lib.ptr(pool), _lib.ptr(h), _lib.ptr(s),
+                                _lib.stream()))
         ctx.specs = (spec1, spec2)
         ctx.rs = rs
         ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2)
@@ -105,7 +107,16 @@ class _RCAB(torch.autograd.Function):
         parts = torch.empty(N, lib.sr_channel_partials_count(H * W), Cp, device=x.device, dtype=torch.float32)
         _lib.check(lib.sr_channel_partials(_lib.dtype_code(dtype), _lib.ptr(dy), Cp, 0, _lib.ptr(u), Cp, 0, N, H * W,
                                            Cp, _lib.ptr(parts), _lib.stream()))
-        dpool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+        # squeeze-MLP backward + du = rs * dy * s + dpool / HW in one launch; the squeeze convs'
+        # parameter gradients follow from the per-image dz2 / dz1 in their own small launch, on
+        # the weight-gradient side stream when one is active (they only feed the optimizer)
+        du = torch.empty_like(dy)
+        dz2 = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+        dz1 = torch.empty(N, Cr, device=x.device, dtype=torch.float32)
+        _lib.check(
+            lib.sr_ca_bwd_apply(_lib.dtype_code(dtype), _lib.ptr(parts), parts.shape[1], float(rs), _lib.ptr(s),
+                                _lib.ptr(h), _lib.ptr(a1), _lib.ptr(a2), _lib.ptr(dy), N, H * W, Cp, Cr, _lib.ptr(du),
+                                _lib.ptr(dz2), _lib.ptr(dz1), _lib.stream()))
         # squeeze-conv gradients: straight into the optimizer's flat .grad views when they exist
         ca = (aw1, ab1, aw2, ab2)
         tg = [C.grad_target(p) for p in ca]
@@ -116,14 +127,20 @@ class _RCAB(torch.autograd.Function):
             dA1, dA2 = torch.empty_like(a1), torch.empty_like(a2)
             dab1 = torch.empty(Cr, device=x.device, dtype=torch.float32) if ab1 is not None else None
             dab2 = torch.empty(Cp, device=x.device, dtype=torch.float32) if ab2 is not None else None
-        _lib.check(
-            lib.sr_ca_mlp_bwd(_lib.ptr(parts), parts.shape[1], rs, _lib.ptr(s), _lib.ptr(h), _lib.ptr(pool),
-                              _lib.ptr(a1), _lib.ptr(a2), N, Cp, Cr, _lib.ptr(dpool), _lib.ptr(dA1), _lib.ptr(dab1),
-                              _lib.ptr(dA2), _lib.ptr(dab2), int(direct), _lib.stream()))
+        args = (_lib.ptr(dz2), _lib.ptr(dz1), _lib.ptr(h), _lib.ptr(pool), N, Cp, Cr, _lib.ptr(dA1), _lib.ptr(dab1),
+                _lib.ptr(dA2), _lib.ptr(dab2), int(direct))
+        side = C.async_side_stream(x.device) if direct else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(x.device))
+            for t_ in (dz2, dz1, h, pool):
+                t_.record_stream(side)
+            with torch.cuda.stream(side):
+                _lib.check(lib.sr_ca_param_grad(*args, _lib.stream()))
+        else:
+            _lib.check(lib.sr_ca_param_grad(*args, _lib.stream()))
         if direct:
             for p in ca:
                 C.grad_ready(p)
-        du = nc_affine(None, dy, s, dpool, 0.0, rs, 1.0 / (H * W))
         _, wd1, _ = C.prepared(w1, b1, spec1, dtype)
         _, wd2, _ = C.prepared(w2, b2, spec2, dtype)
         dz1 = torch.empty_like(t)

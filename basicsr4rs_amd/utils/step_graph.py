@@ -6,27 +6,53 @@ produced that bucket (basicsr/models/base_model.py:87-105 via torch DDP) -- and 
 host-bound on launch-heavy nets (RCAN: 2.7 k launches, 54.5 ms eager against 36.5 ms replayed).
 So the step is captured as segments sharing one memory pool:
 
-    seg 0: forward, loss, backward up to the point where bucket b0 is complete
-    seg 1: backward until bucket b1 is complete
+    fwd:   zero_grad, forward, loss                      (captured on the calling thread)
+    bwd 1: backward until bucket b0 is complete          (captured on autograd's device thread)
+    bwd 2: backward until bucket b1 is complete
     ...
-    seg k: the rest of backward
-    opt:   fused Adam + EMA + weight-image refresh
+    bwd k: the rest of backward
+    opt:   fused Adam + EMA + weight-image refresh         (calling thread)
 
-``GradBucketReducer.on_issue`` is pointed at ``cut`` during capture: the reducer reports a ready
-bucket from its gradient-ready callback, which ends the current segment (after joining the
-side-stream weight-gradient work into the capture stream) and begins the next.  ``replay`` runs
-each segment and, right after it, launches the all-reduces of the buckets that segment completed:
-RCCL orders them after the segment on its own stream while the next segment's kernels run, so the
-exchange overlaps backward exactly as in the eager step, with no per-kernel host work.  After the
-last backward segment the remaining buckets go out, the step joins them (stream waits) and replays
-the optimizer segment.  Segments replay in capture order, which is what sharing one pool requires.
+A stream capture must end on the thread that began it (HIP: hipErrorStreamCaptureWrongThread), and
+autograd runs the backward of CUDA tensors on its own device thread.  So the forward segment ends
+on the calling thread just before ``backward()``; an identity node on the loss (``_BeginBackward``,
+the first node autograd runs) begins the first backward segment on the device thread and queues an
+engine callback that ends the last one there when backward completes.  In between,
+``GradBucketReducer.on_issue`` points at ``cut``: the reducer reports a ready bucket from its
+gradient-ready callback (device thread), which ends the current segment -- after joining the
+side-stream weight-gradient work into the capture stream -- and begins the next.
 
-Every segment starts with one tiny kernel, so that two cuts with nothing launched between them
-(a conv's weight and bias straddling a bucket boundary) never produce an empty graph.
+``replay`` runs each segment and, right after it, launches the all-reduces of the buckets that
+segment completed: RCCL orders them after the segment on its own stream while the next segment's
+kernels run, so the exchange overlaps backward as in the eager step, with no per-kernel host work.
+Buckets that were not complete during backward go out after the last backward segment; the step
+then joins all of them (stream waits) and replays the optimizer segment.  Segments replay in capture
+order, which is what sharing one pool requires.  Every segment starts with one tiny kernel, so that
+two cuts with nothing launched between them (a conv's weight and bias in two buckets) never make an
+empty graph.
 """
 import torch
 
 from ..ops.conv import _ASYNC
+
+
+class _BeginBackward(torch.autograd.Function):
+    """Identity on the loss whose backward (the first backward node) opens the first backward
+    segment on autograd's device thread."""
+
+    @staticmethod
+    def forward(ctx, loss, seg):
+        ctx.seg = seg
+        return loss.view_as(loss)
+
+    @staticmethod
+    def backward(ctx, g):
+        # ``g`` is autograd's ones_like seed, filled eagerly by backward() outside any capture: the
+        # captured backward starts from the seed made inside the forward segment instead
+        seg = ctx.seg
+        seg._begin()
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: seg._end('backward'))
+        return seg._seed, None
 
 
 class SegmentedStepGraph:
@@ -34,7 +60,7 @@ class SegmentedStepGraph:
     def __init__(self, reducer, device):
         self.red = reducer
         self.pool = torch.cuda.graph_pool_handle()
-        self.segments = []  # (graph, buckets completed by it, 'backward' | 'wait')
+        self.segments = []  # [graph, [(bucket, 'backward' | 'wait')] to reduce after it, 'forward' | 'backward' | 'optimizer']
         self._cur = None
         self._cur_buckets = []
         self._tick = torch.zeros(1, device=device, dtype=torch.int32)
@@ -42,43 +68,50 @@ class SegmentedStepGraph:
 
     # ---- capture -------------------------------------------------------------------------
     def _begin(self):
-        g = torch.cuda.CUDAGraph()
-        g.capture_begin(pool=self.pool)
-        self._tick.add_(1)  # the segment's first node
+        assert self._cur is None, 'segment already open'
+        with torch.cuda.stream(self.stream):
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=self.pool)
+            self._tick.add_(1)  # the segment's first node
         self._cur, self._cur_buckets = g, []
 
-    def _end(self, when):
-        cur = torch.cuda.current_stream()
-        for st in _ASYNC['streams'].values():  # rejoin side streams forked during this segment
-            cur.wait_stream(st)
-        self._cur.capture_end()
-        self.segments.append((self._cur, self._cur_buckets, when))
+    def _end(self, kind):
+        with torch.cuda.stream(self.stream):
+            for st in _ASYNC['streams'].values():  # rejoin side streams forked during this segment
+                self.stream.wait_stream(st)
+            self._cur.capture_end()
+        self.segments.append([self._cur, self._cur_buckets, kind])
         self._cur = None
 
     def cut(self, b):
         """GradBucketReducer.on_issue during capture: bucket b is complete here."""
-        self._cur_buckets.append(b)
+        self._cur_buckets.append((b, 'backward'))
         self._end('backward')
         self._begin()
 
-    def capture(self, backward_fn, optimizer_fn):
-        """Capture backward_fn() (forward + loss + backward; returns the loss dict) cut at the ready
-        buckets, then optimizer_fn() as the last segment.  Returns backward_fn's result."""
+    def _before_backward(self, loss):
+        with torch.cuda.stream(self.stream):
+            self._seed = torch.ones_like(loss)  # in the forward segment: a pool tensor refilled per replay
+        self._end('forward')
+        self.red.on_issue = self.cut
+        return _BeginBackward.apply(loss, self)
+
+    def capture(self, step_body, optimizer_fn):
+        """Capture ``step_body(before_backward)`` (forward + loss + backward; returns the loss dict)
+        cut at the ready buckets, then ``optimizer_fn()`` as the last segment."""
         torch.cuda.synchronize()
         self.stream.wait_stream(torch.cuda.current_stream())
-        self.red.on_issue = self.cut
         try:
             with torch.cuda.stream(self.stream):
                 self._begin()
-                out = backward_fn()
-                # buckets whose parameters did not all report ready go out after the last
-                # backward segment (every rank issues the same collectives)
-                self._cur_buckets = []
+                out = step_body(self._before_backward)
+                assert self._cur is None and self.segments[-1][2] == 'backward', 'backward segment left open'
+                # buckets whose parameters did not all report ready go out after the last backward
+                # segment (every rank issues the same collectives)
                 flushed = []
                 self.red.on_issue = flushed.append
                 self.red.flush()
-                self._cur_buckets = flushed
-                self._end('wait')
+                self.segments[-1][1].extend((b, 'wait') for b in flushed)
                 self._begin()
                 optimizer_fn()
                 self._end('optimizer')
@@ -93,14 +126,14 @@ class SegmentedStepGraph:
     # ---- replay --------------------------------------------------------------------------
     def replay(self):
         red = self.red
-        for g, buckets, when in self.segments:
-            if when == 'optimizer':
+        for g, buckets, kind in self.segments:
+            if kind == 'optimizer':
                 for h in red.handles:
                     h.wait()
                 red.last_issue_log, red.issue_log = red.issue_log, []
                 red.reset()
             g.replay()
-            for b in buckets:
+            for b, when in buckets:
                 red.all_reduce_bucket(b)
                 red.issued[b] = True
                 red.issue_log.append((b, when))

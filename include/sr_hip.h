@@ -250,6 +250,24 @@ int sr_ca_mlp_fwd(const float* parts, int P, float scale, const float* w1, const
 int sr_ca_mlp_bwd(const float* parts, int P, float scale, const float* s, const float* h, const float* pool,
                   const float* w1, const float* w2, int N, int C, int Cr, float* dpool, float* dw1, float* db1,
                   float* dw2, float* db2, int accumulate, void* stream);
+/* RCAB channel attention fused with its elementwise pass (rcan_arch.py:8-24, :44-46): every block
+ * of the pass recomputes its image's squeeze MLP from the partial sums (fixed order, identical in
+ * every block), so the MLP is not a dependent single-block launch.
+ *   fwd: pool = scale*sum_p parts, h = relu(W1 pool + b1), s = sigmoid(W2 h + b2), y = x + alpha*u*s;
+ *        pool / h / s are also stored (for the backward);
+ *   bwd: ds = alpha*sum_p parts (parts of dy.u), dz2 = ds*s*(1-s), dz1 = relu'(h)*(W2^T dz2),
+ *        du = alpha*dy*s + (W1^T dz1)/HW; dz2 [N][C] and dz1 [N][Cr] are stored for
+ *   sr_ca_param_grad: dW2 = dz2^T h, dW1 = dz1^T pool, db2 = sum dz2, db1 = sum dz1 (accumulate = 1
+ *        adds into the optimizer's gradient views; db1 / db2 may be NULL).
+ * Dense NHWC [N, HW, C], C % 8 == 0, C <= 256, Cr <= 64; W1 [Cr][C], W2 [C][Cr]. */
+int sr_ca_fwd_apply(int dtype, const float* parts, int P, float scale, const float* w1, const float* b1,
+                    const float* w2, const float* b2, const void* x, const void* u, int N, int HW, int C, int Cr,
+                    float alpha, void* y, float* pool, float* h, float* s, void* stream);
+int sr_ca_bwd_apply(int dtype, const float* parts, int P, float alpha, const float* s, const float* h, const float* w1,
+                    const float* w2, const void* dy, int N, int HW, int C, int Cr, void* du, float* dz2, float* dz1,
+                    void* stream);
+int sr_ca_param_grad(const float* dz2, const float* dz1, const float* h, const float* pool, int N, int C, int Cr,
+                     float* dw1, float* db1, float* dw2, float* db2, int accumulate, void* stream);
 /* out = beta*x + alpha*u*s[n,c] + gamma*t[n,c] on dense NHWC [N,HW,C] (x, t may be NULL):
  * RCAB tail x + rs*u*s and its backward rs*dout*s + dpool/HW. */
 int sr_nc_affine(int dtype, const void* x, const void* u, const float* s, const float* t, int N, int HW, int C,

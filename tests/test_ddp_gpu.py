@@ -21,6 +21,23 @@ def _free_port():
     return p
 
 
+def _collect(q, procs, n, timeout=240):
+    """n results from the worker queue; fails fast (instead of waiting out the timeout) when a
+    worker dies, and prints a heartbeat so a slow run is not mistaken for a hang."""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=10))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f'worker died: exit codes {dead}'
+            assert time.time() - t0 < timeout, 'workers timed out'
+            print(f'  waiting for workers ({time.time() - t0:.0f} s)', flush=True)
+    return out
+
+
 def _opt(dist_, world, rank, bucket_mb, async_wgrad=False, graph=False):
     return dict(model_type='SRModel', is_train=True, dist=dist_, num_gpu=1, world_size=world, rank=rank, path={},
                 bucket_cap_mb=bucket_mb,
@@ -75,8 +92,7 @@ def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb, async_wgrad):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
-        rank, sd, nb, log, _ = q.get(timeout=180)
+    for rank, sd, nb, log, _ in _collect(q, procs, 2):
         res[rank] = (sd, nb, log)
     for p in procs:
         p.join(timeout=60)
@@ -123,8 +139,7 @@ def test_ddp_graph_segments_match_full_batch(cuda, async_wgrad):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
-        rank, sd, nb, log, nseg = q.get(timeout=240)
+    for rank, sd, nb, log, nseg in _collect(q, procs, 2):
         res[rank] = (sd, nb, log, nseg)
     for p in procs:
         p.join(timeout=60)
@@ -188,7 +203,7 @@ def test_ddp_graph_segments_rccl_world1_bitwise(cuda):
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
     p.start()
-    (l0, s0, _), (l1, s1, nseg) = q.get(timeout=240)
+    ((l0, s0, _), (l1, s1, nseg)), = _collect(q, [p], 1)
     p.join(timeout=60)
     assert p.exitcode == 0
     assert nseg >= 3
