@@ -60,6 +60,7 @@ SIGNATURES = {
     'sr_conv3x3_set_variant': (_i, [_i]),
     'sr_conv3x3_set_stamps': (_i, [_vp]),
     'sr_conv3x3_fwd_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(ConvDesc)]),
+    'sr_conv3x3_fwd_launches': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_wgrad_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad_workspace': (_sz, [ctypes.POINTER(WgradDesc)]),
     'sr_conv3x3_wgrad': (_i, [ctypes.POINTER(WgradDesc), _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp, _vp]),

@@ -62,21 +62,24 @@ __global__ void channel_reduce_partial(const T* __restrict__ a, int lda, int aco
   const int g = tid % groups, pl = tid / groups;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if constexpr (PER == 8) {
-    // bf16: 4 pixels' loads in flight per iteration (one load pair per round trip left the
-    // kernel latency-bound: RCAN 13 us for 34 MB)
+    // bf16: 8 pixels' loads in flight per iteration (one load pair per round trip left the
+    // kernel latency-bound: RCAN 13 us for 34 MB; 4 in flight: 11.6 us)
     if (pl < lanes) {
       const int p0 = chunk * RED_CHUNK, p1 = min(HW, p0 + RED_CHUNK);
-      for (int p = p0 + pl; p < p1; p += 4 * lanes) {
-        u32x4 va[4], vb[4];
+      for (int p = p0 + pl; p < p1; p += 8 * lanes) {
+        u32x4 va[8], vb[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {  // unconditional (clamped) loads, masked after: no branch per load
           const int pu = p + u * lanes;
           const size_t pix = (size_t)n * HW + (pu < p1 ? pu : p);
-          va[u] = pu < p1 ? *(const u32x4*)(a + pix * lda + acoff + g * 8) : u32x4{0u, 0u, 0u, 0u};
-          vb[u] = (b && pu < p1) ? *(const u32x4*)(b + pix * ldb + bcoff + g * 8) : u32x4{0u, 0u, 0u, 0u};
+          va[u] = *(const u32x4*)(a + pix * lda + acoff + g * 8);
+          vb[u] = b ? *(const u32x4*)(b + pix * ldb + bcoff + g * 8) : u32x4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 8; ++u)
+          if (p + u * lanes >= p1) va[u] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             float a0 = bf16_to_f32(va[u][k] & 0xffff), a1 = bf16_to_f32(va[u][k] >> 16);
@@ -255,44 +258,59 @@ __global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restric
 }
 
 // ---- Fused channel-attention apply kernels (RCAB, rcan_arch.py:8-24, :44-46) -------------------
-// The squeeze MLP of one image is a few hundred FLOPs; as its own launch it costs a dependent
-// kernel (ca_mlp_fwd 5 us, ca_mlp_bwd 17.6 us on one block) ahead of an elementwise pass over the
-// image (nc_affine 8.5 us).  Here every block of the elementwise pass recomputes its image's MLP
-// from the partial sums (fixed summation order, so every block gets bit-identical s / dpool) and
-// then applies it to its pixel range: one launch instead of two, no single-block kernel on the
-// critical path.  Block 0 of each image also writes the MLP state the backward / the parameter
-// gradients need.  Grid (K, N), 256 threads, C % 8 == 0, C <= CA_FMAXC, Cr <= CA_FMAXR.
-constexpr int CA_FMAXC = 256, CA_FMAXR = 64, CA_FNT = 256;
+// The squeeze MLP of one image is a few hundred FLOPs; as its own launch it is a dependent,
+// latency-bound kernel (ca_mlp_fwd 5 us, ca_mlp_bwd 17.6 us on one block) ahead of an elementwise
+// pass over the image (nc_affine 8.5 us, HBM-bound).  Here every block of the elementwise pass
+// recomputes its image's MLP from the partial sums (fixed summation order, so every block gets
+// bit-identical s / dpool) and applies it to its pixel range: the block first issues the loads of
+// its map vectors (CA_VPT 16-B vectors per thread per map, held in registers) and of the MLP
+// operands (partial rows, weights, per-image state: all loads up front, staged in LDS), so the
+// MLP's latency chain runs under the map traffic instead of ahead of it.  Block 0 of each image
+// also writes the MLP state the backward / the parameter gradients need.  Grid (K, N), 256 threads,
+// C % 8 == 0, C <= CA_FMAXC, Cr <= CA_FMAXR, C * Cr <= CA_FMAXW, P * C <= CA_FMAXP.
+constexpr int CA_FMAXC = 256, CA_FMAXR = 64, CA_FMAXW = 2048, CA_FMAXP = 8192, CA_FNT = 256, CA_VPT = 8;
 
-// pool (forward: scale * sum of parts, groups of rows in a fixed order) -> h -> s into LDS
-SR_DEV void ca_block_fwd_mlp(const float* __restrict__ pn, int P, float scale, const float* __restrict__ w1,
-                             const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
-                             int C, int Cr, float* red, float* pl, float* hr, float* sl) {
-  const int t = threadIdx.x;
-  const int G = CA_FNT / C > 0 ? CA_FNT / C : 1;
-  for (int i = t; i < C * G; i += CA_FNT) {
-    const int c = i % C, g = i / C;
-    red[g * C + c] = strided_sum(pn + c, g, P, G, C);
+// Staging into LDS with every load of the thread issued before the first LDS store (a load/store
+// loop waits one global-memory round trip per iteration: 17 iterations made ca_param_grad 9 us).
+// Up to U 16-B vectors (f4: float4) or U floats per thread; the caller guarantees n <= U * CA_FNT.
+template <int U>
+SR_DEV void ca_stage_f4(const float* __restrict__ src, int n4, float* __restrict__ dst) {
+  f32x4 v[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int i = threadIdx.x + j * CA_FNT;
+    v[j] = ((const f32x4*)src)[i < n4 ? i : 0];
   }
-  __syncthreads();
-  for (int c = t; c < C; c += CA_FNT) {
-    float acc = 0.f;
-    for (int g = 0; g < G; ++g) acc += red[g * C + c];
-    pl[c] = acc * scale;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int i = threadIdx.x + j * CA_FNT;
+    if (i < n4) ((f32x4*)dst)[i] = v[j];
   }
-  __syncthreads();
-  for (int r = t; r < Cr; r += CA_FNT) {
-    float acc = b1 ? b1[r] : 0.f;
-    for (int c = 0; c < C; ++c) acc += w1[r * C + c] * pl[c];
-    hr[r] = acc > 0.f ? acc : 0.f;
+}
+
+template <int U>
+SR_DEV void ca_stage_f1(const float* __restrict__ src, int n, float* __restrict__ dst) {
+  float v[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int i = threadIdx.x + j * CA_FNT;
+    v[j] = src[i < n ? i : 0];
   }
-  __syncthreads();
-  for (int c = t; c < C; c += CA_FNT) {
-    float acc = b2 ? b2[c] : 0.f;
-    for (int r = 0; r < Cr; ++r) acc += w2[c * Cr + r] * hr[r];
-    sl[c] = 1.f / (1.f + expf(-acc));
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int i = threadIdx.x + j * CA_FNT;
+    if (i < n) dst[i] = v[j];
   }
-  __syncthreads();
+}
+
+// this thread's map vectors of pixels [p0, p1) of image n: vector i = p0 * cv + t + j * CA_FNT
+template <typename T>
+SR_DEV void ca_load_vec(const T* __restrict__ m, size_t base, int i0, int i1, u32x4 (&v)[CA_VPT]) {
+#pragma unroll
+  for (int j = 0; j < CA_VPT; ++j) {
+    const int i = i0 + threadIdx.x + j * CA_FNT;
+    v[j] = ((const u32x4*)m)[base + (i < i1 ? i : i0)];  // unconditional (clamped) load: no branch per load
+  }
 }
 
 // y = x + alpha * u * s[n, c] over pixels [k * ppb, (k + 1) * ppb) of image n
@@ -305,32 +323,70 @@ __global__ __launch_bounds__(256) void ca_fwd_apply_kernel(const float* __restri
                                                            float* __restrict__ pool, float* __restrict__ h,
                                                            float* __restrict__ s) {
   constexpr int PER = Elt<T>::PER16;
-  __shared__ float red[CA_FNT], pl[CA_FMAXC], hr[CA_FMAXR], sl[CA_FMAXC];
+  __shared__ __attribute__((aligned(16))) float pr[CA_FMAXP];
+  __shared__ float W1[CA_FMAXW], W2[CA_FMAXW], B1[CA_FMAXR], B2[CA_FMAXC], red[CA_FNT], pl[CA_FMAXC], hr[CA_FMAXR],
+      sl[CA_FMAXC];
   const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x;
-  ca_block_fwd_mlp(parts + (size_t)n * P * C, P, scale, w1, b1, w2, b2, C, Cr, red, pl, hr, sl);
+  const int cv = C / PER;
+  const int i0 = k * ppb * cv, i1 = min(HW, (k + 1) * ppb) * cv;
+  const size_t base = ((size_t)n * HW) * cv;
+  u32x4 vx[CA_VPT], vu[CA_VPT];
+  ca_load_vec(x, base, i0, i1, vx);
+  ca_load_vec(u, base, i0, i1, vu);
+  ca_stage_f4<CA_FMAXP / 4 / CA_FNT>(parts + (size_t)n * P * C, P * C / 4, pr);
+  ca_stage_f1<CA_FMAXW / CA_FNT>(w1, C * Cr, W1);
+  ca_stage_f1<CA_FMAXW / CA_FNT>(w2, C * Cr, W2);
+  if (b1) ca_stage_f1<1>(b1, Cr, B1);
+  if (b2) ca_stage_f1<1>(b2, C, B2);
+  __syncthreads();
+  // pool: G groups of rows per channel in a fixed order, then their sum
+  const int G = CA_FNT / C > 0 ? CA_FNT / C : 1;
+  for (int i = t; i < C * G; i += CA_FNT) {
+    const int c = i % C, g = i / C;
+    float acc = 0.f;
+    for (int p = g; p < P; p += G) acc += pr[p * C + c];
+    red[g * C + c] = acc;
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += CA_FNT) {
+    float acc = 0.f;
+    for (int g = 0; g < G; ++g) acc += red[g * C + c];
+    pl[c] = acc * scale;
+  }
+  __syncthreads();
+  for (int r = t; r < Cr; r += CA_FNT) {
+    float acc = b1 ? B1[r] : 0.f;
+    for (int c = 0; c < C; ++c) acc += W1[r * C + c] * pl[c];
+    hr[r] = acc > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += CA_FNT) {
+    float acc = b2 ? B2[c] : 0.f;
+    for (int r = 0; r < Cr; ++r) acc += W2[c * Cr + r] * hr[r];
+    sl[c] = 1.f / (1.f + expf(-acc));
+  }
+  __syncthreads();
   if (k == 0) {
     for (int c = t; c < C; c += CA_FNT) { pool[n * C + c] = pl[c]; s[n * C + c] = sl[c]; }
     for (int r = t; r < Cr; r += CA_FNT) h[n * Cr + r] = hr[r];
   }
-  const int cv = C / PER;
-  const int p0 = k * ppb, p1 = min(HW, p0 + ppb);
-  const size_t base = ((size_t)n * HW) * cv;
-  for (int i = p0 * cv + t; i < p1 * cv; i += CA_FNT) {
+#pragma unroll
+  for (int j = 0; j < CA_VPT; ++j) {
+    const int i = i0 + t + j * CA_FNT;
+    if (i >= i1) break;
     const int c0 = (i % cv) * PER;
-    const u32x4 vu = ((const u32x4*)u)[base + i];
-    const u32x4 vx = ((const u32x4*)x)[base + i];
     u32x4 o;
     if constexpr (PER == 8) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float u0 = bf16_to_f32(vu[j] & 0xffff), u1 = bf16_to_f32(vu[j] >> 16);
-        const float x0 = bf16_to_f32(vx[j] & 0xffff), x1 = bf16_to_f32(vx[j] >> 16);
-        o[j] = pack_bf16x2(1.f * x0 + alpha * u0 * sl[c0 + 2 * j], 1.f * x1 + alpha * u1 * sl[c0 + 2 * j + 1]);
+      for (int q = 0; q < 4; ++q) {
+        const float u0 = bf16_to_f32(vu[j][q] & 0xffff), u1 = bf16_to_f32(vu[j][q] >> 16);
+        const float x0 = bf16_to_f32(vx[j][q] & 0xffff), x1 = bf16_to_f32(vx[j][q] >> 16);
+        o[q] = pack_bf16x2(1.f * x0 + alpha * u0 * sl[c0 + 2 * q], 1.f * x1 + alpha * u1 * sl[c0 + 2 * q + 1]);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[j] = __float_as_uint(1.f * __uint_as_float(vx[j]) + alpha * __uint_as_float(vu[j]) * sl[c0 + j]);
+      for (int q = 0; q < 4; ++q)
+        o[q] = __float_as_uint(1.f * __uint_as_float(vx[j][q]) + alpha * __uint_as_float(vu[j][q]) * sl[c0 + q]);
     }
     ((u32x4*)y)[base + i] = o;
   }
@@ -346,25 +402,47 @@ __global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restri
                                                            T* __restrict__ du, float* __restrict__ dz2_out,
                                                            float* __restrict__ dz1_out) {
   constexpr int PER = Elt<T>::PER16;
-  __shared__ float sl[CA_FMAXC], dz2[CA_FMAXC], dz1[CA_FMAXR], tp[CA_FMAXC];
+  __shared__ __attribute__((aligned(16))) float pr[CA_FMAXP];
+  __shared__ float W1[CA_FMAXW], W2[CA_FMAXW], sl[CA_FMAXC], hh[CA_FMAXR], dz2[CA_FMAXC], dz1[CA_FMAXR],
+      tp[CA_FMAXC];
   const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x;
+  const int cv = C / PER;
+  const int i0 = k * ppb * cv, i1 = min(HW, (k + 1) * ppb) * cv;
+  const size_t base = ((size_t)n * HW) * cv;
+  u32x4 vd[CA_VPT];
+  ca_load_vec(dy, base, i0, i1, vd);
+  ca_stage_f4<CA_FMAXP / 4 / CA_FNT>(parts + (size_t)n * P * C, P * C / 4, pr);
+  ca_stage_f1<CA_FMAXW / CA_FNT>(w1, C * Cr, W1);
+  ca_stage_f1<CA_FMAXW / CA_FNT>(w2, C * Cr, W2);
+  ca_stage_f1<1>(s + n * C, C, sl);
+  ca_stage_f1<1>(h + n * Cr, Cr, hh);
+  __syncthreads();
   for (int c = t; c < C; c += CA_FNT) {
-    const float ds = strided_sum(parts + (size_t)n * P * C + c, 0, P, 1, C);
-    const float si = s[n * C + c];
-    sl[c] = si;
-    dz2[c] = ds * alpha * si * (1.f - si);
+    // the summation order of strided_sum (G = 1): batches of 8 rows, then the tail
+    float acc = 0.f;
+    int p = 0;
+    for (; p + 7 < P; p += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = pr[(p + q) * C + c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc += v[q];
+    }
+    for (; p < P; ++p) acc += pr[p * C + c];
+    const float si = sl[c];
+    dz2[c] = acc * alpha * si * (1.f - si);
   }
   __syncthreads();
   for (int r = t; r < Cr; r += CA_FNT) {
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += w2[c * Cr + r] * dz2[c];
-    dz1[r] = h[n * Cr + r] > 0.f ? acc : 0.f;
+    for (int c = 0; c < C; ++c) acc += W2[c * Cr + r] * dz2[c];
+    dz1[r] = hh[r] > 0.f ? acc : 0.f;
   }
   __syncthreads();
   const float inv_hw = 1.f / (float)HW;
   for (int c = t; c < C; c += CA_FNT) {
     float acc = 0.f;
-    for (int r = 0; r < Cr; ++r) acc += w1[r * C + c] * dz1[r];
+    for (int r = 0; r < Cr; ++r) acc += W1[r * C + c] * dz1[r];
     tp[c] = inv_hw * acc;
   }
   if (k == 0) {
@@ -372,55 +450,65 @@ __global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restri
     for (int r = t; r < Cr; r += CA_FNT) dz1_out[n * Cr + r] = dz1[r];
   }
   __syncthreads();
-  const int cv = C / PER;
-  const int p0 = k * ppb, p1 = min(HW, p0 + ppb);
-  const size_t base = ((size_t)n * HW) * cv;
-  for (int i = p0 * cv + t; i < p1 * cv; i += CA_FNT) {
+#pragma unroll
+  for (int j = 0; j < CA_VPT; ++j) {
+    const int i = i0 + t + j * CA_FNT;
+    if (i >= i1) break;
     const int c0 = (i % cv) * PER;
-    const u32x4 vd = ((const u32x4*)dy)[base + i];
     u32x4 o;
     if constexpr (PER == 8) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d0 = bf16_to_f32(vd[j] & 0xffff), d1 = bf16_to_f32(vd[j] >> 16);
-        o[j] = pack_bf16x2(0.f * 0.f + alpha * d0 * sl[c0 + 2 * j] + tp[c0 + 2 * j],
-                           0.f * 0.f + alpha * d1 * sl[c0 + 2 * j + 1] + tp[c0 + 2 * j + 1]);
+      for (int q = 0; q < 4; ++q) {
+        const float d0 = bf16_to_f32(vd[j][q] & 0xffff), d1 = bf16_to_f32(vd[j][q] >> 16);
+        o[q] = pack_bf16x2(0.f * 0.f + alpha * d0 * sl[c0 + 2 * q] + tp[c0 + 2 * q],
+                           0.f * 0.f + alpha * d1 * sl[c0 + 2 * q + 1] + tp[c0 + 2 * q + 1]);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[j] = __float_as_uint(0.f * 0.f + alpha * __uint_as_float(vd[j]) * sl[c0 + j] + tp[c0 + j]);
+      for (int q = 0; q < 4; ++q)
+        o[q] = __float_as_uint(0.f * 0.f + alpha * __uint_as_float(vd[j][q]) * sl[c0 + q] + tp[c0 + q]);
     }
     ((u32x4*)du)[base + i] = o;
   }
 }
 
-// squeeze-conv parameter gradients from the per-image dz2 / dz1 (same loop order as ca_mlp_bwd_kernel)
+// squeeze-conv parameter gradients from the per-image dz2 / dz1 (same loop order as ca_mlp_bwd_kernel);
+// one block, the operands staged in LDS first (the per-n loop over global memory was a 25 us
+// latency chain)
 __global__ __launch_bounds__(256) void ca_param_grad_kernel(const float* __restrict__ dz2, const float* __restrict__ dz1,
                                                             const float* __restrict__ h, const float* __restrict__ pool,
                                                             int N, int C, int Cr, float* __restrict__ dw1,
                                                             float* __restrict__ db1, float* __restrict__ dw2,
                                                             float* __restrict__ db2, int accumulate) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nt = gridDim.x * blockDim.x;
-  for (int i = t; i < C * Cr; i += nt) {
+  extern __shared__ float sm[];  // dz2 [N*C] | pool [N*C] | dz1 [N*Cr] | h [N*Cr]
+  float* Z2 = sm;
+  float* PL = Z2 + N * C;
+  float* Z1 = PL + N * C;
+  float* HH = Z1 + N * Cr;
+  const int t = threadIdx.x;
+  ca_stage_f1<16>(dz2, N * C, Z2);
+  ca_stage_f1<16>(pool, N * C, PL);
+  ca_stage_f1<4>(dz1, N * Cr, Z1);
+  ca_stage_f1<4>(h, N * Cr, HH);
+  __syncthreads();
+  for (int i = t; i < C * Cr; i += CA_FNT) {
     const int c = i / Cr, r = i - c * Cr;
     float a2 = 0.f, a1 = 0.f;
     for (int n = 0; n < N; ++n) {
-      a2 += dz2[n * C + c] * h[n * Cr + r];
-      a1 += dz1[n * Cr + r] * pool[n * C + c];
+      a2 += Z2[n * C + c] * HH[n * Cr + r];
+      a1 += Z1[n * Cr + r] * PL[n * C + c];
     }
     dw2[i] = (accumulate ? dw2[i] : 0.f) + a2;
     dw1[r * C + c] = (accumulate ? dw1[r * C + c] : 0.f) + a1;
   }
-  for (int c = t; c < C; c += nt) {
+  for (int c = t; c < C; c += CA_FNT) {
     float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += dz2[n * C + c];
+    for (int n = 0; n < N; ++n) acc += Z2[n * C + c];
     if (db2) db2[c] = (accumulate ? db2[c] : 0.f) + acc;
   }
-  for (int r = t; r < Cr; r += nt) {
+  for (int r = t; r < Cr; r += CA_FNT) {
     float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += dz1[n * Cr + r];
+    for (int n = 0; n < N; ++n) acc += Z1[n * Cr + r];
     if (db1) db1[r] = (accumulate ? db1[r] : 0.f) + acc;
   }
 }
@@ -662,20 +750,25 @@ int sr_ca_mlp_bwd(const float* parts, int P, float scale, const float* s, const 
   return sr_check(hipGetLastError(), "ca_mlp_bwd launch");
 }
 
-// pixels per block of the fused CA kernels: ~8 16-B vectors per thread, at least 64 pixels
+// pixels per block of the fused CA kernels: CA_VPT 16-B vectors per thread
 static int ca_ppb(int HW, int C, int PER) {
-  int ppb = (CA_FNT * 8 * PER) / C;
-  if (ppb < 64) ppb = 64;
+  int ppb = CA_FNT * CA_VPT * PER / C;
   return ppb > HW ? HW : ppb;
+}
+
+static bool ca_shapes_ok(int C, int Cr, int P) {
+  return C % 8 == 0 && C <= CA_FMAXC && Cr >= 1 && Cr <= CA_FMAXR && C * Cr <= CA_FMAXW && P >= 1 &&
+         (int64_t)P * C <= CA_FMAXP;
 }
 
 int sr_ca_fwd_apply(int dtype, const float* parts, int P, float scale, const float* w1, const float* b1,
                     const float* w2, const float* b2, const void* x, const void* u, int N, int HW, int C, int Cr,
                     float alpha, void* y, float* pool, float* h, float* s_out, void* stream) {
   const int PER = dtype == SR_BF16 ? 8 : 4;
-  if (!parts || P < 1 || !w1 || !w2 || !x || !u || !y || !pool || !h || !s_out || N < 1 || HW < 1 || C % 8 ||
-      C > CA_FMAXC || Cr < 1 || Cr > CA_FMAXR || !aligned16(x) || !aligned16(u) || !aligned16(y))
-    return sr_fail(SR_EINVAL, "ca_fwd_apply: bad arguments (C % 8 == 0, C <= 256, Cr <= 64, 16-B aligned maps)");
+  if (!parts || !w1 || !w2 || !x || !u || !y || !pool || !h || !s_out || N < 1 || HW < 1 || !ca_shapes_ok(C, Cr, P) ||
+      !aligned16(x) || !aligned16(u) || !aligned16(y) || !aligned16(parts))
+    return sr_fail(SR_EINVAL, "ca_fwd_apply: bad arguments (C % 8 == 0, C <= 256, Cr <= 64, C*Cr <= 2048, P*C <= 8192, "
+                              "16-B aligned maps and partial rows)");
   if ((int64_t)N * HW * C / PER >= 0x7fffffffll) return sr_fail(SR_ETOOBIG, "ca_fwd_apply: tensor too large");
   const int ppb = ca_ppb(HW, C, PER);
   const dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)N);
@@ -693,9 +786,10 @@ int sr_ca_bwd_apply(int dtype, const float* parts, int P, float alpha, const flo
                     const float* w2, const void* dy, int N, int HW, int C, int Cr, void* du, float* dz2, float* dz1,
                     void* stream) {
   const int PER = dtype == SR_BF16 ? 8 : 4;
-  if (!parts || P < 1 || !s || !h || !w1 || !w2 || !dy || !du || !dz2 || !dz1 || N < 1 || HW < 1 || C % 8 ||
-      C > CA_FMAXC || Cr < 1 || Cr > CA_FMAXR || !aligned16(dy) || !aligned16(du))
-    return sr_fail(SR_EINVAL, "ca_bwd_apply: bad arguments (C % 8 == 0, C <= 256, Cr <= 64, 16-B aligned maps)");
+  if (!parts || !s || !h || !w1 || !w2 || !dy || !du || !dz2 || !dz1 || N < 1 || HW < 1 || !ca_shapes_ok(C, Cr, P) ||
+      !aligned16(dy) || !aligned16(du) || !aligned16(parts))
+    return sr_fail(SR_EINVAL, "ca_bwd_apply: bad arguments (C % 8 == 0, C <= 256, Cr <= 64, C*Cr <= 2048, P*C <= 8192, "
+                              "16-B aligned maps and partial rows)");
   if ((int64_t)N * HW * C / PER >= 0x7fffffffll) return sr_fail(SR_ETOOBIG, "ca_bwd_apply: tensor too large");
   const int ppb = ca_ppb(HW, C, PER);
   const dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)N);
@@ -713,9 +807,11 @@ int sr_ca_param_grad(const float* dz2, const float* dz1, const float* h, const f
                      float* dw1, float* db1, float* dw2, float* db2, int accumulate, void* stream) {
   if (!dz2 || !dz1 || !h || !pool || !dw1 || !dw2 || N < 1 || C < 1 || Cr < 1)
     return sr_fail(SR_EINVAL, "ca_param_grad: bad arguments");
-  const int work = C * Cr > C ? C * Cr : C;
-  hipLaunchKernelGGL(ca_param_grad_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     dz2, dz1, h, pool, N, C, Cr, dw1, db1, dw2, db2, accumulate);
+  const size_t smem = (size_t)N * (C + Cr) * 2 * sizeof(float);
+  if (N * C > 16 * CA_FNT || N * Cr > 4 * CA_FNT)
+    return sr_fail(SR_EINVAL, "ca_param_grad: N * C <= 4096 and N * Cr <= 1024 (split the batch)");
+  hipLaunchKernelGGL(ca_param_grad_kernel, dim3(1), dim3(CA_FNT), smem, (hipStream_t)stream, dz2, dz1, h, pool, N, C,
+                     Cr, dw1, db1, dw2, db2, accumulate);
   return sr_check(hipGetLastError(), "ca_param_grad launch");
 }
 

@@ -15,6 +15,7 @@
 // same 16-byte chunk image.  The epilogue stages the fp32 tile through LDS and applies
 // bias, activation, ReLU-mask gate, scale, residual, pixel-shuffle / NCHW store with
 // 16-byte coalesced stores.
+#include <cstdlib>
 #include "sr_common.h"
 #include "sr_internal.h"
 
@@ -4415,6 +4416,17 @@ bool wg_use_halo(const sr_conv3x3_wgrad_desc* d) {
          g_variant != 1;
 }
 
+// Block target of the narrow (ring / halo) wgrad split plan: 512, or SR_RING_SPLITS (A/B sweeps; read
+// once per process)
+int ring_split_target() {
+  static int v = [] {
+    const char* e = getenv("SR_RING_SPLITS");
+    const int x = e ? atoi(e) : 0;
+    return x >= 16 && x <= 4096 ? x : 512;
+  }();
+  return v;
+}
+
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
 // 256x256 kernel, ~2 rounds for the small ones), pixels per split a multiple of 64.
 void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
@@ -4425,7 +4437,7 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     // ~2 blocks per CU, but at least 8 K-steps per block (the slab costs 8 B per tap-MAC row)
     // (A/B on RCAN / RRDB: twice or half as many splits are 6-12 % slower per step)
     const int chunks = (d->Cin + 63) / 64;
-    int S = 512 / chunks;
+    int S = ring_split_target() / chunks;
     const int maxS = M / 512 > 1 ? M / 512 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
@@ -4647,6 +4659,12 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
     case FK_128_64: return bf ? "conv3x3_fwd_kernel<bf16,128,64>" : "conv3x3_fwd_kernel<f32,128,64>";
     default: return bf ? "conv3x3_fwd_kernel<bf16,128,128>" : "conv3x3_fwd_kernel<f32,128,128>";
   }
+}
+
+int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d) {
+  if (!d) return 0;
+  const FwdArgs a = fwd_shape(d);
+  return fwd_kind(a, d->dtype == SR_BF16) == FK_BANDS ? (a.Cout + 63) / 64 : 1;
 }
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {

@@ -10,10 +10,16 @@ launches (implicit-GEMM convs with fused epilogues + the HBM kernels of csrc/blo
   no torch.cat copies); the two residual scalings of the last RDB fuse into its conv5 epilogue.
 * ``bilinear_up_add`` — MSRResNet ``out += F.interpolate(x, bilinear)`` (srresnet_arch.py:64-65).
 """
+import os
+
 import torch
 
 from .. import _lib
 from . import conv as C
+
+
+# SR_CA_UNFUSED=1: the round-2 channel-attention launches (A/B of the fused kernels, tools/ab_env.sh)
+_CA_UNFUSED = os.environ.get('SR_CA_UNFUSED', '0') == '1'
 
 
 def _ws(nbytes, device):
@@ -78,6 +84,21 @@ class _RCAB(torch.autograd.Function):
         pool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
         h = torch.empty(N, Cr, device=x.device, dtype=torch.float32)
         s = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+        # the fused kernels stage the partial rows and squeeze weights in LDS (csrc/blocks.hip limits)
+        fused = (not _CA_UNFUSED and parts.shape[1] * Cp <= 8192 and Cp * Cr <= 2048 and Cp <= 256 and Cr <= 64
+                 and N * Cp <= 4096 and N * Cr <= 1024)
+        ctx.ca_fused = fused
+        if not fused:  # the separate squeeze-MLP launch + elementwise pass (A/B, or shapes past the limits)
+            _lib.check(
+                lib.sr_ca_mlp_fwd(_lib.ptr(parts), parts.shape[1], 1.0 / (H * W), _lib.ptr(a1),
+                                  _lib.ptr(ab1.detach() if ab1 is not None else None), _lib.ptr(a2),
+                                  _lib.ptr(ab2.detach() if ab2 is not None else None), N, Cp, Cr, _lib.ptr(pool),
+                                  _lib.ptr(h), _lib.ptr(s), _lib.stream()))
+            y = nc_affine(x, u, s, None, 1.0, rs, 0.0)
+            ctx.specs = (spec1, spec2)
+            ctx.rs = rs
+            ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2)
+            return y
         y = torch.empty_like(u)
         # squeeze MLP + y = x + rs * u * s in one launch (csrc/blocks.hip ca_fwd_apply_kernel)
         _lib.check(
@@ -107,6 +128,9 @@ class _RCAB(torch.autograd.Function):
         parts = torch.empty(N, lib.sr_channel_partials_count(H * W), Cp, device=x.device, dtype=torch.float32)
         _lib.check(lib.sr_channel_partials(_lib.dtype_code(dtype), _lib.ptr(dy), Cp, 0, _lib.ptr(u), Cp, 0, N, H * W,
                                            Cp, _lib.ptr(parts), _lib.stream()))
+        if not ctx.ca_fused or parts.shape[1] * Cp > 8192:
+            return _RCAB._backward_unfused(ctx, dy, parts, x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2,
+                                           spec1, spec2, rs, a1, a2, Cr, N, H, W, Cp, dtype)
         # squeeze-MLP backward + du = rs * dy * s + dpool / HW in one launch; the squeeze convs'
         # parameter gradients follow from the per-image dz2 / dz1 in their own small launch, on
         # the weight-gradient side stream when one is active (they only feed the optimizer)
@@ -153,6 +177,44 @@ class _RCAB(torch.autograd.Function):
             return dx, dw1, db1, dw2, db2, None, None, None, None, None, None, None
         return (dx, dw1, db1, dw2, db2, dA1.reshape(Cr, Cp, 1, 1), dab1, dA2.reshape(Cp, Cr, 1, 1), dab2, None, None,
                 None)
+
+
+def _rcab_backward_unfused(ctx, dy, parts, x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2, spec1, spec2, rs,
+                           a1, a2, Cr, N, H, W, Cp, dtype):
+    """The round-2 RCAB backward (single-block squeeze-MLP backward, then the du pass): A/B only."""
+    lib = _lib.load()
+    dpool = torch.empty(N, Cp, device=x.device, dtype=torch.float32)
+    ca = (aw1, ab1, aw2, ab2)
+    tg = [C.grad_target(p) for p in ca]
+    direct = all(g is not None for g in tg)
+    if direct:
+        dA1, dab1, dA2, dab2 = tg
+    else:
+        dA1, dA2 = torch.empty_like(a1), torch.empty_like(a2)
+        dab1 = torch.empty(Cr, device=x.device, dtype=torch.float32) if ab1 is not None else None
+        dab2 = torch.empty(Cp, device=x.device, dtype=torch.float32) if ab2 is not None else None
+    _lib.check(
+        lib.sr_ca_mlp_bwd(_lib.ptr(parts), parts.shape[1], rs, _lib.ptr(s), _lib.ptr(h), _lib.ptr(pool), _lib.ptr(a1),
+                          _lib.ptr(a2), N, Cp, Cr, _lib.ptr(dpool), _lib.ptr(dA1), _lib.ptr(dab1), _lib.ptr(dA2),
+                          _lib.ptr(dab2), int(direct), _lib.stream()))
+    if direct:
+        for p in ca:
+            C.grad_ready(p)
+    du = nc_affine(None, dy, s, dpool, 0.0, rs, 1.0 / (H * W))
+    _, wd1, _ = C.prepared(w1, b1, spec1, dtype)
+    _, wd2, _ = C.prepared(w2, b2, spec2, dtype)
+    dz1 = torch.empty_like(t)
+    C.conv_fwd_raw(du, wd2, None, dz1, N, H, W, spec2.cout_p, spec2.cin_p, spec2.cin_p, gate=t, gate_slope=0.0)
+    dw2, db2 = C.conv_wgrad_raw(du, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout, params=(w2, b2))
+    dx = torch.empty_like(x)
+    C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
+    dw1, db1 = C.conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, params=(w1, b1))
+    if direct:
+        return dx, dw1, db1, dw2, db2, None, None, None, None, None, None, None
+    return (dx, dw1, db1, dw2, db2, dA1.reshape(Cr, Cp, 1, 1), dab1, dA2.reshape(Cp, Cr, 1, 1), dab2, None, None, None)
+
+
+_RCAB._backward_unfused = staticmethod(_rcab_backward_unfused)
 
 
 def rcab(x, conv1, conv2, ca1, ca2, res_scale):

@@ -276,9 +276,21 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     args = (d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res), _lib.ptr(res2),
             _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.ptr(aux), _lib.ptr(parts), _lib.stream())
     keep = (x, wf, bias_g, gate, res, res2, aff_scale, aff_shift, y, aux, parts, kw.get('row_scale'))
-    with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * taps * cin * cout_real,
-                     x.element_size() * (M * (cin + cout) + taps * cin * cout),
-                     relaunch=(lambda a=args, k=keep: lib.sr_conv3x3_fwd(*a)) if ktrace.active() else None):
+    if ktrace.active():
+        # algorithmic HBM bytes of the call: x once (pre-upsample size with in_up), the weight image,
+        # y as stored (fp32 NCHW for the network tail), every epilogue operand (gate / res / res2 read,
+        # aux written: Cout channels per pixel each) and the colsum partial rows
+        esz = x.element_size()
+        up = d.in_up if d.in_up > 1 else 1
+        nbytes = esz * (M // (up * up) * cin + taps * cin * cout)
+        nbytes += (4 * M * cout_real) if d.out_nchw else esz * M * cout
+        nbytes += esz * M * cout * sum(t is not None for t in (gate, res, res2, aux))
+        if parts is not None:
+            nbytes += 4 * parts.numel()
+        with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * taps * cin * cout_real, nbytes,
+                         relaunch=lambda a=args, k=keep: lib.sr_conv3x3_fwd(*a), launches=lib.sr_conv3x3_fwd_launches(d)):
+            _lib.check(lib.sr_conv3x3_fwd(*args))
+    else:
         _lib.check(lib.sr_conv3x3_fwd(*args))
     return (y, parts) if colsum else y
 
@@ -405,8 +417,12 @@ def _wgrad_launch(lib, d, dy, x, ws_bytes, tw, tb, cin_real, cout_real, need_bia
         relaunch = lambda a=rargs, k=keep: lib.sr_conv3x3_wgrad(*a[:-1], _lib.stream())  # noqa: E731
     else:
         relaunch = None
+    up = d.in_up if d.in_up > 1 else 1
+    # dy and x once, dW / db read-modify-written (accumulate) or written, as fp32
+    nbytes = x.element_size() * (M * cout + M // (up * up) * cin) + \
+        (8 if tw is not None else 4) * (kk * kk * cin_real * cout_real + (cout_real if need_bias else 0))
     with ktrace.span(lib.sr_conv3x3_wgrad_kernel_name(d).decode() + '+reduce', 2.0 * M * kk * kk * cin_real * cout_real,
-                     x.element_size() * M * (cin + cout) + 4 * kk * kk * cin * cout, relaunch=relaunch):
+                     nbytes, relaunch=relaunch):
         _lib.check(lib.sr_conv3x3_wgrad(*args))
     if tw is not None and params is not None:
         grad_ready(params[0])

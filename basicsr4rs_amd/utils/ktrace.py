@@ -34,9 +34,10 @@ def stop():
     recs = _STATE['records']
     _STATE['records'] = []
     out = {}
-    for name, flops, nbytes, s, e in recs:
-        d = out.setdefault(name, {'count': 0, 'ms': 0.0, 'flops': 0.0, 'bytes': 0.0})
+    for name, flops, nbytes, launches, s, e in recs:
+        d = out.setdefault(name, {'count': 0, 'launches': 0, 'ms': 0.0, 'flops': 0.0, 'bytes': 0.0})
         d['count'] += 1
+        d['launches'] += launches
         d['ms'] += s.elapsed_time(e)
         d['flops'] += flops
         d['bytes'] += nbytes
@@ -50,7 +51,10 @@ def _event():
 
 
 @contextlib.contextmanager
-def span(name, flops=0.0, nbytes=0.0, relaunch=None):
+def span(name, flops=0.0, nbytes=0.0, relaunch=None, launches=1):
+    """One op call of kernel ``name``: its algorithmic FLOPs and HBM bytes (every operand the call
+    reads or writes, once) and the number of kernel launches it makes (``launches``: the per-launch
+    unit of rocprof's --stats, e.g. the 64-channel slices of a sliced band conv)."""
     if not _STATE['active']:
         yield
         return
@@ -58,7 +62,7 @@ def span(name, flops=0.0, nbytes=0.0, relaunch=None):
     s.record()
     yield
     e.record()
-    _STATE['records'].append((name, float(flops), float(nbytes), s, e))
+    _STATE['records'].append((name, float(flops), float(nbytes), int(launches), s, e))
     if relaunch is not None:
         _STATE['relaunch'].setdefault(name, []).append(relaunch)
 

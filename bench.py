@@ -201,6 +201,73 @@ def _pmc_traffic(workload, kernel):
     return rec
 
 
+def _roof(flops, nbytes, sec):
+    """(bound, achieved, peak, unit, frac) of one launch: bound from its algorithmic arithmetic
+    intensity against the ridge (frac = achieved / min(P, AI * BW))."""
+    ai = flops / nbytes if nbytes > 0 else float('inf')
+    ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    if flops > 0 and ai >= ridge:
+        a = flops / sec / 1e12
+        return 'mfma', a, PEAK_BF16_TFLOPS, 'TFLOP/s', a / PEAK_BF16_TFLOPS
+    a = nbytes / sec / 1e9
+    return 'hbm', a, PEAK_HBM_GBS, 'GB/s', a / PEAK_HBM_GBS
+
+
+def roofline(workload, kstats, traced_steps, step_s, use_graph):
+    """Roofline of the dominant kernel (most time in the traced step), per KERNEL LAUNCH:
+    flops / bytes per launch = the traced calls' algorithmic totals / their launches (a sliced band
+    call is several launches; a wgrad span is its kernel + slab reduce, one 'launch' pair).  Three
+    durations per launch: in-step HIP events around every launch of the traced eager step (launches
+    back to back behind a spin kernel; the headline ``frac``), the same launches re-issued back to
+    back in isolation after the timed region (``frac_isolated``), and the rocprofv3 average inside
+    the timed graph replays from this round's committed --stats summary (``frac_rocprof``)."""
+    name, st = max(kstats.items(), key=lambda kv: kv[1]['ms'])
+    calls, launches = st['count'], st['launches']
+    lpc = launches / calls
+    step_ms = st['ms'] / traced_steps
+    in_step_s = st['ms'] * 1e-3 / launches
+    fl, by = st['flops'] / launches, st['bytes'] / launches
+    bound, ach, peak, unit, frac = _roof(fl, by, in_step_s)
+    roof = {'bound': bound, 'kernel': name, 'achieved': round(ach, 1), 'peak': peak, 'unit': unit,
+            'frac': round(frac, 4), 'traffic': None, 'flops_per_launch': fl, 'bytes_per_launch': by,
+            'arith_intensity': round(fl / by, 1) if by else None, 'ridge': round(PEAK_BF16_TFLOPS / PEAK_HBM_GBS * 1e3, 1),
+            'launches_per_step': launches // traced_steps, 'calls_per_step': calls // traced_steps,
+            'avg_launch_us': round(in_step_s * 1e6, 2), 'share_of_step': round(step_ms * 1e-3 / step_s, 3)}
+    if bound == 'hbm' and fl > 0:
+        roof['mfma_tflops'] = round(fl / in_step_s / 1e12, 1)
+    from basicsr4rs_amd.utils import ktrace
+    rel_ms = ktrace.time_relaunch(name)  # per call
+    ktrace.clear_relaunch()
+    if rel_ms is not None:
+        iso_s = rel_ms * 1e-3 / lpc
+        roof['avg_launch_us_isolated'] = round(iso_s * 1e6, 2)
+        roof['frac_isolated'] = round(_roof(fl, by, iso_s)[4], 4)
+    tr = _pmc_traffic(workload, name)
+    if tr:
+        if tr.get('hbm_bytes_per_launch') is not None:
+            roof['traffic'] = round(tr['hbm_bytes_per_launch'])
+        if tr.get('rocprof_avg_us'):
+            roof['rocprof_avg_us'] = round(tr['rocprof_avg_us'], 2)
+            roof['frac_rocprof'] = round(_roof(fl, by, tr['rocprof_avg_us'] * 1e-6)[4], 4)
+        roof['traffic_source'] = (f"{tr['source']}: rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (own passes) per launch of "
+                                  f"{tr['kernel_regex']}, {tr['correction']}; rocprof_avg_us: --kernel-trace --stats "
+                                  f"average per launch in the timed graph replays ({tr.get('stats_file', '')})")
+    roof['timing'] = ('avg_launch_us: HIP events around each launch of the traced ' +
+                      ('eager step before capture (replays run the same kernels)' if use_graph else
+                       'last (untimed) warm-up step') + ', single stream, launches back to back behind a spin kernel; '
+                      'avg_launch_us_isolated: the same launches re-issued back to back after the timed region '
+                      '(3 passes after a warm-up pass)')
+    roof['kernels'] = {
+        k: {'calls': v['count'] // traced_steps, 'launches': v['launches'] // traced_steps,
+            'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
+            'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 and v['flops'] else None,
+            'gbs': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] > 0 else None,
+            'ms_per_step': round(v['ms'] / traced_steps, 3)}
+        for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]['ms'])
+    }
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -298,52 +365,7 @@ def main():
     value = hr_px / dt
     roof = None
     if kstats:
-        # dominant kernel; its roof from its algorithmic arithmetic intensity against the ridge
-        # (frac = achieved / min(P, AI * BW))
-        name, st = max(kstats.items(), key=lambda kv: kv[1]['ms'])
-        traced_ms = st['ms'] / st['count']
-        # the kernel's steady-state duration: every launch of it from the traced step re-issued back to
-        # back between two events (no per-launch event packets in between; rocprof's view of the same
-        # kernel in the timed replays); falls back to the per-launch events when it has no closure
-        relaunch_ms = ktrace.time_relaunch(name)
-        avg_ms = relaunch_ms if relaunch_ms is not None else traced_ms
-        ktrace.clear_relaunch()
-        st = dict(st, ms=avg_ms * st['count'])
-        ai = st['flops'] / st['bytes'] if st['bytes'] > 0 else float('inf')
-        ridge = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
-        if st['flops'] > 0 and ai >= ridge:
-            achieved = st['flops'] / (st['ms'] * 1e-3) / 1e12
-            roof = {'bound': 'mfma', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS,
-                    'unit': 'TFLOP/s', 'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None}
-        else:
-            achieved = st['bytes'] / (st['ms'] * 1e-3) / 1e9
-            roof = {'bound': 'hbm', 'kernel': name, 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS,
-                    'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 4), 'traffic': None}
-            if st['flops'] > 0:
-                roof['mfma_tflops'] = round(st['flops'] / (st['ms'] * 1e-3) / 1e12, 1)
-        roof.update({'flops_per_launch': st['flops'] / st['count'], 'bytes_per_launch': st['bytes'] / st['count'],
-                     'arith_intensity': round(ai, 1), 'ridge': round(ridge, 1)})
-        roof.update({'avg_launch_us': round(avg_ms * 1e3, 2), 'avg_launch_us_per_launch_events': round(traced_ms * 1e3, 2),
-                     'launches_per_step': st['count'] // traced_steps,
-                     'share_of_step': round(st['ms'] / traced_steps * 1e-3 / (dt / args.steps), 3),
-                     'timing': ('HIP events around all launches of this kernel from the traced step re-issued back to '
-                                'back (same arguments and buffers, 3 passes after a warm-up pass, after the timed region); '
-                                if relaunch_ms is not None else 'HIP events on the stream of each launch; ') +
-                               'per-kernel table: events around each launch of ' +
-                               ('one eager step before capture (replays run the same kernels)' if use_graph
-                                else 'the last (untimed) warm-up step')})
-        tr = _pmc_traffic(args.workload, name)
-        if tr:
-            roof['traffic'] = round(tr['hbm_bytes_per_launch'])
-            roof['traffic_source'] = (f"{tr['source']}: rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (own passes) of this "
-                                      f"kernel, per launch, {tr['correction']}; rocprof avg {tr['rocprof_avg_us']:.1f} us")
-        roof['kernels'] = {
-            k: {'count': v['count'] // traced_steps, 'avg_us': round(v['ms'] / v['count'] * 1e3, 1),
-                'tflops': round(v['flops'] / (v['ms'] * 1e-3) / 1e12, 1) if v['ms'] > 0 and v['flops'] else None,
-                'gbs': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] > 0 and not v['flops'] else None,
-                'ms_per_step': round(v['ms'] / traced_steps, 3)}
-            for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]['ms'])
-        }
+        roof = roofline(args.workload, kstats, traced_steps, dt / args.steps, use_graph)
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_parity:
         parity = parity_check(args.workload, dev)

@@ -113,6 +113,9 @@ int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d);
  * descriptor (static string; for traces and profiler summaries). */
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d);
 const char* sr_conv3x3_wgrad_kernel_name(const struct sr_conv3x3_wgrad_desc* d);
+/* Number of kernel launches one sr_conv3x3_fwd call makes for a descriptor (1, or the 64-channel
+ * output slices of the sliced band form) -- the per-launch unit of traces and profiler summaries. */
+int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d);
 
 /* Kernel-variant selection for A/B tests: 0 = automatic (default), 1 = never use the
  * 256x256 LDS-DMA kernel (all shapes on the 128-row register-staged kernels). */

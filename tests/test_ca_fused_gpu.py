@@ -43,13 +43,14 @@ def test_ca_fused_fwd_bwd(cuda, dtype, N, H, W, C, Cr, P):
     lib = _lib.load()
     dev = lambda t: t.contiguous().to(cuda)  # noqa: E731
     xg, ug, dyg = dev(x), dev(u), dev(dy)
+    w1g, b1g, w2g, b2g = dev(w1), dev(b1), dev(w2), dev(b2)  # held: the launches read them asynchronously
     parts = dev(_parts(u.float(), P))
     yo = torch.empty_like(xg)
     po = torch.empty(N, C, device=cuda)
     ho = torch.empty(N, Cr, device=cuda)
     so = torch.empty(N, C, device=cuda)
-    _lib.check(lib.sr_ca_fwd_apply(_lib.dtype_code(dtype), _lib.ptr(parts), P, 1.0 / (H * W), _lib.ptr(dev(w1)),
-                                   _lib.ptr(dev(b1)), _lib.ptr(dev(w2)), _lib.ptr(dev(b2)), _lib.ptr(xg), _lib.ptr(ug),
+    _lib.check(lib.sr_ca_fwd_apply(_lib.dtype_code(dtype), _lib.ptr(parts), P, 1.0 / (H * W), _lib.ptr(w1g),
+                                   _lib.ptr(b1g), _lib.ptr(w2g), _lib.ptr(b2g), _lib.ptr(xg), _lib.ptr(ug),
                                    N, H * W, C, Cr, rs, _lib.ptr(yo), _lib.ptr(po), _lib.ptr(ho), _lib.ptr(so),
                                    _lib.stream()))
     tol = 1e-5 if dtype == torch.float32 else 1e-2
@@ -63,7 +64,7 @@ def test_ca_fused_fwd_bwd(cuda, dtype, N, H, W, C, Cr, P):
     dz2 = torch.empty(N, C, device=cuda)
     dz1 = torch.empty(N, Cr, device=cuda)
     _lib.check(lib.sr_ca_bwd_apply(_lib.dtype_code(dtype), _lib.ptr(pdu), P, rs, _lib.ptr(so), _lib.ptr(ho),
-                                   _lib.ptr(dev(w1)), _lib.ptr(dev(w2)), _lib.ptr(dyg), N, H * W, C, Cr, _lib.ptr(du),
+                                   _lib.ptr(w1g), _lib.ptr(w2g), _lib.ptr(dyg), N, H * W, C, Cr, _lib.ptr(du),
                                    _lib.ptr(dz2), _lib.ptr(dz1), _lib.stream()))
     ref_du = ud.grad
     assert (du.float().cpu().double() - ref_du).abs().max().item() <= tol * max(1.0, ref_du.abs().max().item())

@@ -18,6 +18,9 @@ import shutil
 import sys
 
 tag, workload, kre, out, bench_kernel = sys.argv[1:6]  # bench_kernel: bench.py's ktrace name
+# time / traffic regex: for a bench span that is a kernel + its slab reduce ('...+reduce'), both
+# kernels' time and bytes per call of the kernel matching kre (default: kre itself)
+tre = sys.argv[6] if len(sys.argv) > 6 else kre
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, 'profiles', tag)
 os.makedirs(dst, exist_ok=True)
@@ -28,25 +31,31 @@ if stats:
 
 
 def per_launch(pass_dir, counter):
-    vals, names = [], set()
+    """Counter total over the kernels matching tre, per launch of the kernels matching kre."""
+    tot, n, names = 0.0, 0, set()
     for f in glob.glob(os.path.join(out, pass_dir, '**', '*counter_collection.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r['Counter_Name'] == counter and re.search(kre, r['Kernel_Name']):
-                vals.append(float(r['Counter_Value']))
+            if r['Counter_Name'] != counter:
+                continue
+            if re.search(tre, r['Kernel_Name']):
+                tot += float(r['Counter_Value'])
                 names.add(r['Kernel_Name'])
-    return (sum(vals) / len(vals) if vals else None), len(vals), sorted(names)
+            if re.search(kre, r['Kernel_Name']):
+                n += 1
+    return (tot / n if n else None), n, sorted(names)
 
 
 fetch_kib, nf, names = per_launch('fetch', 'FETCH_SIZE')
 write_kib, nw, _ = per_launch('write', 'WRITE_SIZE')
 avg_us = None
 if stats:
-    rows = [r for r in csv.DictReader(open(stats[0])) if re.search(kre, r['Name'])]
-    calls = sum(int(r['Calls']) for r in rows)
+    rows = list(csv.DictReader(open(stats[0])))
+    calls = sum(int(r['Calls']) for r in rows if re.search(kre, r['Name']))
     if calls:
-        avg_us = sum(float(r['TotalDurationNs']) for r in rows) / calls / 1e3
+        avg_us = sum(float(r['TotalDurationNs']) for r in rows if re.search(tre, r['Name'])) / calls / 1e3
 rec = {
-    'kernel_regex': kre, 'bench_kernel': bench_kernel, 'kernels': names, 'launches_counted': [nf, nw],
+    'kernel_regex': kre, 'time_regex': tre, 'bench_kernel': bench_kernel, 'kernels': names,
+    'launches_counted': [nf, nw], 'stats_file': f'profiles/{tag}/{workload}_kernel_stats.csv',
     'fetch_size_kib_raw': fetch_kib, 'write_size_kib': write_kib,
     'fetch_bytes': None if fetch_kib is None else fetch_kib * 1024 * 2,
     'write_bytes': None if write_kib is None else write_kib * 1024,
