@@ -141,6 +141,11 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _LIB = lib
+        # SR_CONV_VARIANT=<n>: a kernel-selection variant for the whole process (A/B runs,
+        # tools/ab_val.sh); 0 / unset = automatic
+        v = int(os.environ.get('SR_CONV_VARIANT', '0') or 0)
+        if v:
+            check(lib.sr_conv3x3_set_variant(v))
     return _LIB
 
 

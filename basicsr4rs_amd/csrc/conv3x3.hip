@@ -1284,7 +1284,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
     for (int i = 0; i < NMT; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < MAXKK; ++kk) {
-      if (kk >= nkk) break;
+      // a guarded body, not a break: with MAXKK 12 / 18 (wide K) a break left the loop rolled and
+      // the W fragments indexed dynamically (in scratch)
+      if (kk < nkk) {
       const int ch = kk * 4 + g;  // logical 16-B chunk of the X^T fragment
       // [cg][row][128 B], physical chunk = logical ^ (row & 7); row & 7 == c16 & 7 for all i
       const char* base = smem + (ch >> 3) * MT * 128 + c16 * 128 + ((((ch & 7) ^ (c16 & 7))) << 4);
@@ -1299,6 +1301,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
                                                             __builtin_bit_cast(s16x8, xf[i]), acc[i][0], 0, 0, 0);
         acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, wb[kk][1]),
                                                             __builtin_bit_cast(s16x8, xf[i]), acc[i][1], 0, 0, 0);
+      }
       }
     }
     // the next pass's W fragments load while this pass's epilogue runs
@@ -3385,9 +3388,8 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
 // tiles, ran its two groups in lock-step between the per-step barriers and was slower.)  The
 // first step of a segment loads its three rows itself, after the previous segment's last step
 // (its slots may still be read), so a block has nseg - 1 one-step bubbles.
-template <int CO_T>
+template <int CO_T, int D = 2>  // D: steps in flight
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
-  constexpr int D = 2;              // steps in flight
   constexpr int CW = CO_T;  // co tiles per wave
   constexpr int RS = 3 * 1024;      // one halo row of one 16-ci tile: 96 rows x 32 B (66 used)
   constexpr int RSL = D + 2;        // ring slots: rows q-1 .. q+1 read, D - 1 more in flight
@@ -4182,10 +4184,15 @@ int lin_epi(const FwdArgs& a) {
     default: return -1;
   }
 }
-// short-K 1x1 convs (linears): token tile staged once, all output channels swept
+// short-K 1x1 convs (linears): token tile staged once, all output channels swept.  K <= 192 on
+// 128-token tiles; 192 < K <= 576 (SwinIR fc2 fwd 360 -> 184, fc1 / qkv dgrads 360 / 576 -> 184) on
+// 64-token tiles, Cout <= 384 (variant 55: those on the 256x256 pp kernel instead, for A/B)
 bool fwd_use_lin(const FwdArgs& a, bool bf) {
-  return bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && a.Cin <= 192 &&
-         a.Cout <= 640 && g_variant != 1 && g_variant != 27;
+  if (!(bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && g_variant != 1 &&
+        g_variant != 27))
+    return false;
+  if (a.Cin <= 192) return a.Cout <= 640;
+  return a.Cin <= 576 && a.Cout <= 384 && g_variant != 55;
 }
 // HR tail convs: Cout <= 16 with the NCHW fp32 store, W >= 256 (32-px strips), Cin 64 / 128 / 256
 bool fwd_use_tail(const FwdArgs& a, bool bf) {
@@ -4250,8 +4257,28 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
   switch (fwd_kind(a, sizeof(T) == 2)) {
 case FK_LIN: {
   FwdArgs b = a;
-  b.tiles = (a.M + 127) / 128;
   const int e = lin_epi(a);
+  if (a.Cin > 192) {  // wide K: 64-token tiles, the whole K (<= 384 / 576) staged
+    b.tiles = (a.M + 63) / 64;
+#define SR_LINW_E(CG_, NP_, E_) \
+  case E_: hipLaunchKernelGGL((conv3x3_lin_kernel<64, CG_, NP_, E_>), dim3(b.tiles), dim3(256), 0, s, b); break;
+#define SR_LINW(CG_, NP_) \
+  case NP_: \
+switch (e) { \
+  SR_LINW_E(CG_, NP_, 0) SR_LINW_E(CG_, NP_, 16) SR_LINW_E(CG_, NP_, 144) \
+  default: hipLaunchKernelGGL((conv3x3_lin_kernel<64, CG_, NP_, -1>), dim3(b.tiles), dim3(256), 0, s, b); \
+} \
+break;
+    if (a.Cin <= 384) {
+      switch ((a.Cout + 127) / 128) { SR_LINW(6, 1) SR_LINW(6, 2) SR_LINW(6, 3) default: return hipErrorInvalidValue; }
+    } else {
+      switch ((a.Cout + 127) / 128) { SR_LINW(9, 1) SR_LINW(9, 2) SR_LINW(9, 3) default: return hipErrorInvalidValue; }
+    }
+#undef SR_LINW
+#undef SR_LINW_E
+    return hipGetLastError();
+  }
+  b.tiles = (a.M + 127) / 128;
 #define SR_LIN_E(NP_, E_) \
   case E_: hipLaunchKernelGGL((conv3x3_lin_kernel<128, 3, NP_, E_>), dim3(b.tiles), dim3(256), 0, s, b); break;
 #define SR_LIN(NP_) \
@@ -4423,6 +4450,16 @@ int ring_split_target() {
     const char* e = getenv("SR_RING_SPLITS");
     const int x = e ? atoi(e) : 0;
     return x >= 16 && x <= 4096 ? x : 512;
+  }();
+  return v;
+}
+
+// Steps in flight of the ring wgrad kernel: 2, or SR_RING_D = 3 / 4 (A/B; read once per process)
+int ring_depth() {
+  static int v = [] {
+    const char* e = getenv("SR_RING_D");
+    const int x = e ? atoi(e) : 0;
+    return x == 3 || x == 4 ? x : 2;
   }();
   return v;
 }
@@ -4610,7 +4647,8 @@ int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_ga
       ln_C <= 0 || ln_C > d->Cin || d->ldw < d->Cin)
     return sr_fail(SR_EINVAL, "linear_ln_fwd: bf16 1x1 conv over dense rows (ldx == Cin) with ln_C <= Cin");
   FwdArgs a = fwd_shape(d);
-  if (!fwd_use_lin(a, true)) return sr_fail(SR_EINVAL, "linear_ln_fwd: shape not on the lin kernel (Cin <= 192, Cout <= 640)");
+  if (!fwd_use_lin(a, true) || a.Cin > 192)
+    return sr_fail(SR_EINVAL, "linear_ln_fwd: shape not on the lin kernel (Cin <= 192, Cout <= 640)");
   a.aux = aux;
   const int e = lin_epi(a);
   if (e != 0 && e != 67) return sr_fail(SR_EINVAL, "linear_ln_fwd: epilogue must be plain or GELU + pre-activation aux");
@@ -4678,7 +4716,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 54)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 55)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -4805,10 +4843,16 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     const int ct = (a.Cout + 15) / 16;
     const dim3 grid(S * a.tiles_ci);
     if (wg_use_ring()) {
-      if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<1>, grid, dim3(256), 0, s, a);
-      else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<2>, grid, dim3(256), 0, s, a);
-      else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<3>, grid, dim3(256), 0, s, a);
-      else hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<4>, grid, dim3(256), 0, s, a);
+      const int D = ring_depth();
+#define SR_RING(CT_)                                                                                     \
+  if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);        \
+  else if (D == 3) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 3>), grid, dim3(256), 0, s, a);   \
+  else hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2>), grid, dim3(256), 0, s, a);
+      if (ct == 1) { SR_RING(1) }
+      else if (ct == 2) { SR_RING(2) }
+      else if (ct == 3) { SR_RING(3) }
+      else { SR_RING(4) }
+#undef SR_RING
     } else if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<1>, grid, dim3(256), 0, s, a);
     else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<2>, grid, dim3(256), 0, s, a);
     else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<3>, grid, dim3(256), 0, s, a);

@@ -120,3 +120,59 @@ def test_linear_ln_fused_vs_separate(cuda, which, shape):
     assert (y.float() - y_r.float()).abs().max().item() <= 2e-2 * max(1.0, y_r.float().abs().max().item())
     if aux is not None:
         assert (aux.float() - aux_r.float()).abs().max().item() <= 2e-2 * max(1.0, aux_r.float().abs().max().item())
+
+
+@pytest.mark.parametrize('K,Cout', [(360, 184), (576, 184), (200, 96), (256, 304), (384, 40)])
+@pytest.mark.parametrize('epi', ['plain', 'res', 'res_rowscale', 'gate'])
+def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
+    """The lin kernel on wide K (192 < K <= 576, 64-token tiles: SwinIR fc2 fwd 360 -> 184, fc1 / qkv
+    dgrads 360 / 576 -> 184) against float64 on the same bf16 operands, with the epilogues those
+    calls use (residual, residual + per-image row scale, GELU' gate) and a ragged last token tile;
+    the kernel that ran is the lin kernel (name), and variant 55 (the 256x256 pp kernel for these
+    shapes) agrees within bf16 rounding."""
+    from basicsr4rs_amd import _lib
+    from basicsr4rs_amd.ops import conv as C
+    N, H, W = 3, 8, 40  # 960 tokens: 15 tiles of 64, and H*W % 64 == 0 for the row scale
+    torch.manual_seed(K + Cout)
+    dt = torch.bfloat16
+    x = (torch.randn(N, H, W, K, device=cuda) * 0.5).to(dt)
+    w = (torch.randn(Cout, K, device=cuda) * K**-0.5)
+    bias = torch.randn(Cout, device=cuda) * 0.1
+    wf = w.to(dt).contiguous()
+    res = (torch.randn(N, H, W, Cout, device=cuda)).to(dt) if epi.startswith('res') else None
+    gate = (torch.randn(N, H, W, Cout, device=cuda)).to(dt) if epi == 'gate' else None
+    rs = (torch.rand(N, device=cuda) + 0.5) if epi == 'res_rowscale' else None
+    kw = {}
+    if res is not None:
+        kw.update(res=res, beta=1.0)
+    if rs is not None:
+        kw.update(row_scale=rs)
+    if gate is not None:
+        kw.update(gate=gate, gate_mode=1)  # GELU'(g) (the fc2 dgrad gate)
+
+    def run():
+        y = torch.empty(N, H, W, Cout, device=cuda, dtype=dt)
+        C.conv_fwd_raw(x, wf, bias, y, N, H, W, K, Cout, Cout, ksize=1, **kw)
+        return y
+
+    lib = _lib.load()
+    d = C._desc(dt, N, H, W, K, K, Cout, Cout, Cout, ksize=1)
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_lin_kernel'
+    y = run().double()
+    ref = x.double() @ w.to(dt).double().t() + bias.double()
+    if gate is not None:
+        gd = gate.double()
+        ref = ref * (0.5 * (1 + torch.erf(gd / 2**0.5)) + gd * torch.exp(-gd * gd / 2) / (2 * torch.pi) ** 0.5)
+    if rs is not None:
+        ref = ref * rs.double().view(N, 1, 1, 1)
+    if res is not None:
+        ref = ref + res.double()
+    tol = 1e-2 * max(1.0, ref.abs().max().item())
+    assert (y - ref).abs().max().item() <= tol
+    _lib.check(lib.sr_conv3x3_set_variant(55))
+    try:
+        assert lib.sr_conv3x3_fwd_kernel_name(d) != b'conv3x3_lin_kernel' or K <= 192
+        y55 = run().double()
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    assert (y55 - ref).abs().max().item() <= tol
