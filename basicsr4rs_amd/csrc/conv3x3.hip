@@ -873,7 +873,18 @@ struct PphGeom {
   static_assert(LDS <= 160 * 1024, "pph LDS");
 };
 
-template <int R, int DBG = 0>
+// P2: the two-interval schedule -- per K-step each wave group runs TWO MFMA intervals of two
+// quadrants each (32 MFMAs: (0,0)+(0,1), then (1,1)+(1,0)) instead of four of one, so a K-step
+// costs 4 barriers instead of 8.  Reads per group: R1 = A half 0 + both B halves, R2 = A half 1;
+// DMA issue: B(t+1) (both halves) in R1 -- its buffer was last read at R1 of step t-1 by both
+// groups -- and the halo piece in R2, then a counted vmcnt(1) retires B(t+1) and leaves only this
+// step's halo piece in flight (halo pieces retire one step after issue, as before).  Where: the
+// leading group (waves 0-3) waits after issuing its second MFMA interval, the lagging group at
+// the end of its R2 -- both before the barrier that precedes the leading group's next R1, so
+// every wave's pieces have landed when any wave reads them, and the leading group's DMA gets one
+// more interval in flight.  Each accumulator's K order is unchanged: bitwise equal to the 4-phase
+// form.
+template <int R, int DBG = 0, bool P2 = false>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   using G = PphGeom<R>;
   constexpr int W = G::W, RH = R + 2;
@@ -1044,6 +1055,33 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
       sb = sa + 1;
     }
     if (sb >= G::NSLOT) sb -= G::NSLOT;
+    if constexpr (P2) {
+      // R1: A half 0, B halves 0 and 1 of this step; issue B(t+1) (both halves)
+      read_a(sa, tx);
+      read_b(buf, 0);
+      read_b(buf, 1);
+      if (DBG != 1) {
+        if (more) { issue_b(buf ^ 1, ncc, ntap, 0); issue_b(buf ^ 1, ncc, ntap, 1); }
+        else { issue_b_dummy(); issue_b_dummy(); }
+      }
+      pp_barrier();
+      mma(0, 0);
+      mma(0, 1);
+      pp_barrier();
+      // R2: A half 1; issue this step's halo piece; retire B(t+1)
+      read_a(sb, tx);
+      if (DBG != 1) issue_halo(cc, tap);
+      if (wr) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      pp_barrier();
+      mma(1, 1);
+      mma(1, 0);
+      if (!wr) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      pp_barrier();
+      cc = ncc;
+      tap = ntap;
+      if (++ntap == 9) { ntap = 0; ++ncc; }
+      continue;
+    }
     // phase 1: quadrant (0,0); issue B0(t+1); retire B1(t)
     read_a(sa, tx);
     read_b(buf, 0);
@@ -2739,8 +2777,12 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
 // shuffle slot width) multiples of 128.  Output: fp32 slab tile staged through LDS and
 // written with 16-B row-contiguous stores.
 // ------------------------------------------------------------------------------------
-// DBG (timing ablations, wrong results): 1 no operand DMA, 2 no MFMA, 3 no slab store
-template <int DBG = 0>
+// DBG (timing ablations, wrong results): 1 no operand DMA, 2 no MFMA, 3 no slab store.
+// P2: the two-interval schedule of conv3x3_fwd_pph_kernel<.., P2> -- R1 reads A half 0 and both B
+// halves and issues all four half-tiles of step t+1 (their buffer was last read at R2 of step t-1
+// by both groups), two quadrants per MFMA interval, R2 reads A half 1; the leading group retires
+// step t+1's DMAs after issuing its second MFMA interval, the lagging group at the end of its R2.
+template <int DBG = 0, bool P2 = false>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   constexpr int STAGE = 65536;
   constexpr int CSTR = 256 + 4;
@@ -2922,6 +2964,35 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const bool more = t + 1 < nk;
+    if constexpr (P2) {
+      // step 0's four half-tiles were retired by the prologue's vmcnt(4) only partly: drain once
+      if (t == 0) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); pp_barrier(); pp_barrier(); }
+      read_a(buf, 0);
+      read_b(buf, 0);
+      read_b(buf, 1);
+      if (more) {
+        k_eval(t + 1);
+        issue_a(t + 1, 0);
+        issue_b(t + 1, 0);
+        issue_b(t + 1, 1);
+        issue_a(t + 1, 1);
+      }
+      pp_barrier();
+      mma(0, 0);
+      mma(0, 1);
+      pp_barrier();
+      read_a(buf, 1);
+      // A half 1 is read here and re-filled at the other group's next R1 (one interval later):
+      // these reads complete before the barrier
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (wr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      mma(1, 1);
+      mma(1, 0);
+      if (!wr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      continue;
+    }
     read_a(buf, 0);
     read_b(buf, 0);
     if (more) {
@@ -4084,8 +4155,12 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   a.tiles = tm * a.tiles_n;
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
+  else if (fwd_use_pph(a) && a.W == 128 && g_variant != 59)
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0, true>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a) && a.W == 128)
     hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0>), dim3(a.tiles), dim3(512), 0, s, a);
+  else if (g_variant != 59 && g_variant != 25 && g_variant != 26 && fwd_use_pph(a))
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0, true>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant == 25 && fwd_use_pph(a))
     hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 1>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant == 26 && fwd_use_pph(a))
@@ -4716,7 +4791,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 55)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 59)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -4875,15 +4950,21 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.bias_fused = wg_bias_fused(d) ? 1 : 0;
     if (a.bias_fused) {
       a.bias_group = 0;
-      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+      if (g_variant != 59)
+        hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<0, true>), dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
     } else if (a.bias_group > 0) {
       const int nb = S * taps * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
-      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(nb), dim3(512), 0, s, a);
+      if (g_variant != 59) hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<0, true>), dim3(nb), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(nb), dim3(512), 0, s, a);
     } else if (wg_use_pp(d) && g_variant >= 41 && g_variant <= 43) {  // timing ablations (wrong results)
       if (g_variant == 41) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<1>, dim3(S * per_split), dim3(512), 0, s, a);
       else if (g_variant == 42) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<2>, dim3(S * per_split), dim3(512), 0, s, a);
       else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<3>, dim3(S * per_split), dim3(512), 0, s, a);
-    } else if (wg_use_pp(d))
+    } else if (wg_use_pp(d) && g_variant != 59)
+      hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<0, true>), dim3(S * per_split), dim3(512), 0, s, a);
+    else if (wg_use_pp(d))
       hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * per_split), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);

@@ -687,3 +687,41 @@ def test_fwd_pph_pixel_shuffled_input(cuda, shape):
     tol = 2e-2 * max(1.0, ref.abs().max().item())
     assert (got - ref).abs().max().item() <= tol
     assert (outs[0].float() - outs[1].float()).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize('shape', [(2, 256, 256, 64, 0), (1, 256, 1024, 64, 2), (1, 256, 1024, 128, 2),
+                                   (2, 128, 128, 128, 0)])
+def test_two_interval_schedule_bitwise(cuda, shape):
+    """The two-interval (4 barriers per K-step) schedules of the pph fwd / dgrad kernel and the pp wgrad
+    kernel (the default since round 3) keep every accumulator's K order: outputs, pixel-shuffled
+    dgrads and weight / bias gradients are bitwise equal to the 4-phase kernels (variant 59)."""
+    from basicsr4rs_amd import _lib
+    from basicsr4rs_amd.ops import conv as C
+    N, cin, cout, hw, ps = shape
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    spec = C.ConvSpec(cin, cout, out_ps=ps)
+    x = torch.randn(N, hw, hw, cin, device=cuda).to(dt)
+    wf, wd, bg = C.prepared(conv.weight, conv.bias, spec, dt)
+    yshape = C._out_shape(spec, N, hw, hw)
+    dy = torch.randn(yshape, device=cuda).to(dt)
+    lib = _lib.load()
+
+    def run():
+        y = torch.empty(yshape, device=cuda, dtype=dt)
+        C.conv_fwd_raw(x, wf, bg, y, N, hw, hw, cin, cout, cout, out_ps=ps)
+        dx = torch.empty(N, hw, hw, cin, device=cuda, dtype=dt)
+        C.conv_fwd_raw(dy, wd, None, dx, N, hw, hw, cout, cin, cin, in_ps=ps, ldx=dy.shape[-1])
+        dw, db = C.conv_wgrad_raw(dy, x, N, hw, hw, cin, cin, cout, cout, out_ps=ps)
+        return y, dx, dw, db
+
+    ref = run()
+    for v in (59, ):
+        _lib.check(lib.sr_conv3x3_set_variant(v))
+        try:
+            got = run()
+        finally:
+            _lib.check(lib.sr_conv3x3_set_variant(0))
+        for name, a, b in zip(('y', 'dx', 'dw', 'db'), ref, got):
+            assert torch.equal(a, b), (v, name, (a.float() - b.float()).abs().max().item())
