@@ -884,7 +884,13 @@ struct PphGeom {
 // every wave's pieces have landed when any wave reads them, and the leading group's DMA gets one
 // more interval in flight.  Each accumulator's K order is unchanged: bitwise equal to the 4-phase
 // form.
-template <int R, int DBG = 0, bool P2 = false>
+// P2 == 2 additionally prefetches the B half-tiles two K-steps ahead: B(t+2) is issued in R2 of
+// step t into the buffer step t just read in R1 (both groups' R1 reads complete before the barrier
+// that ends R1: lgkmcnt(0)), so a weight tile has ~5 intervals in flight instead of ~3.  Per step
+// the issue order is [B(t+2) 4 ops][halo(t) 1 op]; the retire point (as above) waits vmcnt(6),
+// which retires B(t+2)'s predecessor B(t+1) and every older halo piece (a halo piece issued at step
+// t is then visible from step t+3 on; the ring schedule's first uses are >= 4 steps after issue).
+template <int R, int DBG = 0, int P2 = 0>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   using G = PphGeom<R>;
   constexpr int W = G::W, RH = R + 2;
@@ -1035,12 +1041,17 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
     for (int p = 0; p < G::PIECES; ++p) issue_row(0, rr, p);
   issue_b(0, 0, 0, 0);
   issue_b(0, 0, 0, 1);
+  if constexpr (P2 == 2) {  // B(1) too: the loop issues B(t+2) from step 0 on
+    if (nk > 1) { issue_b(1, 0, 1, 0); issue_b(1, 0, 1, 1); }  // step 1 = (chunk 0, tap 1)
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
   if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
 
   int cc = 0, tap = 0;   // this step
   int ncc = 0, ntap = 1;  // the next step
+  int n2cc = 0, n2tap = 2;  // the step after (P2 == 2)
+  if (n2tap == 9) { n2tap = 0; ++n2cc; }
 #pragma unroll 1
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
@@ -1055,7 +1066,37 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
       sb = sa + 1;
     }
     if (sb >= G::NSLOT) sb -= G::NSLOT;
-    if constexpr (P2) {
+    if constexpr (P2 == 2) {
+      // R1: A half 0, B halves 0 and 1 of this step (their reads complete before the barrier: R2
+      // re-fills this buffer with B(t+2))
+      read_a(sa, tx);
+      read_b(buf, 0);
+      read_b(buf, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      mma(0, 0);
+      mma(0, 1);
+      pp_barrier();
+      // R2: A half 1; issue B(t+2) into this step's buffer, then this step's halo piece; retire B(t+1)
+      read_a(sb, tx);
+      if (DBG != 1) {
+        if (t + 2 < nk) { issue_b(buf, n2cc, n2tap, 0); issue_b(buf, n2cc, n2tap, 1); }
+        else { issue_b_dummy(); issue_b_dummy(); }
+        issue_halo(cc, tap);
+      }
+      if (wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      pp_barrier();
+      mma(1, 1);
+      mma(1, 0);
+      if (!wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      pp_barrier();
+      cc = ncc;
+      tap = ntap;
+      if (++ntap == 9) { ntap = 0; ++ncc; }
+      if (++n2tap == 9) { n2tap = 0; ++n2cc; }
+      continue;
+    }
+    if constexpr (P2 == 1) {
       // R1: A half 0, B halves 0 and 1 of this step; issue B(t+1) (both halves)
       read_a(sa, tx);
       read_b(buf, 0);
@@ -4156,11 +4197,13 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a) && a.W == 128 && g_variant != 59)
-    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0, true>), dim3(a.tiles), dim3(512), 0, s, a);
+    if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0, 1>), dim3(a.tiles), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0, 2>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a) && a.W == 128)
     hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant != 59 && g_variant != 25 && g_variant != 26 && fwd_use_pph(a))
-    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0, true>), dim3(a.tiles), dim3(512), 0, s, a);
+    if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0, 1>), dim3(a.tiles), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0, 2>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant == 25 && fwd_use_pph(a))
     hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 1>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (g_variant == 26 && fwd_use_pph(a))
@@ -4791,7 +4834,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 59)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 61)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;

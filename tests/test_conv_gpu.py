@@ -717,7 +717,7 @@ def test_two_interval_schedule_bitwise(cuda, shape):
         return y, dx, dw, db
 
     ref = run()
-    for v in (59, ):
+    for v in (59, 61):  # 59: 4-phase kernels; 61: pph two-interval without the two-step-ahead B prefetch
         _lib.check(lib.sr_conv3x3_set_variant(v))
         try:
             got = run()
