@@ -45,9 +45,12 @@ def main():
                 dx = torch.empty(B, hw, hw, C.pad8(cin), device=dev, dtype=dtype)
                 fl = 2.0 * B * hw * hw * cin * cout
                 t = timeit(lambda: C.conv_fwd_raw(x, wf, None, y, B, hw, hw, C.pad8(cin), C.pad8(cout), cout, ksize=1))
-                res.append(dict(v=variant, k='fwd1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+                nb = 2.0 * B * hw * hw * (C.pad8(cin) + C.pad8(cout))  # read X once, write Y once (bf16)
+                res.append(dict(v=variant, k='fwd1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9,
+                                gbps=nb / t / 1e6))
                 t = timeit(lambda: C.conv_fwd_raw(y, wd, None, dx, B, hw, hw, C.pad8(cout), C.pad8(cin), cin, ksize=1))
-                res.append(dict(v=variant, k='dgrad1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9))
+                res.append(dict(v=variant, k='dgrad1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9,
+                                gbps=nb / t / 1e6))
                 continue
             conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(dev)
             spec = C.ConvSpec(cin, cout, out_ps=ps, out_nchw=(cout == 3))
