@@ -3106,6 +3106,171 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Weight gradient of a 1x1 conv (the SwinIR linears: dW[co][ci] = sum_t dy[t][co] x[t][ci] over
+// the tokens t, db[co] = sum_t dy[t][co]), bf16.  A block owns a 192 (co) x 192 (ci) tile over a
+// token K-range (split-K): SwinIR-M's 576 / 184 / 360 / 192 channel counts are 3 / 1 / 2 / 1 such
+// tiles (4-7 % padding, against 28-50 % in 256x256 tiles).  A 64-token K-step is six [64 tok][64 ch]
+// LDS images (128-B rows; 32-B blocks XOR-swizzled by row bits 1 and 3, so the 8 rows a 32-lane
+// half reads with ds_read_b64_tr_b16 land on 8 distinct bank groups): dy co sub-tiles 0-2, then x ci
+// sub-tiles 0-2, DMA'd straight to LDS (wave w: rows 8w .. 8w + 7 of each, the swizzle applied to
+// the lane's source channels).  Three stages, two steps in flight, one barrier per step.  8 waves
+// (2 co x 4 ci), each 96 co x 48 ci (6 x 3 accumulator tiles).  Blocks of the first ci tile also
+// sum dy against a ones operand for the bias (wave (wr, wc): co fragments wc and wc + 4).  Output:
+// the pp kernel's fp32 slab ws[split][Cout][Cin] and bias slab (same reduce).
+// ------------------------------------------------------------------------------------
+SR_DEV uint32_t swz_tr128(uint32_t row, uint32_t byte_in_row) {
+  const uint32_t g = ((row >> 1) & 1u) | (((row >> 3) & 1u) << 1);
+  return row * 128u + ((((byte_in_row >> 5) ^ g) & 3u) << 5) + (byte_in_row & 31u);
+}
+
+__global__ __launch_bounds__(512) void linear_wgrad_kernel(WgArgs a) {
+  constexpr int IMG = 8192;       // [64 tok][64 ch] bf16
+  constexpr int STAGE = 6 * IMG;  // 48 KB
+  constexpr int NST = 3;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = a.tiles_co * a.tiles_ci;
+  const int split = (int)b / ntile;
+  const int rem = (int)b - split * ntile;
+  const int cot = rem / a.tiles_ci, cit = rem - cot * a.tiles_ci;
+  const int co0 = cot * 192, ci0 = cit * 192;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const int nk = (p_end - p_begin + 63) / 64;
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+
+  // DMA lane geometry: image row drow, physical 16-B slot lane & 7 = logical 32-B block
+  // ((lane & 7) >> 1) ^ g(drow), half lane & 1
+  const int drow = 8 * w + (lane >> 3);
+  const int gsw = ((drow >> 1) & 1) | (((drow >> 3) & 1) << 1);
+  const int lch = ((((lane & 7) >> 1) ^ gsw) << 4) + (lane & 1) * 8;
+  uint32_t offy[3], offx[3];
+  bool vy[3], vx[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int co = co0 + i * 64 + lch, ci = ci0 + i * 64 + lch;
+    vy[i] = co < a.Cout;
+    vx[i] = ci < a.Cin;
+    offy[i] = (uint32_t)((drow * a.ldy + a.ycoff + co) * 2);
+    offx[i] = (uint32_t)((drow * a.ldx + a.xcoff + ci) * 2);
+  }
+  auto issue = [&](int ks, int stg) {
+    const int p0 = p_begin + ks * 64;
+    char* st = smem + stg * STAGE + w * 1024;
+    const bool tv = p0 + drow < p_end;
+    const uint32_t by = (uint32_t)p0 * (uint32_t)a.ldy * 2u, bx = (uint32_t)p0 * (uint32_t)a.ldx * 2u;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) glds16(dyr, st + i * IMG, tv && vy[i] ? by + offy[i] : SR_OOB);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) glds16(xr, st + (3 + i) * IMG, tv && vx[i] ? bx + offx[i] : SR_OOB);
+  };
+
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  auto tr8 = [&](const char* img, int r0, int col) -> s16x8 {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + swz_tr128(r0, col * 2)));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + swz_tr128(r0 + 4, col * 2)));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  f32x4 acc[6][3];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const bool bias_here = a.wsb != nullptr && cit == 0;
+  const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+
+  auto compute = [&](int stg) {
+    const char* st = smem + stg * STAGE;
+    s16x8 fa[2][6], fb[2][3];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = kk * 32 + 8 * tg + tq;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int c = wr * 96 + i * 16;
+        fa[kk][i] = tr8(st + (c >> 6) * IMG, r0, (c & 63) + 4 * tp);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int c = wc * 48 + j * 16;
+        fb[kk][j] = tr8(st + (3 + (c >> 6)) * IMG, r0, (c & 63) + 4 * tp);
+      }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[i][j], 0, 0, 0);
+      if (bias_here) {
+        // co fragments wc and wc + 4 of this wave's row block (wave-uniform branches: no indexed
+        // fragment array, which would go to scratch)
+        if (wc == 0) {
+          accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][0], ones, accb[0], 0, 0, 0);
+          accb[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][4], ones, accb[1], 0, 0, 0);
+        } else if (wc == 1) {
+          accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][1], ones, accb[0], 0, 0, 0);
+          accb[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][5], ones, accb[1], 0, 0, 0);
+        } else if (wc == 2) {
+          accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][2], ones, accb[0], 0, 0, 0);
+        } else {
+          accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][3], ones, accb[0], 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if (nk > 0) issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int stg = 0;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();  // step t landed for every wave; every wave finished reading step t - 1's stage
+    if (t + 2 < nk) issue(t + 2, stg == 0 ? 2 : stg - 1);
+    compute(stg);
+    stg = stg == 2 ? 0 : stg + 1;
+  }
+
+  float* ws = a.ws + (size_t)split * a.Cout * a.Cin;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wr * 96 + i * 16 + (lane >> 4) * 4 + r;
+        const int ci = ci0 + wc * 48 + j * 16 + (lane & 15);
+        if (co < a.Cout && ci < a.Cin) ws[(size_t)co * a.Cin + ci] = acc[i][j][r];
+      }
+  if (bias_here && (lane & 15) == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = k == 0 ? wc : wc + 4;
+      if (i < 6) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + wr * 96 + i * 16 + (lane >> 4) * 4 + r;
+          if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[k][r];
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Weight gradient, tap-row form (bf16, Cout and Cin multiples of 128, W % 64 == 0): a block owns
 // one kernel row ty and a 128 (co) x 128 (ci) tile of all THREE taps of that row over a pixel
 // K-range.  A 64-pixel K-step is one image-row segment; per step it DMA's the dy tile [64 px][128
@@ -3514,9 +3679,15 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wl = w;
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = (int)b / a.tiles_ci;
-  const int chunk = (int)b - split * a.tiles_ci;
+  // block = (split, co tile, ci chunk), ci fastest: the tiles of one split (the same x / dy rows)
+  // are consecutive, so xcd_remap keeps them on one XCD's L2
+  const int per_split = a.tiles_ci * a.tiles_co;
+  const int split = (int)b / per_split;
+  const int rem_ = (int)b - split * per_split;
+  const int cot = rem_ / a.tiles_ci;
+  const int chunk = rem_ - cot * a.tiles_ci;
   const int ci0 = chunk * 64;
+  const int co0 = cot * (CO_T * 16);
   const int rows_total = a.N * a.H;
   const int rps = a.kper / a.W;  // image rows per split
   const int r0 = split * rps, r1 = min(rows_total, r0 + rps);
@@ -3590,7 +3761,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
       uint32_t off = SR_OOB;
       if (k < CO_T * 2) {
         const int pr = hrow((k & 1) * 32 + (lane >> 1));
-        const int co = (k >> 1) * 16 + (lane & 1) * 8;
+        const int co = co0 + (k >> 1) * 16 + (lane & 1) * 8;
         dst = st + k * 1024;
         if (co < a.Cout) off = (uint32_t)(((p0s + pr) * a.ldy + a.ycoff + co) * 2);
       }
@@ -3707,7 +3878,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
       float* ws = a.ws + (((size_t)split * 9 + t) * a.Cin + ci) * a.Cout;
 #pragma unroll
       for (int c = 0; c < CW; ++c) {
-        const int co = (ct0 + c) * 16 + g * 4;
+        const int co = co0 + (ct0 + c) * 16 + g * 4;
         if (c < ncw && co < a.Cout) *(f32x4*)(ws + co) = acc[t][c];
       }
     }
@@ -3725,7 +3896,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
     for (int c = 0; c < CW; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = (ct0 + c) * 16 + g * 4 + r;
+        const int co = co0 + (ct0 + c) * 16 + g * 4 + r;
         if (c < ncw && co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
       }
   }
@@ -4555,8 +4726,57 @@ bool wg_bias_fused(const sr_conv3x3_wgrad_desc* d) {
 
 // the row-streaming form of it (variant 37: the tile-row form, for A/B)
 bool wg_use_ring() { return g_variant != 37; }
-// All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2.
+// Row-streaming wgrad over 64-channel output tiles of a wider conv (Cout above 64, the last tile
+// partial): a block is (split, co tile, 64-ci chunk); at 80 KB of LDS two blocks share a CU, so the
+// plan targets 512 blocks.  Taken where the 256x256 pp kernel is not at home -- channel counts that
+// are not multiples of 128 (SwinIR's 184-channel convs: 164 -> 116 us at B 32, 64^2) or Cin < 128
+// (the head convs); on the EDSR-L body shape it ties the pp kernel (193 vs 189 us; 256 blocks 256 us,
+// 3 / 4 steps in flight 250-280 us: LDS for one block per CU), which stays there.
+// SR_RING_WIDE (read once): 0 = off, > 0 = on for every Cout > 64 shape with that block target (A/B);
+// variant 62: on everywhere (parity tests).
+int ring_wide_env() {
+  static int v = [] {
+    const char* e = getenv("SR_RING_WIDE");
+    const int x = e ? atoi(e) : -1;
+    return x >= -1 && x <= 4096 ? x : -1;
+  }();
+  return v;
+}
+int ring_wide_target() {
+  if (g_variant == 62) return 512;
+  const int v = ring_wide_env();
+  return v < 0 ? 512 : v;
+}
+bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d) {
+  if (ring_wide_target() <= 0 || !wg_use_ring() || g_variant == 1 || d->dtype != SR_BF16 || d->ksize == 1 ||
+      d->Cout <= 64 || d->W % 64 || d->in_up > 2 || d->out_ps != 0)
+    return false;
+  if (g_variant == 62 || ring_wide_env() > 0) return true;
+  return d->Cout % 128 != 0 || d->Cin % 128 != 0;
+}
+// 1x1 weight gradient on linear_wgrad_kernel (192x192 tiles): bf16 dense token rows, no pixel
+// shuffle / upsample.  SR_LWG=0 (read once) or variant 63: off (the pp kernel, A/B and tests).
+bool wg_use_lin(const sr_conv3x3_wgrad_desc* d) {
+  static const bool off = [] {
+    const char* e = getenv("SR_LWG");
+    return e && atoi(e) == 0;
+  }();
+  return !off && g_variant != 63 && g_variant != 1 && d->dtype == SR_BF16 && d->ksize == 1 && d->in_up <= 1 &&
+         d->out_ps == 0 && d->Cout >= 64 && d->Cin >= 64;
+}
+// Block target of its split plan: 256 (one 144-KB block per CU), or SR_LWG_T (A/B; read once)
+int lin_wg_target() {
+  static int v = [] {
+    const char* e = getenv("SR_LWG_T");
+    const int x = e ? atoi(e) : 0;
+    return x >= 16 && x <= 4096 ? x : 256;
+  }();
+  return v;
+}
+// All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2 (or the
+// row-streaming form over 64-channel output tiles, wg_ring_wide).
 bool wg_use_halo(const sr_conv3x3_wgrad_desc* d) {
+  if (wg_ring_wide(d)) return true;
   return d->dtype == SR_BF16 && d->ksize != 1 && d->Cout <= 64 && d->W % 64 == 0 && d->in_up <= 2 && d->out_ps == 0 &&
          g_variant != 1;
 }
@@ -4592,7 +4812,7 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     // ~2 blocks per CU, but at least 8 K-steps per block (the slab costs 8 B per tap-MAC row)
     // (A/B on RCAN / RRDB: twice or half as many splits are 6-12 % slower per step)
     const int chunks = (d->Cin + 63) / 64;
-    int S = ring_split_target() / chunks;
+    int S = wg_ring_wide(d) ? ring_wide_target() / (chunks * ((d->Cout + 63) / 64)) : ring_split_target() / chunks;
     const int maxS = M / 512 > 1 ? M / 512 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
@@ -4603,6 +4823,18 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
       *kper = rps * d->W;
       return;
     }
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
+  if (wg_use_lin(d)) {
+    const int tiles = ((d->Cout + 191) / 192) * ((d->Cin + 191) / 192);
+    int S = lin_wg_target() / tiles;
+    const int maxS = (M + 63) / 64;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
     int kp = (M + S - 1) / S;
     kp = (kp + 63) / 64 * 64;
     *splits = (M + kp - 1) / kp;
@@ -4825,6 +5057,7 @@ int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d) {
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
   if (wg_use_halo(d)) return wg_use_ring() ? "conv3x3_wgrad_ring_kernel" : "conv3x3_wgrad_halo_kernel";
+  if (wg_use_lin(d)) return "linear_wgrad_kernel";
   if (wg_use_tr3(d)) return "conv3x3_wgrad_tr3_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
@@ -4834,7 +5067,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 61)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 63)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -4956,10 +5189,10 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   hipError_t e;
   a.stamps = g_stamps;
   if (wg_use_halo(d)) {
-    a.tiles_co = 1;
+    a.tiles_co = wg_ring_wide(d) ? (a.Cout + 63) / 64 : 1;
     a.tiles_ci = (a.Cin + 63) / 64;
-    const int ct = (a.Cout + 15) / 16;
-    const dim3 grid(S * a.tiles_ci);
+    const int ct = wg_ring_wide(d) ? 4 : (a.Cout + 15) / 16;
+    const dim3 grid(S * a.tiles_ci * a.tiles_co);
     if (wg_use_ring()) {
       const int D = ring_depth();
 #define SR_RING(CT_)                                                                                     \
@@ -4975,6 +5208,11 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<2>, grid, dim3(256), 0, s, a);
     else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<3>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<4>, grid, dim3(256), 0, s, a);
+    e = hipGetLastError();
+  } else if (wg_use_lin(d)) {
+    a.tiles_co = (a.Cout + 191) / 192;
+    a.tiles_ci = (a.Cin + 191) / 192;
+    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(S * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
     e = hipGetLastError();
   } else if (wg_use_tr3(d)) {
     a.tiles_co = a.Cout / 128;

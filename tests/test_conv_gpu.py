@@ -283,6 +283,75 @@ def test_wgrad_tr3_vs_fp64(cuda, shape):
     assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
 
 
+@pytest.mark.parametrize('shape', [(2, 64, 64, 184, 576), (1, 64, 64, 192, 184), (3, 8, 64, 184, 360),
+                                   (1, 8, 64, 360, 184), (1, 5, 13, 64, 64), (1, 3, 7, 200, 72),
+                                   (4, 32, 32, 384, 384), (1, 1, 1, 64, 64)])
+def test_linear_wgrad_vs_fp64(cuda, shape):
+    """1x1 weight / bias gradient on linear_wgrad_kernel (192x192 tiles over token K-ranges; SwinIR
+    qkv / proj / fc1 / fc2 shapes, partial channel tiles, ragged token counts down to one) against
+    fp64 on the same bf16 operands and against the 256x256 pp kernel (variant 63)."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(14)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin).to(dt)
+    dy = torch.randn(N, H, W, cout).to(dt)
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, cout, 0, 1
+    assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'linear_wgrad_kernel'
+    outs = []
+    try:
+        for variant in (0, 63):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ksize=1))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    xd, dyd = x.double().reshape(-1, cin), dy.double().reshape(-1, cout)
+    ref_w, ref_b = dyd.t() @ xd, dyd.sum(0)
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    dw = dw.cpu().double().reshape(cout, cin)
+    assert (dw - ref_w).abs().max().item() <= 1e-3 * ref_w.abs().max().item() + 1e-3
+    assert (db.cpu().double() - ref_b).abs().max().item() <= 1e-3 * ref_b.abs().max().item() + 1e-3
+    assert (dw - outs[1][0].cpu().double().reshape(cout, cin)).abs().max().item() <= 1e-3 * ref_w.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize('shape', [(2, 6, 64, 256, 256), (1, 4, 128, 128, 192), (32, 8, 64, 256, 256),
+                                   (3, 3, 64, 8, 256), (1, 5, 64, 96, 128), (2, 64, 64, 256, 256),
+                                   (2, 5, 64, 184, 184), (1, 3, 128, 184, 72)])
+def test_wgrad_ring_wide_vs_fp64(cuda, shape):
+    """Row-streaming wgrad over 64-channel output tiles (Cout above 64, the last tile partial: the
+    EDSR-L body shape, SwinIR's 184-channel convs; variant 62 forces it) against fp64 on the same bf16 operands and against the default
+    kernel; image top / bottom rows, multi-image splits, Cin below one 64-channel chunk."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(13)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin).to(dt)
+    dy = torch.randn(N, H, W, cout).to(dt)
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, cout, 0, 3
+    outs = []
+    try:
+        _lib.check(lib.sr_conv3x3_set_variant(62))
+        assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_ring_kernel'
+        for variant in (62, 0):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
+    assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+
+
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
                                    (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
@@ -472,8 +541,8 @@ def test_fwd_pph_vs_fp64(cuda, shape):
 @pytest.mark.parametrize('shape', [(2, 4, 64, 184, 576), (1, 4, 64, 192, 184), (1, 2, 128, 368, 184),
                                    (2, 2, 64, 184, 368), (1, 3, 64, 128, 136)])
 def test_wgrad_1x1_partial_tiles_vs_fp64(cuda, shape):
-    """Linear-layer weight gradients on the 256x256 kernel with partial co / ci tiles (SwinIR
-    qkv / proj / fc1 / fc2 shapes): dW = dy^T x and db = sum dy against fp64, and equal to
+    """Linear-layer weight gradients on the 256x256 kernel (variant 63: linear_wgrad_kernel off) with
+    partial co / ci tiles (SwinIR qkv / proj / fc1 / fc2 shapes): dW = dy^T x and db = sum dy against fp64, and equal to
     the 128x128 kernel (variant 28) within bf16-operand rounding."""
     N, H, W, cin, cout = shape
     torch.manual_seed(7)
@@ -484,12 +553,13 @@ def test_wgrad_1x1_partial_tiles_vs_fp64(cuda, shape):
     d = _lib.WgradDesc()
     d.dtype, d.N, d.H, d.W, d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.ksize = (
         _lib.SR_BF16, N, H, W, cin, cin, cin, cout, cout, cout, 1)
-    assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_pp_kernel'
     ref_w = dy.reshape(-1, cout).double().cpu().t() @ x.reshape(-1, cin).double().cpu()
     ref_b = dy.reshape(-1, cout).double().cpu().sum(0)
     outs = []
     try:
-        for variant in (0, 28):
+        _lib.check(lib.sr_conv3x3_set_variant(63))  # linear_wgrad_kernel off: the pp kernel
+        assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_pp_kernel'
+        for variant in (63, 28):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
             dw, db = C.conv_wgrad_raw(dy, x, N, H, W, cin, cin, cout, cout, ksize=1)
             outs.append((dw.reshape(cout, cin).cpu().double(), db.cpu().double()))

@@ -51,6 +51,9 @@ def main():
                 t = timeit(lambda: C.conv_fwd_raw(y, wd, None, dx, B, hw, hw, C.pad8(cout), C.pad8(cin), cin, ksize=1))
                 res.append(dict(v=variant, k='dgrad1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9,
                                 gbps=nb / t / 1e6))
+                t = timeit(lambda: C.conv_wgrad_raw(y, x, B, hw, hw, C.pad8(cin), cin, C.pad8(cout), cout, ksize=1))
+                res.append(dict(v=variant, k='wgrad1x1', cin=cin, cout=cout, hw=hw, ms=t, tflops=fl / t / 1e9,
+                                gbps=nb / t / 1e6))  # operand bytes (dy + x once), slab traffic not counted
                 continue
             conv = torch.nn.Conv2d(cin, cout, 3, 1, 1).to(dev)
             spec = C.ConvSpec(cin, cout, out_ps=ps, out_nchw=(cout == 3))
