@@ -1175,6 +1175,147 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// linear_wk_kernel<E>: 1x1 convs with a wide K (192 < K <= 576) and Cout <= 192 -- the SwinIR fc2
+// forward (360 -> 184) and the fc1 / qkv dgrads (360 / 576 -> 184).  A block owns 128 tokens x all
+// output channels and streams K in 64-wide steps through two LDS stages (LDS-DMA of the token tile
+// [128][128 B] and the weight tile [192][128 B], both K-contiguous, chunk ^ (row & 7) swizzle; 40 KB
+// a stage, so two blocks share a CU).  C = W . X^T as in conv3x3_lin_kernel: the weight rows are
+// permuted on load (32-row group p, tile t, row r -> channel 32p + 8(r/4) + 4t + r%4), so a lane ends
+// with 8 consecutive channels of one token and stores them as one 16-B vector with the fused epilogue.
+// 4 waves (2 channel x 2 token halves), each 96 channels x 64 tokens (6 x 4 accumulator tiles).  (The
+// 64-token lin kernel it replaces re-read the whole weight image per 64 tokens -- 434 MB of L2 reads
+// on the qkv dgrad -- and staged all of K before its first MFMA.)
+// E: conv3x3_lin_kernel's epilogue codes 0 (plain), 16 (residual), 144 (residual + row scale); the
+// bias (GEMM column order), alpha and beta always.
+// ------------------------------------------------------------------------------------
+template <int E>
+__global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
+  constexpr int XI = 128 * 128, WI = 192 * 128, STAGE = XI + WI;
+  constexpr bool RES = (E & 16) != 0, RSC = (E & 128) != 0;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int m0 = (int)xcd_remap(blockIdx.x, gridDim.x) * 128;
+  const int K = a.Cin, nk = (K + 63) >> 6;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
+
+  // DMA pieces of 64 lanes = 8 rows x 8 chunks: per stage 16 token pieces then 24 weight pieces,
+  // wave w taking pieces w, w + 4, ...; lane: row rl of the piece, physical chunk pc = logical lc ^ rl
+  const int rl = lane >> 3, lc = (lane & 7) ^ rl;
+  int wch[6];  // source weight channel of this lane's row in weight pieces q = 4..9
+#pragma unroll
+  for (int q = 4; q < 10; ++q) {
+    const int row = (w + 4 * q - 16) * 8 + rl;
+    const int t = (row >> 4) & 1, r = row & 15;
+    wch[q - 4] = (row >> 5) * 32 + 8 * (r >> 2) + 4 * t + (r & 3);
+  }
+  auto issue = [&](int ks, int stg) {
+    char* st = smem + stg * STAGE;
+    const int kc = ks * 8 + lc;
+    const bool kv = kc * 8 < K;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = w + 4 * q, m = m0 + p * 8 + rl;
+      glds16(xr, st + p * 1024, (kv && m < a.M) ? (uint32_t)((m * a.ldx + a.xcoff + kc * 8) * 2) : SR_OOB);
+    }
+#pragma unroll
+    for (int q = 4; q < 10; ++q) {
+      const int p = w + 4 * q - 16, ch = wch[q - 4];
+      glds16(wrs, st + XI + p * 1024, (kv && ch < a.Cout) ? (uint32_t)((ch * a.ldw + kc * 8) * 2) : SR_OOB);
+    }
+  };
+
+  const int c16 = lane & 15, g = lane >> 4;
+  f32x4 acc[6][4];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int stg) {
+    const char* Xs = smem + stg * STAGE;
+    const char* Ws = Xs + XI;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int phys = ((kk * 4 + g) ^ (c16 & 7)) << 4;  // every fragment row has row & 7 == c16 & 7
+      u32x4 fa[6], fb[4];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) fa[i] = *(const u32x4*)(Ws + (wr * 96 + i * 16 + c16) * 128 + phys);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *(const u32x4*)(Xs + (wc * 64 + j * 16 + c16) * 128 + phys);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, fa[i]),
+                                                              __builtin_bit_cast(s16x8, fb[j]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  issue(0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();  // step ks landed for every wave; step ks - 1's stage is free
+    if (ks + 1 < nk) issue(ks + 1, (ks + 1) & 1);
+    compute(ks & 1);
+  }
+
+  // ---- epilogue: pair P (tiles 2P, 2P + 1) gives channels n = (3 wr + P) * 32 + 8g .. + 7 of token
+  // m0 + 64 wc + 16 j + c16
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  const size_t ybytes = (size_t)a.M * a.ldy * 2;
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, ybytes < 0x80000000ull ? (uint32_t)ybytes : 0x7fffffffu);
+  const __amdgpu_buffer_rsrc_t br = make_rsrc(a.bias, a.bias ? (uint32_t)a.Cout * 4u : 0u);
+  float alpha_blk = a.alpha;
+  if constexpr (RSC) alpha_blk = a.alpha * a.row_scale[fdiv((uint32_t)m0, a.fd_hw)];
+  u32x4 rv[3][4];
+  float bv[3][8];
+#pragma unroll
+  for (int P = 0; P < 3; ++P) {
+    const int n = (3 * wr + P) * 32 + 8 * g;
+    const u32x4 b0 = buf_load16(br, (uint32_t)n * 4u), b1 = buf_load16(br, (uint32_t)n * 4u + 16u);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { bv[P][r] = __uint_as_float(b0[r]); bv[P][4 + r] = __uint_as_float(b1[r]); }
+    if constexpr (RES) {
+      const bool rok = n < a.Cout && n < a.rcols;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wc * 64 + j * 16 + c16;
+        rv[P][j] = buf_load16(rr, (rok && m < a.M) ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
+      }
+    }
+  }
+#pragma unroll
+  for (int P = 0; P < 3; ++P) {
+    const int n = (3 * wr + P) * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wc * 64 + j * 16 + c16;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = (acc[2 * P][j][r] + bv[P][r]) * alpha_blk;
+        v[4 + r] = (acc[2 * P + 1][j][r] + bv[P][4 + r]) * alpha_blk;
+      }
+      if constexpr (RES) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] += a.beta * bf16_to_f32(rv[P][j][q] & 0xffff);
+          v[2 * q + 1] += a.beta * bf16_to_f32(rv[P][j][q] >> 16);
+        }
+      }
+      u32x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
+      __builtin_amdgcn_raw_buffer_store_b128(o, yr, (n < a.Cout && m < a.M) ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB, 0, 0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // conv3x3_lin_kernel<MT>: 1x1 convs (nn.Linear over NHWC tokens: SwinIR qkv / proj / fc1 /
 // fc2 and their dgrads, DCN column GEMMs) with a short K (<= 576).  These GEMMs are
 // HBM-bound (AI ~ 100-150 FLOP/B); the 2-D tiled kernels re-read the token rows once per
@@ -4483,6 +4624,17 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
   if (a.Cin <= 192) return a.Cout <= 640;
   return a.Cin <= 576 && a.Cout <= 384 && g_variant != 55;
 }
+// wide-K linears with Cout <= 192 and a plain / residual / residual + row-scale epilogue on
+// linear_wk_kernel; SR_LWK=0 (read once) or variant 64: the 64-token lin kernel (A/B, tests)
+bool lin_use_wk(const FwdArgs& a) {
+  static const bool off = [] {
+    const char* e = getenv("SR_LWK");
+    return e && atoi(e) == 0;
+  }();
+  if (off || g_variant == 64 || a.Cin <= 192 || a.Cin > 576 || a.Cout > 192) return false;
+  const int e = lin_epi(a);
+  return e == 0 || e == 16 || e == 144;
+}
 // HR tail convs: Cout <= 16 with the NCHW fp32 store, W >= 256 (32-px strips), Cin 64 / 128 / 256
 bool fwd_use_tail(const FwdArgs& a, bool bf) {
   return bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && a.out_ps == 0 && a.out_nchw && a.Cout <= 16 &&
@@ -4547,6 +4699,13 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
 case FK_LIN: {
   FwdArgs b = a;
   const int e = lin_epi(a);
+  if (lin_use_wk(a)) {  // wide K, Cout <= 192: 128-token tiles, K streamed
+    const dim3 grid((a.M + 127) / 128);
+    if (e == 0) hipLaunchKernelGGL(linear_wk_kernel<0>, grid, dim3(256), 0, s, b);
+    else if (e == 16) hipLaunchKernelGGL(linear_wk_kernel<16>, grid, dim3(256), 0, s, b);
+    else hipLaunchKernelGGL(linear_wk_kernel<144>, grid, dim3(256), 0, s, b);
+    return hipGetLastError();
+  }
   if (a.Cin > 192) {  // wide K: 64-token tiles, the whole K (<= 384 / 576) staged
     b.tiles = (a.M + 63) / 64;
 #define SR_LINW_E(CG_, NP_, E_) \
@@ -5033,7 +5192,7 @@ int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d) {
 const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
   const bool bf = d->dtype == SR_BF16;
   switch (fwd_kind(fwd_shape(d), bf)) {
-    case FK_LIN: return "conv3x3_lin_kernel";
+    case FK_LIN: return lin_use_wk(fwd_shape(d)) ? "linear_wk_kernel" : "conv3x3_lin_kernel";
     case FK_HALO: return "conv3x3_fwd_halo_kernel";
     case FK_BAND: return "conv3x3_fwd_band_kernel";
     case FK_TAIL: return "conv3x3_fwd_tail_kernel";
@@ -5067,7 +5226,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 63)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 64)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;

@@ -35,7 +35,12 @@ def bump_param_epoch():
 # to the side stream; leaving the context joins it (the current stream waits on it), so the
 # optimizer, the bucketed all-reduce and any reader of .grad see finished gradients.  Results are
 # the same kernels on the same inputs: bitwise equal to the single-stream order.
-_ASYNC = {'depth': 0, 'streams': {}, 'used': False, 'mode': True}
+# ``hold`` keeps every side-stream dy alive until the join: autograd accumulates a tensor's two
+# gradient contributions IN PLACE into one of them when it holds the last reference (e.g. a conv
+# output that is also a residual: RCAN / SwinIR body convs, RSTB convs), and that write on the main
+# stream could land while the side-stream weight gradient still reads the buffer (record_stream only
+# guards reuse after free).  A second reference makes that accumulation out of place.
+_ASYNC = {'depth': 0, 'streams': {}, 'used': False, 'mode': True, 'hold': []}
 
 
 def _side_stream(device):
@@ -80,6 +85,8 @@ class async_wgrad:
             _ASYNC['mode'] = self._prev_mode  # a nested context must not leak its mode outward
             for st in _ASYNC['streams'].values():
                 torch.cuda.current_stream(st.device).wait_stream(st)
+            if _ASYNC['depth'] == 0:
+                _ASYNC['hold'].clear()  # joined: the side stream's reads are ordered before any later write
         return False
 
 
@@ -387,6 +394,7 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
         for t in (dy, x, kw.get('co_map'), kw.get('ci_map')):
             if t is not None:
                 t.record_stream(side)
+        _ASYNC['hold'].append(dy)  # no in-place gradient accumulation into dy before the join
         with torch.cuda.stream(side):
             _wgrad_launch(lib, d, dy, x, ws_bytes, tw, tb, cin_real, cout_real, need_bias, kw)
         grad_ready(params[0])

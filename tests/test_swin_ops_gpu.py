@@ -125,14 +125,15 @@ def test_linear_ln_fused_vs_separate(cuda, which, shape):
 @pytest.mark.parametrize('K,Cout', [(360, 184), (576, 184), (200, 96), (256, 304), (384, 40)])
 @pytest.mark.parametrize('epi', ['plain', 'res', 'res_rowscale', 'gate'])
 def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
-    """The lin kernel on wide K (192 < K <= 576, 64-token tiles: SwinIR fc2 fwd 360 -> 184, fc1 / qkv
-    dgrads 360 / 576 -> 184) against float64 on the same bf16 operands, with the epilogues those
-    calls use (residual, residual + per-image row scale, GELU' gate) and a ragged last token tile;
-    the kernel that ran is the lin kernel (name), and variant 55 (the 256x256 pp kernel for these
-    shapes) agrees within bf16 rounding."""
+    """Wide-K linears (192 < K <= 576: SwinIR fc2 fwd 360 -> 184, fc1 / qkv dgrads 360 / 576 -> 184) --
+    linear_wk_kernel for Cout <= 192, the 64-token lin kernel otherwise (and with variant 64) --
+    against float64 on the same bf16 operands, with the epilogues those calls use (residual, residual
+    + per-image row scale, GELU' gate) and a ragged last token tile; variant 55 (the 256x256 pp kernel
+    for these shapes) agrees within bf16 rounding."""
     from basicsr4rs_amd import _lib
     from basicsr4rs_amd.ops import conv as C
-    N, H, W = 3, 8, 40  # 960 tokens: 15 tiles of 64, and H*W % 64 == 0 for the row scale
+    # 960 tokens (ragged against 128- and 64-token tiles); the row scale needs H*W % 128 == 0
+    N, H, W = (3, 8, 48) if epi == 'res_rowscale' else (3, 8, 40)
     torch.manual_seed(K + Cout)
     dt = torch.bfloat16
     x = (torch.randn(N, H, W, K, device=cuda) * 0.5).to(dt)
@@ -157,7 +158,7 @@ def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
 
     lib = _lib.load()
     d = C._desc(dt, N, H, W, K, K, Cout, Cout, Cout, ksize=1)
-    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_lin_kernel'
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == (b'linear_wk_kernel' if Cout <= 192 else b'conv3x3_lin_kernel')
     y = run().double()
     ref = x.double() @ w.to(dt).double().t() + bias.double()
     if gate is not None:
@@ -173,6 +174,10 @@ def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
     try:
         assert lib.sr_conv3x3_fwd_kernel_name(d) != b'conv3x3_lin_kernel' or K <= 192
         y55 = run().double()
+        _lib.check(lib.sr_conv3x3_set_variant(64))
+        assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_lin_kernel'
+        y64 = run().double()
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
     assert (y55 - ref).abs().max().item() <= tol
+    assert (y64 - ref).abs().max().item() <= tol

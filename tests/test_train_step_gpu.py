@@ -182,6 +182,44 @@ _NETS = {
 }
 
 
+@pytest.mark.parametrize('net', ['rcan', 'swinir', 'edsr'])
+def test_async_wgrad_delayed_side_stream_bitwise(cuda, net):
+    """The side stream held back by a spin kernel queued ahead of each backward: the main stream then
+    runs the whole dgrad chain, including autograd's accumulation of a residual's two gradient
+    contributions, before any side-stream weight gradient reads its dy.  That accumulation would be
+    done IN PLACE into a dy the side stream still has to read (RCAN body conv, SwinIR RSTB conv:
+    round-3 finding, nondeterministic SwinIR runs) unless the dy stays referenced until the join
+    (ops.conv._ASYNC['hold']); losses and parameters must equal the single-stream run bitwise."""
+    import basicsr4rs_amd.archs  # noqa: F401
+    from basicsr4rs_amd.models import build_model
+    from basicsr4rs_amd.ops import conv as C
+    runs = []
+    for use_async in (False, True):
+        torch.manual_seed(0)
+        opt = _opt(amp=True)
+        opt['network_g'] = dict(_NETS[net])
+        opt['train']['cuda_graph'] = False
+        opt['train']['async_wgrad'] = use_async
+        model = build_model(opt)
+        lq = torch.rand(4, 3, 16, 16, generator=torch.Generator().manual_seed(0)).to(cuda)
+        gt = torch.rand(4, 3, 64, 64, generator=torch.Generator().manual_seed(1)).to(cuda)
+        model.feed_data({'lq': lq, 'gt': gt})
+        losses = []
+        for it in range(1, 4):
+            model.update_learning_rate(it)
+            if use_async:
+                with torch.cuda.stream(C._side_stream(torch.device(cuda))):
+                    torch.cuda._sleep(20_000_000)
+            model.optimize_parameters(it)
+            losses.append(model.get_current_log()['l_pix'])
+        torch.cuda.synchronize()
+        net_ = model.get_bare_model(model.net_g)
+        runs.append((losses, {k: v.detach().clone() for k, v in net_.state_dict().items()}))
+    assert runs[0][0] == runs[1][0]
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+
+
 @pytest.mark.parametrize('net', sorted(_NETS))
 @pytest.mark.parametrize('graph', [False, True])
 def test_async_wgrad_bitwise_equals_sync(cuda, net, graph):
