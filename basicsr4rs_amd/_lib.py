@@ -29,7 +29,7 @@ class ConvDesc(ctypes.Structure):
                 ('out_ps', _i), ('out_nchw', _i), ('act', _i), ('slope', _f), ('alpha', _f), ('ldg', _i),
                 ('gcoff', _i), ('gate_slope', _f), ('ldr', _i), ('rcoff', _i), ('beta', _f), ('ldr2', _i),
                 ('r2coff', _i), ('beta2', _f), ('rcols', _i), ('in_up', _i), ('ksize', _i), ('gate_mode', _i),
-                ('gcol0', _i), ('gcol1', _i), ('row_scale', _vp)]
+                ('gcol0', _i), ('gcol1', _i), ('row_scale', _vp), ('dot', _vp), ('ldd', _i), ('dcoff', _i)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -57,6 +57,8 @@ SIGNATURES = {
     'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_linear_ln_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_conv3x3_fwd_colsum_parts': (_i, [ctypes.POINTER(ConvDesc)]),
+    'sr_conv3x3_fwd_dot_ok': (_i, [ctypes.POINTER(ConvDesc)]),
+    'sr_conv3x3_get_variant': (_i, []),
     'sr_conv3x3_set_variant': (_i, [_i]),
     'sr_conv3x3_set_stamps': (_i, [_vp]),
     'sr_conv3x3_fwd_kernel_name': (ctypes.c_char_p, [ctypes.POINTER(ConvDesc)]),

@@ -71,6 +71,9 @@ struct FwdArgs {
   float* ln_rstd;
   int ln_C;      // channels normalised (the rest of the Cin padded columns are written as zeros)
   float ln_eps;
+  const void* dot;  // band kernel, with colsum: partial sums of y * dot (sr_conv3x3_desc.dot)
+  uint32_t d_bytes;
+  int ldd, dcoff;
 };
 
 // alpha of output row m: a.alpha, times the per-image row_scale when given
@@ -1935,13 +1938,15 @@ SR_DEV void vm_wait_dyn(int n) { vm_wait_bs<0, 63>(n < 0 ? 0 : (n > 63 ? 63 : n)
 // E (the epilogue, fixed at compile time: at one wave per SIMD every run-time branch of a
 // per-row epilogue is exposed): bits 0-1 act, 2-3 gate (0 none, 1 pre-residual (g > 0 ? 1 :
 // gate_slope), 2 pre-residual GELU'(g), 3 post-residual (g > 0 ? 1 : gate_slope) on output
-// channels gcol0..gcol1), 4 res, 5 res2, 6 aux, 7 colsum, 8 row_scale.
+// channels gcol0..gcol1), 4 res, 5 res2, 6 aux, 7 colsum, 8 row_scale, 9 dot (with 7: the partial
+// sums are of y * dot, the dot operand staged like the residuals).
 template <int CO, int W, int LA, int KH, int E>
 __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
   constexpr bool RES = (E & 16) != 0, RES2 = (E & 32) != 0, AUX = (E & 64) != 0, CS = (E & 128) != 0,
-                 RSC = (E & 256) != 0;
-  constexpr int IR = GATE ? 1 : 0, IR2 = IR + (RES ? 1 : 0), NSTG = IR2 + (RES2 ? 1 : 0);
+                 RSC = (E & 256) != 0, DOT = (E & 512) != 0;
+  static_assert(!DOT || CS, "band: dot partials need colsum");
+  constexpr int IR = GATE ? 1 : 0, IR2 = IR + (RES ? 1 : 0), ID = IR2 + (RES2 ? 1 : 0), NSTG = ID + (DOT ? 1 : 0);
   constexpr int WC = CO / 32;       // waves along output channels (32 each = 2 co tiles)
   constexpr int WP = 4 / WC;        // waves along the row's pixels
   constexpr int PT = W / 16 / WP;   // 16-pixel tiles per wave
@@ -1978,6 +1983,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
   const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
+  const __amdgpu_buffer_rsrc_t dr = make_rsrc(a.dot, a.d_bytes);
 
   // weights: one coalesced LDS-DMA image [co][tap][ci] (1 KB contiguous per wave instruction),
   // then each wave reads its MFMA fragments from it: co = wc*32 + 8*(c16>>2) + 4*c + (c16&3)
@@ -2074,6 +2080,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
         glds16(rr, epi + (IR * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr + a.rcoff + nn) * 2) : SR_OOB);
       if constexpr (RES2)
         glds16(rr2, epi + (IR2 * PT + i) * 1024, qv && rok ? (uint32_t)((m * a.ldr2 + a.r2coff + nn) * 2) : SR_OOB);
+      if constexpr (DOT)
+        glds16(dr, epi + (ID * PT + i) * 1024, qv ? (uint32_t)((m * a.ldd + a.dcoff + nn) * 2) : SR_OOB);
     }
   };
   // prologue: rows s0 - 1 .. s0 + LA - 1 (s0 - 1 first: the oldest), then row s0's staging
@@ -2254,7 +2262,15 @@ __global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) ov[i][j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
-      if constexpr (CS) {
+      if constexpr (CS && DOT) {  // y as stored times the dot operand
+        float df[8];
+        unpack8(*(const u32x4*)(epi + (ID * PT + i) * 1024 + lane * 16), df);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          cs[2 * j] += bf16_to_f32(ov[i][j] & 0xffff) * df[2 * j];
+          cs[2 * j + 1] += bf16_to_f32(ov[i][j] >> 16) * df[2 * j + 1];
+        }
+      } else if constexpr (CS) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           cs[2 * j] += bf16_to_f32(ov[i][j] & 0xffff);
@@ -2462,6 +2478,7 @@ struct WgArgs {
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   int bias_group;  // pp kernel: > 0 = the bias-role blocks come after all tile blocks, each doing this many splits
   int bias_fused;  // pp kernel: no bias-role blocks; the centre-tap, first-ci-tile blocks sum dy as well
+  int ring_early;  // ring kernel: issue step ks + D before step ks's MFMAs (one barrier per step)
   FastDiv fd_W, fd_H, fd_cps;
   unsigned long long* stamps;  // diagnostics (SR_BAND_STAMPS builds): per-block phase cycles
 };
@@ -3806,16 +3823,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
 // tiles, ran its two groups in lock-step between the per-step barriers and was slower.)  The
 // first step of a segment loads its three rows itself, after the previous segment's last step
 // (its slots may still be read), so a block has nseg - 1 one-step bubbles.
-template <int CO_T, int D = 2>  // D: steps in flight
+// EARLY (opt-in, SR_RING_EARLY=1, one image-row segment per block row): step ks + D is issued right
+// after step ks's barrier, before its MFMAs, into a slot / dy stage nobody reads in step ks (one more
+// ring slot and dy stage), so a step needs ONE barrier; otherwise the issue waits for a second barrier
+// after the MFMAs.  Measured slower: the extra LDS (RCAN 78 -> 99 KB, RRDB 70 -> 87 KB) costs the
+// second block per CU (RRDB 65.5 -> 73 ms).  LA: fragment reads in flight ahead of the MFMA group.
+template <int CO_T, int D = 2, int LA = 3, bool EARLY = false>  // D: steps in flight
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   constexpr int CW = CO_T;  // co tiles per wave
   constexpr int RS = 3 * 1024;      // one halo row of one 16-ci tile: 96 rows x 32 B (66 used)
-  constexpr int RSL = D + 2;        // ring slots: rows q-1 .. q+1 read, D - 1 more in flight
+  constexpr int RSL = D + (EARLY ? 3 : 2);  // ring slots: rows q-1 .. q+1 read, D - 1 in flight (+1 being issued)
   constexpr int RING = (RSL + 1) * RS;  // + the zero slot, per ci tile
   constexpr int DYB = CO_T * 2048;  // dy image: CO_T tiles x 64 rows x 32 B
   constexpr int DYS = DYB + 1024;   // + 1 KB target for padding DMAs
   constexpr int DYI = (CO_T * 2 + 3) / 4;  // dy DMAs per wave
-  __shared__ __attribute__((aligned(16))) char smem[4 * RING + D * DYS];
+  constexpr int DST = D + (EARLY ? 1 : 0);  // dy stages
+  __shared__ __attribute__((aligned(16))) char smem[4 * RING + DST * DYS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wl = w;
@@ -3894,7 +3917,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
       issue_row(q + 1, seg);
     }
     const int p0s = q * a.W + seg * 64;
-    char* st = dys + (j % D) * DYS;
+    char* st = dys + (j % DST) * DYS;
 #pragma unroll
     for (int i = 0; i < DYI; ++i) {
       const int k = w + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
@@ -3924,12 +3947,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
     const int y = q - (int)fdiv((uint32_t)q, a.fd_H) * a.H;
     const char* rows3[3] = {ring + (y == 0 ? RSL : slot(q - 1)) * RS, ring + slot(q) * RS,
                             ring + (y == a.H - 1 ? RSL : slot(q + 1)) * RS};
-    const char* ds = dys + (j % D) * DYS + ct0 * 2048;
+    const char* ds = dys + (j % DST) * DYS + ct0 * 2048;
     // Fragment reads (per K half: this wave's dy tiles, then the 9 taps' x tiles) run LA reads
     // ahead of the MFMA group (one tap x CW co tiles) that needs them, in program order fixed by
     // scheduling barriers (the compiler otherwise sinks each read to just before its MFMAs); at
     // most ~2 (LA + 1) reads are in flight, within what lgkmcnt counts, so its waits stay exact.
-    constexpr int NR = CW + 9, LA = 3;
+    constexpr int NR = CW + 9;
     s16x8 fr[2 * NR];
     auto rd = [&](int r) {
       const int kk = r / NR, i = r - kk * NR;
@@ -3967,6 +3990,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   const unsigned long long t_start = __builtin_readcyclecounter();
 #endif
   __syncthreads();  // zero slots written
+  const bool early = EARLY && nseg == 1;
   int next = 0;  // steps issued so far, in step order (issue_iter is non-decreasing)
   while (next < nk && issue_iter(next) < 0) issue(next++);
   for (int ks = 0; ks < nk; ++ks) {
@@ -3986,6 +4010,8 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
     const unsigned long long t1 = __builtin_readcyclecounter();
 #endif
     __builtin_amdgcn_s_barrier();
+    if (early)  // step ks + D: its slot / stage were last read in step ks - 1, finished by every wave
+      while (next < nk && issue_iter(next) <= ks) issue(next++);
 #ifdef SR_BAND_STAMPS
     const unsigned long long t2 = __builtin_readcyclecounter();
 #endif
@@ -3994,8 +4020,10 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
 #ifdef SR_BAND_STAMPS
     const unsigned long long t3 = __builtin_readcyclecounter();
 #endif
-    __builtin_amdgcn_s_barrier();
-    while (next < nk && issue_iter(next) <= ks) issue(next++);
+    if (!early) {
+      __builtin_amdgcn_s_barrier();
+      while (next < nk && issue_iter(next) <= ks) issue(next++);
+    }
 #ifdef SR_BAND_STAMPS
     const unsigned long long t4 = __builtin_readcyclecounter();
     ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
@@ -4569,13 +4597,14 @@ int band_epi(const FwdArgs& a, int grid) {
   int gate = 0;
   if (a.gate) gate = a.gate_mode == 2 ? 3 : (a.gate_mode == 1 ? 2 : 1);
   const int e = a.act | (gate << 2) | (a.res ? 16 : 0) | (a.res2 ? 32 : 0) | (a.aux ? 64 : 0) |
-                (a.colsum ? 128 : 0) | (a.row_scale ? 256 : 0);
+                (a.colsum || a.dot ? 128 : 0) | (a.row_scale ? 256 : 0) | (a.dot ? 512 : 0);  // dot implies colsum
   if (a.row_scale) {  // the images of one band fit one wave's lanes
     const int rows = (a.N * a.H + grid - 1) / grid;
     if ((rows + a.H - 1) / a.H + 1 > 64) return -1;
   }
   switch (e) {
     case 0: case 1: case 2: case 4: case 16: case 20: case 28: case 48: case 72: case 128: case 304: return e;
+    case 656: return a.Cin == 64 && a.Cout == 64 ? e : -1;  // RCAB conv1 dgrad + the CA dot partials
     default: return -1;
   }
 }
@@ -4672,6 +4701,11 @@ hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
   ab.stamps = g_stamps;
   const dim3 grid(rows < gmax ? rows : gmax);
   const int e = band_epi(a, grid.x);
+  if (e == 656) {  // instantiated for the RCAN shapes only
+    if (a.W == 64) hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 64, 5, 2, 656>), grid, dim3(256), 0, s, ab);
+    else hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 2, 656>), grid, dim3(256), 0, s, ab);
+    return hipGetLastError();
+  }
 #define SR_BAND_E(CO_, W_, LA_, KH_, E_) \
   case E_: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<CO_, W_, LA_, KH_, E_>), grid, dim3(256), 0, s, ab); break;
 #define SR_BAND(CO_, W_, LA_, KH_) \
@@ -4961,6 +4995,23 @@ int ring_depth() {
   return v;
 }
 
+// Early DMA issue in the ring wgrad (one barrier per step, one more LDS slot): SR_RING_EARLY=1 (A/B; read once)
+bool ring_early() {
+  static const bool v = [] {
+    const char* e = getenv("SR_RING_EARLY");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+// Fragment-read lookahead of the ring wgrad (D = 2): 3, or SR_RING_LA=5 (A/B; read once)
+int ring_la() {
+  static const int v = [] {
+    const char* e = getenv("SR_RING_LA");
+    return e && atoi(e) == 5 ? 5 : 3;
+  }();
+  return v;
+}
+
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
 // 256x256 kernel, ~2 rounds for the small ones), pixels per split a multiple of 64.
 void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
@@ -5089,6 +5140,11 @@ FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
   a.fd_r = make_fastdiv(d->in_ps > 0 ? d->in_ps : 1);
   a.row_scale = d->row_scale;
   a.fd_hw = make_fastdiv(d->H * d->W > 0 ? d->H * d->W : 1);
+  a.dot = d->dot; a.ldd = d->ldd; a.dcoff = d->dcoff;
+  if (d->dot) {  // the dot epilogue comes with a residual: the pointer-free kind / parts / name queries
+    static const char one = 1;  // see the launch's epilogue code (sr_conv3x3_fwd sets the real res)
+    a.res = &one;
+  }
   return a;
 }
 
@@ -5138,6 +5194,13 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
     return sr_fail(SR_ETOOBIG, "conv3x3_fwd: tensor >= 2 GiB (split the batch)");
   a.x = x; a.w = w; a.bias = bias; a.gate = gate; a.res = res; a.res2 = res2;
   a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.y = y; a.aux = aux; a.colsum = colsum;
+  if (d->dot) {  // with every operand pointer set: the band kernel's epilogue code decides
+    if (!colsum || !res || d->dtype != SR_BF16 || fwd_kind(a, true) != FK_BAND || d->ldd % 8 || d->dcoff % 8)
+      return sr_fail(SR_EINVAL, "conv3x3_fwd: dot partials need colsum on the band kernel (bf16, 64 -> 64 ch)");
+    const size_t db = (size_t)d->N * d->H * d->W * d->ldd * 2;
+    if (db >= 0x80000000ull) return sr_fail(SR_ETOOBIG, "conv3x3_fwd: dot operand >= 2 GiB");
+    a.d_bytes = (uint32_t)db;
+  }
   a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
   a.g_bytes = gate ? (uint32_t)((size_t)M * d->ldg * SZ) : 0;
   a.r_bytes = res ? (uint32_t)((size_t)M * d->ldr * SZ) : 0;
@@ -5180,6 +5243,20 @@ int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_ga
   }
 #undef SR_LNL
   return sr_check(hipGetLastError(), "linear_ln_fwd launch");
+}
+
+// 1 when sr_conv3x3_fwd can fuse the dot partials (d->dot) into this conv with a residual operand:
+// the band kernel's residual + colsum + dot epilogue (RCAB conv1 dgrad shapes).
+int sr_conv3x3_fwd_dot_ok(const sr_conv3x3_desc* d) {
+  if (!d || d->N <= 0 || d->H <= 0 || d->W <= 0 || d->dtype != SR_BF16) return 0;
+  FwdArgs a = fwd_shape(d);
+  static const char one = 1;
+  a.res = &one;
+  a.dot = &one;
+  a.colsum = (float*)&one;
+  sr_conv3x3_desc dd = *d;
+  dd.dot = &one;
+  return fwd_kind(a, true) == FK_BAND && colsum_parts(&dd, a) > 0 ? 1 : 0;
 }
 
 int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d) {
@@ -5231,6 +5308,8 @@ int sr_conv3x3_set_variant(int variant) {
   g_variant = variant;
   return SR_OK;
 }
+
+int sr_conv3x3_get_variant(void) { return g_variant; }
 
 // Diagnostics: the band kernel writes 16 clock values per block (wave 0: start, weights loaded,
 // end, rows, cycles summed over rows in the row wait / barrier / MFMA / epilogue phases, then
@@ -5354,9 +5433,13 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     const dim3 grid(S * a.tiles_ci * a.tiles_co);
     if (wg_use_ring()) {
       const int D = ring_depth();
+      a.ring_early = ring_early() ? 1 : 0;
+      const int la = ring_la();
 #define SR_RING(CT_)                                                                                     \
   if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);        \
   else if (D == 3) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 3>), grid, dim3(256), 0, s, a);   \
+  else if (la == 5) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 5>), grid, dim3(256), 0, s, a); \
+  else if (a.ring_early) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 3, true>), grid, dim3(256), 0, s, a); \
   else hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2>), grid, dim3(256), 0, s, a);
       if (ct == 1) { SR_RING(1) }
       else if (ct == 2) { SR_RING(2) }

@@ -251,7 +251,25 @@ def _desc(dtype, N, H, W, cin, ldx, cout, cout_real, ldy, **kw):
     if rs is not None:
         assert rs.dtype == torch.float32 and rs.is_cuda and rs.numel() == N, 'row_scale: fp32 [N] on the device'
         d.row_scale = rs.data_ptr()
+    dot = kw.get('dot')
+    if dot is not None:
+        assert dot.dtype == dtype and dot.is_contiguous() and dot.shape[:3] == (N, H, W), 'dot: like y'
+        d.dot, d.ldd, d.dcoff = dot.data_ptr(), dot.shape[-1], 0
     return d
+
+
+_DOT_OK = {}
+
+
+def dot_partials_ok(dtype, N, H, W, cin, cout):
+    """Whether a conv (cin -> cout, with a residual) can also emit the partial channel sums of
+    y * dot in its epilogue (sr_conv3x3_fwd_dot_ok: the band kernel); cached per shape."""
+    key = (dtype, N, H, W, cin, cout, _lib.load().sr_conv3x3_get_variant())
+    v = _DOT_OK.get(key)
+    if v is None:
+        d = _desc(dtype, N, H, W, cin, cin, cout, cout, cout)
+        v = _DOT_OK[key] = bool(_lib.load().sr_conv3x3_fwd_dot_ok(d))
+    return v
 
 
 def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res=None, aff_scale=None,
@@ -259,7 +277,8 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     """Launch sr_conv3x3_fwd on already-prepared GEMM weights (shapes checked here).
 
     ``colsum=True`` also returns the [N, P, cout] fp32 partial channel sums of y (as stored;
-    summed over P they are the per-image channel sums): ``(y, parts)``."""
+    summed over P they are the per-image channel sums): ``(y, parts)``; with ``dot=t`` (bf16, y's
+    shape) they are the partial sums of y * t instead (band kernel only, dot_partials_ok)."""
     assert x.is_contiguous() and y.is_contiguous()
     ldx = kw.pop('ldx', x.shape[-1])
     ldy = kw.pop('ldy', y.shape[-1] if not kw.get('out_nchw') else 0)
@@ -282,7 +301,7 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
         parts = torch.empty(N, P, cout, device=y.device, dtype=torch.float32)
     args = (d, _lib.ptr(x), _lib.ptr(wf), _lib.ptr(bias_g), _lib.ptr(gate), _lib.ptr(res), _lib.ptr(res2),
             _lib.ptr(aff_scale), _lib.ptr(aff_shift), _lib.ptr(y), _lib.ptr(aux), _lib.ptr(parts), _lib.stream())
-    keep = (x, wf, bias_g, gate, res, res2, aff_scale, aff_shift, y, aux, parts, kw.get('row_scale'))
+    keep = (x, wf, bias_g, gate, res, res2, aff_scale, aff_shift, y, aux, parts, kw.get('row_scale'), kw.get('dot'))
     if ktrace.active():
         # algorithmic HBM bytes of the call: x once (pre-upsample size with in_up), the weight image,
         # y as stored (fp32 NCHW for the network tail), every epilogue operand (gate / res / res2 read,
@@ -291,7 +310,7 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
         up = d.in_up if d.in_up > 1 else 1
         nbytes = esz * (M // (up * up) * cin + taps * cin * cout)
         nbytes += (4 * M * cout_real) if d.out_nchw else esz * M * cout
-        nbytes += esz * M * cout * sum(t is not None for t in (gate, res, res2, aux))
+        nbytes += esz * M * cout * sum(t is not None for t in (gate, res, res2, aux, kw.get('dot')))
         if parts is not None:
             nbytes += 4 * parts.numel()
         with ktrace.span(lib.sr_conv3x3_fwd_kernel_name(d).decode(), 2.0 * M * taps * cin * cout_real, nbytes,

@@ -83,6 +83,11 @@ typedef struct sr_conv3x3_desc {
   const float* row_scale; /* optional fp32 [N]: alpha of every output pixel of image n is multiplied by
                              row_scale[n] (per-sample stochastic depth, swinir_arch.py:14-40, fused into
                              the proj / fc2 residual epilogues); NULL = 1 */
+  const void* dot; /* optional, with colsum: the partial sums are of y * dot (bf16 [M][ldd], channel
+                      columns dcoff.. in y's channel order) instead of y -- RCAN's channel-attention
+                      backward dot sum_p dy * u (rcan_arch.py:19-27) fused into the conv dgrad that
+                      produces dy; band kernel only (bf16, 64 -> 64 channels, W 64 / 128) */
+  int ldd, dcoff;
 } sr_conv3x3_desc;
 
 /* A SwinIR block's LayerNorm fused into the following linear (norm1 -> attn.qkv, norm2 -> mlp.fc1:
@@ -107,6 +112,9 @@ int sr_conv3x3_fwd(const sr_conv3x3_desc* d, const void* x, const void* w, const
                    const void* gate, const void* res, const void* res2, const float* aff_scale,
                    const float* aff_shift, void* y, void* aux, float* colsum, void* stream);
 /* Partial rows per image of sr_conv3x3_fwd's colsum for this descriptor (0: not available). */
+/* 1 when a call with this descriptor plus a residual, colsum and the dot operand (sr_conv3x3_desc.dot)
+ * runs on the band kernel's fused epilogue, else 0 (the caller then computes the dot separately). */
+int sr_conv3x3_fwd_dot_ok(const sr_conv3x3_desc* d);
 int sr_conv3x3_fwd_colsum_parts(const sr_conv3x3_desc* d);
 
 /* Name of the GPU kernel that sr_conv3x3_fwd / sr_conv3x3_wgrad would launch for a
@@ -120,6 +128,7 @@ int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d);
 /* Kernel-variant selection for A/B tests: 0 = automatic (default), 1 = never use the
  * 256x256 LDS-DMA kernel (all shapes on the 128-row register-staged kernels). */
 int sr_conv3x3_set_variant(int variant);
+int sr_conv3x3_get_variant(void); /* the current kernel-variant switch */
 /* Diagnostics (not part of the reference interface): per-block clock stamps of the row-band
  * forward kernel into a device buffer of 16 uint64 per block; NULL turns them off. */
 int sr_conv3x3_set_stamps(void* buf);

@@ -795,3 +795,38 @@ def test_two_interval_schedule_bitwise(cuda, shape):
             _lib.check(lib.sr_conv3x3_set_variant(0))
         for name, a, b in zip(('y', 'dx', 'dw', 'db'), ref, got):
             assert torch.equal(a, b), (v, name, (a.float() - b.float()).abs().max().item())
+
+
+@pytest.mark.parametrize('shape', [(2, 64, 64), (3, 20, 128), (1, 5, 64)])
+def test_band_dot_partials(cuda, shape):
+    """Band kernel residual + dot epilogue (RCAB conv1 dgrad with the previous block's channel-attention
+    dot fused, rcan_arch.py:19-27): y equals the plain residual call bitwise, and the partial rows sum
+    per image to sum_p y[n, p, c] * dot[n, p, c] over the stored bf16 y (fp64 reference, fp32 sums)."""
+    N, H, W = shape
+    cin = cout = 64
+    dt = torch.bfloat16
+    torch.manual_seed(21)
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    wf = (torch.randn(cout, 9 * cin, device=cuda) * 0.05).to(dt)
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    dot = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    assert C.dot_partials_ok(dt, N, H, W, cin, cout)
+    y0 = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+    C.conv_fwd_raw(x, wf, None, y0, N, H, W, cin, cout, cout, res=res, beta=1.0)
+    y1 = torch.empty_like(y0)
+    y1, parts = C.conv_fwd_raw(x, wf, None, y1, N, H, W, cin, cout, cout, res=res, beta=1.0, colsum=True, dot=dot)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    ref = (y1.double() * dot.double()).sum((1, 2))
+    got = parts.double().sum(1)
+    scale = (y1.double() * dot.double()).abs().sum((1, 2)).max().item()
+    assert (got - ref).abs().max().item() <= 1e-5 * scale
+    # not on the band kernel (variant 34: the tile kernel) the dot request fails loudly
+    _lib.check(lib.sr_conv3x3_set_variant(34))
+    try:
+        assert not C.dot_partials_ok(dt, N, H, W, cin, cout)
+        with pytest.raises((RuntimeError, ValueError)):  # C status, or no fused sums on that kernel at all
+            C.conv_fwd_raw(x, wf, None, y1, N, H, W, cin, cout, cout, res=res, beta=1.0, colsum=True, dot=dot)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
