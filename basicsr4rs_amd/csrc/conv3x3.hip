@@ -1178,28 +1178,36 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// linear_wk_kernel<E>: 1x1 convs with a wide K (192 < K <= 576) and Cout <= 192 -- the SwinIR fc2
-// forward (360 -> 184) and the fc1 / qkv dgrads (360 / 576 -> 184).  A block owns 128 tokens x all
-// output channels and streams K in 64-wide steps through two LDS stages (LDS-DMA of the token tile
-// [128][128 B] and the weight tile [192][128 B], both K-contiguous, chunk ^ (row & 7) swizzle; 40 KB
-// a stage, so two blocks share a CU).  C = W . X^T as in conv3x3_lin_kernel: the weight rows are
-// permuted on load (32-row group p, tile t, row r -> channel 32p + 8(r/4) + 4t + r%4), so a lane ends
-// with 8 consecutive channels of one token and stores them as one 16-B vector with the fused epilogue.
-// 4 waves (2 channel x 2 token halves), each 96 channels x 64 tokens (6 x 4 accumulator tiles).  (The
-// 64-token lin kernel it replaces re-read the whole weight image per 64 tokens -- 434 MB of L2 reads
-// on the qkv dgrad -- and staged all of K before its first MFMA.)
-// E: conv3x3_lin_kernel's epilogue codes 0 (plain), 16 (residual), 144 (residual + row scale); the
-// bias (GEMM column order), alpha and beta always.
+// linear_wk_kernel<E>: 1x1 convs streamed over K -- the SwinIR fc2 forward (360 -> 184), the fc1 /
+// qkv dgrads (360 / 576 -> 184), and (K <= 192) the fc2 / proj dgrads and proj forward.  A block owns
+// 128 tokens x one 192-wide tile of the output channels (Cout <= 384: the tiles of one token tile are
+// consecutive blocks, so its token rows are read from L2 by the second) and streams K in 64-wide steps
+// through two LDS stages (LDS-DMA of the token tile [128][128 B] and the weight tile [192][128 B], both
+// K-contiguous, chunk ^ (row & 7) swizzle; 40 KB a stage, so two blocks share a CU).  C = W . X^T as in
+// conv3x3_lin_kernel: the weight rows are permuted on load (32-row group p, tile t, row r -> channel
+// 32p + 8(r/4) + 4t + r%4), so a lane ends with 8 consecutive channels of one token and stores them as
+// one 16-B vector with the fused epilogue.  4 waves (2 channel x 2 token halves), each 96 channels x
+// 64 tokens (6 x 4 accumulator tiles).  (The 64-token lin kernel it replaces on wide K re-read the
+// whole weight image per 64 tokens -- 434 MB of L2 reads on the qkv dgrad -- and staged all of K
+// before its first MFMA.)
+// E: conv3x3_lin_kernel's epilogue codes (bits 0-1 act, 2-3 gate 1 / 2 pre-residual, 4 res, 7 row
+// scale) for 0 (plain), 8 (GELU' gate: fc2 dgrad), 16 (residual), 144 (residual + row scale); the bias
+// (GEMM column order), alpha and beta always.
 // ------------------------------------------------------------------------------------
 template <int E>
 __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   constexpr int XI = 128 * 128, WI = 192 * 128, STAGE = XI + WI;
+  constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
   constexpr bool RES = (E & 16) != 0, RSC = (E & 128) != 0;
+  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 128)) == 0, "linear_wk: epilogue subset");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
-  const int m0 = (int)xcd_remap(blockIdx.x, gridDim.x) * 128;
+  const int nct = (a.Cout + 191) / 192;  // output-channel tiles (consecutive blocks)
+  const int bt = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int tt = bt / nct, ct = bt - tt * nct;
+  const int m0 = tt * 128, n0 = ct * 192;
   const int K = a.Cin, nk = (K + 63) >> 6;
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, a.w_bytes);
@@ -1212,7 +1220,7 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   for (int q = 4; q < 10; ++q) {
     const int row = (w + 4 * q - 16) * 8 + rl;
     const int t = (row >> 4) & 1, r = row & 15;
-    wch[q - 4] = (row >> 5) * 32 + 8 * (r >> 2) + 4 * t + (r & 3);
+    wch[q - 4] = n0 + (row >> 5) * 32 + 8 * (r >> 2) + 4 * t + (r & 3);
   }
   auto issue = [&](int ks, int stg) {
     char* st = smem + stg * STAGE;
@@ -1266,22 +1274,30 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
     compute(ks & 1);
   }
 
-  // ---- epilogue: pair P (tiles 2P, 2P + 1) gives channels n = (3 wr + P) * 32 + 8g .. + 7 of token
-  // m0 + 64 wc + 16 j + c16
+  // ---- epilogue: pair P (tiles 2P, 2P + 1) gives channels n = n0 + (3 wr + P) * 32 + 8g .. + 7 of
+  // token m0 + 64 wc + 16 j + c16
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const size_t ybytes = (size_t)a.M * a.ldy * 2;
   const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, ybytes < 0x80000000ull ? (uint32_t)ybytes : 0x7fffffffu);
   const __amdgpu_buffer_rsrc_t br = make_rsrc(a.bias, a.bias ? (uint32_t)a.Cout * 4u : 0u);
   float alpha_blk = a.alpha;
   if constexpr (RSC) alpha_blk = a.alpha * a.row_scale[fdiv((uint32_t)m0, a.fd_hw)];
-  u32x4 rv[3][4];
+  u32x4 rv[3][4], gv[3][4];
   float bv[3][8];
 #pragma unroll
   for (int P = 0; P < 3; ++P) {
-    const int n = (3 * wr + P) * 32 + 8 * g;
+    const int n = n0 + (3 * wr + P) * 32 + 8 * g;
     const u32x4 b0 = buf_load16(br, (uint32_t)n * 4u), b1 = buf_load16(br, (uint32_t)n * 4u + 16u);
 #pragma unroll
     for (int r = 0; r < 4; ++r) { bv[P][r] = __uint_as_float(b0[r]); bv[P][4 + r] = __uint_as_float(b1[r]); }
+    if constexpr (GATE != 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wc * 64 + j * 16 + c16;
+        gv[P][j] = buf_load16(gr, (n < a.Cout && m < a.M) ? (uint32_t)(((size_t)m * a.ldg + a.gcoff + n) * 2) : SR_OOB);
+      }
+    }
     if constexpr (RES) {
       const bool rok = n < a.Cout && n < a.rcols;
 #pragma unroll
@@ -1293,16 +1309,43 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   }
 #pragma unroll
   for (int P = 0; P < 3; ++P) {
-    const int n = (3 * wr + P) * 32 + 8 * g;
+    const int n = n0 + (3 * wr + P) * 32 + 8 * g;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + wc * 64 + j * 16 + c16;
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = (acc[2 * P][j][r] + bv[P][r]) * alpha_blk;
-        v[4 + r] = (acc[2 * P + 1][j][r] + bv[P][4 + r]) * alpha_blk;
+        v[r] = acc[2 * P][j][r] + bv[P][r];
+        v[4 + r] = acc[2 * P + 1][j][r] + bv[P][4 + r];
       }
+      if constexpr (ACT == 1) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : 0.f;
+      } else if constexpr (ACT == 2) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : v[q] * a.slope;
+      } else if constexpr (ACT == 3) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = gelu_exact(v[q]);
+      }
+      if constexpr (GATE != 0) {
+        float gf[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          gf[2 * q] = bf16_to_f32(gv[P][j][q] & 0xffff);
+          gf[2 * q + 1] = bf16_to_f32(gv[P][j][q] >> 16);
+        }
+        if constexpr (GATE == 1) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] *= gf[q] > 0.f ? 1.f : a.gate_slope;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] *= gelu_grad(gf[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= alpha_blk;
       if constexpr (RES) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -4653,16 +4696,19 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
   if (a.Cin <= 192) return a.Cout <= 640;
   return a.Cin <= 576 && a.Cout <= 384 && g_variant != 55;
 }
-// wide-K linears with Cout <= 192 and a plain / residual / residual + row-scale epilogue on
-// linear_wk_kernel; SR_LWK=0 (read once) or variant 64: the 64-token lin kernel (A/B, tests)
+// linear_wk_kernel for the linears with K > SR_LWK_MINK (default 0: all; 192: only the wide-K ones,
+// which the 64-token lin kernel took), K <= 576, 96 < Cout <= 384 and a plain / GELU' gate / residual /
+// residual + row-scale epilogue; SR_LWK=0 (read once) or variant 64: the lin kernel (A/B, tests)
 bool lin_use_wk(const FwdArgs& a) {
-  static const bool off = [] {
+  static const int mink = [] {
     const char* e = getenv("SR_LWK");
-    return e && atoi(e) == 0;
+    if (e && atoi(e) == 0) return 1 << 30;
+    const char* k = getenv("SR_LWK_MINK");
+    return k ? atoi(k) : 0;
   }();
-  if (off || g_variant == 64 || a.Cin <= 192 || a.Cin > 576 || a.Cout > 192) return false;
+  if (g_variant == 64 || a.Cin <= mink || a.Cin > 576 || a.Cout > 384 || a.Cout <= 96) return false;
   const int e = lin_epi(a);
-  return e == 0 || e == 16 || e == 144;
+  return e == 0 || e == 8 || e == 16 || e == 144;
 }
 // HR tail convs: Cout <= 16 with the NCHW fp32 store, W >= 256 (32-px strips), Cin 64 / 128 / 256
 bool fwd_use_tail(const FwdArgs& a, bool bf) {
@@ -4733,9 +4779,10 @@ hipError_t dispatch_fwd(const FwdArgs& a, hipStream_t s) {
 case FK_LIN: {
   FwdArgs b = a;
   const int e = lin_epi(a);
-  if (lin_use_wk(a)) {  // wide K, Cout <= 192: 128-token tiles, K streamed
-    const dim3 grid((a.M + 127) / 128);
+  if (lin_use_wk(a)) {  // 128-token x 192-channel tiles, K streamed
+    const dim3 grid(((a.M + 127) / 128) * ((a.Cout + 191) / 192));
     if (e == 0) hipLaunchKernelGGL(linear_wk_kernel<0>, grid, dim3(256), 0, s, b);
+    else if (e == 8) hipLaunchKernelGGL(linear_wk_kernel<8>, grid, dim3(256), 0, s, b);
     else if (e == 16) hipLaunchKernelGGL(linear_wk_kernel<16>, grid, dim3(256), 0, s, b);
     else hipLaunchKernelGGL(linear_wk_kernel<144>, grid, dim3(256), 0, s, b);
     return hipGetLastError();

@@ -122,11 +122,11 @@ def test_linear_ln_fused_vs_separate(cuda, which, shape):
         assert (aux.float() - aux_r.float()).abs().max().item() <= 2e-2 * max(1.0, aux_r.float().abs().max().item())
 
 
-@pytest.mark.parametrize('K,Cout', [(360, 184), (576, 184), (200, 96), (256, 304), (384, 40)])
+@pytest.mark.parametrize('K,Cout', [(360, 184), (576, 184), (200, 96), (256, 304), (384, 40), (184, 184), (184, 360)])
 @pytest.mark.parametrize('epi', ['plain', 'res', 'res_rowscale', 'gate'])
 def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
     """Wide-K linears (192 < K <= 576: SwinIR fc2 fwd 360 -> 184, fc1 / qkv dgrads 360 / 576 -> 184) --
-    linear_wk_kernel for Cout <= 192, the 64-token lin kernel otherwise (and with variant 64) --
+    linear_wk_kernel for 96 < Cout <= 384, the 64-token lin kernel otherwise (and with variant 64) --
     against float64 on the same bf16 operands, with the epilogues those calls use (residual, residual
     + per-image row scale, GELU' gate) and a ragged last token tile; variant 55 (the 256x256 pp kernel
     for these shapes) agrees within bf16 rounding."""
@@ -158,7 +158,7 @@ def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
 
     lib = _lib.load()
     d = C._desc(dt, N, H, W, K, K, Cout, Cout, Cout, ksize=1)
-    assert lib.sr_conv3x3_fwd_kernel_name(d) == (b'linear_wk_kernel' if Cout <= 192 else b'conv3x3_lin_kernel')
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == (b'linear_wk_kernel' if 96 < Cout <= 384 else b'conv3x3_lin_kernel')
     y = run().double()
     ref = x.double() @ w.to(dt).double().t() + bias.double()
     if gate is not None:

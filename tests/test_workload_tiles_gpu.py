@@ -123,7 +123,7 @@ def test_edsr_l_workload_tile_bf16_fwd_bwd(cuda):
 
 
 def test_swinir_m_workload_tile_bf16(cuda):
-    _run(cuda, SWINIR_M2, 2, 64, ['conv3x3_lin_kernel', 'conv3x3_lin_kernel+ln', 'wattn_fwd_kernel', 'wattn_bwd_kernel',
+    _run(cuda, SWINIR_M2, 2, 64, ['conv3x3_lin_kernel+ln', 'wattn_fwd_kernel', 'wattn_bwd_kernel',
                                   'linear_wgrad_kernel+reduce', 'linear_wk_kernel', 'conv3x3_wgrad_ring_kernel+reduce'],
          out_tol=5e-3, grad_tol=0.15)
 
