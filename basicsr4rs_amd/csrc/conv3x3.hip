@@ -1180,7 +1180,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // ------------------------------------------------------------------------------------
 // linear_wk_kernel<E>: 1x1 convs streamed over K -- the SwinIR fc2 forward (360 -> 184), the fc1 /
 // qkv dgrads (360 / 576 -> 184), and (K <= 192) the fc2 / proj dgrads and proj forward.  A block owns
-// 128 tokens x one 192-wide tile of the output channels (Cout <= 384: the tiles of one token tile are
+// 128 tokens x one 192-wide tile of the output channels (Cout <= 576: the tiles of one token tile are
 // consecutive blocks, so its token rows are read from L2 by the second) and streams K in 64-wide steps
 // through two LDS stages (LDS-DMA of the token tile [128][128 B] and the weight tile [192][128 B], both
 // K-contiguous, chunk ^ (row & 7) swizzle; 40 KB a stage, so two blocks share a CU).  C = W . X^T as in
@@ -1190,16 +1190,17 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // 64 tokens (6 x 4 accumulator tiles).  (The 64-token lin kernel it replaces on wide K re-read the
 // whole weight image per 64 tokens -- 434 MB of L2 reads on the qkv dgrad -- and staged all of K
 // before its first MFMA.)
-// E: conv3x3_lin_kernel's epilogue codes (bits 0-1 act, 2-3 gate 1 / 2 pre-residual, 4 res, 7 row
-// scale) for 0 (plain), 8 (GELU' gate: fc2 dgrad), 16 (residual), 144 (residual + row scale); the bias
+// E: conv3x3_lin_kernel's epilogue codes (bits 0-1 act, 2-3 gate 1 / 2 pre-residual, 4 res, 6 aux, 7
+// row scale) for 0 (plain), 8 (GELU' gate: fc2 dgrad), 16 (residual), 67 (GELU + pre-activation aux:
+// fc1 forward), 144 (residual + row scale); the bias
 // (GEMM column order), alpha and beta always.
 // ------------------------------------------------------------------------------------
 template <int E>
 __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   constexpr int XI = 128 * 128, WI = 192 * 128, STAGE = XI + WI;
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
-  constexpr bool RES = (E & 16) != 0, RSC = (E & 128) != 0;
-  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 128)) == 0, "linear_wk: epilogue subset");
+  constexpr bool RES = (E & 16) != 0, AUX = (E & 64) != 0, RSC = (E & 128) != 0;
+  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 64 | 128)) == 0, "linear_wk: epilogue subset");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1280,6 +1281,7 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const size_t ybytes = (size_t)a.M * a.ldy * 2;
   const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, ybytes < 0x80000000ull ? (uint32_t)ybytes : 0x7fffffffu);
+  const __amdgpu_buffer_rsrc_t ar = make_rsrc(a.aux, AUX ? (ybytes < 0x80000000ull ? (uint32_t)ybytes : 0x7fffffffu) : 0u);
   const __amdgpu_buffer_rsrc_t br = make_rsrc(a.bias, a.bias ? (uint32_t)a.Cout * 4u : 0u);
   float alpha_blk = a.alpha;
   if constexpr (RSC) alpha_blk = a.alpha * a.row_scale[fdiv((uint32_t)m0, a.fd_hw)];
@@ -1318,6 +1320,12 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
       for (int r = 0; r < 4; ++r) {
         v[r] = acc[2 * P][j][r] + bv[P][r];
         v[4 + r] = acc[2 * P + 1][j][r] + bv[P][4 + r];
+      }
+      if constexpr (AUX) {  // the pre-activation value (GELU backward)
+        u32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
+        __builtin_amdgcn_raw_buffer_store_b128(o, ar, (n < a.Cout && m < a.M) ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB, 0, 0);
       }
       if constexpr (ACT == 1) {
 #pragma unroll
@@ -4697,8 +4705,8 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
   return a.Cin <= 576 && a.Cout <= 384 && g_variant != 55;
 }
 // linear_wk_kernel for the linears with K > SR_LWK_MINK (default 0: all; 192: only the wide-K ones,
-// which the 64-token lin kernel took), K <= 576, 96 < Cout <= 384 and a plain / GELU' gate / residual /
-// residual + row-scale epilogue; SR_LWK=0 (read once) or variant 64: the lin kernel (A/B, tests)
+// which the 64-token lin kernel took), K <= 576, 96 < Cout <= 576 and a plain / GELU' gate / GELU +
+// pre-activation / residual / residual + row-scale epilogue; SR_LWK=0 (read once) or variant 64: the lin kernel (A/B, tests)
 bool lin_use_wk(const FwdArgs& a) {
   static const int mink = [] {
     const char* e = getenv("SR_LWK");
@@ -4706,9 +4714,9 @@ bool lin_use_wk(const FwdArgs& a) {
     const char* k = getenv("SR_LWK_MINK");
     return k ? atoi(k) : 0;
   }();
-  if (g_variant == 64 || a.Cin <= mink || a.Cin > 576 || a.Cout > 384 || a.Cout <= 96) return false;
+  if (g_variant == 64 || a.Cin <= mink || a.Cin > 576 || a.Cout > 576 || a.Cout <= 96) return false;
   const int e = lin_epi(a);
-  return e == 0 || e == 8 || e == 16 || e == 144;
+  return e == 0 || e == 8 || e == 16 || e == 67 || e == 144;
 }
 // HR tail convs: Cout <= 16 with the NCHW fp32 store, W >= 256 (32-px strips), Cin 64 / 128 / 256
 bool fwd_use_tail(const FwdArgs& a, bool bf) {
@@ -4783,6 +4791,7 @@ case FK_LIN: {
     const dim3 grid(((a.M + 127) / 128) * ((a.Cout + 191) / 192));
     if (e == 0) hipLaunchKernelGGL(linear_wk_kernel<0>, grid, dim3(256), 0, s, b);
     else if (e == 8) hipLaunchKernelGGL(linear_wk_kernel<8>, grid, dim3(256), 0, s, b);
+    else if (e == 67) hipLaunchKernelGGL(linear_wk_kernel<67>, grid, dim3(256), 0, s, b);
     else if (e == 16) hipLaunchKernelGGL(linear_wk_kernel<16>, grid, dim3(256), 0, s, b);
     else hipLaunchKernelGGL(linear_wk_kernel<144>, grid, dim3(256), 0, s, b);
     return hipGetLastError();
