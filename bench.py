@@ -76,10 +76,10 @@ GRAPH_DEFAULT = {'swinir': False}
 def make_opt(world, batch, workload='edsr', graph=False):
     net, mtype, lr = WORKLOADS[workload][:3]
     aw = ASYNC_WGRAD.get(workload, False)
-    # side-stream weight gradients: the eager DDP step would issue its bucket all-reduces from the
-    # side stream (kept to one process until a multi-GPU RCCL run of that ordering exists, ADVICE
-    # r2); the graph step issues them from the main stream between replayed segments
-    aw = bool(aw) and (graph if aw == 'graph' else (world == 1 or graph))
+    # side-stream weight gradients only in one process: the two-rank gloo rehearsal of the segmented
+    # DDP graph step with them ran RCAN at 11.4 s / step against 182 ms without (tools/gloo2_rcan.sh,
+    # round 3), and no multi-GPU RCCL run of that ordering exists yet
+    aw = bool(aw) and world == 1 and (graph if aw == 'graph' else True)
     return dict(
         model_type=mtype, is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
         network_g=dict(net),
