@@ -151,7 +151,8 @@ def linear_ln_fwd(x, weight, bias, Creal, wf, bg, spec, N, H, W, act=0, aux=None
     Cp = x.shape[-1]
     if x.dtype != torch.bfloat16 or Cp != spec.cin_p or spec.cin_p > 192 or spec.cout_p > 640:
         return None
-    if os.environ.get('SR_LN_UNFUSED') == '1':  # A/B: the standalone LayerNorm kernel + linear
+    unf = os.environ.get('SR_LN_UNFUSED')  # A/B: the standalone LayerNorm kernel + linear ('1': both
+    if unf == '1' or (unf == 'fc1' and aux is not None) or (unf == 'qkv' and aux is None):  # or one of them)
         return None
     M = N * H * W
     ln = torch.empty_like(x)
