@@ -88,3 +88,70 @@ def test_struct_layouts_match_header():
         assert [f[0] for f in cls._fields_] == [n for n, _ in fields]
         assert [f[1] is ctypes.c_void_p for f in cls._fields_] == [p for _, p in fields]
         assert ctypes.sizeof(cls) == size
+
+
+def test_round3_kernel_selection():
+    """Host-side choice of the round-3 kernels (no GPU launch): the 1x1 weight gradient and the streamed
+    linear on the SwinIR-M shapes, the row-streaming wgrad over output tiles for 184-channel convs, the
+    variant switches that turn each off, and the band kernel's dot-partials query."""
+    from basicsr4rs_amd.ops import conv as C
+    lib = _lib.load()
+    bf = torch.bfloat16
+
+    def wname(cin, cout, ks, N=32, H=64, W=64):
+        d = _lib.WgradDesc()
+        d.dtype, d.N, d.H, d.W = _lib.dtype_code(bf), N, H, W
+        d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.ksize = cin, cin, cin, cout, cout, cout, ks
+        return lib.sr_conv3x3_wgrad_kernel_name(d)
+
+    def fname(cin, cout, ks=1):
+        return lib.sr_conv3x3_fwd_kernel_name(C._desc(bf, 32, 64, 64, cin, cin, cout, cout, cout, ksize=ks))
+
+    try:
+        for cin, cout in ((184, 576), (192, 184), (184, 360), (360, 184)):  # qkv / proj / fc1 / fc2
+            assert wname(cin, cout, 1) == b'linear_wgrad_kernel'
+        assert wname(184, 184, 3) == b'conv3x3_wgrad_ring_kernel'   # SwinIR RSTB conv
+        assert wname(8, 256, 3) == b'conv3x3_wgrad_ring_kernel'     # EDSR conv_first
+        assert wname(256, 256, 3) == b'conv3x3_wgrad_pp_kernel'     # EDSR-L body stays on pp
+        for cin, cout in ((576, 184), (360, 184), (184, 360), (184, 184), (192, 184)):
+            assert fname(cin, cout) == b'linear_wk_kernel'
+        assert fname(184, 576) == b'linear_wk_kernel'                 # qkv unfused (SR_LN_UNFUSED): 3 tiles
+        assert fname(184, 640) == b'conv3x3_lin_kernel'               # Cout > 576: lin
+        assert fname(384, 40) == b'conv3x3_lin_kernel'                # Cout <= 96: lin
+        _lib.check(lib.sr_conv3x3_set_variant(63))
+        assert wname(184, 576, 1) == b'conv3x3_wgrad_pp_kernel'
+        _lib.check(lib.sr_conv3x3_set_variant(64))
+        assert fname(576, 184) == b'conv3x3_lin_kernel'
+        _lib.check(lib.sr_conv3x3_set_variant(62))
+        assert lib.sr_conv3x3_get_variant() == 62
+        assert wname(256, 256, 3) == b'conv3x3_wgrad_ring_kernel'
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+        # dot partials: the band kernel's residual + colsum + dot epilogue on the RCAB conv shape only
+        assert C.dot_partials_ok(bf, 32, 64, 64, 64, 64)
+        assert not C.dot_partials_ok(bf, 32, 64, 64, 64, 32)
+        assert not C.dot_partials_ok(torch.float32, 32, 64, 64, 64, 64)
+        _lib.check(lib.sr_conv3x3_set_variant(34))
+        assert not C.dot_partials_ok(bf, 32, 64, 64, 64, 64)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+
+
+def test_dot_parts_handoff_and_async_hold():
+    """The RCAB dot-partials hand-off takes the partials only for the same u and an unmodified dy, once;
+    the side-stream dy references are dropped when the outermost async_wgrad context exits."""
+    from basicsr4rs_amd.ops import blocks as B
+    from basicsr4rs_amd.ops import conv as C
+    u, dy, parts = torch.zeros(2, 3), torch.zeros(2, 3), torch.ones(1)
+    B._dot_parts_put(dy, parts, u)
+    assert B._dot_parts_take(dy, torch.zeros(2, 3)) is None  # another u
+    B._dot_parts_put(dy, parts, u)
+    dy.add_(1.0)  # an in-place accumulation after the hand-off
+    assert B._dot_parts_take(dy, u) is None
+    B._dot_parts_put(dy, parts, u)
+    assert B._dot_parts_take(dy, u) is parts
+    assert B._dot_parts_take(dy, u) is None  # consumed
+    with C.async_wgrad(True):
+        with C.async_wgrad(True):
+            C._ASYNC['hold'].append(dy)
+        assert C._ASYNC['hold'] == [dy]  # inner exit: still inside the outer backward
+    assert C._ASYNC['hold'] == []
