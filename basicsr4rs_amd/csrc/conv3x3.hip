@@ -5057,7 +5057,7 @@ bool ring_early() {
     const char* e = getenv("SR_RING_EARLY");
     return e && atoi(e) == 1;
   }();
-  return v;
+  return v || g_variant == 65;  // variant 65: on (parity tests)
 }
 // Fragment-read lookahead of the ring wgrad (D = 2): 3, or SR_RING_LA=5 (A/B; read once)
 int ring_la() {
@@ -5359,7 +5359,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 64)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 65)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;

@@ -355,12 +355,13 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
                                    (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
-def test_wgrad_halo_vs_fp64(cuda, shape):
+@pytest.mark.parametrize('variant', [0, 65])
+def test_wgrad_halo_vs_fp64(cuda, shape, variant):
     """All-taps halo wgrad (Cout <= 64, W % 64 == 0), row-streaming form: channel slices of
     wider buffers (ldx, xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather
     (in_up = 2), splits that cross image boundaries (rows per split not dividing H), several
     64-px column segments per row, ragged last split, against an fp64 CPU reference on the same
-    bf16 operands."""
+    bf16 operands; variant 65: the opt-in early-issue schedule (one barrier per step, W 64 only)."""
     N, H, W, cin, cout, up = shape
     torch.manual_seed(9)
     dt = torch.bfloat16
@@ -381,9 +382,13 @@ def test_wgrad_halo_vs_fp64(cuda, shape):
     d.Cout = d.Cout_real = cout
     d.ldx, d.xcoff, d.ldy, d.ycoff = cin + 24, 8, cout + 16, 16
     assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_ring_kernel'
-    dw, db = C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
-                              xcoff=8, ldy=cout + 16, ycoff=16, in_up=up)
-    torch.cuda.synchronize()
+    _lib.check(lib.sr_conv3x3_set_variant(variant))
+    try:
+        dw, db = C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
+                                  xcoff=8, ldy=cout + 16, ycoff=16, in_up=up)
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
     tol = 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (dw.cpu().double() - w.grad).abs().max().item() <= tol
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
