@@ -3903,6 +3903,9 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   const int chunk = rem_ - cot * a.tiles_ci;
   const int ci0 = chunk * 64;
   const int co0 = cot * (CO_T * 16);
+  // out_ps: the co tile lies in one shuffle slot (C' a multiple of the tile width, checked on the host)
+  const int ps_sl = a.out_ps > 0 ? (int)fdiv((uint32_t)co0, a.fd_cps) : 0;
+  const int ps_si = a.out_ps > 0 ? ps_sl / a.out_ps : 0, ps_sj = a.out_ps > 0 ? ps_sl - ps_si * a.out_ps : 0;
   const int rows_total = a.N * a.H;
   const int rps = a.kper / a.W;  // image rows per split
   const int r0 = split * rps, r1 = min(rows_total, r0 + rps);
@@ -3978,7 +3981,15 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
         const int pr = hrow((k & 1) * 32 + (lane >> 1));
         const int co = co0 + (k >> 1) * 16 + (lane & 1) * 8;
         dst = st + k * 1024;
-        if (co < a.Cout) off = (uint32_t)(((p0s + pr) * a.ldy + a.ycoff + co) * 2);
+        if (co < a.Cout) {
+          if (a.out_ps == 0) {
+            off = (uint32_t)(((p0s + pr) * a.ldy + a.ycoff + co) * 2);
+          } else {  // pixel-shuffled dy: GEMM column sl * C' + c of LR pixel (q, x) = HR pixel (q r + si, x r + sj), channel c
+            const int r = a.out_ps;
+            const int hp = (q * r + ps_si) * (a.W * r) + (seg * 64 + pr) * r + ps_sj;
+            off = (uint32_t)((hp * a.ldy + a.ycoff + co - ps_sl * a.fd_cps.d) * 2);
+          }
+        }
       }
       glds16(dyr, dst, off);
     }
@@ -4383,14 +4394,17 @@ __global__ __launch_bounds__(1024) void wgrad_reduce4_kernel(const float* ws, co
 __global__ __launch_bounds__(1024) void wgrad_reduce_tr_kernel(const float* ws, const float* wsb, float* dw, float* db,
                                                                int S, int Cout, int Cin, int Cout_real, int Cin_real,
                                                                int taps, const int* co_map, const int* ci_map,
-                                                               float scale, int wblocks, int accumulate) {
+                                                               float scale, int wblocks, int accumulate, int out_ps) {
   __shared__ f32x4 red[16][64];
   const int t = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r2 = out_ps > 0 ? out_ps * out_ps : 1, cps = Cout_real / r2;
+  // GEMM column of parameter output channel c (co_map, or the PixelShuffle order: slot c % r^2)
+  auto gcol = [&](int c) { return co_map ? co_map[c] : (out_ps > 0 ? (c % r2) * cps + c / r2 : c); };
   if ((int)blockIdx.x >= wblocks) {  // bias
     const int c = ((int)blockIdx.x - wblocks) * 64 + t;
     float sb = 0.f;
     if (c < Cout_real) {
-      const int cop = co_map ? co_map[c] : c;
+      const int cop = gcol(c);
       for (int k = wv; k < S; k += 16) sb += wsb[(size_t)k * Cout + cop];
     }
     red[wv][t] = f32x4{sb, 0.f, 0.f, 0.f};
@@ -4416,10 +4430,10 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_tr_kernel(const float* ws, 
     const int cip = ci_map ? ci_map[ci] : ci;
     const size_t stride = (size_t)taps * Cin * Cout;
     const float* row = ws + ((size_t)tap * Cin + cip) * Cout;
-    if (co_map) {  // GEMM columns of the 4 parameter channels: gathered loads
+    if (co_map || out_ps > 0) {  // GEMM columns of the 4 parameter channels: gathered loads
       int cop[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) cop[e] = co4 * 4 + e < Cout_real ? co_map[co4 * 4 + e] : 0;
+      for (int e = 0; e < 4; ++e) cop[e] = co4 * 4 + e < Cout_real ? gcol(co4 * 4 + e) : 0;
       for (int k = wv; k < S; k += 16) {
         const float* sk = row + (size_t)k * stride;
         acc += f32x4{sk[cop[0]], sk[cop[1]], sk[cop[2]], sk[cop[3]]};
@@ -4998,8 +5012,14 @@ int ring_wide_target() {
 }
 bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d) {
   if (ring_wide_target() <= 0 || !wg_use_ring() || g_variant == 1 || d->dtype != SR_BF16 || d->ksize == 1 ||
-      d->Cout <= 64 || d->W % 64 || d->in_up > 2 || d->out_ps != 0)
+      d->Cout <= 64 || d->W % 64 || d->in_up > 2)
     return false;
+  static const bool ps_off = [] {
+    const char* e = getenv("SR_RING_PS");
+    return e && atoi(e) == 0;
+  }();
+  if (d->out_ps > 0 && (d->in_up > 1 || (d->Cout / (d->out_ps * d->out_ps)) % 64 != 0 || g_variant == 67 || ps_off))
+    return false;  // pixel-shuffled dy: each 64-wide co tile inside one shuffle slot; variant 67 / SR_RING_PS=0: off (A/B)
   if (g_variant == 62 || ring_wide_env() > 0) return true;
   return d->Cout % 128 != 0 || d->Cin % 128 != 0;
 }
@@ -5359,7 +5379,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 65)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 67)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -5420,7 +5440,7 @@ int wgrad_reduce_launch(const sr_conv3x3_wgrad_desc* d, int S, int taps, const f
     const int bblocks = db ? (Cout_real + 63) / 64 : 0;
     hipLaunchKernelGGL(wgrad_reduce_tr_kernel, dim3((unsigned)(wblocks + bblocks)), dim3(1024), 0, s,
                        (const float*)ws, (const float*)wsb, dw, db, S, d->Cout, d->Cin, Cout_real, Cin_real, taps,
-                       co_map, ci_map, d->scale, wblocks, acc1);
+                       co_map, ci_map, d->scale, wblocks, acc1, d->out_ps);
   } else if (Cin_real % 4 == 0) {
     const int64_t work4 = (int64_t)taps * Cout_real * (Cin_real / 4);
     const int wblocks = (int)((work4 + 63) / 64);

@@ -319,37 +319,47 @@ def test_linear_wgrad_vs_fp64(cuda, shape):
 
 @pytest.mark.parametrize('shape', [(2, 6, 64, 256, 256), (1, 4, 128, 128, 192), (32, 8, 64, 256, 256),
                                    (3, 3, 64, 8, 256), (1, 5, 64, 96, 128), (2, 64, 64, 256, 256),
-                                   (2, 5, 64, 184, 184), (1, 3, 128, 184, 72)])
+                                   (2, 5, 64, 184, 184), (1, 3, 128, 184, 72), (2, 6, 64, 64, 256, 2),
+                                   (1, 4, 128, 64, 256, 2), (3, 2, 64, 32, 256, 2), (1, 3, 64, 64, 576, 3)])
 def test_wgrad_ring_wide_vs_fp64(cuda, shape):
     """Row-streaming wgrad over 64-channel output tiles (Cout above 64, the last tile partial: the
     EDSR-L body shape, SwinIR's 184-channel convs; variant 62 forces it) against fp64 on the same bf16 operands and against the default
-    kernel; image top / bottom rows, multi-image splits, Cin below one 64-channel chunk."""
-    N, H, W, cin, cout = shape
+    kernel; image top / bottom rows, multi-image splits, Cin below one 64-channel chunk, and (round 3)
+    pixel-shuffled dy (the RCAN / SwinIR upsample convs 64 -> 256, r 2: each co tile inside one slot)."""
+    N, H, W, cin, cout = shape[:5]
+    ps = shape[5] if len(shape) > 5 else 0
     torch.manual_seed(13)
     dt = torch.bfloat16
     lib = _lib.load()
     x = torch.randn(N, H, W, cin).to(dt)
-    dy = torch.randn(N, H, W, cout).to(dt)
+    if ps:
+        dy = torch.randn(N, H * ps, W * ps, cout // (ps * ps)).to(dt)
+        dy_gemm = O.pixel_unshuffle(dy.permute(0, 3, 1, 2).double(), ps)
+    else:
+        dy = torch.randn(N, H, W, cout).to(dt)
+        dy_gemm = dy.permute(0, 3, 1, 2).double()
     d = _lib.WgradDesc()
     d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
-    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, cout, 0, 3
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, dy.shape[-1], ps, 3
     outs = []
     try:
         _lib.check(lib.sr_conv3x3_set_variant(62))
         assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_ring_kernel'
-        for variant in (62, 0):
+        for variant in (62, 0, 67):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
-            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0))
+            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
     w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
     b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
-    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy_gemm).sum().backward()
     torch.cuda.synchronize()
     dw, db = outs[0]
     assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
-    assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+    for other in outs[1:]:  # the automatic choice, and variant 67 (no shuffled-dy ring)
+        assert (dw - other[0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+        assert (db - other[1]).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
 
 
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
