@@ -1784,10 +1784,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   const int lc = (lane & 7) ^ (lane >> 3);  // logical 16-B chunk of this lane's DMA slot
   const int nch = (a.Cin + 63) >> 6;
   const int ninstr = (HR + 7) >> 3;
+  const int rps = a.in_ps > 0 ? a.in_ps : 1;
   for (int ch = 0; ch < nch; ++ch) {
     const int ci0 = ch * 64;
     if (ch) __syncthreads();  // every wave is done with the previous chunk's halo
     const bool cv = ci0 + lc * 8 < a.Cin;
+    // in_ps = r (pixel-shuffled input: the upsample convs' dgrads): LR channel sl * C' + c of LR pixel
+    // (y, x) is channel c of HR pixel (y r + si, x r + sj); a 64-channel chunk lies in one slot
+    int si = 0, sj = 0, cch0 = ci0;
+    if (a.in_ps > 0) {
+      const int sl = (int)fdiv((uint32_t)ci0, a.fd_cps);
+      si = sl / rps;
+      sj = sl - si * rps;
+      cch0 = ci0 - sl * a.fd_cps.d;
+    }
     // the chunk's upper 32 channels exist (not for Cin 32: RRDB dense dgrads).  A runtime flag
     // even for Cin 64: measured 2-3 % faster on RCAN / RRDB than the constant-folded form
     const bool khi = ci0 + 32 < a.Cin;
@@ -1796,7 +1806,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
       const int hy = hr / WPAD, hx = hr - hy * WPAD;
       const int yy = y0 - 1 + hy, xx = hx - 1;
       const bool v = cv && hr < HR && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-      const uint32_t off = (uint32_t)((((n * H + yy) * W + xx) * a.ldx + a.xcoff + ci0 + lc * 8) * 2);
+      const int pix = a.in_ps > 0 ? ((n * H + yy) * rps + si) * (W * rps) + xx * rps + sj : (n * H + yy) * W + xx;
+      const uint32_t off = (uint32_t)((pix * a.ldx + a.xcoff + cch0 + lc * 8) * 2);
       if (DBG != 2) glds16(xr, smem + k * 1024, v ? off : SR_OOB);
     }
     // this wave's weights, one kernel row (3 taps x 2 K halves x CW co tiles) at a time, the
@@ -4627,7 +4638,14 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
 // Narrow-conv halo kernel: bf16 3x3, W 64 or 128, whole-row 256-pixel tiles; Cout <= 64 in one
 // block column, Cout 65..255 (RRDB dense-block dgrads) in 64-channel block columns.
 bool fwd_use_halo(const FwdArgs& a, bool bf) {
-  if (!bf || a.in_up != 1 || a.in_ps != 0 || a.tap0 != 0 || g_variant == 1) return false;
+  static const bool ps_off = [] {
+    const char* e = getenv("SR_HALO_PS");
+    return e && atoi(e) == 0;
+  }();
+  // pixel-shuffled input (the upsample convs' dgrads into 64 channels) when each 64-channel chunk lies
+  // in one shuffle slot; SR_HALO_PS=0 / variant 68: the tile kernel for those (A/B)
+  const bool ps_ok = a.in_ps > 0 && a.fd_cps.d % 64 == 0 && a.W != 256 && !ps_off && g_variant != 68;
+  if (!bf || a.in_up != 1 || (a.in_ps != 0 && !ps_ok) || a.tap0 != 0 || g_variant == 1) return false;
   if (a.W == 256)  // HR-resolution tail convs (conv_last, Cout <= 16, NCHW store): one row per tile
     return a.Cout <= 16 && g_variant != 29;
   return !a.out_nchw && a.Cout < 256 && (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
@@ -5379,7 +5397,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 67)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 68)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;

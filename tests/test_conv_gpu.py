@@ -774,6 +774,43 @@ def test_fwd_pph_pixel_shuffled_input(cuda, shape):
     assert (outs[0].float() - outs[1].float()).abs().max().item() <= tol
 
 
+@pytest.mark.parametrize('shape', [(2, 4, 64, 256, 64, 2), (1, 6, 128, 256, 64, 2), (2, 4, 64, 576, 64, 3),
+                                   (1, 2, 128, 256, 32, 2)])
+def test_fwd_halo_pixel_shuffled_input(cuda, shape):
+    """The narrow halo kernel reading a pixel-shuffled input (the RCAN / SwinIR upsample convs' dgrads
+    into 64 channels: a 64-channel chunk is one shuffle slot, its halo pixels r HR pixels apart): against
+    fp64 on the same bf16 operands and against the tile kernel (variant 68)."""
+    N, H, W, cin, cout, r = shape
+    torch.manual_seed(22)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    cp = cin // (r * r)
+    xh = torch.randn(N, H * r, W * r, cp, device=cuda).to(dt)
+    wt = torch.randn(cout, cin, 3, 3, device=cuda) * 0.03
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    spec = C.ConvSpec(cin, cout)
+    wf, _, bg = C.prepared(torch.nn.Parameter(wt), None, spec, dt)
+    d = C._desc(dt, N, H, W, cin, cp, cout, cout, cout, in_ps=r)
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_halo_kernel'
+    outs = []
+    try:
+        for variant in (0, 68):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+            C.conv_fwd_raw(xh, wf, None, y, N, H, W, cin, cout, cout, in_ps=r, ldx=cp, res=res, beta=1.0)
+            outs.append(y)
+        assert lib.sr_conv3x3_fwd_kernel_name(d) != b'conv3x3_fwd_halo_kernel'
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    xl = xh.view(N, H, r, W, r, cp).permute(0, 2, 4, 5, 1, 3).reshape(N, r * r * cp, H, W)
+    ref = F.conv2d(xl.double().cpu(), bf(wt.cpu()).double(), padding=1) + res.permute(0, 3, 1, 2).double().cpu()
+    got = outs[0].permute(0, 3, 1, 2).double().cpu()
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    assert (got - ref).abs().max().item() <= tol
+    assert (outs[0].float() - outs[1].float()).abs().max().item() <= tol
+
+
 @pytest.mark.parametrize('shape', [(2, 256, 256, 64, 0), (1, 256, 1024, 64, 2), (1, 256, 1024, 128, 2),
                                    (2, 128, 128, 128, 0)])
 def test_two_interval_schedule_bitwise(cuda, shape):
