@@ -112,6 +112,8 @@ SIGNATURES = {
     'sr_add_pos_embed': (_i, [_i, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
     'sr_pos_embed_grad': (_i, [_i, _vp, _i, _i, _i, _i, _vp, _i, _vp]),
     'sr_dcn_im2col': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp]),
+    'sr_dcn_fwd_fused_ok': (_i, [ctypes.POINTER(DcnDesc), _i]),
+    'sr_dcn_fwd_fused': (_i, [ctypes.POINTER(DcnDesc), _vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     'sr_dcn_col2im_workspace': (_sz, [ctypes.POINTER(DcnDesc)]),
     'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     'sr_deform_conv_workspace': (_sz, [_i] * 16),

@@ -16,11 +16,15 @@
 //                   channels in registers, no atomics) and dcn_grad_x_kernel (col2im:
 //                   bilinear scatter accumulated in an LDS image of the output tile's input
 //                   footprint, flushed with channel-contiguous atomics).
+//   sr_dcn_fwd_fused : (bf16, C = 64, Cout <= 64) the sampling and the GEMM in one kernel,
+//                   the column tile built in LDS per tap (dcn_fwd_mfma_kernel).
 // Offsets and masks are staged through LDS per pixel tile so their NCHW reads and writes
 // stay coalesced while the item loop runs deformable-group-fastest (adjacent lanes touch
 // adjacent channel vectors of the same pixel).
 #include "sr_common.h"
 #include "sr_internal.h"
+
+#include <cstdlib>
 
 namespace {
 
@@ -324,6 +328,148 @@ __global__ void __launch_bounds__(256) dcn_grad_x_kernel(DcnArgs a, XGeom xg, co
   }
 }
 
+// Fused deformable forward (bf16, one conv group, C = cgp = Cp = 64, Cout <= 64): the column
+// matrix never reaches HBM.  A block owns DF_TP consecutive output pixels of one image and
+// every output channel; per tap it gathers the DF_TP x 64 modulated samples (the im2col item
+// math above, same expression, so the rows equal sr_dcn_im2col's) straight into an LDS tile
+// and multiplies it by the tap's 64 x 64 weight slice on v_mfma_f32_16x16x32_bf16 (B fragments
+// from L2 into registers, issued before the gather so they land under it).  Thread t keeps one
+// pixel (t % DF_TP) for all taps and 4 of its 8 channel vectors, so the offset / mask reads of a
+// wave are 64 consecutive floats of one NCHW plane.  x is read either as NHWC (pixel stride
+// 128 B, vector stride 16 B) or, faster, channel-vector-blocked [N][8][H][W][8] (pixel stride
+// 16 B, vector stride H*W*16 B): then the corners a wave gathers for one vector of 64
+// neighbouring pixels share cache lines (NHWC puts every lane on its own 128-B line: the kernel
+// was L1-line bound, 504 us against the unfused im2col's 318 us on the C5 shape).  LDS rows are padded to 144 B: the 16 rows
+// one A-fragment read touches start on 16 distinct 4-bank groups.  Epilogue: bias, bf16
+// rounding (the unfused path stores its GEMM output as bf16), fp32 NCHW store of 4 consecutive
+// pixels per lane.  cols (optional) receives the column rows for the backward's weight
+// gradient.  Replaces im2col + 1x1 GEMM + NHWC->NCHW of the unfused path; the reference's
+// per-image modulated_deformable_im2col_cuda + addmm (deform_conv_cuda.cpp:560-590).
+constexpr int DF_TP = 128, DF_RS = 72;  // pixels per block; LDS row stride in bf16 (144 B)
+
+SR_DEV void mfma_bf16(const u32x4& a, const u32x4& b, f32x4& acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s16x8, a), __builtin_bit_cast(s16x8, b), acc, 0,
+                                                0, 0);
+}
+
+__global__ void __launch_bounds__(256) dcn_fwd_mfma_kernel(DcnArgs a, const bf16_t* __restrict__ x,
+                                                           const float* __restrict__ off,
+                                                           const float* __restrict__ msk,
+                                                           const bf16_t* __restrict__ wf, int ldw, int wrows,
+                                                           int cout, const float* __restrict__ bias,
+                                                           float* __restrict__ y, bf16_t* __restrict__ cols,
+                                                           uint32_t pxb, uint32_t vb) {
+  __shared__ __attribute__((aligned(16))) bf16_t sA[DF_TP * DF_RS];
+  const int HWo = a.Ho * a.Wo;
+  const int tiles = (HWo + DF_TP - 1) / DF_TP;
+  const int n = blockIdx.x / tiles, p0 = (blockIdx.x - n * tiles) * DF_TP;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int px = tid & (DF_TP - 1), v0 = tid >> 7;  // pixel; first channel vector (then +2, +4, +6)
+  const int p = p0 + px;
+  const bool pv = p < HWo;
+  const int ho = pv ? p / a.Wo : 0, wo = pv ? p - ho * a.Wo : 0;
+  const float hb = (float)(ho * a.sh - a.ph), wb = (float)(wo * a.sw - a.pw);
+  const int64_t HWo64 = HWo;
+  const auto xr = make_rsrc(x + (int64_t)n * a.H * a.W * a.Cp, (uint32_t)((size_t)a.H * a.W * a.Cp * 2));
+  const auto wr = make_rsrc(wf, (uint32_t)((size_t)wrows * ldw * 2));
+  const float* offn = off + (int64_t)n * a.DG * 2 * a.K * HWo64 + p;
+  const float* mskn = msk ? msk + (int64_t)n * a.DG * a.K * HWo64 + p : nullptr;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < a.K; ++k) {
+    // this tap's B fragments: B[k = ci][col = co] = wf[co][k*64 + ci]
+    u32x4 bq[4][2];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bq[cb][kk] = buf_load16(wr, (uint32_t)(((16 * cb + (lane & 15)) * ldw + k * 64 + 32 * kk + 8 * (lane >> 4)) * 2));
+    const int ti = k / a.kw, tj = k - ti * a.kw;
+    const float hk = hb + (float)(ti * a.dh), wk = wb + (float)(tj * a.dw);
+    float wt[4][4], mm[4];
+    uint32_t co[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int v = v0 + 2 * j, dgi = v * 8 / a.cpg;
+      float oh = 0.f, ow = 0.f, m = 0.f;
+      if (pv) {
+        oh = offn[(int64_t)(dgi * 2 * a.K + 2 * k) * HWo64];
+        ow = offn[(int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64];
+        m = mskn ? mskn[(int64_t)(dgi * a.K + k) * HWo64] : 1.f;
+      }
+      const Sample s = make_sample(hk + oh, wk + ow, a.H, a.W);
+      const bool ok = pv && s.valid;
+      wt[j][0] = s.hh * s.hw; wt[j][1] = s.hh * s.lw; wt[j][2] = s.lh * s.hw; wt[j][3] = s.lh * s.lw;
+      mm[j] = m;
+      const uint32_t cb16 = (uint32_t)v * vb;
+      co[j][0] = ok && s.o1 >= 0 ? (uint32_t)s.o1 * pxb + cb16 : SR_OOB;
+      co[j][1] = ok && s.o2 >= 0 ? (uint32_t)s.o2 * pxb + cb16 : SR_OOB;
+      co[j][2] = ok && s.o3 >= 0 ? (uint32_t)s.o3 * pxb + cb16 : SR_OOB;
+      co[j][3] = ok && s.o4 >= 0 ? (uint32_t)s.o4 * pxb + cb16 : SR_OOB;
+    }
+    u32x4 cv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cv[j][q] = buf_load16(xr, co[j][q]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v1[8], v2[8], v3[8], v4[8], r[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v1[2 * e] = __uint_as_float(cv[j][0][e] << 16); v1[2 * e + 1] = __uint_as_float(cv[j][0][e] & 0xffff0000u);
+        v2[2 * e] = __uint_as_float(cv[j][1][e] << 16); v2[2 * e + 1] = __uint_as_float(cv[j][1][e] & 0xffff0000u);
+        v3[2 * e] = __uint_as_float(cv[j][2][e] << 16); v3[2 * e + 1] = __uint_as_float(cv[j][2][e] & 0xffff0000u);
+        v4[2 * e] = __uint_as_float(cv[j][3][e] << 16); v4[2 * e + 1] = __uint_as_float(cv[j][3][e] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        r[e] = (wt[j][0] * v1[e] + wt[j][1] * v2[e] + wt[j][2] * v3[e] + wt[j][3] * v4[e]) * mm[j];
+      u32x4 u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) u[e] = pack_bf16x2(r[2 * e], r[2 * e + 1]);
+      const int v = v0 + 2 * j;
+      *(u32x4*)&sA[px * DF_RS + v * 8] = u;
+      if (cols && pv) *(u32x4*)(cols + ((int64_t)n * HWo64 + p) * a.L + k * 64 + v * 8) = u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const u32x4 af = *(const u32x4*)&sA[(32 * wv + 16 * rb + (lane & 15)) * DF_RS + 32 * kk + 8 * (lane >> 4)];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) mfma_bf16(af, bq[cb][kk], acc[rb][cb]);
+      }
+    __syncthreads();
+  }
+  const bool vec4 = (HWo & 3) == 0;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int c = 16 * cb + (lane & 15);
+    if (c >= cout) continue;
+    const float b = bias ? bias[c] : 0.f;
+    float* yc = y + ((int64_t)n * cout + c) * HWo64;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int pr = p0 + 32 * wv + 16 * rb + 4 * (lane >> 4);
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = bf16_to_f32(f32_to_bf16(acc[rb][cb][i] + b));
+      if (vec4 && pr + 3 < HWo) {
+        *(f32x4*)(yc + pr) = f32x4{o[0], o[1], o[2], o[3]};
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (pr + i < HWo) yc[pr + i] = o[i];
+      }
+    }
+  }
+}
+
 int make_args(const sr_dcn_desc* d, DcnArgs& a) {
   if (!d) return sr_fail(SR_EINVAL, "dcn: null descriptor");
   a.N = d->N; a.C = d->C; a.H = d->H; a.W = d->W; a.Cp = d->Cp; a.Ho = d->Ho; a.Wo = d->Wo;
@@ -413,9 +559,246 @@ int launch_col2im(const DcnArgs& a, const void* dcols, const void* x, const floa
   return sr_check(hipGetLastError(), "dcn_col2im launch");
 }
 
+// Windowed form of the fused forward (x NHWC): the block's output tile is 8 x 16 pixels, and
+// the x window it can sample (its receptive field grown by R pixels on each side for the
+// offsets; 15 x 23 pixels x 64 channels = 44 KB at 3x3, stride 1, R 2) is staged in LDS once,
+// coalesced.  The per-tap gathers then read LDS; a sample whose 2 x 2 corners leave the window
+// (|offset| > R) reads them from global memory, so the result never depends on the offset
+// range.  The window holds pixel pix's channel vector v in slot v ^ (pix & 7): the vectors of 16
+// different pixels land on 16 distinct 4-bank groups.  Offsets and masks of tap k + 1 are loaded
+// while tap k gathers.  Tiles of one image are remapped onto one XCD (shared L2 for the window
+// rows of neighbouring tiles).  Sample math, A tile, MFMA and epilogue as dcn_fwd_mfma_kernel.
+constexpr int DW_TH = 8, DW_TW = 16, DW_NT = 512;
+
+__global__ void __launch_bounds__(DW_NT, 2) dcn_fwd_win_kernel(DcnArgs a, const bf16_t* __restrict__ x,
+                                                               const float* __restrict__ off,
+                                                               const float* __restrict__ msk,
+                                                               const bf16_t* __restrict__ wf, int ldw, int wrows,
+                                                               int cout, const float* __restrict__ bias,
+                                                               float* __restrict__ y, bf16_t* __restrict__ cols,
+                                                               int R, int WH, int WW, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  bf16_t* sA = (bf16_t*)s_raw;                           // [DF_TP][DF_RS]
+  bf16_t* sB = sA + DF_TP * DF_RS;                       // [64 co][DF_RS]: this tap's weight slice
+  unsigned char* sX = (unsigned char*)(sB + 64 * DF_RS);  // [WH * WW][8 slots][16 B]
+  const int HWo = a.Ho * a.Wo;
+  const int64_t HWo64 = HWo;
+  const int tw = (a.Wo + DW_TW - 1) / DW_TW, th = (a.Ho + DW_TH - 1) / DW_TH;
+  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / (tw * th), t = bid - n * (tw * th);
+  const int ho0 = (t / tw) * DW_TH, wo0 = (t - (t / tw) * tw) * DW_TW;
+  const int y0 = ho0 * a.sh - a.ph - R, x0 = wo0 * a.sw - a.pw - R;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;  // 8 waves
+  const int px = tid & (DF_TP - 1), v0 = tid >> 7;              // pixel; channel vectors v0 and v0 + 4
+  const int ho = ho0 + (px >> 4), wo = wo0 + (px & 15);
+  const bool pv = ho < a.Ho && wo < a.Wo;
+  const int p = pv ? ho * a.Wo + wo : 0;
+  const float hb = (float)(ho * a.sh - a.ph), wb = (float)(wo * a.sw - a.pw);
+  const uint32_t pxb = (uint32_t)a.Cp * 2u;
+  const auto xr = make_rsrc(x + (int64_t)n * a.H * a.W * a.Cp, (uint32_t)((size_t)a.H * a.W * a.Cp * 2));
+  const auto wr = make_rsrc(wf, (uint32_t)((size_t)wrows * ldw * 2));
+  // stage the window: 4 loads in flight per thread, then their stores
+  const int nwin = (dbg & 8) ? 0 : WH * WW * 8;
+  for (int b0 = 0; b0 < nwin; b0 += 4 * DW_NT) {
+    u32x4 val[4];
+    int dst[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = b0 + u * DW_NT + tid;
+      const int pix = i >> 3, v = i & 7;
+      const int wy = pix / WW, wx = pix - wy * WW;
+      const int yy = y0 + wy, xx = x0 + wx;
+      const bool in = i < nwin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      val[u] = buf_load16(xr, in ? (uint32_t)(yy * a.W + xx) * pxb + (uint32_t)v * 16u : SR_OOB);
+      dst[u] = i < nwin ? pix * 128 + ((v ^ (pix & 7)) << 4) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (dst[u] >= 0) *(u32x4*)(sX + dst[u]) = val[u];
+  }
+  const float* offn = off + (int64_t)n * a.DG * 2 * a.K * HWo64 + p;
+  const float* mskn = msk ? msk + (int64_t)n * a.DG * a.K * HWo64 + p : nullptr;
+  const int dg0 = v0 * 8 / a.cpg, dg1 = (v0 + 4) * 8 / a.cpg;
+  float om[2][3];
+  auto load_om = [&](int k, float (&o)[2][3]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int dgi = j ? dg1 : dg0;
+      if (dbg & 2) {
+        o[j][0] = 0.3f; o[j][1] = -0.2f; o[j][2] = 0.5f;
+        continue;
+      }
+      o[j][0] = pv ? offn[(int64_t)(dgi * 2 * a.K + 2 * k) * HWo64] : 0.f;
+      o[j][1] = pv ? offn[(int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64] : 0.f;
+      o[j][2] = pv ? (mskn ? mskn[(int64_t)(dgi * a.K + k) * HWo64] : 1.f) : 0.f;
+    }
+  };
+  load_om(0, om);
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // window staged
+  for (int k = 0; k < a.K; ++k) {
+    // this tap's 64 x 64 weight slice, one 16-B piece per thread, written to LDS after the gather
+    // (every wave reading its B fragments from L2 moved 8x the bytes: 1.2 GB per C5 call)
+    const u32x4 wpiece = buf_load16(wr, (uint32_t)(((tid >> 3) * ldw + k * 64 + (tid & 7) * 8) * 2));
+    float omn[2][3];
+    if (k + 1 < a.K) load_om(k + 1, omn);
+    const int ti = k / a.kw, tj = k - ti * a.kw;
+    const float hk = hb + (float)(ti * a.dh), wk = wb + (float)(tj * a.dw);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int v = v0 + 4 * j;
+      const float h = hk + om[j][0], w = wk + om[j][1];
+      const Sample s = make_sample(h, w, a.H, a.W);
+      const bool ok = pv && s.valid;
+      const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+      const int hl = ok ? (int)floorf(h) : 0, wl = ok ? (int)floorf(w) : 0;
+      const int ly = hl - y0, lx = wl - x0;
+      u32x4 cv[4];
+      if ((dbg & 1) || (ok && ly >= 0 && ly + 1 < WH && lx >= 0 && lx + 1 < WW)) {
+        const int q0 = (dbg & 1) ? ((ly & 7) * WW + (lx & 15)) : ly * WW + lx;
+        const int qs[4] = {q0, q0 + 1, q0 + WW, q0 + WW + 1};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cv[q] = *(const u32x4*)(sX + qs[q] * 128 + ((v ^ (qs[q] & 7)) << 4));
+      } else {
+        const uint32_t cb16 = (uint32_t)v * 16u;
+        cv[0] = buf_load16(xr, ok && s.o1 >= 0 ? (uint32_t)s.o1 * pxb + cb16 : SR_OOB);
+        cv[1] = buf_load16(xr, ok && s.o2 >= 0 ? (uint32_t)s.o2 * pxb + cb16 : SR_OOB);
+        cv[2] = buf_load16(xr, ok && s.o3 >= 0 ? (uint32_t)s.o3 * pxb + cb16 : SR_OOB);
+        cv[3] = buf_load16(xr, ok && s.o4 >= 0 ? (uint32_t)s.o4 * pxb + cb16 : SR_OOB);
+      }
+      u32x4 u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float r2[2];
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi) {
+          const auto f = [&](uint32_t w32) { return __uint_as_float(hi ? (w32 & 0xffff0000u) : (w32 << 16)); };
+          r2[hi] = (w1 * f(cv[0][e]) + w2 * f(cv[1][e]) + w3 * f(cv[2][e]) + w4 * f(cv[3][e])) * om[j][2];
+        }
+        u[e] = pack_bf16x2(r2[0], r2[1]);
+      }
+      *(u32x4*)&sA[px * DF_RS + v * 8] = u;
+      if (cols && pv) *(u32x4*)(cols + ((int64_t)n * HWo64 + p) * a.L + k * 64 + v * 8) = u;
+    }
+    *(u32x4*)&sB[(tid >> 3) * DF_RS + (tid & 7) * 8] = wpiece;
+    __syncthreads();
+    if (!(dbg & 4)) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const u32x4 af = *(const u32x4*)&sA[(16 * wv + (lane & 15)) * DF_RS + 32 * kk + 8 * (lane >> 4)];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          // B[k = ci][col = co] = wf[co][k*64 + ci]
+          const u32x4 bf = *(const u32x4*)&sB[(16 * cb + (lane & 15)) * DF_RS + 32 * kk + 8 * (lane >> 4)];
+          mfma_bf16(af, bf, acc[cb]);
+        }
+      }
+    }
+    __syncthreads();
+    if (k + 1 < a.K) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 3; ++e) om[j][e] = omn[j][e];
+    }
+  }
+  const bool vec4 = (a.Wo & 3) == 0;
+  const int oh = ho0 + wv, ow = wo0 + 4 * (lane >> 4);
+  if (oh >= a.Ho) return;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int c = 16 * cb + (lane & 15);
+    if (c >= cout) continue;
+    const float b = bias ? bias[c] : 0.f;
+    float* yc = y + ((int64_t)n * cout + c) * HWo64 + oh * a.Wo;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = bf16_to_f32(f32_to_bf16(acc[cb][i] + b));
+    if (vec4 && ow + 3 < a.Wo) {
+      *(f32x4*)(yc + ow) = f32x4{o[0], o[1], o[2], o[3]};
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (ow + i < a.Wo) yc[ow + i] = o[i];
+    }
+  }
+}
+
+// Ablation mask of dcn_fwd_win_kernel (SR_DCN_DBG, read per call; tools/dcn_ablate.py): 1 no global
+// fallback, 2 constant offsets (no offset / mask reads), 4 no MFMA, 8 no window staging.  Results are
+// wrong under any of them; 0 (unset) is the kernel.
+int dcn_dbg() {
+  const char* e = getenv("SR_DCN_DBG");
+  return e ? atoi(e) : 0;
+}
+
+// Window geometry of dcn_fwd_win_kernel: the largest R <= 2 whose LDS (A tile + window) fits 64 KB.
+bool win_geom(const DcnArgs& a, int* R, int* WH, int* WW, size_t* lds) {
+  const char* e = getenv("SR_DCN_R");
+  const int r0 = e && atoi(e) >= 0 && atoi(e) <= 6 ? atoi(e) : 2;
+  for (int r = r0; r >= 0; --r) {
+    const int wh = (DW_TH - 1) * a.sh + (a.kh - 1) * a.dh + 2 + 2 * r;
+    const int ww = (DW_TW - 1) * a.sw + (a.kw - 1) * a.dw + 2 + 2 * r;
+    const size_t l = (size_t)(DF_TP + 64) * DF_RS * 2 + (size_t)wh * ww * 128;
+    if (l <= 160 * 1024) {
+      *R = r; *WH = wh; *WW = ww; *lds = l;
+      return true;
+    }
+  }
+  return false;
+}
+
+// Shapes the fused forward takes (see dcn_fwd_mfma_kernel); SR_DCN_FUSED=0 turns it off (A/B).
+bool dcn_fused_ok(const sr_dcn_desc* d, const DcnArgs& a, int cout) {
+  static const bool off = [] {
+    const char* e = getenv("SR_DCN_FUSED");
+    return e && atoi(e) == 0;
+  }();
+  return !off && d->dtype == SR_BF16 && a.G == 1 && a.C == 64 && a.Cp == 64 && a.cgp == 64 && cout >= 1 &&
+         cout <= 64 && a.cpg % 8 == 0 && (size_t)a.H * a.W * a.Cp * 2 < 0x80000000ull;
+}
+
 }  // namespace
 
 extern "C" {
+
+int sr_dcn_fwd_fused_ok(const sr_dcn_desc* d, int cout) {
+  DcnArgs a;
+  if (make_args(d, a) != SR_OK) return 0;
+  return dcn_fused_ok(d, a, cout) ? 1 : 0;
+}
+
+int sr_dcn_fwd_fused(const sr_dcn_desc* d, const void* x, int x_blocked, const float* offset, const float* mask,
+                     const void* wf, int ldw, int wrows, int cout, const float* bias, float* y, void* cols,
+                     void* stream) {
+  DcnArgs a;
+  int rc = make_args(d, a);
+  if (rc) return rc;
+  if (!dcn_fused_ok(d, a, cout)) return sr_fail(SR_EINVAL, "dcn_fwd_fused: unsupported shape (query sr_dcn_fwd_fused_ok)");
+  if (!x || !offset || !wf || !y) return sr_fail(SR_EINVAL, "dcn_fwd_fused: null pointer");
+  if (ldw < a.K * 64 || wrows < cout || (size_t)wrows * ldw * 2 >= 0x80000000ull)
+    return sr_fail(SR_EINVAL, "dcn_fwd_fused: weight image must be [>= cout][>= K*64] bf16");
+  int R, WH, WW;
+  size_t lds;
+  if (!x_blocked && win_geom(a, &R, &WH, &WW, &lds)) {
+    const int wt = ((a.Ho + DW_TH - 1) / DW_TH) * ((a.Wo + DW_TW - 1) / DW_TW);
+    if (lds > 65536 &&
+        hipFuncSetAttribute((const void*)dcn_fwd_win_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess)
+      return sr_fail(SR_ELAUNCH, "dcn_fwd_fused: LDS attribute");
+    hipLaunchKernelGGL(dcn_fwd_win_kernel, dim3((unsigned)(a.N * wt)), dim3(DW_NT), lds, (hipStream_t)stream, a,
+                       (const bf16_t*)x, offset, mask, (const bf16_t*)wf, ldw, wrows, cout, bias, y, (bf16_t*)cols,
+                       R, WH, WW, dcn_dbg());
+    return sr_check(hipGetLastError(), "dcn_fwd_fused launch");
+  }
+  const int tiles = (a.Ho * a.Wo + DF_TP - 1) / DF_TP;
+  hipLaunchKernelGGL(dcn_fwd_mfma_kernel, dim3((unsigned)(a.N * tiles)), dim3(256), 0, (hipStream_t)stream, a,
+                     (const bf16_t*)x, offset, mask, (const bf16_t*)wf, ldw, wrows, cout, bias, y, (bf16_t*)cols,
+                     x_blocked ? 16u : 128u, x_blocked ? (uint32_t)(a.H * a.W * 16) : 16u);
+  return sr_check(hipGetLastError(), "dcn_fwd_fused launch");
+}
 
 int sr_dcn_im2col(const sr_dcn_desc* d, const void* x, const float* offset, const float* mask, void* cols,
                   void* stream) {

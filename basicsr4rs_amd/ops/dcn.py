@@ -10,7 +10,9 @@ distributions.
 Execution (per call, all images at once instead of the reference's per-image loop):
   forward : x -> NHWC, ``sr_dcn_im2col`` (mask * bilinear samples as pixel-major column
             rows), 1x1 MFMA GEMM with the bias in its epilogue (``sr_conv3x3_fwd``,
-            ksize 1, one call per conv group), NHWC -> NCHW.
+            ksize 1, one call per conv group), NHWC -> NCHW; in bf16 with groups 1, 64 input
+            and <= 64 output channels (EDVR's PCD / TSA shapes) one fused kernel instead
+            (``sr_dcn_fwd_fused``), which stores the columns only when a backward will run.
   backward: dcols = dy x W (same GEMM on the transposed weight image), dW / db by the
             split-K wgrad kernel over (dy, cols), ``sr_dcn_col2im`` for grad x (fp32
             atomics), grad offset and grad mask in one pass.
@@ -119,7 +121,14 @@ def _prepared(weight, bias, g, spec, dtype):
     return images
 
 
-def _dcn_forward(x, offset, mask, weight, bias, g, dtype):
+def fused_ok(g, dtype):
+    """True when the forward runs as one kernel (``sr_dcn_fwd_fused``: bf16, groups 1, 64 input
+    channels, <= 64 outputs; the column matrix is built per tap in LDS and not stored unless the
+    backward needs it)."""
+    return dtype == torch.bfloat16 and bool(_lib.load().sr_dcn_fwd_fused_ok(g.desc(dtype), g.cout))
+
+
+def _dcn_forward(x, offset, mask, weight, bias, g, dtype, need_cols=True):
     lib = _lib.load()
     off = offset.float().contiguous()
     msk = None if mask is None else mask.float().contiguous()
@@ -127,6 +136,15 @@ def _dcn_forward(x, offset, mask, weight, bias, g, dtype):
         raise RuntimeError(f'offset shape {tuple(off.shape)} != {(g.N, g.DG * 2 * g.K, g.Ho, g.Wo)}')
     if msk is not None and tuple(msk.shape) != (g.N, g.DG * g.K, g.Ho, g.Wo):
         raise RuntimeError(f'mask shape {tuple(msk.shape)} != {(g.N, g.DG * g.K, g.Ho, g.Wo)}')
+    if fused_ok(g, dtype):
+        xh = C.nchw_to_nhwc(x.float(), g.Cp, dtype)
+        wf, _, bg = _prepared(weight, bias, g, _spec(g), dtype)[0]
+        y = torch.empty(g.N, g.cout, g.Ho, g.Wo, device=x.device, dtype=torch.float32)
+        cols = torch.empty(g.N, g.Ho, g.Wo, g.L, device=x.device, dtype=dtype) if need_cols else None
+        _lib.check(lib.sr_dcn_fwd_fused(g.desc(dtype), _lib.ptr(xh), 0, _lib.ptr(off), _lib.ptr(msk), _lib.ptr(wf),
+                                        wf.shape[1], wf.shape[0], g.cout, _lib.ptr(bg if bias is not None else None),
+                                        _lib.ptr(y), _lib.ptr(cols), _lib.stream()))
+        return y, (xh, off, msk, cols)
     xh = C.nchw_to_nhwc(x.float(), g.Cp, dtype)
     cols = torch.empty(g.N, g.Ho, g.Wo, g.L, device=x.device, dtype=dtype)
     _lib.check(lib.sr_dcn_im2col(g.desc(dtype), _lib.ptr(xh), _lib.ptr(off), _lib.ptr(msk), _lib.ptr(cols),
@@ -201,7 +219,7 @@ class DeformConvFunction(Function):
             raise AssertionError('im2col step must divide batchsize')
         dtype = C.feature_dtype()
         g = _Geom(input, weight, stride, padding, dilation, groups, deformable_groups)
-        out, saved = _dcn_forward(input, offset, None, weight, None, g, dtype)
+        out, saved = _dcn_forward(input, offset, None, weight, None, g, dtype, any(ctx.needs_input_grad))
         _save(ctx, g, dtype, input, saved, weight, None)
         return out.to(input.dtype)
 
@@ -225,7 +243,7 @@ class ModulatedDeformConvFunction(Function):
         _require_gpu(input, offset, mask, weight)
         dtype = C.feature_dtype()
         g = _Geom(input, weight, stride, padding, dilation, groups, deformable_groups)
-        out, saved = _dcn_forward(input, offset, mask, weight, bias, g, dtype)
+        out, saved = _dcn_forward(input, offset, mask, weight, bias, g, dtype, any(ctx.needs_input_grad))
         _save(ctx, g, dtype, input, saved, weight, bias)
         return out.to(input.dtype)
 

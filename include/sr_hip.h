@@ -367,6 +367,17 @@ typedef struct sr_dcn_desc {
  * (deform_conv_cuda_kernel.cu:191-278, :571-634), batched over all images. */
 int sr_dcn_im2col(const sr_dcn_desc* d, const void* x, const float* offset, const float* mask, void* cols,
                   void* stream);
+/* Fused forward (bf16 only; groups 1, C = Cp = cgp = 64, Cout <= 64, cpg % 8 == 0 -- query with
+ * sr_dcn_fwd_fused_ok): y[N][cout][Ho][Wo] fp32 = bf16(W x columns + bias), the columns gathered per
+ * tap into LDS and never stored unless cols != NULL (then written as sr_dcn_im2col would, for the
+ * backward's weight gradient).  x_blocked: x is [N][8][H][W][8] (channel vectors of 8 as planes; faster
+ * gathers) instead of the NHWC [N][H][W][64] of the other entries.  wf: the GEMM weight image [wrows >= cout][ldw >= kh*kw*64] bf16, column
+ * tap*64 + ci; bias fp32 [cout] or NULL.  Replaces modulated_deformable_im2col_cuda + the per-image
+ * addmm of modulated_deform_conv_cuda_forward (deform_conv_cuda.cpp:560-590). */
+int sr_dcn_fwd_fused_ok(const sr_dcn_desc* d, int cout);
+int sr_dcn_fwd_fused(const sr_dcn_desc* d, const void* x, int x_blocked, const float* offset, const float* mask,
+                     const void* wf, int ldw, int wrows, int cout, const float* bias, float* y, void* cols,
+                     void* stream);
 /* From dcols (= dy x W, column layout): grad_x += scatter (fp32 NHWC [N][H][W][Cp], caller
  * zeroes it; LDS fixed-point accumulation + fp32 atomics), grad_offset / grad_mask written in
  * full (grad_mask NULL for v1).  Workspace: sr_dcn_col2im_workspace bytes (per-image scale).

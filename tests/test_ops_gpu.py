@@ -85,6 +85,85 @@ def test_dcn_bf16_autocast(cuda):
         assert rel(tt.grad, g) < 5e-2, (name, rel(tt.grad, g))
 
 
+FUSED_CASES = [
+    # N, C, H, W, Cout, k, stride, pad, dil, groups, dg, modulated
+    (2, 64, 16, 16, 64, 3, 1, 1, 1, 1, 8, True),  # C5 / EDVR PCD geometry, two 128-px tiles per image
+    (1, 64, 12, 10, 48, 3, 1, 1, 1, 1, 1, True),  # one deformable group, Cout < 64, ragged last tile
+    (2, 64, 9, 13, 64, 3, 2, 1, 1, 1, 4, False),  # DCNv1, stride 2, Ho*Wo not a multiple of 4
+    (1, 64, 11, 11, 16, 3, 1, 2, 2, 1, 2, True),  # dilation 2
+    (1, 64, 20, 36, 64, 3, 1, 1, 1, 1, 8, True),  # 3 x 3 partial 8 x 16 window tiles
+]
+
+
+@pytest.mark.parametrize('case', FUSED_CASES)
+@pytest.mark.parametrize('need_grad', [True, False])
+def test_dcn_fused_forward(cuda, case, need_grad):
+    """sr_dcn_fwd_fused (im2col in LDS + MFMA, one kernel) against the fp64 oracle on the same
+    bf16-rounded x / weight, and its column rows against sr_dcn_im2col's (same sample
+    expression: equal up to fp contraction, <= 1 bf16 ulp)."""
+    N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
+    x, off, msk, w, b, dy = _dcn_inputs(case, seed=2)
+    t = [torch.tensor(a, device=cuda, requires_grad=need_grad) if a is not None else None
+         for a in (x, off, msk, w, b)]
+    g = D._Geom(t[0], t[3], s, p, d, groups, dg)
+    assert D.fused_ok(g, torch.bfloat16)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        if modulated:
+            out = D.modulated_deform_conv(t[0], t[1], t[2], t[3], t[4], s, p, d, groups, dg)
+        else:
+            out = D.deform_conv(t[0], t[1], t[3], s, p, d, groups, dg)
+    bfr = lambda a: torch.tensor(a).to(torch.bfloat16).double().numpy()  # noqa: E731
+    ref = O.dcn_forward(bfr(x), off, msk, bfr(w), b, s, p, d, groups, dg)
+    assert out.shape == ref.shape
+    assert rel(out, ref) < 2e-2, rel(out, ref)
+    # the kernel's column rows equal the unfused im2col's
+    lib = _lib.load()
+    xh = D.C.nchw_to_nhwc(t[0].detach().float(), g.Cp, torch.bfloat16)
+    offc = t[1].detach().float().contiguous()
+    mskc = t[2].detach().float().contiguous() if modulated else None
+    cols_ref = torch.empty(g.N, g.Ho, g.Wo, g.L, device=cuda, dtype=torch.bfloat16)
+    _lib.check(lib.sr_dcn_im2col(g.desc(torch.bfloat16), _lib.ptr(xh), _lib.ptr(offc), _lib.ptr(mskc),
+                                 _lib.ptr(cols_ref), _lib.stream()))
+    wf, _, bg = D._prepared(t[3], t[4], g, D._spec(g), torch.bfloat16)[0]
+    # both x layouts: NHWC (the LDS-window kernel the op uses; offsets of std 2 send many samples
+    # past its R = 2 window onto the global fallback) and the channel-vector planes (global gathers)
+    xb = D.C.nchw_to_nhwc(t[0].detach().float().reshape(N * 8, 8, H, W), 8, torch.bfloat16)
+    for blocked, xin in ((0, xh), (1, xb)):
+        y2 = torch.empty(g.N, g.cout, g.Ho, g.Wo, device=cuda)
+        cols = torch.full_like(cols_ref, float('nan'))
+        _lib.check(lib.sr_dcn_fwd_fused(g.desc(torch.bfloat16), _lib.ptr(xin), blocked, _lib.ptr(offc),
+                                        _lib.ptr(mskc), _lib.ptr(wf), wf.shape[1], wf.shape[0], g.cout,
+                                        _lib.ptr(bg if modulated else None), _lib.ptr(y2), _lib.ptr(cols),
+                                        _lib.stream()))
+        dcol = (cols.float() - cols_ref.float()).abs()
+        assert torch.isfinite(cols.float()).all()
+        assert (dcol <= cols_ref.float().abs() * 2.0 ** -7 + 1e-30).all(), (blocked, dcol.max())
+        assert torch.equal(y2, out.detach().float()), blocked
+    # the same GEMM on the unfused path (1x1 kernel over cols_ref): equal up to summation order
+    y3 = torch.empty(g.N, g.Ho, g.Wo, g.ldy, device=cuda, dtype=torch.bfloat16)
+    D.C.conv_fwd_raw(cols_ref, wf, bg if modulated else None, y3, g.N, g.Ho, g.Wo, g.K * g.cgp, g.cout_gp,
+                     g.cout_gp, ksize=1, ldx=g.L, xcoff=0, ldy=g.ldy, ycoff=0)
+    y3 = D.C.nhwc_to_nchw(y3, g.cout)
+    assert rel(y2, y3.double().cpu().numpy()) < 1e-2
+    if need_grad:
+        out.backward(torch.tensor(dy, device=cuda))
+        grads = O.dcn_backward(bfr(x), off, msk, bfr(w), b, s, p, d, groups, dg, bfr(dy))
+        for name, gr, tt in zip(('x', 'offset', 'mask', 'weight', 'bias'), grads, t):
+            if tt is None:
+                continue
+            assert rel(tt.grad, gr) < 5e-2, (name, rel(tt.grad, gr))
+
+
+def test_dcn_fused_ok_query(cuda):
+    """Shapes outside the fused kernel keep the unfused path (fp32, C != 64, Cout > 64, groups 2)."""
+    mk = lambda C, Co, gr: D._Geom(torch.empty(1, C, 8, 8), torch.empty(Co, C // gr, 3, 3), 1, 1, 1, gr, 1)  # noqa
+    assert D.fused_ok(mk(64, 64, 1), torch.bfloat16)
+    assert not D.fused_ok(mk(64, 64, 1), torch.float32)
+    assert not D.fused_ok(mk(32, 64, 1), torch.bfloat16)
+    assert not D.fused_ok(mk(64, 128, 1), torch.bfloat16)
+    assert not D.fused_ok(mk(64, 64, 2), torch.bfloat16)
+
+
 def test_dcn_packs(cuda):
     torch.manual_seed(0)
     m2 = D.ModulatedDeformConvPack(16, 16, 3, padding=1, deformable_groups=2).to(cuda)
