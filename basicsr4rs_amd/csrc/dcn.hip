@@ -535,18 +535,18 @@ XGeom grad_x_geom(const DcnArgs& a) {
 
 template <typename T>
 int launch_col2im(const DcnArgs& a, const void* dcols, const void* x, const float* off, const float* msk, float* gx,
-                  float* goff, float* gmsk, unsigned* amax, hipStream_t s) {
-  if (hipMemsetAsync(amax, 0, (size_t)a.N * sizeof(unsigned), s) != hipSuccess)
-    return sr_fail(SR_ELAUNCH, "dcn_col2im: memset failed");
+                  float* goff, float* gmsk, unsigned* amax, hipStream_t s, bool coord = true) {
   const int tiles = (a.Ho * a.Wo + a.TP - 1) / a.TP;
   const size_t lds = (size_t)a.DG * 3 * a.K * a.TP * 4;
   const bool vec = vec_width<T>(a) > 1;
-  if (vec)
+  if (!coord) {  // the coordinate pass (and amax) ran already (dcn_coord_win_kernel)
+  } else if (vec)
     hipLaunchKernelGGL((dcn_coord_grad_kernel<T, Elt<T>::PER16>), dim3((unsigned)(a.N * tiles)), dim3(256), lds, s, a,
                        (const T*)dcols, (const T*)x, off, msk, goff, gmsk, amax);
   else
     hipLaunchKernelGGL((dcn_coord_grad_kernel<T, 1>), dim3((unsigned)(a.N * tiles)), dim3(256), lds, s, a,
                        (const T*)dcols, (const T*)x, off, msk, goff, gmsk, amax);
+  if (coord && hipGetLastError() != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_coord_grad launch");
   const XGeom xg = grad_x_geom(a);
   const int xt = ((a.Ho + xg.TT - 1) / xg.TT) * ((a.Wo + xg.TT - 1) / xg.TT);
   const size_t xlds = (size_t)xg.RH * xg.RW * (xg.CPP + 1) * 8;
@@ -570,7 +570,7 @@ int launch_col2im(const DcnArgs& a, const void* dcols, const void* x, const floa
 // rows of neighbouring tiles).  Sample math, A tile, MFMA and epilogue as dcn_fwd_mfma_kernel.
 constexpr int DW_TH = 8, DW_TW = 16, DW_NT = 512;
 
-__global__ void __launch_bounds__(DW_NT, 2) dcn_fwd_win_kernel(DcnArgs a, const bf16_t* __restrict__ x,
+__global__ void __launch_bounds__(DW_NT, 4) dcn_fwd_win_kernel(DcnArgs a, const bf16_t* __restrict__ x,
                                                                const float* __restrict__ off,
                                                                const float* __restrict__ msk,
                                                                const bf16_t* __restrict__ wf, int ldw, int wrows,
@@ -760,6 +760,174 @@ bool dcn_fused_ok(const sr_dcn_desc* d, const DcnArgs& a, int cout) {
          cout <= 64 && a.cpg % 8 == 0 && (size_t)a.H * a.W * a.Cp * 2 < 0x80000000ull;
 }
 
+// Offset / mask gradients with the forward's LDS x window (bf16, one conv group, C = 64): the
+// block owns an 8 x 16 output tile and stages its x window once (as dcn_fwd_win_kernel); per tap
+// it stages the tap's offsets and masks for the tile in LDS (coalesced 16-pixel row segments),
+// then item (pixel, channel vector v) reads its 16-B dcols piece (8 consecutive lanes = one
+// pixel's 128-B row), its four corners from the window (global memory past it), and sums
+// d bilinear / d h, / d w and the un-masked sample against dcols over its 8 channels; lanes of one
+// deformable group combine by xor-shuffles and the group's first lane writes the three results
+// over the LDS words it read, which are then stored coalesced.  Per-image max |mask * dcols| for
+// the scatter's fixed-point scale as dcn_coord_grad_kernel.  Same math as that kernel (the
+// reference's col2im_coord, deform_conv_cuda_kernel.cu:696-770); the channel sums run 8 per lane
+// then across lanes.
+__global__ void __launch_bounds__(DW_NT, 2) dcn_coord_win_kernel(DcnArgs a, const bf16_t* __restrict__ dcols,
+                                                                 const bf16_t* __restrict__ x,
+                                                                 const float* __restrict__ off,
+                                                                 const float* __restrict__ msk,
+                                                                 float* __restrict__ goff, float* __restrict__ gmsk,
+                                                                 unsigned* __restrict__ amax, int R, int WH, int WW) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  float* sO = (float*)s_raw;                                  // [3 * DG][DF_TP]: dh, dw per group, then masks
+  unsigned char* sX = s_raw + (size_t)3 * a.DG * DF_TP * 4;  // [WH * WW][8 slots][16 B]
+  const int HWo = a.Ho * a.Wo;
+  const int64_t HWo64 = HWo;
+  const int tw = (a.Wo + DW_TW - 1) / DW_TW, th = (a.Ho + DW_TH - 1) / DW_TH;
+  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / (tw * th), t = bid - n * (tw * th);
+  const int ho0 = (t / tw) * DW_TH, wo0 = (t - (t / tw) * tw) * DW_TW;
+  const int y0 = ho0 * a.sh - a.ph - R, x0 = wo0 * a.sw - a.pw - R;
+  const int tid = threadIdx.x;
+  const int v = tid & 7, pxl = tid >> 3;  // channel vector; pixel (and pixel + 64)
+  const uint32_t pxb = (uint32_t)a.Cp * 2u;
+  const auto xr = make_rsrc(x + (int64_t)n * a.H * a.W * a.Cp, (uint32_t)((size_t)a.H * a.W * a.Cp * 2));
+  const int nwin = WH * WW * 8;
+  for (int b0 = 0; b0 < nwin; b0 += 4 * DW_NT) {
+    u32x4 val[4];
+    int dst[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = b0 + u * DW_NT + tid;
+      const int pix = i >> 3, vv = i & 7;
+      const int wy = pix / WW, wx = pix - wy * WW;
+      const int yy = y0 + wy, xx = x0 + wx;
+      const bool in = i < nwin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      val[u] = buf_load16(xr, in ? (uint32_t)(yy * a.W + xx) * pxb + (uint32_t)vv * 16u : SR_OOB);
+      dst[u] = i < nwin ? pix * 128 + ((vv ^ (pix & 7)) << 4) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (dst[u] >= 0) *(u32x4*)(sX + dst[u]) = val[u];
+  }
+  const int gl = a.cpg / 8;             // lanes per deformable group (1, 2, 4 or 8)
+  const int dgi = v * 8 / a.cpg;
+  const int nrow = 3 * a.DG;            // staged rows per tap
+  const int64_t obase = (int64_t)n * a.DG * 2 * a.K * HWo64, mbase = (int64_t)n * a.DG * a.K * HWo64;
+  float vmax = 0.f;
+  for (int k = 0; k < a.K; ++k) {
+    // stage this tap's offsets and masks: row r < 2*DG is (group r/2, component r%2), then masks
+    // (loading the next tap's a tap ahead in registers measured slower: 445 vs 421 us)
+    for (int i = tid; i < nrow * DF_TP; i += DW_NT) {
+      const int r = i / DF_TP, q = i - r * DF_TP;
+      const int ho = ho0 + (q >> 4), wo = wo0 + (q & 15);
+      float val = 0.f;
+      if (ho < a.Ho && wo < a.Wo) {
+        const int64_t pp = (int64_t)ho * a.Wo + wo;
+        if (r < 2 * a.DG) val = off[obase + (int64_t)((r >> 1) * 2 * a.K + 2 * k + (r & 1)) * HWo64 + pp];
+        else val = msk ? msk[mbase + (int64_t)((r - 2 * a.DG) * a.K + k) * HWo64 + pp] : 1.f;
+      }
+      sO[i] = val;
+    }
+    __syncthreads();
+    const int ti = k / a.kw, tj = k - ti * a.kw;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int px = pxl + 64 * j;
+      const int ho = ho0 + (px >> 4), wo = wo0 + (px & 15);
+      const bool pv = ho < a.Ho && wo < a.Wo;
+      const int p = pv ? ho * a.Wo + wo : 0;
+      u32x4 dcu = u32x4{0u, 0u, 0u, 0u};
+      if (pv) dcu = *(const u32x4*)(dcols + ((int64_t)n * HWo64 + p) * a.L + k * 64 + v * 8);
+      float* ph = &sO[(2 * dgi) * DF_TP + px];
+      float* pw = &sO[(2 * dgi + 1) * DF_TP + px];
+      float* pm = &sO[(2 * a.DG + dgi) * DF_TP + px];
+      const float m = *pm;
+      const float h = (float)(ho * a.sh - a.ph + ti * a.dh) + *ph;
+      const float w = (float)(wo * a.sw - a.pw + tj * a.dw) + *pw;
+      const Sample s = make_sample(h, w, a.H, a.W);
+      const bool ok = pv && s.valid;
+      float acc_h = 0.f, acc_w = 0.f, acc_m = 0.f;
+      if (ok) {
+        const int ly = (int)floorf(h) - y0, lx = (int)floorf(w) - x0;
+        u32x4 cv[4];
+        if (ly >= 0 && ly + 1 < WH && lx >= 0 && lx + 1 < WW) {
+          const int q0 = ly * WW + lx;
+          const int qs[4] = {q0, q0 + 1, q0 + WW, q0 + WW + 1};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cv[q] = *(const u32x4*)(sX + qs[q] * 128 + ((v ^ (qs[q] & 7)) << 4));
+        } else {
+          const uint32_t cb16 = (uint32_t)v * 16u;
+          cv[0] = buf_load16(xr, s.o1 >= 0 ? (uint32_t)s.o1 * pxb + cb16 : SR_OOB);
+          cv[1] = buf_load16(xr, s.o2 >= 0 ? (uint32_t)s.o2 * pxb + cb16 : SR_OOB);
+          cv[2] = buf_load16(xr, s.o3 >= 0 ? (uint32_t)s.o3 * pxb + cb16 : SR_OOB);
+          cv[3] = buf_load16(xr, s.o4 >= 0 ? (uint32_t)s.o4 * pxb + cb16 : SR_OOB);
+        }
+        const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const auto f = [&](uint32_t w32) { return __uint_as_float((e & 1) ? (w32 & 0xffff0000u) : (w32 << 16)); };
+          const float v1 = f(cv[0][e >> 1]), v2 = f(cv[1][e >> 1]), v3 = f(cv[2][e >> 1]), v4 = f(cv[3][e >> 1]);
+          const float dc = f(dcu[e >> 1]);
+          const float wh = -s.hw * v1 - s.lw * v2 + s.hw * v3 + s.lw * v4;
+          const float ww = -s.hh * v1 + s.hh * v2 - s.lh * v3 + s.lh * v4;
+          acc_h += wh * dc * m;
+          acc_w += ww * dc * m;
+          acc_m += dc * (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
+          vmax = fmaxf(vmax, fabsf(dc * m));
+          if (!(fabsf(dc * m) <= 3.0e38f)) vmax = __builtin_inff();
+        }
+      }
+      // combine the group's lanes (consecutive: v is the lane's low 3 bits)
+      for (int o = 1; o < gl; o <<= 1) {
+        acc_h += __shfl_xor(acc_h, o);
+        acc_w += __shfl_xor(acc_w, o);
+        acc_m += __shfl_xor(acc_m, o);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if ((v & (gl - 1)) == 0) {  // every lane of the group has read these words (same wave)
+        *ph = acc_h;
+        *pw = acc_w;
+        *pm = acc_m;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nrow * DF_TP; i += DW_NT) {
+      const int r = i / DF_TP, q = i - r * DF_TP;
+      const int ho = ho0 + (q >> 4), wo = wo0 + (q & 15);
+      if (ho >= a.Ho || wo >= a.Wo) continue;
+      const int64_t pp = (int64_t)ho * a.Wo + wo;
+      if (r < 2 * a.DG) goff[obase + (int64_t)((r >> 1) * 2 * a.K + 2 * k + (r & 1)) * HWo64 + pp] = sO[i];
+      else if (gmsk) gmsk[mbase + (int64_t)((r - 2 * a.DG) * a.K + k) * HWo64 + pp] = sO[i];
+    }
+    __syncthreads();
+  }
+  for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+  if ((tid & 63) == 0 && vmax > 0.f) atomicMax(amax + n, __float_as_uint(vmax));
+}
+
+// dcn_coord_win_kernel's shapes (as the fused forward's, any Cout) and window (R <= 2, LDS <= 80 KB
+// so two blocks share a CU); SR_DCN_COORD_WIN=0 keeps dcn_coord_grad_kernel (A/B).
+bool coord_win_ok(const sr_dcn_desc* d, const DcnArgs& a) {
+  static const bool off = [] {
+    const char* e = getenv("SR_DCN_COORD_WIN");
+    return e && atoi(e) == 0;
+  }();
+  return !off && d->dtype == SR_BF16 && a.G == 1 && a.C == 64 && a.Cp == 64 && a.cgp == 64 && a.cpg % 8 == 0 &&
+         (size_t)a.H * a.W * a.Cp * 2 < 0x80000000ull;
+}
+bool coord_win_geom(const DcnArgs& a, int* R, int* WH, int* WW, size_t* lds) {
+  for (int r = 2; r >= 0; --r) {
+    const int wh = (DW_TH - 1) * a.sh + (a.kh - 1) * a.dh + 2 + 2 * r;
+    const int ww = (DW_TW - 1) * a.sw + (a.kw - 1) * a.dw + 2 + 2 * r;
+    const size_t l = (size_t)3 * a.DG * DF_TP * 4 + (size_t)wh * ww * 128;
+    if (l <= 80 * 1024) {
+      *R = r; *WH = wh; *WW = ww; *lds = l;
+      return true;
+    }
+  }
+  return false;
+}
+
 }  // namespace
 
 extern "C" {
@@ -825,8 +993,25 @@ int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const 
   unsigned* amax = (unsigned*)workspace;
   if (grad_mask && !mask) return sr_fail(SR_EINVAL, "dcn_col2im: grad_mask needs mask");
   hipStream_t s = (hipStream_t)stream;
-  if (d->dtype == SR_BF16)
+  if (hipMemsetAsync(amax, 0, (size_t)a.N * sizeof(unsigned), s) != hipSuccess)
+    return sr_fail(SR_ELAUNCH, "dcn_col2im: memset failed");
+  if (d->dtype == SR_BF16) {
+    int R, WH, WW;
+    size_t lds;
+    if (coord_win_ok(d, a) && coord_win_geom(a, &R, &WH, &WW, &lds)) {
+      const int wt = ((a.Ho + DW_TH - 1) / DW_TH) * ((a.Wo + DW_TW - 1) / DW_TW);
+      if (lds > 65536 &&
+          hipFuncSetAttribute((const void*)dcn_coord_win_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds) != hipSuccess)
+        return sr_fail(SR_ELAUNCH, "dcn_col2im: LDS attribute");
+      hipLaunchKernelGGL(dcn_coord_win_kernel, dim3((unsigned)(a.N * wt)), dim3(DW_NT), lds, s, a,
+                         (const bf16_t*)dcols, (const bf16_t*)x, offset, mask, grad_offset, grad_mask, amax, R, WH,
+                         WW);
+      if (hipGetLastError() != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_coord_win launch");
+      return launch_col2im<bf16_t>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, amax, s, false);
+    }
     return launch_col2im<bf16_t>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, amax, s);
+  }
   if (d->dtype == SR_F32)
     return launch_col2im<float>(a, dcols, x, offset, mask, grad_x, grad_offset, grad_mask, amax, s);
   return sr_fail(SR_EINVAL, "dcn_col2im: bad dtype");
