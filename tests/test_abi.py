@@ -44,6 +44,31 @@ def test_invalid_arguments_raise():
     assert lib.sr_pixel_shuffle_nchw(0, dummy, 1, 3, 4, 4, 2, dummy, None) == -1  # C % r^2 != 0
 
 
+def test_dcn_fused_forward_query_and_validation():
+    """The fused DCN forward's shape query (host only) and its refusals (no launch)."""
+    from basicsr4rs_amd.ops import dcn as D
+    lib = _lib.load()
+
+    def geom(C, Co, groups=1, dg=8):
+        return D._Geom(torch.empty(2, C, 16, 16), torch.empty(Co, C // groups, 3, 3), 1, 1, 1, groups, dg)
+
+    assert D.fused_ok(geom(64, 64), torch.bfloat16)
+    assert D.fused_ok(geom(64, 16, dg=1), torch.bfloat16)
+    assert not D.fused_ok(geom(64, 64), torch.float32)      # exact-f32 mode keeps im2col + GEMM
+    assert not D.fused_ok(geom(32, 64, dg=4), torch.bfloat16)  # 64 input channels only
+    assert not D.fused_ok(geom(64, 128), torch.bfloat16)    # <= 64 outputs
+    assert not D.fused_ok(geom(64, 64, groups=2), torch.bfloat16)
+    g = geom(64, 128)
+    dummy = ctypes.c_void_p(16)
+    rc = lib.sr_dcn_fwd_fused(g.desc(torch.bfloat16), dummy, 0, dummy, dummy, dummy, 576, 128, 128, None, dummy,
+                              None, None)
+    assert rc == -1 and b'unsupported shape' in lib.sr_last_error()
+    g = geom(64, 64)
+    rc = lib.sr_dcn_fwd_fused(g.desc(torch.bfloat16), dummy, 0, dummy, dummy, dummy, 288, 64, 64, None, dummy,
+                              None, None)
+    assert rc == -1 and b'weight image' in lib.sr_last_error()
+
+
 def test_colsum_geometry():
     """Host-side kernel choice behind the fused channel sums (no GPU launch)."""
     from basicsr4rs_amd.ops import conv as C
