@@ -520,15 +520,23 @@ XGeom grad_x_geom(const DcnArgs& a) {
   // largest (tile, halo) whose LDS footprint fits 64 KB; halo 0 still covers the
   // undeformed footprint, anything outside goes to global atomics
   static const int cfg[][2] = {{16, 4}, {16, 2}, {8, 4}, {8, 2}, {8, 0}, {4, 0}};
+  // channels per pass: 8, or SR_DCN_CPP = 16 / 32 (A/B: fewer passes over dcols, a larger LDS image)
+  static const int cpp = [] {
+    const char* e = getenv("SR_DCN_CPP");
+    const int v = e ? atoi(e) : 8;
+    return v == 16 || v == 32 ? v : 8;
+  }();
   XGeom g;
-  g.CPP = 8;
+  g.CPP = cpp;
+  const size_t lim = cpp == 8 ? 65536 : 160 * 1024;
   for (const auto& c : cfg) {
     g.TT = c[0];
     g.R = c[1];
     g.RH = (g.TT - 1) * a.sh + (a.kh - 1) * a.dh + 2 * g.R + 2;
     g.RW = (g.TT - 1) * a.sw + (a.kw - 1) * a.dw + 2 * g.R + 2;
-    if ((size_t)g.RH * g.RW * (g.CPP + 1) * 8 <= 65536) return g;
+    if ((size_t)g.RH * g.RW * (g.CPP + 1) * 8 <= lim) return g;
   }
+  g.CPP = 8;
   g.TT = 4; g.R = 0; g.RH = g.RW = 1;  // degenerate footprint: everything through global atomics
   return g;
 }
@@ -550,6 +558,13 @@ int launch_col2im(const DcnArgs& a, const void* dcols, const void* x, const floa
   const XGeom xg = grad_x_geom(a);
   const int xt = ((a.Ho + xg.TT - 1) / xg.TT) * ((a.Wo + xg.TT - 1) / xg.TT);
   const size_t xlds = (size_t)xg.RH * xg.RW * (xg.CPP + 1) * 8;
+  if (xlds > 65536) {
+    const hipError_t e1 = vec ? hipFuncSetAttribute((const void*)dcn_grad_x_kernel<T, Elt<T>::PER16>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)xlds)
+                              : hipFuncSetAttribute((const void*)dcn_grad_x_kernel<T, 1>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)xlds);
+    if (e1 != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_col2im: LDS attribute");
+  }
   if (vec)
     hipLaunchKernelGGL((dcn_grad_x_kernel<T, Elt<T>::PER16>), dim3((unsigned)(a.N * xt)), dim3(256), xlds, s, a, xg,
                        (const T*)dcols, off, msk, amax, gx);
