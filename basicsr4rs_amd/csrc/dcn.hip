@@ -335,11 +335,11 @@ __global__ void __launch_bounds__(256) dcn_grad_x_kernel(DcnArgs a, XGeom xg, co
 // and multiplies it by the tap's 64 x 64 weight slice on v_mfma_f32_16x16x32_bf16 (B fragments
 // from L2 into registers, issued before the gather so they land under it).  Thread t keeps one
 // pixel (t % DF_TP) for all taps and 4 of its 8 channel vectors, so the offset / mask reads of a
-// wave are 64 consecutive floats of one NCHW plane.  x is read either as NHWC (pixel stride
-// 128 B, vector stride 16 B) or, faster, channel-vector-blocked [N][8][H][W][8] (pixel stride
-// 16 B, vector stride H*W*16 B): then the corners a wave gathers for one vector of 64
-// neighbouring pixels share cache lines (NHWC puts every lane on its own 128-B line: the kernel
-// was L1-line bound, 504 us against the unfused im2col's 318 us on the C5 shape).  LDS rows are padded to 144 B: the 16 rows
+// wave are 64 consecutive floats of one NCHW plane.  This global-gather form runs for
+// x_blocked = 1: x as channel-vector planes [N][8][H][W][8] (pixel stride 16 B, vector stride
+// H*W*16 B), so the corners a wave gathers for one vector of 64 neighbouring pixels share cache
+// lines (on NHWC every lane hit its own 128-B line: 504 us on the C5 shape, 373 us blocked).  NHWC
+// x (what the op passes) takes dcn_fwd_win_kernel below, which gathers from an LDS window (160 us).  LDS rows are padded to 144 B: the 16 rows
 // one A-fragment read touches start on 16 distinct 4-bank groups.  Epilogue: bias, bf16
 // rounding (the unfused path stores its GEMM output as bf16), fp32 NCHW store of 4 consecutive
 // pixels per lane.  cols (optional) receives the column rows for the backward's weight
