@@ -58,6 +58,7 @@ class _QueuedIterator:
             self._q.put(_END)  # stay exhausted on repeated next()
             raise StopIteration
         if isinstance(item, _LoaderError):
+            self._q.put(item)  # the producer is gone: a repeated next() raises again instead of blocking
             raise item.exc
         return item
 

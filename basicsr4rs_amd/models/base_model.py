@@ -29,10 +29,10 @@ class SRDistributed(nn.Module):
     """DDP-equivalent wrapper: ``.module`` is the bare net; gradients are averaged by the
     reducer (launched from backward hooks, joined in ``BaseModel.sync_gradients``)."""
 
-    def __init__(self, module, flat, bucket_mb=25.0):
+    def __init__(self, module, flat, bucket_mb=25.0, find_unused_parameters=False):
         super().__init__()
         self.module = module
-        self.reducer = GradBucketReducer(flat, bucket_mb=bucket_mb)
+        self.reducer = GradBucketReducer(flat, bucket_mb=bucket_mb, find_unused=find_unused_parameters)
         self.reducer.broadcast_params(0)
 
     def forward(self, *args, **kwargs):
@@ -115,7 +115,9 @@ class BaseModel:
             self.flat_g = FlatParams(net)
         if self.opt.get('dist', False):
             bucket_mb = self.opt.get('bucket_cap_mb', 25.0)
-            net = SRDistributed(net, self.flat_g, bucket_mb=bucket_mb)
+            # base_model.py:96-99 passes find_unused_parameters to DDP
+            net = SRDistributed(net, self.flat_g, bucket_mb=bucket_mb,
+                                find_unused_parameters=self.opt.get('find_unused_parameters', False))
         return net
 
     def sync_gradients(self):

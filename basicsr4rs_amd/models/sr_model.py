@@ -65,6 +65,15 @@ class SRModel(BaseModel):
         env = os.environ.get('SR_ASYNC_WGRAD')
         mode = train_opt.get('async_wgrad', False)
         self.async_wgrad = {'0': False, '1': True, 'reduce': 'reduce'}.get(env, mode if mode == 'reduce' else bool(mode))
+        if self.async_wgrad and self.opt.get('dist', False) and env != '1':
+            from ..utils.dist_util import get_dist_info
+            world = get_dist_info()[1]
+            if world > max(1, torch.cuda.device_count()):
+                # several ranks on one GPU (a gloo rehearsal): their side-stream graphs with
+                # cross-queue waits stall each other for seconds per step
+                get_root_logger().warning(f'train.async_wgrad disabled: {world} ranks share '
+                                          f'{torch.cuda.device_count()} GPU(s)')
+                self.async_wgrad = False
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)

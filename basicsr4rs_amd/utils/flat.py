@@ -168,9 +168,14 @@ class GradBucketReducer:
     replay all-reduces the bucket between graph segments (``all_reduce_bucket``).
     """
 
-    def __init__(self, flat, group=None, bucket_mb=25.0, last_bucket_mb=1.0):
+    def __init__(self, flat, group=None, bucket_mb=25.0, last_bucket_mb=1.0, find_unused=False):
         self.flat = flat
         self.group = group
+        # find_unused_parameters (basicsr/models/base_model.py:96-99): the set of contributions may
+        # change from step to step, so no bucket can be known complete during backward -- every
+        # bucket goes out at the join (correct, without overlap)
+        self.find_unused = bool(find_unused)
+        self._grad_sig = None  # requires_grad of every parameter when ``expected`` was learned
         self.world = dist.get_world_size(group)
         n = len(flat.params)
         cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
@@ -219,6 +224,9 @@ class GradBucketReducer:
     def reset(self):
         self.counts = [0] * len(self.flat.params)
         self.issued = [False] * len(self.buckets)
+        self._started = False
+        if self.find_unused:
+            self.expected = None
         if self.expected is None:
             self.pending = [None] * len(self.buckets)  # learning step: everything at the join
         else:
@@ -251,6 +259,15 @@ class GradBucketReducer:
     def _make_hook(self, i):
 
         def hook(_p):
+            if not self._started:  # first gradient of this step
+                self._started = True
+                sig = tuple(p.requires_grad for p in self.flat.params)
+                if sig != self._grad_sig and self.expected is not None:
+                    # a freeze / unfreeze since the counts were learned (EDVR tsa_iter, BasicVSR
+                    # fix_flow) changes which parameters receive gradients: learn them again
+                    self.expected = None
+                    self.pending = [None] * len(self.buckets)
+                self._grad_sig = sig
             self.counts[i] += 1
             if self.expected is None:
                 return

@@ -12,13 +12,18 @@ import numpy as np
 import torch
 
 
-def make_grid(t, nrow=8, padding=2, pad_value=0.0):
-    """torchvision.utils.make_grid(normalize=False) for a [B, C, H, W] batch (the 4-D branch of
-    tensor2img, img_util.py:72-76): tiles on a pad_value canvas, 1-channel maps repeated to 3."""
-    if t.size(0) == 1:
-        return t.squeeze(0)
+def make_grid(t, nrow=8, padding=2, pad_value=0.0, value_range=None):
+    """torchvision.utils.make_grid for a [B, C, H, W] batch (the 4-D branch of tensor2img,
+    img_util.py:72-76, and ``minusone_one_tensor_to_ubyte_numpy``): 1-channel maps repeated to 3,
+    ``value_range=(lo, hi)`` = normalize=True over that range (clamp, then (x - lo) / (hi - lo)),
+    a single image returned as is, else tiles on a pad_value canvas, ``nrow`` per row."""
     if t.size(1) == 1:
         t = torch.cat((t, t, t), 1)
+    if value_range is not None:
+        lo, hi = value_range
+        t = t.clamp(min=lo, max=hi).sub(lo).div(max(hi - lo, 1e-5))
+    if t.size(0) == 1:
+        return t.squeeze(0)
     nmaps = t.size(0)
     xmaps = min(nrow, nmaps)
     ymaps = int(math.ceil(float(nmaps) / xmaps))
@@ -63,6 +68,39 @@ def tensor2img(tensor, rgb2bgr=True, out_type=np.uint8, min_max=(0, 1)):
             img = (img * 255.0).round()
         result.append(np.ascontiguousarray(img).astype(out_type))
     return result[0] if len(result) == 1 else result
+
+
+def img_as_ubyte(img):
+    """skimage.util.img_as_ubyte of a float image in [-1, 1] (the fork's conversion,
+    basicsr/utils/img_util.py:8,128): x * 255 in the input's float type, round half to even, clip to
+    [0, 255]; negative values clip to 0."""
+    img = np.asarray(img)
+    if img.dtype.kind != 'f':
+        raise TypeError(f'img_as_ubyte: float image expected, got {img.dtype}')
+    if img.size and (img.min() < -1.0 or img.max() > 1.0):
+        raise ValueError('Images of type float must be between -1 and 1.')
+    ct = np.float32 if img.dtype.itemsize <= 4 else img.dtype
+    out = np.multiply(img, 255, dtype=ct)
+    np.rint(out, out=out)
+    np.clip(out, 0, 255, out=out)
+    return out.astype(np.uint8)
+
+
+def zero_one_tensor_to_ubyte_numpy(tensor):
+    """A [B, C, H, W] tensor in [0, 1] -> one H x (B W) x C uint8 image (basicsr/utils/img_util.py:
+    115-128): the batch tiled in one row by make_grid (2-px zero padding when B > 1, normalized over
+    (0, 1)), channel order kept (no RGB -> BGR flip), then img_as_ubyte."""
+    t = tensor.detach().float().cpu()
+    grid = make_grid(t, nrow=t.size(0), value_range=(0, 1))
+    return img_as_ubyte(grid.numpy().transpose(1, 2, 0))
+
+
+def minusone_one_tensor_to_ubyte_numpy(tensor):
+    """The fork's remote-sensing image conversion (basicsr/utils/img_util.py:99-112): a [B, C, H, W]
+    tensor in [-1, 1] is clamped to [-1, 1], mapped to (x + 1) / 2 and converted as
+    ``zero_one_tensor_to_ubyte_numpy``."""
+    t = torch.clamp(tensor.detach().float().cpu(), -1, 1)
+    return zero_one_tensor_to_ubyte_numpy((t + 1) / 2)
 
 
 def imwrite(img, file_path, params=None, auto_mkdir=True):

@@ -31,9 +31,13 @@ order, which is what sharing one pool requires.  Every segment starts with one t
 two cuts with nothing launched between them (a conv's weight and bias in two buckets) never make an
 empty graph.
 """
+import os
+
 import torch
 
 from ..ops.conv import _ASYNC
+
+_TRACE = os.environ.get('SR_STEP_TRACE') or None
 
 
 class _BeginBackward(torch.autograd.Function):
@@ -83,6 +87,23 @@ class SegmentedStepGraph:
         self.segments.append([self._cur, self._cur_buckets, kind])
         self._cur = None
 
+    def _abandon(self):
+        """An exception inside ``capture``: end the open segment's capture (its graph and every
+        segment so far are dropped), so the capture stream is not left in capture mode and later
+        CUDA work does not fail with capture-state errors on top of the original one."""
+        g, self._cur = self._cur, None
+        if g is not None:
+            try:
+                with torch.cuda.stream(self.stream):
+                    for st in _ASYNC['streams'].values():
+                        self.stream.wait_stream(st)
+                    g.capture_end()
+            except RuntimeError:  # invalidated capture (or begun on autograd's thread): nothing to keep
+                pass
+        self.segments = []
+        self._cur_buckets = []
+        self.red.reset()
+
     def cut(self, b):
         """GradBucketReducer.on_issue during capture: bucket b is complete here."""
         self._cur_buckets.append((b, 'backward'))
@@ -115,6 +136,9 @@ class SegmentedStepGraph:
                 self._begin()
                 optimizer_fn()
                 self._end('optimizer')
+        except BaseException:
+            self._abandon()
+            raise
         finally:
             self.red.on_issue = None
         torch.cuda.current_stream().wait_stream(self.stream)
@@ -126,17 +150,37 @@ class SegmentedStepGraph:
     # ---- replay --------------------------------------------------------------------------
     def replay(self):
         red = self.red
-        for g, buckets, kind in self.segments:
+        tr = _TRACE and [('start', self._stamp())]
+        for i, (g, buckets, kind) in enumerate(self.segments):
             if kind == 'optimizer':
                 for h in red.handles:
                     h.wait()
+                if tr is not None:
+                    tr.append(('join', self._stamp()))
                 red.last_issue_log, red.issue_log = red.issue_log, []
                 red.reset()
             g.replay()
+            if tr is not None:
+                tr.append((f'seg{i}:{kind}', self._stamp()))
             for b, when in buckets:
                 red.all_reduce_bucket(b)
                 red.issued[b] = True
                 red.issue_log.append((b, when))
+                if tr is not None:
+                    tr.append((f'ar{b}', self._stamp()))
+        if tr is not None:
+            self.trace.append(tr)
+
+    # SR_STEP_TRACE=host: host time after each segment launch / all-reduce issue / join;
+    # SR_STEP_TRACE=sync: the same after a device synchronize (per-phase GPU time, no overlap)
+    trace = []
+
+    @staticmethod
+    def _stamp():
+        import time
+        if _TRACE == 'sync':
+            torch.cuda.synchronize()
+        return time.perf_counter()
 
     @property
     def n_segments(self):

@@ -6,7 +6,10 @@ train step in bf16, per-GPU batch 32 x 3 x 64 x 64 LR -> 32 x 3 x 256 x 256 HR (
 backward, gradient all-reduce (N>1, RCCL), fused Adam(0.9, 0.99) + EMA(0.999).  Inputs
 are synthetic U[0,1) tiles already resident in HBM (seed 0 / 1, + rank).
 
-Run: python bench.py --gpus N --steps K --warmup W   (N>1 under torch.distributed.run).
+Run: python bench.py --gpus N --steps K --warmup W.  N > 1 runs one rank per GPU (RCCL): under
+torch.distributed.run as launched by the driver, or -- started plainly -- bench.py itself starts
+torch.distributed.run with N ranks as a child process before touching the GPU.  A WORLD_SIZE from a
+launcher that disagrees with --gpus is an error.
 `--workload` selects another BASELINE.json config in the same HR-pixels/s unit (rcan = C3,
 swinir = C4, rrdb = C5); the default (edsr = C2) is the north-star line.
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on an
@@ -28,6 +31,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+BASELINE_METRIC = 'HR-pixels/sec/node (x4 SR train step) + PSNR parity vs CPU ref'
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
@@ -73,15 +77,17 @@ PSNR_FLOOR_BF16 = {'edsr': 66.0, 'rcan': 48.0, 'swinir': 60.0, 'rrdb': 42.0}
 GRAPH_DEFAULT = {'swinir': False}
 
 
-def make_opt(world, batch, workload='edsr', graph=False):
+def make_opt(world, batch, workload='edsr', graph=False, ddp=None, shared_gpu=False):
     net, mtype, lr = WORKLOADS[workload][:3]
     aw = ASYNC_WGRAD.get(workload, False)
-    # side-stream weight gradients only in one process: the two-rank gloo rehearsal of the segmented
-    # DDP graph step with them ran RCAN at 11.4 s / step against 182 ms without (tools/gloo2_rcan.sh,
-    # round 3), and no multi-GPU RCCL run of that ordering exists yet
-    aw = bool(aw) and world == 1 and (graph if aw == 'graph' else True)
+    # side-stream weight gradients need a GPU per rank: with several ranks on one GPU (the gloo
+    # rehearsal) the segmented DDP graph step with them stalls for seconds once the host runs ahead
+    # (RCAN 5.9-13 s / step; with a device sync per segment 97 ms): the ranks' multi-queue graphs
+    # with cross-queue waits compete for one GPU's queues (profiles/r04/ddp_async/).
+    # The model applies the same guard (models/sr_model.py).
+    aw = bool(aw) and not shared_gpu and (graph if aw == 'graph' else True)
     return dict(
-        model_type=mtype, is_train=True, dist=world > 1, num_gpu=1, rank=0, world_size=world,
+        model_type=mtype, is_train=True, dist=world > 1 if ddp is None else ddp, num_gpu=1, rank=0, world_size=world,
         network_g=dict(net),
         train=dict(ema_decay=0.999, use_amp=True, cuda_graph=graph, async_wgrad=aw,
                    optim_g=dict(type='Adam', lr=lr, weight_decay=0, betas=[0.9, 0.99]),
@@ -268,6 +274,64 @@ def roofline(workload, kstats, traced_steps, step_s, use_graph):
     return roof
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """``--gpus N`` (N > 1) started as a plain ``python bench.py``: run the N rank processes (one
+    per GPU, RCCL) under torch.distributed.run as a CHILD process -- this process has not touched
+    the GPU and never does -- and return its exit code (rank 0 prints the one JSON line)."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC only on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def _config(workload, B, world, use_graph, async_wgrad):
+    wl = WORKLOADS[workload]
+    return {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
+            'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph,
+            'async_wgrad': bool(async_wgrad)}
+
+
+def dry_run(args, world, rank):
+    """The launch and reporting skeleton of ``main`` without a GPU: gloo rendezvous, barrier,
+    ``--steps`` no-op steps timed between barriers, MAX over ranks, one JSON line from rank 0 with
+    the configuration the real run would report (value null: nothing is measured)."""
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('gloo')
+    B = args.batch or WORKLOADS[args.workload][3]
+    use_graph = (GRAPH_DEFAULT.get(args.workload, True) or world > 1) if args.graph < 0 else bool(args.graph)
+    opt = make_opt(world, B, args.workload, use_graph)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({'metric': BASELINE_METRIC, 'value': None, 'unit': 'HR-pixels/s', 'n_gpus': world,
+                          'steps': args.steps, 'warmup': args.warmup, 'dry_run': True, 'ranks_seen': world,
+                          'max_rank_s': t.item(), 'config': _config(args.workload, B, world, use_graph,
+                                                                     opt['train']['async_wgrad'])}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -280,14 +344,36 @@ def main():
     ap.add_argument('--no-parity', action='store_true')
     ap.add_argument('--graph', type=int, default=-1,
                     help='capture the train step in a HIP graph (1/0; default: on for a single process)')
+    ap.add_argument('--ddp', action='store_true',
+                    help='run the distributed step (bucketed reducer, segmented graph, RCCL) also at N=1')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launch / rendezvous / barrier / max-over-ranks timing / JSON line only, with a no-op step '
+                         'on the CPU (gloo); no GPU, no measurement (tests/test_bench_launch.py)')
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        # `python bench.py --gpus N`: one rank per GPU, launched before anything touches the GPU
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or '1')
+    if world != args.gpus:
+        print(f'bench: --gpus {args.gpus} disagrees with WORLD_SIZE={world} from the launcher', file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    ddp = world > 1 or args.ddp
+    shared_gpu = world > max(1, torch.cuda.device_count())  # ranks sharing a GPU (gloo rehearsal)
+    if ddp:
         from basicsr4rs_amd.utils.dist_util import init_dist
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        if world == 1:  # --ddp on one process: a world of one
+            os.environ.setdefault('MASTER_PORT', str(_free_port()))
+            os.environ.setdefault('RANK', '0')
+            os.environ.setdefault('WORLD_SIZE', '1')
         # RCCL ('nccl') for the real runs; SR_DIST_BACKEND=gloo rehearses the N > 1 path of this
         # script (barriers, max-over-ranks timing, bucketed reducer) with several ranks on one GPU
         init_dist('pytorch', backend=os.environ.get('SR_DIST_BACKEND', 'nccl'))
@@ -306,8 +392,8 @@ def main():
     hr_px_tile = (4 * lr_px) ** 2
     # the step as HIP-graph replay (one graph; under DDP a chain of graphs cut at the gradient
     # buckets, utils/step_graph.py), except single-process SwinIR whose eager step is faster
-    use_graph = (GRAPH_DEFAULT.get(args.workload, True) or world > 1) if args.graph < 0 else bool(args.graph)
-    opt = make_opt(world, B, args.workload, use_graph)
+    use_graph = (GRAPH_DEFAULT.get(args.workload, True) or ddp) if args.graph < 0 else bool(args.graph)
+    opt = make_opt(world, B, args.workload, use_graph, ddp=ddp, shared_gpu=shared_gpu)
     opt['rank'] = rank
     model = build_model(opt)
     g0 = torch.Generator(device=dev).manual_seed(0 + rank)
@@ -360,6 +446,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     loss = model.get_current_log().get('l_pix', float('nan'))
+    if os.environ.get('SR_STEP_TRACE') and getattr(model, '_graph', None) is not None and \
+            hasattr(model._graph, 'trace'):  # segmented DDP replay: per-phase host times (ms) of the last steps
+        for tr in model._graph.trace[-3:]:
+            ph = [(k, round((t - p) * 1e3, 3)) for (k, t), (_, p) in zip(tr[1:], tr[:-1])]
+            print(json.dumps({'rank': rank, 'step_trace': os.environ['SR_STEP_TRACE'], 'phases_ms': ph,
+                              'total_ms': round((tr[-1][1] - tr[0][1]) * 1e3, 3)}), file=sys.stderr)
 
     hr_px = world * B * hr_px_tile * args.steps
     value = hr_px / dt
@@ -373,13 +465,11 @@ def main():
         cpu = cpu_baseline(args.workload)
     if rank == 0:
         line = {
-            'metric': 'HR-pixels/sec/node (x4 SR train step) + PSNR parity vs CPU ref', 'value': round(value, 1), 'unit': 'HR-pixels/s',
+            'metric': BASELINE_METRIC, 'value': round(value, 1), 'unit': 'HR-pixels/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
             'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
-            'config': {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
-                       'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph,
-                       'async_wgrad': bool(opt['train']['async_wgrad'])},
+            'config': _config(args.workload, B, world, use_graph, opt['train']['async_wgrad']),
             'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
             'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu, 'parity': parity,
         }

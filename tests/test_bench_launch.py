@@ -1,0 +1,49 @@
+"""bench.py's launch contract on the CPU (no GPU): ``--gpus N`` must run N ranks.
+
+``python bench.py --gpus 2`` started without a launcher spawns torch.distributed.run with two rank
+processes; the rank-0 line reports ``n_gpus: 2`` and ``dp2`` and the max-over-ranks timing ran
+over both (``--dry-run``: gloo rendezvous, barriers and the MAX all-reduce with a no-op step).  A
+launcher WORLD_SIZE that disagrees with ``--gpus`` exits non-zero.  Reference launch:
+scripts/dist_train.sh:7 (torch.distributed.launch --nproc_per_node)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout, cwd=ROOT)
+
+
+def _line(p):
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, (p.stdout, p.stderr)
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    p = _run(['--gpus', '2', '--dry-run', '--steps', '3', '--workload', 'rcan'])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p)
+    assert d['n_gpus'] == 2 and d['ranks_seen'] == 2
+    assert d['config']['parallelism'] == 'dp2'
+    assert d['config']['global_batch'] == 2 * d['config']['per_gpu_batch'] == 64
+    assert d['config']['hip_graph'] is True
+
+
+def test_bench_gpus1_single_process():
+    p = _run(['--dry-run', '--steps', '2'])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p)
+    assert d['n_gpus'] == 1 and d['config']['parallelism'] == 'dp1'
+
+
+def test_bench_world_size_mismatch_fails():
+    p = _run(['--gpus', '4', '--dry-run'], env_extra={'WORLD_SIZE': '2', 'RANK': '0', 'LOCAL_RANK': '0'})
+    assert p.returncode != 0
+    assert 'disagrees with WORLD_SIZE' in p.stderr

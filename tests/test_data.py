@@ -191,6 +191,12 @@ def test_prefetch_loader_and_cpu_prefetcher():
 
     with pytest.raises(ValueError, match='corrupt sample 2'):
         list(PrefetchDataLoader(num_prefetch_queue=1, dataset=Bad(), batch_size=1))
+    # a caller that catches and continues gets the error again, not a blocked queue
+    bad_it = iter(PrefetchDataLoader(num_prefetch_queue=1, dataset=Bad(), batch_size=1))
+    assert next(bad_it).item() == 0 and next(bad_it).item() == 1
+    for _ in range(2):
+        with pytest.raises(ValueError, match='corrupt sample 2'):
+            next(bad_it)
     pf = CPUPrefetcher(torch.utils.data.DataLoader(data, batch_size=5))
     assert pf.next().shape == (5, 1) and pf.next() is not None and pf.next() is None
     pf.reset()

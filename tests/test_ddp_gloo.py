@@ -201,3 +201,39 @@ def test_reducer_raises_on_extra_contribution():
         red.remove()
     finally:
         dist.destroy_process_group()
+
+
+def test_reducer_relearns_after_unfreeze():
+    """a parameter frozen on the first step (EDVR ``tsa_iter``, BasicVSR ``fix_flow``)
+    and unfrozen later must not abort the step: a change of the requires_grad set makes the next
+    step a learning step (every bucket at the join), after which buckets go out during backward
+    again.  ``find_unused_parameters`` keeps every step at the join (world 1, gloo)."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(_free_port())
+    dist.init_process_group('gloo', rank=0, world_size=1)
+    try:
+        net = _TwiceNet()
+        flat = FlatParams(net)
+        red = GradBucketReducer(flat, bucket_mb=0.0005, last_bucket_mb=0.0005)
+        x = torch.randn(2, 16)
+        logs = []
+        for step in range(4):
+            net.w1.requires_grad_(step >= 1)
+            flat.zero_grad()
+            net(x).sum().backward()
+            red.wait()
+            logs.append(sorted(w for _, w in red.last_issue_log))
+            if step == 0:
+                assert red.expected[0] == 0
+        assert red.expected == [3, 2]
+        assert logs[1] == ['wait', 'wait'] and logs[2] == ['backward', 'backward'], logs
+        red.remove()
+        red = GradBucketReducer(flat, bucket_mb=0.0005, last_bucket_mb=0.0005, find_unused=True)
+        for step in range(2):
+            flat.zero_grad()
+            net(x).sum().backward()
+            red.wait()
+            assert all(w == 'wait' for _, w in red.last_issue_log)
+        red.remove()
+    finally:
+        dist.destroy_process_group()

@@ -138,3 +138,25 @@ def test_metric_registry_dispatch():
     assert abs(v - calculate_ssim(a, b, 4, test_y_channel=True)) < 1e-12
     v = calculate_metric(dict(img=a, img2=b), dict(type='calculate_psnr', crop_border=4, test_y_channel=False))
     assert abs(v - calculate_psnr(a, b, 4)) < 1e-12
+
+
+def test_minusone_one_to_ubyte_matches_oracle():
+    """The fork's [-1, 1] -> uint8 conversion (basicsr/utils/img_util.py:99-128: clamp, (x + 1) / 2,
+    make_grid normalize over (0, 1), img_as_ubyte) against the numpy restatement in
+    oracle/metrics.py, bit-exact: 4-band and 1-band images, one image and a padded batch row,
+    values outside [-1, 1]; known answers -1 -> 0, 0 -> 128 (127.5 rounds half to even), 1 -> 255."""
+    import numpy as np
+    import torch
+
+    from basicsr4rs_amd.utils.img_util import minusone_one_tensor_to_ubyte_numpy
+    from oracle import metrics as OM
+    g = torch.Generator().manual_seed(5)
+    for shape in ((1, 4, 9, 7), (3, 4, 5, 6), (1, 1, 4, 4), (2, 1, 3, 5), (2, 3, 4, 4)):
+        t = torch.rand(shape, generator=g) * 3 - 1.5
+        got = minusone_one_tensor_to_ubyte_numpy(t)
+        ref = OM.minusone_one_to_ubyte(t.numpy())
+        assert got.dtype == np.uint8 and got.shape == ref.shape, (shape, got.shape, ref.shape)
+        assert np.array_equal(got, ref), shape
+    k = minusone_one_tensor_to_ubyte_numpy(torch.tensor([-1.0, 0.0, 1.0, -7.0]).view(1, 1, 1, 4))
+    assert k[0, :, 0].tolist() == [0, 128, 255, 0]
+    assert minusone_one_tensor_to_ubyte_numpy(torch.zeros(2, 4, 3, 3)).shape == (3 + 4, 2 * (3 + 2) + 2, 4)

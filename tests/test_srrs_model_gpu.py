@@ -125,3 +125,74 @@ def test_srrs_bf16_step_and_nan_skip(cuda, mtype, net):
     cos = torch.nn.functional.cosine_similarity(d_gpu.double(), d_ref.double(), dim=0).item()
     print(f'{mtype} bf16: loss {loss:.6f} vs oracle fp32 {losses[0]:.6f}, update cosine {cos:.4f}')
     assert cos >= 0.98, cos
+
+
+class _ValSet(torch.utils.data.Dataset):
+    """Two 4-band [-1, 1] LR / GT pairs (a 16x16 and a 12x12 LR tile: the second is padded to the
+    window by SwinIRModel.test) with reference-style paths."""
+
+    def __init__(self):
+        self.opt = {'name': 'S2N_val'}
+        g = torch.Generator().manual_seed(11)
+        self.items = []
+        for i, hw in enumerate((16, 12)):
+            lq = torch.rand(4, hw, hw, generator=g) * 2.2 - 1.1
+            gt = torch.rand(4, 4 * hw, 4 * hw, generator=g) * 2 - 1
+            self.items.append({'lq': lq, 'gt': gt, 'lq_path': f'val/lq/tile_{i}.png'})
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        return self.items[i]
+
+
+def test_swinirrs_validation_minusone_one(cuda, tmp_path):
+    """SwinIRRSModel validation on [-1, 1] 4-band tensors (basicsr/models/srrs_model.py:93-138,
+    basicsr/utils/img_util.py:99-128): per-image PSNR / SSIM on the clamp / (x + 1) / 2 / uint8
+    images equal the oracle's (net forward restated on the CPU in fp32, SwinIRModel.test's reflect
+    pad and crop, oracle/metrics.py conversion and PSNR) within 0.05 dB; the averages, the per-image
+    CSV and the RGB / NIR images land where the reference writes them."""
+    import csv
+    import os
+
+    import numpy as np
+    from torch.nn import functional as F
+
+    from basicsr4rs_amd.models import build_model
+    from oracle import metrics as OM
+    net = dict(SWINIR, in_chans=4)
+    opt = _opt('SwinIRRSModel', net, amp=False)
+    opt['name'] = 'rs_val'
+    opt['path'] = {'visualization': str(tmp_path / 'vis')}
+    opt['val'] = {'metrics': {'psnr': {'type': 'calculate_psnr', 'crop_border': 4, 'test_y_channel': False},
+                              'ssim': {'type': 'calculate_ssim', 'crop_border': 4, 'test_y_channel': False}}}
+    torch.manual_seed(0)
+    model = build_model(opt)
+    sd = {k: v.detach().cpu().clone() for k, v in model.net_g_ema.state_dict().items()}
+    ds = _ValSet()
+    loader = torch.utils.data.DataLoader(ds, batch_size=1)
+    model.validation(loader, 7, None, save_img=True)
+
+    ref_psnr = []
+    for it in ds.items:
+        lq = it['lq'][None]
+        h = lq.shape[-1]
+        pad = (8 - h % 8) % 8
+        x = F.pad(lq, (0, pad, 0, pad), 'reflect')
+        with torch.no_grad():
+            out = _oracle(net, sd, x)[:, :, :4 * h, :4 * h]
+        ref_psnr.append(OM.psnr(OM.minusone_one_to_ubyte(out.numpy()),
+                                OM.minusone_one_to_ubyte(it['gt'][None].numpy()), 4))
+    rows = list(csv.reader(open(tmp_path / 'vis' / 'S2N_val_7.csv')))
+    assert rows[0] == ['', 'psnr', 'ssim']
+    assert [r[0] for r in rows[1:]] == ['val/lq/tile_0', 'val/lq/tile_1']  # srrs_model.py:150-152
+    got = [float(r[1]) for r in rows[1:]]
+    print('validation psnr', got, 'oracle', ref_psnr)
+    assert np.allclose(got, ref_psnr, atol=0.05), (got, ref_psnr)
+    assert abs(model.metric_results['psnr'] - float(np.mean(ref_psnr))) < 0.05
+    assert all(0.0 < float(r[2]) <= 1.0 for r in rows[1:])
+    for key in ('lq', 'gt', 'sr_7'):
+        assert os.path.exists(tmp_path / 'vis' / 'RGB' / 'S2N_val' / 'val/lq/tile_0' / f'{key}.png')
+        assert os.path.exists(tmp_path / 'vis' / 'NIR' / 'S2N_val' / 'val/lq/tile_1' / f'{key}.png')
+    assert not os.path.exists(tmp_path / 'vis' / 'RGB' / 'S2N_val' / 'val/lq/tile_0' / 'sr.png')
