@@ -75,7 +75,11 @@ class SegmentedStepGraph:
         assert self._cur is None, 'segment already open'
         with torch.cuda.stream(self.stream):
             g = torch.cuda.CUDAGraph()
-            g.capture_begin(pool=self.pool)
+            # thread-local capture mode: RCCL's watchdog thread polls its collectives' events
+            # (hipEventQuery) while a segment is being captured; in the default global mode that
+            # poll fails with 'operation not permitted when stream is capturing' and the
+            # watchdog aborts the process (seen with --ddp at world 1, round 4)
+            g.capture_begin(pool=self.pool, capture_error_mode='thread_local')
             self._tick.add_(1)  # the segment's first node
         self._cur, self._cur_buckets = g, []
 

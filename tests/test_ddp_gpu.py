@@ -182,11 +182,22 @@ def _nccl_worker(port, q):
         o = _opt(True, 1, 0, 0.05, False, graph)
         o['train']['use_amp'] = True
         model = build_model(o)
+        if graph:
+            # hold each capture for a while so RCCL's watchdog thread polls its pending work (an event
+            # query) during it: in the global capture mode that poll aborts the process
+            import time
+
+            def _slow_capture(mod, inp):
+                if torch.cuda.is_current_stream_capturing():
+                    time.sleep(0.3)
+            model.get_bare_model(model.net_g).register_forward_pre_hook(_slow_capture)
         losses = []
         for step in range(1, 6):
             lq, gt = _batch(step)
             model.feed_data({'lq': lq, 'gt': gt})
             model.update_learning_rate(step)
+            if graph and step == 3:  # the capture step: a collective still in the watchdog's list
+                dist.all_reduce(torch.ones(1, device='cuda'))
             model.optimize_parameters(step)
             losses.append(model.get_current_log()['l_pix'])
         net = model.get_bare_model(model.net_g)
@@ -198,7 +209,8 @@ def _nccl_worker(port, q):
 
 def test_ddp_graph_segments_rccl_world1_bitwise(cuda):
     """The segmented-graph DDP step over RCCL (world 1 on the one card, bf16): graph replays are
-    bitwise equal to the eager DDP steps."""
+    bitwise equal to the eager DDP steps, and a capture that overlaps a poll of RCCL's watchdog
+    thread survives it (thread-local capture mode; round 4: `bench.py --ddp` aborted in global mode)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))

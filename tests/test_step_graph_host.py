@@ -12,8 +12,10 @@ from basicsr4rs_amd.utils import step_graph
 
 class _FakeGraph:
     log = []
+    modes = []
 
-    def capture_begin(self, pool=None):
+    def capture_begin(self, pool=None, capture_error_mode="global"):
+        _FakeGraph.modes.append(capture_error_mode)
         _FakeGraph.log.append('begin')
 
     def capture_end(self):
@@ -85,3 +87,5 @@ def test_capture_segments_in_order(fake_cuda):
     assert [k for _, _, k in seg.segments] == ['forward', 'backward', 'backward', 'optimizer']
     assert seg.segments[1][1] == [(1, 'backward')]
     assert fake_cuda.log.count('begin') == fake_cuda.log.count('end') == 4
+    # thread-local capture: RCCL's watchdog thread may poll events while a segment is captured
+    assert set(fake_cuda.modes) == {'thread_local'}
