@@ -3721,6 +3721,181 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Tap-row weight gradient over 12 waves (round 4): a block owns kernel row ty (taps 3 ty + tx),
+// a 128 (co) x 128 (ci) tile and a pixel K-range of whole 64-px row segments.  Per K-step it DMAs
+// the dy tile [64 px][128 co] and ONE x halo row [66 px][128 ci] (x row y + ty - 1, columns
+// x0 - 1 .. x0 + 64) -- 33 KB for 3 x 128 x 128 x 64 MACs, against the pp kernel's 64 KB for
+// 256 x 256 x 64: 1.5x fewer L2 -> LDS bytes per MAC (the pp kernel is bound by them: DMA-only
+// 121 us, MFMA-only 116 us, both 184 us on the EDSR-L body, DESIGN.md note 2c).  Wave w = (tap
+// tx = w / 4, co half, ci half) owns 64 x 64 of one tap (16 accumulator tiles, 64 registers), so
+// the three taps' MFMAs run on different waves at once instead of in three barrier-separated
+// phases (conv3x3_wgrad_tr3_kernel: six barriers per step, 172 us MFMA + LDS only).  Three stages,
+// two steps in flight, ONE barrier per step; every wave issues exactly three 1-KB LDS-DMAs per
+// step (dy pieces, x pieces, padding to a dummy slot), so its vmcnt waits are constants.  Bias
+// gradient by grouped bias-role blocks (the pp kernel's, 8 waves of 12).  Slab and reduce: the pp
+// kernel's [split][tap][co][ci].  DBG (timing ablations, wrong results): 1 no DMA after the
+// prologue, 2 no MFMA.
+// ------------------------------------------------------------------------------------
+template <int DBG = 0>
+__global__ __launch_bounds__(768, 1) void conv3x3_wgrad_tw_kernel(WgArgs a) {
+  constexpr int DYB = 64 * 256;          // dy image [64 px][256 B], stage s at s * DYB
+  constexpr int XB = 68 * 256;           // x halo image [66 (68) px][256 B], stage s at XOFF + s * XB
+  constexpr int XOFF = 3 * DYB;
+  constexpr int DUMMY = XOFF + 3 * XB;   // target of the padding DMAs
+  constexpr int SMEM = DUMMY + 1024;
+  static_assert(SMEM >= 64 * 1024 + 32 * 1024, "bias role LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = 3 * a.tiles_co * a.tiles_ci;
+  if ((int)b >= a.splits * ntile) {  // bias role: bias_group splits of one 256-co tile (8 waves)
+    if (w >= 8) return;
+    const int bb = (int)b - a.splits * ntile;
+    const int t256 = (a.Cout + 255) / 256;
+    const int grp = bb / t256, co_t = bb - grp * t256;
+    const int s1 = min(a.splits, (grp + 1) * a.bias_group);
+    for (int sp = grp * a.bias_group; sp < s1; ++sp) {
+      if (sp > grp * a.bias_group) __syncthreads();
+      wgrad_bias_role(a, smem, sp, co_t * 256);
+    }
+    return;
+  }
+  const int split = (int)b / ntile;
+  int rem = (int)b - split * ntile;
+  const int ty = rem / (a.tiles_co * a.tiles_ci);
+  rem -= ty * a.tiles_co * a.tiles_ci;
+  const int co0 = (rem / a.tiles_ci) * 128;
+  const int ci0 = (rem % a.tiles_ci) * 128;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+
+  // DMA slots m = 0..2 of this wave: slot s = w + 12 m < 16: dy piece s (rows 4s ..); < 33: x piece
+  // s - 16 (halo rows 4(s - 16) ..); else the dummy target.  Lane -> row base + (lane >> 4), 16-B
+  // slot lane & 15 holding the logical chunk lc of the swizzled 256-B row.
+  auto lchunk = [&](int R) {
+    const int f = (R & 3) | (((R >> 3) & 1) << 2);
+    const int sl = lane & 15;
+    return (((sl >> 1) ^ f) << 1) | (sl & 1);
+  };
+  int kind[3], lrow[3];
+  uint32_t loff[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int sl = w + 12 * m;
+    kind[m] = sl < 16 ? 0 : (sl < 33 ? 1 : 2);
+    const int R = (kind[m] == 0 ? 4 * sl : 4 * (sl - 16)) + (lane >> 4);
+    lrow[m] = kind[m] == 1 ? (R < 66 ? R : -1000000) : R;
+    loff[m] = kind[m] == 0 ? (uint32_t)(R * a.ldy) * 2u + (uint32_t)lchunk(R) * 16u
+                           : (uint32_t)(R * a.ldx) * 2u + (uint32_t)lchunk(R) * 16u;
+  }
+  int s_ua = 0, s_ub = 0, s_xm1 = 0, s_yv = 0;
+  auto k_eval = [&](int ks) {
+    const int p0s = p_begin + ks * 64;
+    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
+    const int x0 = p0s - q * a.W;
+    const int n = (int)fdiv((uint32_t)q, a.fd_H);
+    const int y = q - n * a.H;
+    const int yy = y + ty - 1;
+    s_ua = __builtin_amdgcn_readfirstlane((p0s * a.ldy + a.ycoff + co0) * 2);
+    s_ub = __builtin_amdgcn_readfirstlane((((n * a.H + yy) * a.W + x0 - 1) * a.ldx + a.xcoff + ci0) * 2);
+    s_xm1 = __builtin_amdgcn_readfirstlane(x0 - 1);
+    s_yv = __builtin_amdgcn_readfirstlane((unsigned)yy < (unsigned)a.H ? 1 : 0);
+  };
+  auto issue = [&](int ks, bool real) {
+    if (DBG == 1 && ks > 1) real = false;
+    const int st = ks % 3;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int sl = w + 12 * m;
+      if (kind[m] == 0) {
+        glds16(dyr, real ? smem + st * DYB + sl * 1024 : smem + DUMMY, real ? (uint32_t)s_ua + loff[m] : SR_OOB);
+      } else if (kind[m] == 1) {
+        const bool v = real && s_yv && (unsigned)(s_xm1 + lrow[m]) < (unsigned)a.W;
+        glds16(xr, real ? smem + XOFF + st * XB + (sl - 16) * 1024 : smem + DUMMY, v ? (uint32_t)s_ub + loff[m] : SR_OOB);
+      } else {
+        glds16(xr, smem + DUMMY, SR_OOB);
+      }
+    }
+  };
+
+  // fragment offsets (kk = 0 rows; kk = 1 is +8192 B), computed once
+  const int tx = w >> 2, wco = (w >> 1) & 1, wci = w & 1;
+  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  uint32_t offA[4][2], offB[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+      offA[i][hl] = swz_tr(8 * tg + tq + 4 * hl, (wco * 64 + i * 16 + 4 * tp) * 2, 256);
+      offB[i][hl] = XOFF + swz_tr(tx + 8 * tg + tq + 4 * hl, (wci * 64 + i * 16 + 4 * tp) * 2, 256);
+    }
+  auto lds_tr = [&](uint32_t off) -> s16x4 {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(smem + off));
+  };
+  auto cat8 = [](s16x4 lo, s16x4 hi) { return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}; };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p_end - p_begin) / 64;  // >= 1 (whole 64-px row segments)
+  k_eval(0);
+  issue(0, true);
+  if (nk > 1) k_eval(1);
+  issue(1, nk > 1);
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // step ks + 1's 3 DMAs stay in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    // stage (ks + 2) % 3 was last read in step ks - 1, finished by every wave before this barrier
+    if (ks + 2 < nk) {
+      k_eval(ks + 2);
+      issue(ks + 2, true);
+    } else {
+      issue(ks + 2, false);  // keep the per-step DMA count (vmcnt arithmetic) constant
+    }
+    const int st = ks % 3;
+    const uint32_t sa = st * DYB, sb = st * XB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = cat8(lds_tr(offA[i][0] + sa + kk * 8192), lds_tr(offA[i][1] + sa + kk * 8192));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = cat8(lds_tr(offB[j][0] + sb + kk * 8192), lds_tr(offB[j][1] + sb + kk * 8192));
+      if constexpr (DBG != 2) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // slab [split][tap][co][ci]: 16 lanes store 64 consecutive bytes of a co row
+  const int tap = 3 * ty + tx;
+  float* ws = a.ws + ((size_t)split * 9 + tap) * a.Cout * a.Cin;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wco * 64 + 16 * i + 4 * tg + r;
+        const int ci = ci0 + wci * 64 + 16 * j + (lane & 15);
+        ws[(size_t)co * a.Cin + ci] = acc[i][j][r];
+      }
+}
+
+// ------------------------------------------------------------------------------------
 // Weight gradient for narrow convs (Cout <= 64: RCAN / RRDB / SRResNet bodies), all nine
 // taps in one block.  A 64-pixel K-step is one image-row segment (W % 64 == 0); the block
 // stages dy[64 px][Cout] once and the x halo rows y-1..y+1, cols x0-1..x0+64 of its
@@ -3890,8 +4065,14 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
 // ring slot and dy stage), so a step needs ONE barrier; otherwise the issue waits for a second barrier
 // after the MFMAs.  Measured slower: the extra LDS (RCAN 78 -> 99 KB, RRDB 70 -> 87 KB) costs the
 // second block per CU (RRDB 65.5 -> 73 ms).  LA: fragment reads in flight ahead of the MFMA group.
-template <int CO_T, int D = 2, int LA = 3, bool EARLY = false>  // D: steps in flight
-__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
+// VB = 2 (round 4): an 8-wave block of two 4-wave row groups, each with its own ring and dy stages
+// (2 x 78 KB of LDS), walking the two halves of the split's rows in lock-step (same barriers; a
+// group with fewer rows idles through the extra steps); at the end group 1 hands its accumulators
+// to group 0 through LDS and group 0 writes ONE slab for the block.  Against two 4-wave blocks per
+// CU (VB = 1) it halves the slab written per CU (and read by the reduce) at the same occupancy.
+template <int CO_T, int D = 2, int LA = 3, bool EARLY = false, int VB = 1>  // D: steps in flight
+__global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
+  static_assert(VB == 1 || (VB == 2 && !EARLY), "two row groups: the two-barrier schedule only");
   constexpr int CW = CO_T;  // co tiles per wave
   constexpr int RS = 3 * 1024;      // one halo row of one 16-ci tile: 96 rows x 32 B (66 used)
   constexpr int RSL = D + (EARLY ? 3 : 2);  // ring slots: rows q-1 .. q+1 read, D - 1 in flight (+1 being issued)
@@ -3900,10 +4081,13 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   constexpr int DYS = DYB + 1024;   // + 1 KB target for padding DMAs
   constexpr int DYI = (CO_T * 2 + 3) / 4;  // dy DMAs per wave
   constexpr int DST = D + (EARLY ? 1 : 0);  // dy stages
-  __shared__ __attribute__((aligned(16))) char smem[4 * RING + DST * DYS];
+  constexpr int GRP = 4 * RING + DST * DYS;  // LDS of one row group
+  static_assert(VB == 1 || GRP * VB >= (4 * 9 * CW + CW) * 64 * 16, "LDS hand-over of group 1's accumulators");
+  __shared__ __attribute__((aligned(16))) char smem[VB * GRP];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wl = w;
+  const int wl = w & 3;  // wave within its row group
+  const int vb = w >> 2;  // row group
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
   // block = (split, co tile, ci chunk), ci fastest: the tiles of one split (the same x / dy rows)
   // are consecutive, so xcd_remap keeps them on one XCD's L2
@@ -3919,14 +4103,18 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   const int ps_si = a.out_ps > 0 ? ps_sl / a.out_ps : 0, ps_sj = a.out_ps > 0 ? ps_sl - ps_si * a.out_ps : 0;
   const int rows_total = a.N * a.H;
   const int rps = a.kper / a.W;  // image rows per split
-  const int r0 = split * rps, r1 = min(rows_total, r0 + rps);
+  const int rs0 = split * rps, rs1 = min(rows_total, rs0 + rps);
+  // this row group's rows: the first ceil(n / VB) of the split's n rows, or the rest
+  const int rhalf = (rs1 - rs0 + VB - 1) / VB;
+  const int r0 = min(rs1, rs0 + vb * rhalf), r1 = min(rs1, r0 + rhalf);
   const int nrows = r1 - r0, nseg = a.W >> 6, nk = nrows * nseg;
+  const int nk_all = rhalf * nseg;  // steps of the block (group 0 has the most rows)
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const int sh = a.in_up > 1 ? 1 : 0;  // in_up is 1 or 2 here
   const int Hs = a.H >> sh, Ws = a.W >> sh;
-  char* ring = smem + wl * RING;
-  char* dys = smem + 4 * RING;
+  char* ring = smem + vb * GRP + wl * RING;
+  char* dys = smem + vb * GRP + 4 * RING;
   auto slot = [](int q) { return (q + RSL) % RSL; };  // q >= -1
   constexpr bool xdma = true;  // every wave loads its ci tile's x rows and some dy
 
@@ -3985,7 +4173,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
     char* st = dys + (j % DST) * DYS;
 #pragma unroll
     for (int i = 0; i < DYI; ++i) {
-      const int k = w + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
+      const int k = wl + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
       char* dst = st + DYB;
       uint32_t off = SR_OOB;
       if (k < CO_T * 2) {
@@ -4066,7 +4254,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   const bool early = EARLY && nseg == 1;
   int next = 0;  // steps issued so far, in step order (issue_iter is non-decreasing)
   while (next < nk && issue_iter(next) < 0) issue(next++);
-  for (int ks = 0; ks < nk; ++ks) {
+  for (int ks = 0; ks < nk_all; ++ks) {
+    if (VB > 1 && ks >= nk) {  // a group out of rows keeps the block's barriers
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
+      continue;
+    }
 #ifdef SR_BAND_STAMPS
     const unsigned long long t0 = __builtin_readcyclecounter();
 #endif
@@ -4110,6 +4303,27 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (VB > 1) {
+    // every wave passed the last step's second barrier after its LDS reads (lgkmcnt(0)) and no
+    // DMA is in flight: the rings are free.  Group 1 stores its accumulators (and wave 0's bias
+    // sums), group 0 adds them in a fixed order (deterministic).
+    f32x4* hand = (f32x4*)smem;
+    f32x4* handb = hand + 4 * 9 * CW * 64;
+    if (vb == 1) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int c = 0; c < CW; ++c) hand[((wl * 9 + t) * CW + c) * 64 + lane] = acc[t][c];
+      if (do_bias)
+#pragma unroll
+        for (int c = 0; c < CW; ++c) handb[c * 64 + lane] = accb[c];
+    }
+    __syncthreads();
+    if (vb == 1) return;
+    if (do_bias)
+#pragma unroll
+      for (int c = 0; c < CW; ++c) accb[c] += handb[c * 64 + lane];
+  }
   // slab [split][tap][ci][co] (co fastest): a lane's 4 accumulator rows are 4 consecutive co,
   // so one 16-B store per (tap, co tile) per lane (a [co][ci] slab takes four 4-B ones)
   const int c16 = lane & 15;
@@ -4121,8 +4335,12 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
 #pragma unroll
       for (int c = 0; c < CW; ++c) {
         const int co = co0 + (ct0 + c) * 16 + g * 4;
-        if (c < ncw && co < a.Cout) *(f32x4*)(ws + co) = acc[t][c];
+        f32x4 v = acc[t][c];
+        if constexpr (VB > 1) v += ((const f32x4*)smem)[((wl * 9 + t) * CW + c) * 64 + lane];  // group 1's sums
+        if (c < ncw && co < a.Cout) *(f32x4*)(ws + co) = v;
       }
+      // one tap at a time: the hand-over reads must not be hoisted next to 36 live accumulators
+      if constexpr (VB > 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
 #ifdef SR_BAND_STAMPS
@@ -4985,6 +5203,31 @@ bool wg_use_tr3(const sr_conv3x3_wgrad_desc* d) {
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
 
+// 12-wave tap-row wgrad (conv3x3_wgrad_tw_kernel): bf16 3x3, no pixel shuffle / upsample,
+// Cout, Cin multiples of 128, W % 64 == 0 (the EDSR-L body shape).  Opt-in while it is measured:
+// SR_WG_TW=1 (read once) or variant 70; variants 71 / 72 are its DBG ablations (wrong results).
+bool wg_use_tw(const sr_conv3x3_wgrad_desc* d) {
+  static const bool on = [] {
+    const char* e = getenv("SR_WG_TW");
+    return e && atoi(e) == 1;
+  }();
+  if (!(on || (g_variant >= 70 && g_variant <= 72))) return false;
+  return d->dtype == SR_BF16 && d->ksize == 3 && d->in_up <= 1 && d->out_ps == 0 && d->W % 64 == 0 &&
+         d->Cout % 128 == 0 && d->Cin % 128 == 0 && (size_t)d->N * d->H * d->W * d->Cin * 2 < 0x80000000ull;
+}
+
+// Splits per bias-role block of the tw kernel: 1, or SR_TW_BG (read once).  A bias block streams
+// dy at ~60 GB/s (one block per CU, two stages in flight), so at the tw plan's ~100 K-steps per split
+// a group of 3 splits (the pp kernel's) made the bias blocks the critical path (190 vs 186 us).
+int tw_bias_group() {
+  static const int v = [] {
+    const char* e = getenv("SR_TW_BG");
+    const int x = e ? atoi(e) : 1;
+    return x >= 1 && x <= 8 ? x : 1;
+  }();
+  return v;
+}
+
 // Splits per bias-role block of the pp kernel (0: one bias block per split, interleaved with the
 // tile blocks).  The bias role reads dy only, so a third of the CUs' worth of bias blocks can take
 // three splits each and the tile blocks get more, shorter splits (EDSR-L body wgrad, 247 blocks:
@@ -5089,6 +5332,24 @@ int ring_depth() {
   return v;
 }
 
+bool ring_early();
+int ring_depth();
+int ring_la();
+bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d);
+// 16-channel co tiles per wave of the ring / halo wgrad
+int ring_ct(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? 4 : (d->Cout + 15) / 16; }
+// Row groups per ring-wgrad block: 2 (8-wave blocks, one per CU, one slab per block; CO_T <= 2 --
+// at 3 / 4 co tiles per wave the two-waves-per-SIMD register budget spills), or
+// SR_RING_VB=1 (4-wave blocks, two per CU; A/B) / variant 69 (parity tests of the 4-wave form).
+// The early-issue and deeper-pipeline A/B forms are 4-wave only.
+int ring_vb() {
+  static const int v = [] {
+    const char* e = getenv("SR_RING_VB");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return (g_variant == 69 || ring_early() || ring_depth() != 2 || ring_la() != 3) ? 1 : v;
+}
+
 // Early DMA issue in the ring wgrad (one barrier per step, one more LDS slot): SR_RING_EARLY=1 (A/B; read once)
 bool ring_early() {
   static const bool v = [] {
@@ -5116,7 +5377,9 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     // ~2 blocks per CU, but at least 8 K-steps per block (the slab costs 8 B per tap-MAC row)
     // (A/B on RCAN / RRDB: twice or half as many splits are 6-12 % slower per step)
     const int chunks = (d->Cin + 63) / 64;
-    int S = wg_ring_wide(d) ? ring_wide_target() / (chunks * ((d->Cout + 63) / 64)) : ring_split_target() / chunks;
+    // (an 8-wave two-row-group block takes a CU alone: half the block target)
+    const int vbdiv = wg_use_ring() && ring_ct(d) <= 2 ? ring_vb() : 1;
+    int S = (wg_ring_wide(d) ? ring_wide_target() / (chunks * ((d->Cout + 63) / 64)) : ring_split_target() / chunks) / vbdiv;
     const int maxS = M / 512 > 1 ? M / 512 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
@@ -5137,6 +5400,19 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     const int tiles = ((d->Cout + 191) / 192) * ((d->Cin + 191) / 192);
     int S = lin_wg_target() / tiles;
     const int maxS = (M + 63) / 64;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
+  if (wg_use_tw(d)) {  // one 12-wave block per CU, bias-role blocks of tw_bias_group() splits
+    const int tco = (d->Cout + 255) / 256, ntile = 3 * (d->Cout / 128) * (d->Cin / 128), bg = tw_bias_group();
+    int S = (int)(256.0 / (ntile + (double)tco / bg));
+    while (S > 1 && S * ntile + (S + bg - 1) / bg * tco > 256) --S;
+    const int maxS = (M + 255) / 256;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
     int kp = (M + S - 1) / S;
@@ -5388,6 +5664,7 @@ int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d) {
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
   if (wg_use_halo(d)) return wg_use_ring() ? "conv3x3_wgrad_ring_kernel" : "conv3x3_wgrad_halo_kernel";
   if (wg_use_lin(d)) return "linear_wgrad_kernel";
+  if (wg_use_tw(d)) return "conv3x3_wgrad_tw_kernel";
   if (wg_use_tr3(d)) return "conv3x3_wgrad_tr3_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
@@ -5397,7 +5674,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 68)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 72)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -5523,14 +5800,16 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   if (wg_use_halo(d)) {
     a.tiles_co = wg_ring_wide(d) ? (a.Cout + 63) / 64 : 1;
     a.tiles_ci = (a.Cin + 63) / 64;
-    const int ct = wg_ring_wide(d) ? 4 : (a.Cout + 15) / 16;
+    const int ct = ring_ct(d);
     const dim3 grid(S * a.tiles_ci * a.tiles_co);
     if (wg_use_ring()) {
       const int D = ring_depth();
       a.ring_early = ring_early() ? 1 : 0;
       const int la = ring_la();
+      const int vbn = ring_vb();
 #define SR_RING(CT_)                                                                                     \
-  if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);        \
+  if (vbn == 2 && CT_ <= 2) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<(CT_ <= 2 ? CT_ : 2), 2, 3, false, 2>), grid, dim3(512), 0, s, a); \
+  else if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);   \
   else if (D == 3) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 3>), grid, dim3(256), 0, s, a);   \
   else if (la == 5) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 5>), grid, dim3(256), 0, s, a); \
   else if (a.ring_early) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 3, true>), grid, dim3(256), 0, s, a); \
@@ -5549,6 +5828,16 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.tiles_co = (a.Cout + 191) / 192;
     a.tiles_ci = (a.Cin + 191) / 192;
     hipLaunchKernelGGL(linear_wgrad_kernel, dim3(S * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+    e = hipGetLastError();
+  } else if (wg_use_tw(d)) {
+    a.tiles_co = a.Cout / 128;
+    a.tiles_ci = a.Cin / 128;
+    a.bias_group = tw_bias_group();
+    const int nb = S * 3 * a.tiles_co * a.tiles_ci +
+                   (a.wsb ? (S + a.bias_group - 1) / a.bias_group * ((a.Cout + 255) / 256) : 0);
+    if (g_variant == 71) hipLaunchKernelGGL(conv3x3_wgrad_tw_kernel<1>, dim3(nb), dim3(768), 0, s, a);
+    else if (g_variant == 72) hipLaunchKernelGGL(conv3x3_wgrad_tw_kernel<2>, dim3(nb), dim3(768), 0, s, a);
+    else hipLaunchKernelGGL(conv3x3_wgrad_tw_kernel<0>, dim3(nb), dim3(768), 0, s, a);
     e = hipGetLastError();
   } else if (wg_use_tr3(d)) {
     a.tiles_co = a.Cout / 128;

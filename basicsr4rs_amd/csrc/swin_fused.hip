@@ -1,0 +1,422 @@
+// Fused SwinIR attention half-block forward (round 4):
+//
+//   x2 = x + s1[n] * proj(WindowAttention(qkv(LN1(x))))          (basicsr/archs/swinir_arch.py:283-314,
+//                                                                   WindowAttention :144-175)
+//
+// in ONE kernel, for bf16, window 8, head_dim <= 32 (heads padded to 32), nH * 32 <= 192, Cp <= 192:
+// SwinIR-M / -S (embed 180 / 60 .. 192, 6 heads) and the remote-sensing configs.  A 512-thread block
+// owns two windows (128 tokens); the token rows are gathered through the cyclic shift and window
+// partition (token_pixel), so roll / partition / reverse never materialise.  Per block:
+//
+//   0. x rows -> LayerNorm (fp32 statistics) -> LDS token tile sX [3][128][128 B] (XOR-swizzled
+//      16-B chunks), also stored to ln_out with the row mean / rstd (training: the qkv weight
+//      gradient and the LayerNorm backward read them);
+//   per head h:
+//   A. q/k/v of head h = W_h . sX^T + b (96 x 128, K = Cp): W_h's 96 rows staged in LDS sW (loaded
+//      into registers during the previous head, so the L2 round trip hides under its attention and
+//      projection); 8 waves = 2 (48 rows) x 4 (32 tokens), v_mfma_f32_16x16x32_bf16.  The results go
+//      to LDS (Q, K rows; V in the tr-read image of the attention kernel) and, training, to qkv;
+//   B. window attention of head h for both windows: wave = (window, 16-query tile): S^T = K Q^T,
+//      relative-position bias + shift mask, softmax over keys (lse stored for the backward),
+//      O^T = V^T P^T -- the wattn_fwd_mfma_kernel contractions (swin.hip) on LDS operands; O to LDS
+//      and, training, to the attention output `ao` (the proj weight gradient's input);
+//   C. x2acc += Wp[:, h*32 .. h*32 + 31] . O_h^T (184(192) x 128, K = 32), accumulated over the
+//      heads in registers (wave = 48 output channels x 64 tokens);
+//   epilogue: x2 = x + s1[n] * (x2acc + bp), 8-B stores, padded channels stay exactly zero.
+//
+// HBM per block (training): x read once, ln_out / qkv / ao / x2 written once = 343 MB per SwinIR-M
+// layer at B 32 against 540 MB for the three kernels it replaces (LN+qkv lin kernel, attention,
+// proj); inference (no saved activations): x read + x2 written, 94 MB.  The backward is unchanged
+// (it reads ln_out, qkv, ao, lse exactly as written by the unfused path).
+#include "sr_common.h"
+#include "sr_internal.h"
+#include "swin_common.h"
+
+namespace {
+
+struct SabArgs {
+  const bf16_t* x;
+  const float* ln_g;
+  const float* ln_b;
+  const bf16_t* wq;  // qkv GEMM image [3 nH 32][Cp] (row = which * nH * 32 + h * 32 + d)
+  const float* bq;   // [3 nH 32]
+  const float* table;  // [225][nH]
+  const bf16_t* wp;  // proj GEMM image [Cp][nH 32]
+  const float* bp;   // [Cp]
+  const float* rsc;  // per-image DropPath factor [N] or null
+  bf16_t* x2;
+  bf16_t* ln_out;  // training outputs (all null for inference)
+  float* mean;
+  float* rstd;
+  bf16_t* qkv;
+  bf16_t* ao;
+  float* lse;
+  int N, H, W, shift, nH, C, Cp, KC;
+  int ldq, ldo;
+  float eps, scale;
+  int nwx, nwin, nwin_total;
+};
+
+constexpr int SAB_X = 0;                      // [3 cg][128 rows][128 B]
+constexpr int SAB_W = SAB_X + 3 * 128 * 128;  // [3 cg][96 rows][128 B]
+constexpr int SAB_Q = SAB_W + 3 * 96 * 128;   // [128 tokens][64 B]
+constexpr int SAB_K = SAB_Q + 128 * 64;
+constexpr int SAB_V = SAB_K + 128 * 64;  // [2 windows][64][64 B], sx_byte layout (tr reads)
+constexpr int SAB_O = SAB_V + 128 * 64;  // [128 tokens][64 B]
+constexpr int SAB_TB = SAB_O + 128 * 64;  // float [256]: the head's bias-table column
+constexpr int SAB_GB = SAB_TB + 256 * 4;  // float [2][192]: LayerNorm gamma, beta
+constexpr int SAB_LDS = SAB_GB + 2 * 192 * 4;
+constexpr int SAB_WPIECES = 96 * 24;  // 16-B pieces of W_h (K <= 192)
+constexpr int SAB_WREG = (SAB_WPIECES + 511) / 512;
+
+// 16-B chunk ch of row r of a [cg][rows][128 B] image (chunk XOR row & 7 within its 128-B group)
+SR_DEV uint32_t tile_off(int rows, int r, int ch) {
+  return (uint32_t)((ch >> 3) * rows * 128 + r * 128 + (((ch & 7) ^ (r & 7)) << 4));
+}
+// 16-B chunk c (0..3) of token row t of a [128][64 B] image; rows 4a..4a+3 rotate the chunks by a,
+// so 16 consecutive rows reading one chunk hit 16 distinct 4-bank groups
+SR_DEV uint32_t qk_off16(int t, int c) { return (uint32_t)(t * 64 + ((c ^ ((t >> 2) & 3)) << 4)); }
+SR_DEV uint32_t qk_off(int t, int d) { return qk_off16(t, d >> 3) + (uint32_t)((d & 7) * 2); }
+
+__global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[SAB_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int blk = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const bool train = a.qkv != nullptr;
+  float* sTB = (float*)(smem + SAB_TB);
+  float* sGB = (float*)(smem + SAB_GB);
+
+  // window geometry of the block's two windows
+  auto win_of = [&](int wi, int& n, int& wy, int& wx) -> bool {
+    const int gw = 2 * blk + wi;
+    n = gw / a.nwin;
+    const int win = gw - n * a.nwin;
+    wy = win / a.nwx;
+    wx = win - wy * a.nwx;
+    return gw < a.nwin_total;
+  };
+  // token t (0..127) of the block -> pixel row (through the cyclic shift), image; false past the end
+  auto tok_pix = [&](int t, int64_t& pix, int& n) -> bool {
+    int wy, wx;
+    const bool v = win_of(t >> 6, n, wy, wx);
+    const int i = t & 63;
+    int oy = wy * 8 + (i >> 3) + a.shift, ox = wx * 8 + (i & 7) + a.shift;
+    if (oy >= a.H) oy -= a.H;
+    if (ox >= a.W) ox -= a.W;
+    pix = ((int64_t)n * a.H + oy) * a.W + ox;
+    return v;
+  };
+
+  // ---- head 0's weights into registers first (their L2 round trip overlaps the LayerNorm)
+  u32x4 wreg[SAB_WREG];
+  auto w_load = [&](int h) {
+#pragma unroll
+    for (int k = 0; k < SAB_WREG; ++k) {
+      const int p = tid + 512 * k;
+      const int rr = p / 24, ch = p - rr * 24;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (p < SAB_WPIECES && ch < a.KC) {
+        const int grow = (rr >> 5) * a.nH * 32 + h * 32 + (rr & 31);
+        v = *(const u32x4*)(a.wq + (size_t)grow * a.Cp + ch * 8);
+      }
+      wreg[k] = v;
+    }
+  };
+  auto w_store = [&]() {
+#pragma unroll
+    for (int k = 0; k < SAB_WREG; ++k) {
+      const int p = tid + 512 * k;
+      const int rr = p / 24, ch = p - rr * 24;
+      if (p < SAB_WPIECES) *(u32x4*)(smem + SAB_W + tile_off(96, rr, ch)) = wreg[k];
+    }
+  };
+  auto t_store = [&](int h) {
+    if (tid < 256) sTB[tid] = tid < 225 ? a.table[tid * a.nH + h] : 0.f;
+  };
+  w_load(0);
+  if (tid < 192) {
+    sGB[tid] = tid < a.C ? a.ln_g[tid] : 0.f;
+    sGB[192 + tid] = tid < a.C ? a.ln_b[tid] : 0.f;
+  }
+
+  // ---- 0. LayerNorm of the 128 token rows: 4 lanes per row, chunks part, part + 4, ...
+  {
+    const int r = tid >> 2, part = tid & 3;
+    int64_t pr;
+    int nr;
+    const bool vr = tok_pix(r, pr, nr);
+    u32x4 raw[6];
+    float sm = 0.f;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int ch = part + 4 * q;
+      raw[q] = (vr && ch < a.KC) ? *(const u32x4*)(a.x + pr * a.Cp + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 8 + 2 * j;
+        sm += (c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) : 0.f) + (c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) : 0.f);
+      }
+    }
+    sm += __shfl_xor(sm, 1);
+    sm += __shfl_xor(sm, 2);
+    const float mu = sm / a.C;
+    float sq = 0.f;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int ch = part + 4 * q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 8 + 2 * j;
+        const float d0 = c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) - mu : 0.f;
+        const float d1 = c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) - mu : 0.f;
+        sq += d0 * d0 + d1 * d1;
+      }
+    }
+    sq += __shfl_xor(sq, 1);
+    sq += __shfl_xor(sq, 2);
+    const float rs = rsqrtf(sq / a.C + a.eps);
+    __syncthreads();  // gamma / beta staged
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int ch = part + 4 * q;
+      u32x4 o4 = u32x4{0u, 0u, 0u, 0u};
+      if (vr && ch < a.KC) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = ch * 8 + j;
+          const float xv = bf16_to_f32((raw[q][j >> 1] >> (16 * (j & 1))) & 0xffff);
+          o[j] = c < a.C ? (xv - mu) * rs * sGB[c] + sGB[192 + c] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
+        if (train) *(u32x4*)(a.ln_out + pr * a.Cp + ch * 8) = o4;
+      }
+      *(u32x4*)(smem + SAB_X + tile_off(128, r, ch)) = o4;
+    }
+    if (train && vr && part == 0) {
+      a.mean[pr] = mu;
+      a.rstd[pr] = rs;
+    }
+  }
+  w_store();
+  t_store(0);
+  __syncthreads();
+
+  // per-wave constants
+  const int og = w & 1, tg = w >> 1;   // step A: 48 q/k/v rows x 32 tokens
+  const int wi = w >> 2, jq = w & 3;   // step B: window, 16-query tile
+  const int pog = w & 3, ptg = w >> 2;  // step C: 48 output channels x 64 tokens
+  int64_t pixA[2];
+  bool vA[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int n_;
+    vA[j] = tok_pix(tg * 32 + 16 * j + c16, pixA[j], n_);
+  }
+  int nB, wyB, wxB;
+  const bool vB = win_of(wi, nB, wyB, wxB);
+  int64_t pixB;
+  {
+    int n_;
+    tok_pix(wi * 64 + 16 * jq + c16, pixB, n_);
+  }
+  const int qq = 16 * jq + c16;  // this lane's query (B)
+  const int rq = region(wyB * 8 + (qq >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (qq & 7), a.W, 8, a.shift);
+  int rk[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = 16 * i + 4 * g + r;
+      rk[i][r] = region(wyB * 8 + (k >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (k & 7), a.W, 8, a.shift);
+    }
+
+  f32x4 xacc[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int h = 0; h < a.nH; ++h) {
+    // this head's projection columns (A operand of step C) and the next head's weights, in flight
+    u32x4 wpf[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int row = pog * 48 + 16 * i + c16;
+      wpf[i] = row < a.Cp ? *(const u32x4*)(a.wp + (size_t)row * a.ldo + h * 32 + 8 * g) : u32x4{0u, 0u, 0u, 0u};
+    }
+    if (h + 1 < a.nH) w_load(h + 1);
+
+    // ---- A: q / k / v of head h
+    f32x4 acc[3][2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const int ch = 4 * kk + g;
+      s16x8 af[3], bf[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) af[i] = *(const s16x8*)(smem + SAB_W + tile_off(96, og * 48 + 16 * i + c16, ch));
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = *(const s16x8*)(smem + SAB_X + tile_off(128, tg * 32 + 16 * j + c16, ch));
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int oc = og * 48 + 16 * i + 4 * g;  // 4 consecutive rows of q / k / v (one of them)
+      const int which = oc >> 5, d = oc & 31;
+      const int gr = which * a.nH * 32 + h * 32 + d;
+      const f32x4 bias = *(const f32x4*)(a.bq + gr);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int t = tg * 32 + 16 * j + c16;
+        uint2 u;
+        u.x = pack_bf16x2(acc[i][j][0] + bias[0], acc[i][j][1] + bias[1]);
+        u.y = pack_bf16x2(acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]);
+        if (train && vA[j]) *(uint2*)(a.qkv + pixA[j] * a.ldq + gr) = u;
+        if (which == 0) *(uint2*)(smem + SAB_Q + qk_off(t, d)) = u;
+        else if (which == 1) *(uint2*)(smem + SAB_K + qk_off(t, d)) = u;
+        else *(uint2*)(smem + SAB_V + (t >> 6) * 4096 + sx_byte(t & 63, d)) = u;
+      }
+    }
+    __syncthreads();  // S1: Q, K, V of head h in LDS
+
+    // ---- B: window attention, wave = (window wi, queries 16 jq ..)
+    {
+      const s16x8 qf = *(const s16x8*)(smem + SAB_Q + qk_off16(wi * 64 + qq, g));
+      f32x4 s[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const s16x8 kf = *(const s16x8*)(smem + SAB_K + qk_off16(wi * 64 + 16 * i + c16, g));
+        s[i] = mfma16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f});  // S^T[key 16i + 4g + r][query qq]
+      }
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * i + 4 * g + r;
+          float v = s[i][r] * a.scale + sTB[bin8(qq, k)];
+          if (a.shift && rk[i][r] != rq) v -= 100.f;
+          s[i][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(s[i][r] - mx);
+          s[i][r] = e;
+          sm += e;
+        }
+      sm += __shfl_xor(sm, 16);
+      sm += __shfl_xor(sm, 32);
+      const float inv = 1.f / sm;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[i][r] *= inv;
+      if (train && vB && g == 0) a.lse[((int64_t)(2 * blk + wi) * a.nH + h) * 64 + qq] = mx + __logf(sm);
+      f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      const char* sVw = smem + SAB_V + wi * 4096;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const s16x8 pb = frag_c2(s[2 * st], s[2 * st + 1]);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) o[d] = mfma16(frag_tr64(sVw, st, g, tq, tp, 16 * d), pb, o[d]);
+      }
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {  // O^T[dim 16d + 4g + r][query qq]
+        uint2 u;
+        u.x = pack_bf16x2(o[d][0], o[d][1]);
+        u.y = pack_bf16x2(o[d][2], o[d][3]);
+        if (train && vB) *(uint2*)(a.ao + pixB * a.ldo + h * 32 + 16 * d + 4 * g) = u;
+        *(uint2*)(smem + SAB_O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
+      }
+    }
+    __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW) and step B (sTB)
+    if (h + 1 < a.nH) {
+      w_store();
+      t_store(h + 1);
+    }
+
+    // ---- C: x2acc += Wp[:, head h] . O_h^T
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x8 of = *(const s16x8*)(smem + SAB_O + qk_off16(ptg * 64 + 16 * j + c16, g));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xacc[i][j] = mfma16(__builtin_bit_cast(s16x8, wpf[i]), of, xacc[i][j]);
+    }
+    __syncthreads();  // S3: sO read; the next head's sW / sTB written
+  }
+
+  // ---- epilogue: x2 = x + s1[n] * (proj + bias)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int oc = pog * 48 + 16 * i + 4 * g;
+    if (oc >= a.Cp) continue;
+    const f32x4 bias = *(const f32x4*)(a.bp + oc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t pix;
+      int n;
+      if (!tok_pix(ptg * 64 + 16 * j + c16, pix, n)) continue;
+      const float sc = a.rsc ? a.rsc[n] : 1.f;
+      const uint2 xv = *(const uint2*)(a.x + pix * a.Cp + oc);
+      uint2 u;
+      u.x = pack_bf16x2(bf16_to_f32(xv.x & 0xffff) + sc * (xacc[i][j][0] + bias[0]),
+                        bf16_to_f32(xv.x >> 16) + sc * (xacc[i][j][1] + bias[1]));
+      u.y = pack_bf16x2(bf16_to_f32(xv.y & 0xffff) + sc * (xacc[i][j][2] + bias[2]),
+                        bf16_to_f32(xv.y >> 16) + sc * (xacc[i][j][3] + bias[3]));
+      *(uint2*)(a.x2 + pix * a.Cp + oc) = u;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int sr_swin_attn_fused_ok(int dtype, int N, int H, int W, int ws, int nH, int hd, int hdp, int C, int Cp) {
+  return dtype == SR_BF16 && ws == 8 && hdp == 32 && hd <= 32 && nH >= 1 && nH * 32 <= 192 && Cp % 8 == 0 &&
+         Cp <= 192 && C <= Cp && C > 0 && H % 8 == 0 && W % 8 == 0 && N > 0;
+}
+
+int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, int C, float eps, const void* wqkv,
+                           const float* bqkv, const float* bias_table, const void* wproj, const float* bproj,
+                           const float* row_scale, int N, int H, int W, int shift, int nH, int Cp, float scale, void* x2,
+                           void* ln_out, float* ln_mean, float* ln_rstd, void* qkv, void* attn_out, float* lse,
+                           void* stream) {
+  if (!x || !ln_g || !ln_b || !wqkv || !bqkv || !bias_table || !wproj || !bproj || !x2)
+    return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: null pointer");
+  const bool train = qkv != nullptr;
+  if (train && (!ln_out || !ln_mean || !ln_rstd || !attn_out || !lse))
+    return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: training needs ln_out, mean, rstd, qkv, attn_out and lse");
+  if (!sr_swin_attn_fused_ok(SR_BF16, N, H, W, 8, nH, 32, 32, C, Cp) || shift < 0 || shift >= 8)
+    return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: bf16, window 8, head dim <= 32, nH * 32 <= 192, Cp <= 192");
+  SabArgs a{};
+  a.x = (const bf16_t*)x; a.ln_g = ln_g; a.ln_b = ln_b; a.wq = (const bf16_t*)wqkv; a.bq = bqkv;
+  a.table = bias_table; a.wp = (const bf16_t*)wproj; a.bp = bproj; a.rsc = row_scale;
+  a.x2 = (bf16_t*)x2; a.ln_out = (bf16_t*)ln_out; a.mean = ln_mean; a.rstd = ln_rstd;
+  a.qkv = (bf16_t*)qkv; a.ao = (bf16_t*)attn_out; a.lse = lse;
+  a.N = N; a.H = H; a.W = W; a.shift = shift; a.nH = nH; a.C = C; a.Cp = Cp; a.KC = Cp / 8;
+  a.ldq = 3 * nH * 32; a.ldo = nH * 32;
+  a.eps = eps; a.scale = scale;
+  a.nwx = W / 8; a.nwin = (H / 8) * (W / 8); a.nwin_total = N * a.nwin;
+  const int blocks = (a.nwin_total + 1) / 2;
+  hipLaunchKernelGGL(swin_attn_block_fwd_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
+  return sr_check(hipGetLastError(), "swin_attn_fused_fwd launch");
+}
+
+}  // extern "C"

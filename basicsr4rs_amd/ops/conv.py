@@ -13,6 +13,7 @@ autocast is enabled (the reference's AMP path, basicsr/models/srrs_model.py:28-3
 fp16; bf16 is the documented divergence), fp32 otherwise.
 """
 import ctypes
+import weakref
 import math
 
 import torch
@@ -123,10 +124,13 @@ class ConvSpec:
 
 class _Prep:
     """Cached GEMM images of one (weight, layout) pair and the arguments that rebuild them."""
-    __slots__ = ('weight', 'bias', 'dtype', 'shape', 'maps', 'val', 'key', 'used')
+    __slots__ = ('weight', 'bias', 'dtype', 'shape', 'maps', 'val', 'key', 'used', '__weakref__')
 
 
-_PREP_ALL = {}  # (id(weight), static key) -> _Prep
+# (id(weight), static key) -> _Prep, WEAK: an entry lives as long as its weight (which holds it in
+# weight.__dict__['_sr_prep']) or a batched-refresh table / captured graph that uses it, so weights
+# of discarded nets (and their GEMM images) are freed
+_PREP_ALL = weakref.WeakValueDictionary()
 _PREP_TABLE = {}  # dtype -> (entries, device item table, device block starts, total blocks)
 # tables launched by refresh_prepared while a HIP graph was being captured: the graph keeps
 # launching the batched refresh on their device buffers, so whoever owns the graph takes these

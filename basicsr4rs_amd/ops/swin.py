@@ -10,7 +10,11 @@ is exactly our NHWC feature map, so PatchEmbed / PatchUnEmbed are free.  A SwinT
     ln2 = LN(x2); h = GELU(Linear_fc1(ln2))    (GELU + pre-activation side output fused)
     out = x2 + Linear_fc2(h)
 
-with a hand-written backward (GELU' fused into fc2's dgrad epilogue, LN residual fused).
+with a hand-written backward (GELU' fused into fc2's dgrad epilogue, LN residual fused).  In bf16
+with window 8 and heads of <= 32 (SwinIR-M / -S / the RS configs) the first three lines run as ONE
+kernel (round 4, csrc/swin_fused.hip, ``swin_attn_fused``): LayerNorm, qkv, window attention and proj
++ residual on a two-window token tile in LDS, which also writes what the backward reads (ln1, its
+statistics, qkv, the attention output, lse) -- or, without autograd (validation / inference), x2 only.
 Linears are 1x1 convs: nn.Linear.weight [out][in] is the 1x1 conv weight; the padded head
 layout is produced by index maps in the HIP weight-prep kernel.
 
@@ -34,6 +38,8 @@ GELU = 3
 _PARAM_REDUCE_SIDE = os.environ.get('SR_PARAM_REDUCE_MAIN') != '1'
 # SR_ROWSCALE_UNFUSED=1: the proj-branch stochastic-depth gradient by a separate row-scale pass (A/B)
 _ROWSCALE_FUSED = os.environ.get('SR_ROWSCALE_UNFUSED') != '1'
+# SR_SWIN_FUSED=0: the attention half of a block as three launches (LN+qkv, attention, proj) (A/B)
+_SWIN_FUSED = os.environ.get('SR_SWIN_FUSED') != '0'
 
 
 class LinearSpec:
@@ -315,6 +321,46 @@ def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table, table_param=N
     return dqkv, dtable
 
 
+def attn_block_flops(g, N, H, W):
+    """Algorithmic FLOPs of the attention half of a block: qkv and proj linears (unpadded C) and
+    QK^T + AV (attn_flops)."""
+    M = N * H * W
+    return 2.0 * M * g.dim * 3 * g.dim + attn_flops(g, N, H, W) + 2.0 * M * g.dim * g.dim
+
+
+def swin_attn_fused(x, n1w, n1b, Creal, qwf, qbg, tab, pwf, pbg, s1, g, scale, train):
+    """x2 = x + s1 * proj(WindowAttention(qkv(LN1(x)))) in one launch (sr_swin_attn_fused_fwd), or
+    None when the call is not on that path (fp32 parity mode, other window / head geometries,
+    SR_SWIN_FUSED=0).  Training also returns ln1, mean, rstd, qkv, the attention output and lse
+    exactly as the unfused path writes them (the backward is shared)."""
+    N, H, W, Cp = x.shape
+    lib = _lib.load()
+    if not _SWIN_FUSED or not lib.sr_swin_attn_fused_ok(_lib.dtype_code(x.dtype), N, H, W, g.ws, g.nH, g.hd, g.hdp,
+                                                       Creal, Cp):
+        return None
+    M = N * H * W
+    dev = x.device
+    x2 = torch.empty_like(x)
+    ln1 = m1 = r1 = qkv = a = lse = None
+    if train:
+        ln1 = torch.empty_like(x)
+        m1 = torch.empty(M, device=dev, dtype=torch.float32)
+        r1 = torch.empty(M, device=dev, dtype=torch.float32)
+        qkv = torch.empty(N, H, W, 3 * g.nH * g.hdp, device=dev, dtype=x.dtype)
+        a = torch.empty(N, H, W, g.nH * g.hdp, device=dev, dtype=x.dtype)
+        lse = torch.empty(N * (H // g.ws) * (W // g.ws) * g.nH * g.ws * g.ws, device=dev, dtype=torch.float32)
+    # HBM bytes: x read twice (LayerNorm, residual), x2 written; training also ln1, qkv, attention out
+    nbytes = x.element_size() * M * (3 * Cp + ((Cp + 3 * g.nH * g.hdp + g.nH * g.hdp) if train else 0))
+    with ktrace.span('swin_attn_block_fwd_kernel', attn_block_flops(g, N, H, W), nbytes):
+        _lib.check(
+            lib.sr_swin_attn_fused_fwd(_lib.ptr(x), _lib.ptr(n1w.detach()), _lib.ptr(n1b.detach()), Creal, 1e-5,
+                                       _lib.ptr(qwf), _lib.ptr(qbg), _lib.ptr(tab), _lib.ptr(pwf), _lib.ptr(pbg),
+                                       _lib.ptr(s1), N, H, W, g.shift, g.nH, Cp, float(scale), _lib.ptr(x2),
+                                       _lib.ptr(ln1), _lib.ptr(m1), _lib.ptr(r1), _lib.ptr(qkv), _lib.ptr(a),
+                                       _lib.ptr(lse), _lib.stream()))
+    return x2, ln1, m1, r1, qkv, a, lse
+
+
 class _STB(torch.autograd.Function):
 
     @staticmethod
@@ -323,17 +369,21 @@ class _STB(torch.autograd.Function):
         N, H, W, Cp = x.shape
         Cr = geom.dim
         qwf, _, qbg = prepared_linear(qw, qb, geom.qkv, dtype)
-        fused = linear_ln_fwd(x, n1w, n1b, Cr, qwf, qbg, geom.qkv, N, H, W)  # norm1 -> qkv in one launch
-        if fused is not None:
-            qkv, ln1, m1, r1 = fused
-        else:
-            ln1, m1, r1 = layernorm(x, n1w, n1b, Cr)
-            qkv = linear_fwd(ln1, qwf, qbg, geom.qkv, N, H, W)
         tab = table.detach().float().contiguous()
-        a, lse = window_attn(qkv, geom, N, H, W, scale, tab)
         pwf, _, pbg = prepared_linear(pw, pb, geom.proj, dtype)
         s1, s2 = dp if dp is not None else (None, None)  # per-sample DropPath factors (fp32 [N])
-        x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0, row_scale=s1)
+        fused = swin_attn_fused(x, n1w, n1b, Cr, qwf, qbg, tab, pwf, pbg, s1, geom, scale, any(ctx.needs_input_grad))
+        if fused is not None:  # LN1 -> qkv -> window attention -> proj + residual in one launch
+            x2, ln1, m1, r1, qkv, a, lse = fused
+        else:
+            fused = linear_ln_fwd(x, n1w, n1b, Cr, qwf, qbg, geom.qkv, N, H, W)  # norm1 -> qkv in one launch
+            if fused is not None:
+                qkv, ln1, m1, r1 = fused
+            else:
+                ln1, m1, r1 = layernorm(x, n1w, n1b, Cr)
+                qkv = linear_fwd(ln1, qwf, qbg, geom.qkv, N, H, W)
+            a, lse = window_attn(qkv, geom, N, H, W, scale, tab)
+            x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0, row_scale=s1)
         f1wf, _, f1bg = prepared_linear(f1w, f1b, fc1s, dtype)
         z = torch.empty(N, H, W, fc1s.cout_p, device=x.device, dtype=dtype)
         fused = linear_ln_fwd(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)  # norm2 -> fc1

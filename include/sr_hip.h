@@ -330,6 +330,21 @@ int sr_layernorm_bwd_reduce(const float* workspace, int nparts, int C, float* dg
 int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W, int ws, int shift, int nH,
                        int hd, int hdp, float scale, const float* bias_table, void* out, int ldo, float* lse,
                        void* stream);
+/* Fused attention half of a SwinTransformerBlock (basicsr/archs/swinir_arch.py:283-314 with
+ * WindowAttention :144-175; round 4): x2 = x + row_scale[n] * proj(WindowAttention(qkv(LN1(x)))) in
+ * one launch on bf16 token maps [N][H][W][Cp] (Cp <= 192), window 8, nH heads of dim <= 32 padded
+ * to 32 (nH * 32 <= 192), cyclic shift `shift`.  wqkv / wproj are the GEMM images of the qkv
+ * (rows [3][nH][32], Cp columns) and proj (Cp rows, nH * 32 columns) linears with their fp32
+ * biases; bias_table [(2*8-1)^2][nH]; row_scale [N] (DropPath) or NULL.  Training: qkv != NULL
+ * and ln_out / ln_mean / ln_rstd / attn_out / lse receive what sr_linear_ln_fwd and
+ * sr_window_attn_fwd write (the backward reads them unchanged); inference: all NULL, only x2 is
+ * written.  sr_swin_attn_fused_ok: 1 when a geometry is on this path. */
+int sr_swin_attn_fused_ok(int dtype, int N, int H, int W, int ws, int nH, int hd, int hdp, int C, int Cp);
+int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, int C, float eps, const void* wqkv,
+                           const float* bqkv, const float* bias_table, const void* wproj, const float* bproj,
+                           const float* row_scale, int N, int H, int W, int shift, int nH, int Cp, float scale, void* x2,
+                           void* ln_out, float* ln_mean, float* ln_rstd, void* qkv, void* attn_out, float* lse,
+                           void* stream);
 size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH);
 int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo,
                        const float* lse, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp,

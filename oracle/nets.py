@@ -268,7 +268,7 @@ def window_attention_core(qkv, nH, ws, shift, scale, table):
     t = qkv
     if shift > 0:
         t = torch.roll(t, shifts=(-shift, -shift), dims=(1, 2))
-    tw = window_partition(t, ws).view(-1, ws * ws, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    tw = window_partition(t, ws).reshape(-1, ws * ws, 3, nH, hd).permute(2, 0, 3, 1, 4)
     q, k, v = tw[0] * scale, tw[1], tw[2]
     n = ws * ws
     attn = q @ k.transpose(-2, -1)

@@ -243,6 +243,41 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize('shape', [(2, 6, 64, 128, 128), (1, 4, 192, 256, 128), (32, 8, 64, 256, 256),
+                                   (1, 5, 64, 384, 256), (1, 1, 64, 128, 256), (4, 64, 64, 256, 256)])
+def test_wgrad_tw_vs_fp64(cuda, shape):
+    """12-wave tap-row wgrad (round 4, conv3x3_wgrad_tw_kernel: a kernel row's three taps on
+    different waves, one x halo row per K-step): image top / bottom rows, the left / right halo
+    columns, several 64-px segments per row, multi-image splits, the EDSR-L body shape, against
+    fp64 on the same bf16 operands and against the per-tap pp kernel (variant 0); opt-in (variant 70)."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(13)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin).to(dt)
+    dy = torch.randn(N, H, W, cout).to(dt)
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, cout, 0, 3
+    outs = []
+    try:
+        _lib.check(lib.sr_conv3x3_set_variant(70))
+        assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_tw_kernel'
+        for variant in (70, 0):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0))
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    torch.cuda.synchronize()
+    dw, db = outs[0]
+    assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
+    assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
+
+
 @pytest.mark.parametrize('shape', [(2, 6, 64, 128, 128, 0), (1, 4, 192, 256, 128, 0), (32, 8, 64, 256, 256, 0),
                                    (2, 2, 128, 128, 512, 2), (1, 5, 64, 384, 256, 0), (3, 3, 128, 256, 1024, 2),
                                    (1, 1, 64, 128, 256, 0)])
@@ -365,13 +400,14 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
                                    (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
-@pytest.mark.parametrize('variant', [0, 65])
+@pytest.mark.parametrize('variant', [0, 65, 69])
 def test_wgrad_halo_vs_fp64(cuda, shape, variant):
     """All-taps halo wgrad (Cout <= 64, W % 64 == 0), row-streaming form: channel slices of
     wider buffers (ldx, xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather
     (in_up = 2), splits that cross image boundaries (rows per split not dividing H), several
     64-px column segments per row, ragged last split, against an fp64 CPU reference on the same
-    bf16 operands; variant 65: the opt-in early-issue schedule (one barrier per step, W 64 only)."""
+    bf16 operands; variant 0: two row groups per 8-wave block for Cout <= 32 (round 4); 65: the opt-in
+    early-issue schedule (one barrier per step, W 64 only); 69: the 4-wave one-row-group form."""
     N, H, W, cin, cout, up = shape
     torch.manual_seed(9)
     dt = torch.bfloat16
@@ -882,3 +918,20 @@ def test_band_dot_partials(cuda, shape):
             C.conv_fwd_raw(x, wf, None, y1, N, H, W, cin, cout, cout, res=res, beta=1.0, colsum=True, dot=dot)
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
+
+
+def test_prepared_images_freed_with_their_weight(cuda):
+    """The GEMM-image registry (ops.conv._PREP_ALL) is weak: a discarded weight's images are freed
+    (round-3 verdict: the registry held every weight ever prepared for the process lifetime)."""
+    import gc
+    gc.collect()
+    n0 = len(C._PREP_ALL)
+    conv = torch.nn.Conv2d(16, 16, 3, 1, 1).to(cuda)
+    spec = C.ConvSpec(16, 16)
+    C.prepared(conv.weight, conv.bias, spec, torch.bfloat16)
+    assert len(C._PREP_ALL) == n0 + 1
+    del conv
+    gc.collect()
+    C._retire_table(torch.bfloat16)
+    gc.collect()
+    assert len(C._PREP_ALL) == n0

@@ -196,3 +196,27 @@ def test_swinirrs_validation_minusone_one(cuda, tmp_path):
         assert os.path.exists(tmp_path / 'vis' / 'RGB' / 'S2N_val' / 'val/lq/tile_0' / f'{key}.png')
         assert os.path.exists(tmp_path / 'vis' / 'NIR' / 'S2N_val' / 'val/lq/tile_1' / f'{key}.png')
     assert not os.path.exists(tmp_path / 'vis' / 'RGB' / 'S2N_val' / 'val/lq/tile_0' / 'sr.png')
+
+
+def test_swinir_four_band_forward_fp32(cuda):
+    """The 4-band (RGB + NIR) SwinIR of the remote-sensing configs (in_chans 4: zero mean,
+    swinir_arch.py:750-754) in fp32 against the oracle, on [-1, 1] inputs, direct and through
+    SwinIRModel.test's reflect pad (a 12 x 12 LR tile)."""
+    from torch.nn import functional as F
+
+    from basicsr4rs_amd.archs import build_network
+    net = dict(SWINIR, in_chans=4)
+    torch.manual_seed(0)
+    g = build_network(dict(net)).eval()
+    sd = {k: v.detach().clone() for k, v in g.state_dict().items()}
+    gen = torch.Generator().manual_seed(5)
+    for hw in (16, 12):
+        lq = torch.rand(1, 4, hw, hw, generator=gen) * 2.2 - 1.1
+        pad = (8 - hw % 8) % 8
+        x = F.pad(lq, (0, pad, 0, pad), 'reflect')
+        with torch.no_grad():
+            ref = _oracle(net, sd, x)
+            out = g.to(cuda)(x.to(cuda)).cpu()
+        err = (out - ref).abs().max().item()
+        print(f'SwinIR 4-band fp32 {hw}x{hw}: max-abs {err:.2e}, out range {ref.abs().max().item():.3f}')
+        assert err <= 1e-3

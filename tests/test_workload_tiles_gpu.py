@@ -21,8 +21,10 @@ magnitude (bound per net, below).  ``ktrace`` records the kernel of every conv /
 launch; the test asserts the production kernels ran.
 
 Tolerances: bf16 keeps 8 mantissa bits, so every stored activation and gradient carries a relative
-rounding error up to 2^-9; the bounds are the observed values of round 3 with ~2x margin
-(printed by each test).  A defect in a kernel (a wrong tap, a missed row, a race) shows up as a
+rounding error up to 2^-9.  The per-parameter max-error bounds are ~2x the maxima observed in round 4
+(printed by each test; profiles/r04/tests): RCAN B 8 0.062 -> 0.12, RCAN B 32 0.036 -> 0.07, EDSR
+0.068 -> 0.13; RRDB (0.105) and SwinIR (0.117) keep 0.15 (~1.4x) -- their worst tensors are biases
+of 32-channel convs / the qkv weight, whose gradients sum many bf16-rounded terms.  A defect in a kernel (a wrong tap, a missed row, a race) shows up as a
 cosine far below 0.99 on the affected tensors, not as a few percent of max error.
 
 ``test_rrdb_full_depth_error_is_bf16_storage_rounding`` explains the bench's RRDB bf16 parity
@@ -109,7 +111,7 @@ def _run(cuda, cfg, batch, lr_px, kernels, out_tol, grad_tol, cos_min=0.995, see
 def test_rcan_workload_tile_bf16(cuda):
     # B 8: 512 LR rows over 256 band blocks, two rows per band (the bench's B 32 has eight)
     _run(cuda, RCAN, 8, 64, ['conv3x3_fwd_band_kernel', 'conv3x3_wgrad_ring_kernel+reduce', 'conv3x3_fwd_pph_kernel',
-                             'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.15)
+                             'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.12)
 
 
 def test_rrdb_workload_tile_bf16(cuda):
@@ -119,13 +121,24 @@ def test_rrdb_workload_tile_bf16(cuda):
 
 def test_edsr_l_workload_tile_bf16_fwd_bwd(cuda):
     _run(cuda, EDSR_L4, 2, 64, ['conv3x3_fwd_pph_kernel', 'conv3x3_fwd_tail_kernel', 'conv3x3_wgrad_pp_kernel+reduce'],
-         out_tol=5e-3, grad_tol=0.15)
+         out_tol=5e-3, grad_tol=0.13)
 
 
 def test_swinir_m_workload_tile_bf16(cuda):
-    _run(cuda, SWINIR_M2, 2, 64, ['conv3x3_lin_kernel+ln', 'wattn_fwd_kernel', 'wattn_bwd_kernel',
+    # the attention half of every block runs fused (swin_attn_block_fwd_kernel, round 4); the MLP half
+    # keeps the LayerNorm-prologue lin kernel
+    _run(cuda, SWINIR_M2, 2, 64, ['swin_attn_block_fwd_kernel', 'conv3x3_lin_kernel+ln', 'wattn_bwd_kernel',
                                   'linear_wgrad_kernel+reduce', 'linear_wk_kernel', 'conv3x3_wgrad_ring_kernel+reduce'],
          out_tol=5e-3, grad_tol=0.15)
+
+
+def test_rcan_b32_bench_geometry_bf16(cuda):
+    """RCAN at the bench's batch (B 32 x 64^2 LR, C3) with 1 group x 1 RCAB: the band kernels' rows per
+    band and the ring wgrad's split plan are those of the benchmarked step (the B 8 tile above runs
+    a quarter of them), checked against fp64 instead of only graph == eager."""
+    _run(cuda, dict(RCAN, num_group=1, num_block=1), 32, 64,
+         ['conv3x3_fwd_band_kernel', 'conv3x3_wgrad_ring_kernel+reduce', 'conv3x3_fwd_pph_kernel',
+          'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.07)
 
 
 def test_rrdb_full_depth_error_is_bf16_storage_rounding(cuda):
