@@ -109,6 +109,9 @@ SIGNATURES = {
     'sr_swin_attn_fused_ok': (_i, [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i]),
     'sr_swin_attn_fused_fwd': (_i, [_vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _f, _vp,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_swin_mlp_fused_ok': (_i, [_i, _i, _i, _i]),
+    'sr_swin_mlp_fused_fwd': (_i, [_vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _vp]),
     'sr_window_attn_bwd_workspace': (_sz, [_i, _i, _i, _i, _i]),
     'sr_window_attn_bwd': (_i, [_i, _vp, _i, _vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _f, _vp, _vp, _vp, _vp,
                                _sz, _i, _vp]),

@@ -384,6 +384,240 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused MLP half of a SwinTransformerBlock (round 4):
+//
+//   out = x2 + s2[n] * fc2(GELU(fc1(LN2(x2))))          (swinir_arch.py:322-323, Mlp :43-60)
+//
+// bf16, Cp <= 192, hidden Hp <= 384 (mlp_ratio 2: 360).  A 512-thread block owns 128 consecutive
+// token rows: LN2 into an LDS tile (and, training, ln_out / mean / rstd), fc1 with W1 fragments from
+// L2 into registers (wave w: hidden tiles w, w + 8, w + 16 over all 128 tokens), bias + exact GELU
+// in the epilogue (training: z and h stored, as the lin kernel's aux / output), h into an LDS tile
+// that overlays the dead LN tile, then fc2 (wave: 48 output channels x 64 tokens) + bias, DropPath
+// row scale and the residual.  HBM (training): x2 read twice, ln_out / z / h / out written once =
+// 376 MB per SwinIR-M layer at B 32 against 470 MB for the lin kernel + linear_wk_kernel pair; h is
+// never re-read for fc2.
+struct SmbArgs {
+  const bf16_t* x;   // x2 [M][Cp]
+  const float* ln_g;
+  const float* ln_b;
+  const bf16_t* w1;  // fc1 image [Hp][Cp]
+  const float* b1;   // [Hp]
+  const bf16_t* w2;  // fc2 image [Cp][Hp]
+  const float* b2;   // [Cp]
+  const float* rsc;  // [N] or null
+  bf16_t* out;
+  bf16_t* ln_out;  // training outputs (null for inference)
+  float* mean;
+  float* rstd;
+  bf16_t* z;
+  bf16_t* h;
+  int M, HW, C, Cp, KC, Hp, HC;  // HC = Hp / 8 (16-B chunks of a hidden row)
+  float eps;
+};
+
+constexpr int SMB_H = 0;                 // [6 cg][128][128 B]: LN(x2) tile (cg 0..2), then h (cg 0..5)
+constexpr int SMB_GB = 6 * 128 * 128;    // float [2][192]
+constexpr int SMB_LDS = SMB_GB + 2 * 192 * 4;
+
+__global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[SMB_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int m0 = (int)xcd_remap(blockIdx.x, gridDim.x) * 128;
+  const bool train = a.z != nullptr;
+  float* sGB = (float*)(smem + SMB_GB);
+  if (tid < 192) {
+    sGB[tid] = tid < a.C ? a.ln_g[tid] : 0.f;
+    sGB[192 + tid] = tid < a.C ? a.ln_b[tid] : 0.f;
+  }
+  // ---- LayerNorm of the 128 rows: 4 lanes per row
+  {
+    const int r = tid >> 2, part = tid & 3, m = m0 + r;
+    const bool vr = m < a.M;
+    u32x4 raw[6];
+    float sm = 0.f;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int ch = part + 4 * q;
+      raw[q] = (vr && ch < a.KC) ? *(const u32x4*)(a.x + (int64_t)m * a.Cp + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 8 + 2 * j;
+        sm += (c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) : 0.f) + (c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) : 0.f);
+      }
+    }
+    sm += __shfl_xor(sm, 1);
+    sm += __shfl_xor(sm, 2);
+    const float mu = sm / a.C;
+    float sq = 0.f;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int ch = part + 4 * q;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = ch * 8 + 2 * j;
+        const float d0 = c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) - mu : 0.f;
+        const float d1 = c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) - mu : 0.f;
+        sq += d0 * d0 + d1 * d1;
+      }
+    }
+    sq += __shfl_xor(sq, 1);
+    sq += __shfl_xor(sq, 2);
+    const float rs = rsqrtf(sq / a.C + a.eps);
+    __syncthreads();  // gamma / beta staged
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int ch = part + 4 * q;
+      u32x4 o4 = u32x4{0u, 0u, 0u, 0u};
+      if (vr && ch < a.KC) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = ch * 8 + j;
+          const float xv = bf16_to_f32((raw[q][j >> 1] >> (16 * (j & 1))) & 0xffff);
+          o[j] = c < a.C ? (xv - mu) * rs * sGB[c] + sGB[192 + c] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
+        if (train) *(u32x4*)(a.ln_out + (int64_t)m * a.Cp + ch * 8) = o4;
+      }
+      *(u32x4*)(smem + SMB_H + tile_off(128, r, ch)) = o4;
+    }
+    if (train && vr && part == 0) {
+      a.mean[m] = mu;
+      a.rstd[m] = rs;
+    }
+  }
+  __syncthreads();
+
+  // ---- fc1: hidden tiles t = w, w + 8, w + 16 (< 23) x all 128 tokens
+  const int ntl = (a.Hp + 15) / 16;
+  f32x4 acc[3][8];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto w1_frag = [&](int i, int kk) -> s16x8 {
+    const int row = 16 * (w + 8 * i) + c16, ch = 4 * kk + g;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (w + 8 * i < ntl && row < a.Hp && ch < a.KC) v = *(const u32x4*)(a.w1 + (size_t)row * a.Cp + ch * 8);
+    return __builtin_bit_cast(s16x8, v);
+  };
+  s16x8 af[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) af[i] = w1_frag(i, 0);
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    s16x8 an[3];
+    if (kk + 1 < 6) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) an[i] = w1_frag(i, kk + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const s16x8 bf = *(const s16x8*)(smem + SMB_H + tile_off(128, 16 * j + c16, 4 * kk + g));
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (w + 8 * i < ntl) acc[i][j] = mfma16(af[i], bf, acc[i][j]);
+    }
+    if (kk + 1 < 6) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) af[i] = an[i];
+    }
+  }
+  __syncthreads();  // every wave done with the LN tile: h overwrites it
+  // hidden chunks past the last computed tile read as zeros in fc2 (0 x stale LDS could be NaN)
+  for (int i = tid; i < 128 * 48; i += 512) {
+    const int r = i / 48, ch = i - r * 48;
+    if (ch >= 2 * ntl) *(u32x4*)(smem + SMB_H + tile_off(128, r, ch)) = u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (w + 8 * i >= ntl) continue;
+    const int hr = 16 * (w + 8 * i) + 4 * g;  // 4 consecutive hidden channels
+    f32x4 bias = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (hr < a.Hp) bias = *(const f32x4*)(a.b1 + hr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = 16 * j + c16, m = m0 + t;
+      float zv[4], hv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        zv[r] = hr + r < a.Hp ? acc[i][j][r] + bias[r] : 0.f;
+        hv[r] = gelu_exact(zv[r]);
+      }
+      uint2 uz, uh;
+      uz.x = pack_bf16x2(zv[0], zv[1]);
+      uz.y = pack_bf16x2(zv[2], zv[3]);
+      uh.x = pack_bf16x2(hv[0], hv[1]);
+      uh.y = pack_bf16x2(hv[2], hv[3]);
+      if (train && m < a.M && hr < a.Hp) {
+        *(uint2*)(a.z + (int64_t)m * a.Hp + hr) = uz;
+        *(uint2*)(a.h + (int64_t)m * a.Hp + hr) = uh;
+      }
+      *(uint2*)(smem + SMB_H + tile_off(128, t, hr >> 3) + (hr & 7) * 2) = uh;
+    }
+  }
+  __syncthreads();  // h tile complete
+
+  // ---- fc2: wave = 48 output channels (og) x 64 tokens (tg), K = 384 hidden (zero past Hp)
+  const int og = w & 3, tg = w >> 2;
+  f32x4 acc2[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto w2_frag = [&](int i, int kk) -> s16x8 {
+    const int row = og * 48 + 16 * i + c16, ch = 4 * kk + g;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (row < a.Cp && ch < a.HC) v = *(const u32x4*)(a.w2 + (size_t)row * a.Hp + ch * 8);
+    return __builtin_bit_cast(s16x8, v);
+  };
+  s16x8 bf2[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) bf2[i] = w2_frag(i, 0);
+#pragma unroll
+  for (int kk = 0; kk < 12; ++kk) {
+    s16x8 bn[3];
+    if (kk + 1 < 12) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) bn[i] = w2_frag(i, kk + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const s16x8 hf = *(const s16x8*)(smem + SMB_H + tile_off(128, tg * 64 + 16 * j + c16, 4 * kk + g));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) acc2[i][j] = mfma16(bf2[i], hf, acc2[i][j]);
+    }
+    if (kk + 1 < 12) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) bf2[i] = bn[i];
+    }
+  }
+  // ---- out = x2 + s2[n] * (fc2 + bias)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int oc = og * 48 + 16 * i + 4 * g;
+    if (oc >= a.Cp) continue;
+    const f32x4 bias = *(const f32x4*)(a.b2 + oc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + tg * 64 + 16 * j + c16;
+      if (m >= a.M) continue;
+      const float sc = a.rsc ? a.rsc[m / a.HW] : 1.f;
+      const uint2 xv = *(const uint2*)(a.x + (int64_t)m * a.Cp + oc);
+      uint2 u;
+      u.x = pack_bf16x2(bf16_to_f32(xv.x & 0xffff) + sc * (acc2[i][j][0] + bias[0]),
+                        bf16_to_f32(xv.x >> 16) + sc * (acc2[i][j][1] + bias[1]));
+      u.y = pack_bf16x2(bf16_to_f32(xv.y & 0xffff) + sc * (acc2[i][j][2] + bias[2]),
+                        bf16_to_f32(xv.y >> 16) + sc * (acc2[i][j][3] + bias[3]));
+      *(uint2*)(a.out + (int64_t)m * a.Cp + oc) = u;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -417,6 +651,30 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
   const int blocks = (a.nwin_total + 1) / 2;
   hipLaunchKernelGGL(swin_attn_block_fwd_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
   return sr_check(hipGetLastError(), "swin_attn_fused_fwd launch");
+}
+
+int sr_swin_mlp_fused_ok(int dtype, int C, int Cp, int Hp) {
+  return dtype == SR_BF16 && Cp % 8 == 0 && Cp <= 192 && C > 0 && C <= Cp && Hp % 8 == 0 && Hp > 0 && Hp <= 368;
+}
+
+int sr_swin_mlp_fused_fwd(const void* x, const float* ln_g, const float* ln_b, int C, float eps, const void* w1,
+                          const float* b1, const void* w2, const float* b2, const float* row_scale, int N, int HW,
+                          int Cp, int Hp, void* out, void* ln_out, float* ln_mean, float* ln_rstd, void* z, void* h,
+                          void* stream) {
+  if (!x || !ln_g || !ln_b || !w1 || !b1 || !w2 || !b2 || !out) return sr_fail(SR_EINVAL, "swin_mlp_fused_fwd: null pointer");
+  const bool train = z != nullptr;
+  if (train && (!ln_out || !ln_mean || !ln_rstd || !h))
+    return sr_fail(SR_EINVAL, "swin_mlp_fused_fwd: training needs ln_out, mean, rstd, z and h");
+  if (!sr_swin_mlp_fused_ok(SR_BF16, C, Cp, Hp) || N <= 0 || HW <= 0)
+    return sr_fail(SR_EINVAL, "swin_mlp_fused_fwd: bf16, Cp <= 192, hidden <= 368 (multiples of 8)");
+  SmbArgs a{};
+  a.x = (const bf16_t*)x; a.ln_g = ln_g; a.ln_b = ln_b; a.w1 = (const bf16_t*)w1; a.b1 = b1;
+  a.w2 = (const bf16_t*)w2; a.b2 = b2; a.rsc = row_scale; a.out = (bf16_t*)out;
+  a.ln_out = (bf16_t*)ln_out; a.mean = ln_mean; a.rstd = ln_rstd; a.z = (bf16_t*)z; a.h = (bf16_t*)h;
+  a.M = N * HW; a.HW = HW; a.C = C; a.Cp = Cp; a.KC = Cp / 8; a.Hp = Hp; a.HC = Hp / 8; a.eps = eps;
+  const int blocks = (a.M + 127) / 128;
+  hipLaunchKernelGGL(swin_mlp_block_fwd_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
+  return sr_check(hipGetLastError(), "swin_mlp_fused_fwd launch");
 }
 
 }  // extern "C"

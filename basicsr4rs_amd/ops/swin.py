@@ -361,6 +361,37 @@ def swin_attn_fused(x, n1w, n1b, Creal, qwf, qbg, tab, pwf, pbg, s1, g, scale, t
     return x2, ln1, m1, r1, qkv, a, lse
 
 
+def swin_mlp_fused(x, n2w, n2b, Creal, f1wf, f1bg, fc1s, f2wf, f2bg, s2, train):
+    """out = x + s2 * fc2(GELU(fc1(LN2(x)))) in one launch (sr_swin_mlp_fused_fwd), or None off that
+    path (fp32, wider maps, SR_SWIN_FUSED=0).  Training also returns ln2, mean, rstd, z and h as the
+    lin kernel writes them (the backward is shared)."""
+    N, H, W, Cp = x.shape
+    lib = _lib.load()
+    Hp = fc1s.cout_p
+    if not _SWIN_FUSED or Cp != fc1s.cin_p or fc2s.cin_p != Hp or fc2s.cout_p != Cp or \
+            not lib.sr_swin_mlp_fused_ok(_lib.dtype_code(x.dtype), Creal, Cp, Hp):
+        return None
+    M = N * H * W
+    dev = x.device
+    out = torch.empty_like(x)
+    ln2 = m2 = r2 = z = h = None
+    if train:
+        ln2 = torch.empty_like(x)
+        m2 = torch.empty(M, device=dev, dtype=torch.float32)
+        r2 = torch.empty(M, device=dev, dtype=torch.float32)
+        z = torch.empty(N, H, W, Hp, device=dev, dtype=x.dtype)
+        h = torch.empty(N, H, W, Hp, device=dev, dtype=x.dtype)
+    flops = 2.0 * M * fc1s.cin * fc1s.cout * 2  # fc1 + fc2, unpadded
+    nbytes = x.element_size() * M * (3 * Cp + ((Cp + 2 * Hp) if train else 0))
+    with ktrace.span('swin_mlp_block_fwd_kernel', flops, nbytes):
+        _lib.check(
+            lib.sr_swin_mlp_fused_fwd(_lib.ptr(x), _lib.ptr(n2w.detach()), _lib.ptr(n2b.detach()), Creal, 1e-5,
+                                      _lib.ptr(f1wf), _lib.ptr(f1bg), _lib.ptr(f2wf), _lib.ptr(f2bg), _lib.ptr(s2), N,
+                                      H * W, Cp, Hp, _lib.ptr(out), _lib.ptr(ln2), _lib.ptr(m2), _lib.ptr(r2),
+                                      _lib.ptr(z), _lib.ptr(h), _lib.stream()))
+    return out, ln2, m2, r2, z, h
+
+
 class _STB(torch.autograd.Function):
 
     @staticmethod
@@ -385,15 +416,19 @@ class _STB(torch.autograd.Function):
             a, lse = window_attn(qkv, geom, N, H, W, scale, tab)
             x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0, row_scale=s1)
         f1wf, _, f1bg = prepared_linear(f1w, f1b, fc1s, dtype)
-        z = torch.empty(N, H, W, fc1s.cout_p, device=x.device, dtype=dtype)
-        fused = linear_ln_fwd(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)  # norm2 -> fc1
-        if fused is not None:
-            h, ln2, m2, r2 = fused
-        else:
-            ln2, m2, r2 = layernorm(x2, n2w, n2b, Cr)
-            h = linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)
         f2wf, _, f2bg = prepared_linear(f2w, f2b, fc2s, dtype)
-        out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0, row_scale=s2)
+        fm = swin_mlp_fused(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, f2wf, f2bg, s2, any(ctx.needs_input_grad))
+        if fm is not None:  # LN2 -> fc1 -> GELU -> fc2 + residual in one launch
+            out, ln2, m2, r2, z, h = fm
+        else:
+            z = torch.empty(N, H, W, fc1s.cout_p, device=x.device, dtype=dtype)
+            fused = linear_ln_fwd(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)  # norm2 -> fc1
+            if fused is not None:
+                h, ln2, m2, r2 = fused
+            else:
+                ln2, m2, r2 = layernorm(x2, n2w, n2b, Cr)
+                h = linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=GELU, aux=z)
+            out = linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x2, beta=1.0, row_scale=s2)
         ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale, ctx.dp = geom, fc1s, fc2s, scale, dp
         ctx.save_for_backward(x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w,
                               f1b, f2w, f2b, n1b, n2b, table)

@@ -345,6 +345,17 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
                            const float* row_scale, int N, int H, int W, int shift, int nH, int Cp, float scale, void* x2,
                            void* ln_out, float* ln_mean, float* ln_rstd, void* qkv, void* attn_out, float* lse,
                            void* stream);
+/* Fused MLP half of a SwinTransformerBlock (swinir_arch.py:322-323, Mlp :43-60; round 4):
+ * out = x + row_scale[n] * fc2(GELU(fc1(LN2(x)))) on bf16 token rows [N * HW][Cp] (Cp <= 192,
+ * hidden Hp <= 368, multiples of 8): w1 / w2 the fc1 [Hp][Cp] / fc2 [Cp][Hp] GEMM images with fp32
+ * biases.  Training: z != NULL, and ln_out / ln_mean / ln_rstd / z (pre-activation) / h
+ * (activation) receive what sr_linear_ln_fwd writes for norm2 -> fc1 (the backward reads them);
+ * inference: all NULL. */
+int sr_swin_mlp_fused_ok(int dtype, int C, int Cp, int Hp);
+int sr_swin_mlp_fused_fwd(const void* x, const float* ln_g, const float* ln_b, int C, float eps, const void* w1,
+                          const float* b1, const void* w2, const float* b2, const float* row_scale, int N, int HW,
+                          int Cp, int Hp, void* out, void* ln_out, float* ln_mean, float* ln_rstd, void* z, void* h,
+                          void* stream);
 size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH);
 int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo,
                        const float* lse, int N, int H, int W, int ws, int shift, int nH, int hd, int hdp,

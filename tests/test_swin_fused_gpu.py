@@ -120,3 +120,62 @@ def test_swin_attn_fused_vs_unfused_and_fp64(cuda, geom):
     print(f'{geom}: fused-unfused x2 {dx2:.3e}; vs fp64 qkv {e_qkv:.3e} attn {e_att:.3e} x2 {e_x2:.3e}')
     assert dx2 <= 2e-2 * oproj.abs().max().item() + 1e-2
     assert e_qkv < 2e-2 and e_att < 3e-2 and e_x2 < 3e-2
+
+
+MLP_GEOMS = [  # N, H, W, C, hidden, row_scale
+    (2, 16, 16, 180, 360, False),
+    (1, 8, 24, 180, 360, True),
+    (2, 16, 24, 60, 120, False),
+    (1, 16, 16, 96, 192, True),
+]
+
+
+@pytest.mark.parametrize('geom', MLP_GEOMS)
+def test_swin_mlp_fused_vs_unfused_and_fp64(cuda, geom):
+    """The fused MLP half, out = x2 + s2 * fc2(GELU(fc1(LN2(x2)))) (swinir_arch.py:322-323, Mlp :43-60):
+    ln2 / z / h / out against the unfused path (LN-prologue lin kernel with GELU + aux, then the fc2
+    linear with the residual) and out against fp64; inference writes the same out."""
+    from basicsr4rs_amd.ops import conv as Cv
+    from basicsr4rs_amd.ops import swin as S
+    N, H, W, C, hid, rsc = geom
+    torch.manual_seed(N * 100 + C + hid)
+    Cp = Cv.pad8(C)
+    x = torch.zeros(N, H, W, Cp)
+    x[..., :C] = torch.randn(N, H, W, C)
+    x = x.to(torch.bfloat16).to(cuda)
+    n2w, n2b = (1 + 0.1 * torch.randn(C)).to(cuda), (0.1 * torch.randn(C)).to(cuda)
+    f1w, f1b = (torch.randn(hid, C) * 0.08).to(cuda), (torch.randn(hid) * 0.05).to(cuda)
+    f2w, f2b = (torch.randn(C, hid) * 0.06).to(cuda), (torch.randn(C) * 0.05).to(cuda)
+    s2 = (torch.rand(N) * 2).to(cuda) if rsc else None
+    fc1s, fc2s = S.plain_spec(C, hid), S.plain_spec(hid, C)
+    f1wf, _, f1bg = S.prepared_linear(f1w, f1b, fc1s, torch.bfloat16)
+    f2wf, _, f2bg = S.prepared_linear(f2w, f2b, fc2s, torch.bfloat16)
+    fm = S.swin_mlp_fused(x, n2w, n2b, C, f1wf, f1bg, fc1s, f2wf, f2bg, s2, True)
+    assert fm is not None, 'geometry not on the fused path'
+    inf = S.swin_mlp_fused(x, n2w, n2b, C, f1wf, f1bg, fc1s, f2wf, f2bg, s2, False)
+    z = torch.empty(N, H, W, fc1s.cout_p, device=cuda, dtype=torch.bfloat16)
+    uf = S.linear_ln_fwd(x, n2w, n2b, C, f1wf, f1bg, fc1s, N, H, W, act=S.GELU, aux=z)
+    if uf is not None:
+        h, ln2, m2, r2 = uf
+    else:
+        ln2, m2, r2 = S.layernorm(x, n2w, n2b, C)
+        h = S.linear_fwd(ln2, f1wf, f1bg, fc1s, N, H, W, act=S.GELU, aux=z)
+    out = S.linear_fwd(h, f2wf, f2bg, fc2s, N, H, W, res=x, beta=1.0, row_scale=s2)
+    torch.cuda.synchronize()
+    fo, fln2, fm2, fr2, fz, fh = fm
+    assert torch.equal(inf[0], fo) and all(t is None for t in inf[1:])
+    for name, got, want in (('ln2', fln2, ln2), ('z', fz, z), ('h', fh, h), ('out', fo, out)):
+        err = (got.float() - want.float()).abs().max().item()
+        assert err <= 2e-2 * want.float().abs().max().item(), (name, err)
+    assert torch.allclose(fm2, m2, rtol=1e-5, atol=1e-5) and torch.allclose(fr2, r2, rtol=1e-4, atol=1e-5)
+    if C < Cp:
+        assert fo[..., C:].abs().max().item() == 0.0
+    xd = x[..., :C].double().cpu()
+    t = torch.nn.functional.layer_norm(xd, (C, ), n2w.double().cpu(), n2b.double().cpu(), 1e-5)
+    t = torch.nn.functional.gelu(t @ f1w.cpu().to(torch.bfloat16).double().t() + f1b.double().cpu())
+    br = t @ f2w.cpu().to(torch.bfloat16).double().t() + f2b.double().cpu()
+    if s2 is not None:
+        br = br * s2.double().cpu().view(-1, 1, 1, 1)
+    e = (fo[..., :C].double().cpu() - (xd + br)).abs().max().item() / br.abs().max().item()
+    print(f'{geom}: mlp fused vs fp64 {e:.3e}')
+    assert e < 3e-2

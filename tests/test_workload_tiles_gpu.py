@@ -125,9 +125,9 @@ def test_edsr_l_workload_tile_bf16_fwd_bwd(cuda):
 
 
 def test_swinir_m_workload_tile_bf16(cuda):
-    # the attention half of every block runs fused (swin_attn_block_fwd_kernel, round 4); the MLP half
-    # keeps the LayerNorm-prologue lin kernel
-    _run(cuda, SWINIR_M2, 2, 64, ['swin_attn_block_fwd_kernel', 'conv3x3_lin_kernel+ln', 'wattn_bwd_kernel',
+    # both halves of every block run fused (swin_attn_block_fwd_kernel, swin_mlp_block_fwd_kernel,
+    # round 4); the backward keeps its kernels
+    _run(cuda, SWINIR_M2, 2, 64, ['swin_attn_block_fwd_kernel', 'swin_mlp_block_fwd_kernel', 'wattn_bwd_kernel',
                                   'linear_wgrad_kernel+reduce', 'linear_wk_kernel', 'conv3x3_wgrad_ring_kernel+reduce'],
          out_tol=5e-3, grad_tol=0.15)
 

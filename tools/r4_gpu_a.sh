@@ -12,7 +12,7 @@ run_t() {  # $1 tag, rest: pytest args
   grep -E "passed|failed|error" $OUT/$tag.log | tail -2
   return $rc
 }
-run_t fused tests/test_swin_fused_gpu.py && \
+
 run_t tw tests/test_conv_gpu.py -k "wgrad_tw or prepared_images" && \
 run_t ring tests/test_conv_gpu.py -k "halo_vs_fp64 or ring" && \
 run_t tiles tests/test_workload_tiles_gpu.py && \
