@@ -5339,7 +5339,8 @@ bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d);
 // 16-channel co tiles per wave of the ring / halo wgrad
 int ring_ct(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? 4 : (d->Cout + 15) / 16; }
 // Row groups per ring-wgrad block: 2 (8-wave blocks, one per CU, one slab per block; CO_T <= 2 --
-// at 3 / 4 co tiles per wave the two-waves-per-SIMD register budget spills), or
+// at 3 / 4 co tiles per wave the two-waves-per-SIMD register budget spills: 12 / 132 VGPRs, with
+// fragment lookahead 3 or 1 alike), or
 // SR_RING_VB=1 (4-wave blocks, two per CU; A/B) / variant 69 (parity tests of the 4-wave form).
 // The early-issue and deeper-pipeline A/B forms are 4-wave only.
 int ring_vb() {
@@ -5806,7 +5807,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
       const int D = ring_depth();
       a.ring_early = ring_early() ? 1 : 0;
       const int la = ring_la();
-      const int vbn = ring_vb();
+      const int vbn = ct <= 2 ? ring_vb() : 1;
 #define SR_RING(CT_)                                                                                     \
   if (vbn == 2 && CT_ <= 2) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<(CT_ <= 2 ? CT_ : 2), 2, 3, false, 2>), grid, dim3(512), 0, s, a); \
   else if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);   \

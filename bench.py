@@ -195,6 +195,59 @@ def parity_check(workload, dev):
             'bar': f'fp32 max-abs <= 1e-3 (north_star); bf16 PSNR >= {PSNR_FLOOR_BF16[workload]} dB'}
 
 
+def swin_fused_roofline(model, batch, lr_px, dev, reps=20):
+    """North-star check 'MFMA peak on SwinIR window attention': the fused attention half of one
+    SwinTransformerBlock (LN1 -> qkv -> shifted-window attention -> proj + residual,
+    swin_attn_block_fwd_kernel) timed on its own with HIP events on the bench's token map
+    (B x 64 x 64 x 184 bf16), training mode (ln1 / qkv / attention output / lse written for the
+    backward) and inference mode (x2 only), plus the fused MLP half.  FLOPs are algorithmic
+    (qkv + QK^T + AV + proj, unpadded); fraction of the 2.5 PF dense bf16 peak."""
+    from basicsr4rs_amd.ops import swin as S
+    net = model.get_bare_model(model.net_g)
+    blk = net._blocks()[1]  # a shifted block
+    at = blk.attn
+    g, fc1s, fc2s = blk._geom, blk._fc1, blk._fc2
+    Cp = fc1s.cin_p
+    x = torch.randn(batch, lr_px, lr_px, Cp, device=dev).to(torch.bfloat16)
+    x[..., g.dim:] = 0
+    qwf, _, qbg = S.prepared_linear(at.qkv.weight, at.qkv.bias, g.qkv, torch.bfloat16)
+    pwf, _, pbg = S.prepared_linear(at.proj.weight, at.proj.bias, g.proj, torch.bfloat16)
+    f1wf, _, f1bg = S.prepared_linear(blk.mlp.fc1.weight, blk.mlp.fc1.bias, fc1s, torch.bfloat16)
+    f2wf, _, f2bg = S.prepared_linear(blk.mlp.fc2.weight, blk.mlp.fc2.bias, fc2s, torch.bfloat16)
+    tab = at.relative_position_bias_table.detach().float().contiguous()
+    out = {}
+    calls = {
+        'attention_train': lambda: S.swin_attn_fused(x, blk.norm1.weight, blk.norm1.bias, g.dim, qwf, qbg, tab, pwf, pbg,
+                                                     None, g, float(at.scale), True),
+        'attention_inference': lambda: S.swin_attn_fused(x, blk.norm1.weight, blk.norm1.bias, g.dim, qwf, qbg, tab, pwf,
+                                                         pbg, None, g, float(at.scale), False),
+        'mlp_train': lambda: S.swin_mlp_fused(x, blk.norm2.weight, blk.norm2.bias, g.dim, f1wf, f1bg, fc1s, f2wf, f2bg,
+                                              None, True),
+    }
+    N, H, W = batch, lr_px, lr_px
+    flops = {'attention_train': S.attn_block_flops(g, N, H, W), 'attention_inference': S.attn_block_flops(g, N, H, W),
+             'mlp_train': 4.0 * N * H * W * fc1s.cin * fc1s.cout}
+    with torch.no_grad():
+        for name, fn in calls.items():
+            if fn() is None:
+                return None
+            for _ in range(3):
+                fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            s.record()
+            for _ in range(reps):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            us = s.elapsed_time(e) / reps * 1e3
+            tf = flops[name] / (us * 1e-6) / 1e12
+            out[name] = {'us': round(us, 2), 'tflops': round(tf, 1), 'frac_mfma_peak': round(tf / PEAK_BF16_TFLOPS, 4)}
+    out['kernels'] = 'swin_attn_block_fwd_kernel / swin_mlp_block_fwd_kernel'
+    out['flops'] = 'attention: qkv + QK^T + AV + proj (unpadded C 180, head dim 30); mlp: fc1 + fc2'
+    return out
+
+
 def _pmc_traffic(workload, kernel):
     """HBM bytes per launch of ``kernel`` from this round's committed PMC passes
     (tools/profile_round.sh -> profiles/pmc_traffic.json), or None."""
@@ -458,7 +511,9 @@ def main():
     roof = None
     if kstats:
         roof = roofline(args.workload, kstats, traced_steps, dt / args.steps, use_graph)
-    cpu = parity = None
+    cpu = parity = swin_att = None
+    if rank == 0 and args.workload == 'swinir':
+        swin_att = swin_fused_roofline(model, B, lr_px, dev)
     if rank == 0 and world == 1 and not args.no_parity:
         parity = parity_check(args.workload, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -472,6 +527,7 @@ def main():
             'config': _config(args.workload, B, world, use_graph, opt['train']['async_wgrad']),
             'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
             'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu, 'parity': parity,
+            'swin_fused_attention': swin_att,
         }
         print(json.dumps(line))
         if not math.isfinite(loss):  # a step that trains on NaNs is not a measurement
