@@ -383,15 +383,20 @@ class SwinIR(nn.Module):
     def forward(self, x):
         dev = x.device
         if self._consts is None or self._consts[0] != dev:
+            # the reference broadcasts self.mean ([1, 3 | 1, 1, 1], swinir_arch.py:750-754, 860-861,
+            # 918) over the input and output channels: the kernels take one value per channel (a
+            # 4-band remote-sensing net has a 1-element zero mean and 4 channels each side)
             mean = self.mean.reshape(-1).float().to(dev)
-            self._consts = (dev, mean, C.vec([self.img_range] * self.num_in_ch, dev),
+            mean_in = torch.broadcast_to(mean, (self.num_in_ch, )).contiguous()
+            mean_out = torch.broadcast_to(mean, (self.num_out_ch, )).contiguous()
+            self._consts = (dev, mean_in, mean_out, C.vec([self.img_range] * self.num_in_ch, dev),
                             C.inv_range(self.img_range, self.num_out_ch, dev))
-        _, mean, rng, inv = self._consts
+        _, mean_in, mean, rng, inv = self._consts
         H, W = x.shape[2], x.shape[3]
         if H % self.window_size or W % self.window_size:
             raise ValueError('SwinIR input must be a multiple of window_size (pad it as SwinIRModel.test does)')
         dt = C.feature_dtype()
-        h = C.to_nhwc(x, C.pad8(self.num_in_ch), dt, shift=mean, scale=rng)
+        h = C.to_nhwc(x, C.pad8(self.num_in_ch), dt, shift=mean_in, scale=rng)
         x0 = C.conv3x3(h, self.conv_first)
         res = C.conv3x3(self.forward_features(x0), self.conv_after_body, res=x0)
         if self.upsampler == 'pixelshuffle':

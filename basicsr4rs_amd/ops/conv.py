@@ -284,6 +284,8 @@ def conv_fwd_raw(x, wf, bias_g, y, N, H, W, cin, cout, cout_real, gate=None, res
     summed over P they are the per-image channel sums): ``(y, parts)``; with ``dot=t`` (bf16, y's
     shape) they are the partial sums of y * t instead (band kernel only, dot_partials_ok)."""
     assert x.is_contiguous() and y.is_contiguous()
+    _check_channel_vec(aff_scale, cout_real, 'conv aff_scale')
+    _check_channel_vec(aff_shift, cout_real, 'conv aff_shift')
     ldx = kw.pop('ldx', x.shape[-1])
     ldy = kw.pop('ldy', y.shape[-1] if not kw.get('out_nchw') else 0)
     if gate is not None:
@@ -636,9 +638,17 @@ class _ToNHWC(torch.autograd.Function):
         return nhwc_to_nchw(dy.contiguous(), ctx.c, scale=ctx.scale), None, None, None, None
 
 
+def _check_channel_vec(v, c, what):
+    """A per-channel fp32 vector the kernels index 0 .. c - 1 (a short one would be read past its end)."""
+    if v is not None and v.numel() < c:
+        raise ValueError(f'{what} has {v.numel()} values for {c} channels')
+
+
 def to_nhwc(x, cp, dtype, shift=None, scale=None):
     if x.shape[1] > cp:
         raise ValueError('channel padding smaller than the input channels')
+    _check_channel_vec(shift, x.shape[1], 'to_nhwc shift')
+    _check_channel_vec(scale, x.shape[1], 'to_nhwc scale')
     return _ToNHWC.apply(x.contiguous().float(), cp, dtype, shift, scale)
 
 
@@ -685,4 +695,6 @@ class _ToNCHW(torch.autograd.Function):
 
 
 def to_nchw(x, c, scale=None, shift=None):
+    _check_channel_vec(shift, c, 'to_nchw shift')
+    _check_channel_vec(scale, c, 'to_nchw scale')
     return _ToNCHW.apply(x, c, scale, shift)
