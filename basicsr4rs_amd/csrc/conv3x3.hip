@@ -4070,16 +4070,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
 // group with fewer rows idles through the extra steps); at the end group 1 hands its accumulators
 // to group 0 through LDS and group 0 writes ONE slab for the block.  Against two 4-wave blocks per
 // CU (VB = 1) it halves the slab written per CU (and read by the reduce) at the same occupancy.
-template <int CO_T, int D = 2, int LA = 3, bool EARLY = false, int VB = 1>  // D: steps in flight
-__global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
+// CS = 2 (round 4): an 8-wave block of two 4-wave CO groups over the same rows: both read one x ring
+// (loaded by group 0), group c multiplies the c-th half of the dy tiles.  Against two 4-wave blocks
+// per CU it halves the slab (and the reduce) and the x DMAs per pixel at the same MFMA work per
+// SIMD, with half the accumulators per wave (no spill at CO_T 4).
+template <int CO_T, int D = 2, int LA = 3, bool EARLY = false, int VB = 1, int CS = 1>  // D: steps in flight
+__global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   static_assert(VB == 1 || (VB == 2 && !EARLY), "two row groups: the two-barrier schedule only");
-  constexpr int CW = CO_T;  // co tiles per wave
+  static_assert(CS == 1 || (CS == 2 && VB == 1 && !EARLY && CO_T % 2 == 0), "co split: even co tiles, one row group");
+  constexpr int CW = CO_T / CS;  // co tiles per wave
   constexpr int RS = 3 * 1024;      // one halo row of one 16-ci tile: 96 rows x 32 B (66 used)
   constexpr int RSL = D + (EARLY ? 3 : 2);  // ring slots: rows q-1 .. q+1 read, D - 1 in flight (+1 being issued)
   constexpr int RING = (RSL + 1) * RS;  // + the zero slot, per ci tile
   constexpr int DYB = CO_T * 2048;  // dy image: CO_T tiles x 64 rows x 32 B
   constexpr int DYS = DYB + 1024;   // + 1 KB target for padding DMAs
-  constexpr int DYI = (CO_T * 2 + 3) / 4;  // dy DMAs per wave
+  constexpr int NWD = 4 * CS;  // waves sharing the dy DMAs of a step
+  constexpr int DYI = (CO_T * 2 + NWD - 1) / NWD;  // dy DMAs per wave
   constexpr int DST = D + (EARLY ? 1 : 0);  // dy stages
   constexpr int GRP = 4 * RING + DST * DYS;  // LDS of one row group
   static_assert(VB == 1 || GRP * VB >= (4 * 9 * CW + CW) * 64 * 16, "LDS hand-over of group 1's accumulators");
@@ -4087,7 +4093,9 @@ __global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wl = w & 3;  // wave within its row group
-  const int vb = w >> 2;  // row group
+  const int vb = VB > 1 ? w >> 2 : 0;  // row group
+  const int cs = CS > 1 ? w >> 2 : 0;  // co group
+  const int wd = CS > 1 ? w : wl;  // index among the waves sharing the dy DMAs
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
   // block = (split, co tile, ci chunk), ci fastest: the tiles of one split (the same x / dy rows)
   // are consecutive, so xcd_remap keeps them on one XCD's L2
@@ -4116,7 +4124,7 @@ __global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs 
   char* ring = smem + vb * GRP + wl * RING;
   char* dys = smem + vb * GRP + 4 * RING;
   auto slot = [](int q) { return (q + RSL) % RSL; };  // q >= -1
-  constexpr bool xdma = true;  // every wave loads its ci tile's x rows and some dy
+  const bool xdma = cs == 0;  // the (first co group's) waves load their ci tile's x rows; all load some dy
 
   // this lane's halo pixels of its 3 DMAs per row: physical row 32i + (lane >> 1) holds pixel
   // hrow(.) (x0 - 1 + that), channel half lane & 1
@@ -4138,7 +4146,8 @@ __global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs 
     for (int c = 0; c < CW; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < CW; ++c) accb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int ct0 = 0, ncw = CW;
+  const int ct0 = cs * CW;
+  constexpr int ncw = CW;
   const bool do_bias = a.wsb != nullptr && chunk == 0 && wl == 0;
 
   // x halo row q (global image row; outside [0, rows_total) -> zeros), column segment seg
@@ -4173,7 +4182,7 @@ __global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs 
     char* st = dys + (j % DST) * DYS;
 #pragma unroll
     for (int i = 0; i < DYI; ++i) {
-      const int k = wl + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
+      const int k = wd + NWD * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
       char* dst = st + DYB;
       uint32_t off = SR_OOB;
       if (k < CO_T * 2) {
@@ -4266,7 +4275,10 @@ __global__ __launch_bounds__(256 * VB, 1) void conv3x3_wgrad_ring_kernel(WgArgs 
     // step ks's DMAs landed; the steps issued after it may stay in flight
     if (next == ks + D && (ks + 1) % nrows != 0 && (ks + 1) / nrows == (next - 1) / nrows) {
       // steady state: the D - 1 steps after ks, none of them a segment's first
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (DYI + 3)) : "memory");
+      if (xdma)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (DYI + 3)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * DYI) : "memory");
     } else {
       int younger = 0;
       for (int j = ks + 1; j < next; ++j) younger += nops(j);
@@ -5336,19 +5348,50 @@ bool ring_early();
 int ring_depth();
 int ring_la();
 bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d);
+// Co split of the narrow ring wgrad (opt-in SR_RING_COSPLIT=1 / variant 75; A/B): Cout 64 (or 48 / 40 ..,
+// a multiple of 32 above 32) as two 32-channel co tiles of separate blocks over twice the rows each:
+// the same block count, half the slab (and reduce) per block and in total, x read by both co
+// tiles (the second time from L2: the tiles of one split are consecutive blocks on one XCD).
+bool ring_cosplit(const sr_conv3x3_wgrad_desc* d) {
+  static const bool v = [] {
+    const char* e = getenv("SR_RING_COSPLIT");
+    return e && atoi(e) == 1;
+  }();
+  return (v || g_variant == 75) && wg_use_ring() && !wg_ring_wide(d) && d->Cout > 32 && d->Cout % 32 == 0;
+}
 // 16-channel co tiles per wave of the ring / halo wgrad
-int ring_ct(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? 4 : (d->Cout + 15) / 16; }
-// Row groups per ring-wgrad block: 2 (8-wave blocks, one per CU, one slab per block; CO_T <= 2 --
-// at 3 / 4 co tiles per wave the two-waves-per-SIMD register budget spills: 12 / 132 VGPRs, with
-// fragment lookahead 3 or 1 alike), or
-// SR_RING_VB=1 (4-wave blocks, two per CU; A/B) / variant 69 (parity tests of the 4-wave form).
+int ring_ct(const sr_conv3x3_wgrad_desc* d) {
+  return wg_ring_wide(d) ? 4 : ring_cosplit(d) ? 2 : (d->Cout + 15) / 16;
+}
+int ring_tiles_co(const sr_conv3x3_wgrad_desc* d) {
+  return wg_ring_wide(d) ? (d->Cout + 63) / 64 : ring_cosplit(d) ? d->Cout / 32 : 1;
+}
+// Row groups per ring-wgrad block: 1 (4-wave blocks, two per CU), or SR_RING_VB=2 (A/B; CO_T <= 2:
+// 8-wave blocks, one per CU, one slab per block -- at 3 / 4 co tiles per wave the two-waves-per-SIMD
+// register budget spills: 12 / 132 VGPRs, with fragment lookahead 3 or 1 alike).  Measured on RRDB
+// (profiles/r04/ab/): 66.6 ms at 1 vs 68.0 ms at 2 (ring + reduce 60.3 vs 64.7 us per call): two
+// independent 4-wave blocks overlap each other's barriers, one 8-wave block does not, and that
+// costs more than the halved slab saves.  Variant 69: the 4-wave form; 0 keeps the default.
 // The early-issue and deeper-pipeline A/B forms are 4-wave only.
 int ring_vb() {
   static const int v = [] {
     const char* e = getenv("SR_RING_VB");
-    return e && atoi(e) == 1 ? 1 : 2;
+    return e && atoi(e) == 2 ? 2 : 1;
   }();
-  return (g_variant == 69 || ring_early() || ring_depth() != 2 || ring_la() != 3) ? 1 : v;
+  return (g_variant == 69 || ring_early() || ring_depth() != 2 || ring_la() != 3) ? 1 : (g_variant == 74 ? 2 : v);
+}
+
+// Co groups per ring-wgrad block (CO_T 4, 4-wave form otherwise): 2 with SR_RING_CS=1 (A/B) or
+// variant 73 (parity tests): one 8-wave block per CU over twice the rows, half the slab.  Measured
+// on RCAN (profiles/r04/ab/): ring + reduce 39.1 vs 38.8 us per call, step 40.1 vs 37.9 ms -- the
+// halved slab is paid back by the lost overlap of two independent blocks, as for SR_RING_VB=2.
+int ring_cs(int ct) {
+  static const int v = [] {
+    const char* e = getenv("SR_RING_CS");
+    return e && atoi(e) == 1 ? 2 : 1;
+  }();
+  if (ct != 4 || ring_early() || ring_depth() != 2 || ring_la() != 3) return 1;
+  return g_variant == 73 ? 2 : (g_variant == 69 ? 1 : v);
 }
 
 // Early DMA issue in the ring wgrad (one barrier per step, one more LDS slot): SR_RING_EARLY=1 (A/B; read once)
@@ -5379,8 +5422,8 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     // (A/B on RCAN / RRDB: twice or half as many splits are 6-12 % slower per step)
     const int chunks = (d->Cin + 63) / 64;
     // (an 8-wave two-row-group block takes a CU alone: half the block target)
-    const int vbdiv = wg_use_ring() && ring_ct(d) <= 2 ? ring_vb() : 1;
-    int S = (wg_ring_wide(d) ? ring_wide_target() / (chunks * ((d->Cout + 63) / 64)) : ring_split_target() / chunks) / vbdiv;
+    const int vbdiv = !wg_use_ring() ? 1 : ring_ct(d) <= 2 ? ring_vb() : ring_cs(ring_ct(d));
+    int S = (wg_ring_wide(d) ? ring_wide_target() : ring_split_target()) / (chunks * ring_tiles_co(d)) / vbdiv;
     const int maxS = M / 512 > 1 ? M / 512 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
@@ -5675,7 +5718,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 72)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 75)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
@@ -5799,7 +5842,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   hipError_t e;
   a.stamps = g_stamps;
   if (wg_use_halo(d)) {
-    a.tiles_co = wg_ring_wide(d) ? (a.Cout + 63) / 64 : 1;
+    a.tiles_co = ring_tiles_co(d);
     a.tiles_ci = (a.Cin + 63) / 64;
     const int ct = ring_ct(d);
     const dim3 grid(S * a.tiles_ci * a.tiles_co);
@@ -5810,6 +5853,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
       const int vbn = ct <= 2 ? ring_vb() : 1;
 #define SR_RING(CT_)                                                                                     \
   if (vbn == 2 && CT_ <= 2) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<(CT_ <= 2 ? CT_ : 2), 2, 3, false, 2>), grid, dim3(512), 0, s, a); \
+  else if (CT_ == 4 && ring_cs(4) == 2) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<4, 2, 3, false, 1, 2>), grid, dim3(512), 0, s, a); \
   else if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);   \
   else if (D == 3) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 3>), grid, dim3(256), 0, s, a);   \
   else if (la == 5) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 5>), grid, dim3(256), 0, s, a); \

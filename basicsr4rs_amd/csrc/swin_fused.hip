@@ -32,7 +32,13 @@
 #include "sr_internal.h"
 #include "swin_common.h"
 
+#include <type_traits>
+
 namespace {
+
+SR_DEV uint2 buf_load8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
 
 struct SabArgs {
   const bf16_t* x;
@@ -63,9 +69,11 @@ constexpr int SAB_Q = SAB_W + 3 * 96 * 128;   // [128 tokens][64 B]
 constexpr int SAB_K = SAB_Q + 128 * 64;
 constexpr int SAB_V = SAB_K + 128 * 64;  // [2 windows][64][64 B], sx_byte layout (tr reads)
 constexpr int SAB_O = SAB_V + 128 * 64;  // [128 tokens][64 B]
-constexpr int SAB_TB = SAB_O + 128 * 64;  // float [256]: the head's bias-table column
-constexpr int SAB_GB = SAB_TB + 256 * 4;  // float [2][192]: LayerNorm gamma, beta
-constexpr int SAB_LDS = SAB_GB + 2 * 192 * 4;
+constexpr int SAB_TB = SAB_O + 128 * 64;  // float [225][nH <= 6]: the relative-position bias table
+constexpr int SAB_GB = SAB_TB + 5408;         // float [2][192]: LayerNorm gamma, beta (table padded to 16 B)
+constexpr int SAB_BQ = SAB_GB + 2 * 192 * 4;  // float [3 nH 32 <= 576]: qkv bias
+constexpr int SAB_BP = SAB_BQ + 576 * 4;      // float [192]: proj bias
+constexpr int SAB_LDS = SAB_BP + 192 * 4;
 constexpr int SAB_WPIECES = 96 * 24;  // 16-B pieces of W_h (K <= 192)
 constexpr int SAB_WREG = (SAB_WPIECES + 511) / 512;
 
@@ -87,6 +95,8 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   const bool train = a.qkv != nullptr;
   float* sTB = (float*)(smem + SAB_TB);
   float* sGB = (float*)(smem + SAB_GB);
+  float* sBQ = (float*)(smem + SAB_BQ);
+  float* sBP = (float*)(smem + SAB_BP);
 
   // window geometry of the block's two windows
   auto win_of = [&](int wi, int& n, int& wy, int& wx) -> bool {
@@ -110,18 +120,18 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   };
 
   // ---- head 0's weights into registers first (their L2 round trip overlaps the LayerNorm)
+  // weight loads through buffer resources (out of range -> 0, no branches: the compiler's vmcnt
+  // bookkeeping stays exact across them)
+  const auto wqr = make_rsrc(a.wq, (uint32_t)((size_t)3 * a.nH * 32 * a.Cp * 2));
+  const auto wpr = make_rsrc(a.wp, (uint32_t)((size_t)a.Cp * a.ldo * 2));
   u32x4 wreg[SAB_WREG];
   auto w_load = [&](int h) {
 #pragma unroll
     for (int k = 0; k < SAB_WREG; ++k) {
       const int p = tid + 512 * k;
       const int rr = p / 24, ch = p - rr * 24;
-      u32x4 v = u32x4{0u, 0u, 0u, 0u};
-      if (p < SAB_WPIECES && ch < a.KC) {
-        const int grow = (rr >> 5) * a.nH * 32 + h * 32 + (rr & 31);
-        v = *(const u32x4*)(a.wq + (size_t)grow * a.Cp + ch * 8);
-      }
-      wreg[k] = v;
+      const int grow = (rr >> 5) * a.nH * 32 + h * 32 + (rr & 31);
+      wreg[k] = buf_load16(wqr, (p < SAB_WPIECES && ch < a.KC) ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB);
     }
   };
   auto w_store = [&]() {
@@ -132,10 +142,12 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       if (p < SAB_WPIECES) *(u32x4*)(smem + SAB_W + tile_off(96, rr, ch)) = wreg[k];
     }
   };
-  auto t_store = [&](int h) {
-    if (tid < 256) sTB[tid] = tid < 225 ? a.table[tid * a.nH + h] : 0.f;
-  };
   w_load(0);
+  // every small operand (bias table, qkv / proj biases) into LDS before the first global store: on
+  // gfx9 vmcnt counts stores too, so a global load issued after stores makes its wait drain them
+  for (int i = tid; i < 225 * a.nH; i += 512) sTB[i] = a.table[i];
+  for (int i = tid; i < 3 * a.nH * 32; i += 512) sBQ[i] = a.bq[i];
+  if (tid < 192) sBP[tid] = tid < a.Cp ? a.bp[tid] : 0.f;
   if (tid < 192) {
     sGB[tid] = tid < a.C ? a.ln_g[tid] : 0.f;
     sGB[192 + tid] = tid < a.C ? a.ln_b[tid] : 0.f;
@@ -202,7 +214,6 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
     }
   }
   w_store();
-  t_store(0);
   __syncthreads();
 
   // per-wave constants
@@ -241,12 +252,15 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
     for (int j = 0; j < 4; ++j) xacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   for (int h = 0; h < a.nH; ++h) {
+    // The head's global loads (projection columns, the next head's weights) are issued here, before
+    // its qkv / ao / lse stores; the biases and the table come from LDS (a bias loaded from global
+    // after the stores drained all of them, three times per head, in the first version).
     // this head's projection columns (A operand of step C) and the next head's weights, in flight
     u32x4 wpf[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int row = pog * 48 + 16 * i + c16;
-      wpf[i] = row < a.Cp ? *(const u32x4*)(a.wp + (size_t)row * a.ldo + h * 32 + 8 * g) : u32x4{0u, 0u, 0u, 0u};
+      wpf[i] = buf_load16(wpr, row < a.Cp ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
     }
     if (h + 1 < a.nH) w_load(h + 1);
 
@@ -274,7 +288,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       const int oc = og * 48 + 16 * i + 4 * g;  // 4 consecutive rows of q / k / v (one of them)
       const int which = oc >> 5, d = oc & 31;
       const int gr = which * a.nH * 32 + h * 32 + d;
-      const f32x4 bias = *(const f32x4*)(a.bq + gr);
+      const f32x4 bias = *(const f32x4*)(sBQ + gr);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int t = tg * 32 + 16 * j + c16;
@@ -304,7 +318,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = 16 * i + 4 * g + r;
-          float v = s[i][r] * a.scale + sTB[bin8(qq, k)];
+          float v = s[i][r] * a.scale + sTB[bin8(qq, k) * a.nH + h];
           if (a.shift && rk[i][r] != rq) v -= 100.f;
           s[i][r] = v;
           mx = fmaxf(mx, v);
@@ -345,11 +359,8 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         *(uint2*)(smem + SAB_O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
       }
     }
-    __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW) and step B (sTB)
-    if (h + 1 < a.nH) {
-      w_store();
-      t_store(h + 1);
-    }
+    __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW)
+    if (h + 1 < a.nH) w_store();
 
     // ---- C: x2acc += Wp[:, head h] . O_h^T
 #pragma unroll
@@ -358,22 +369,42 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
 #pragma unroll
       for (int i = 0; i < 3; ++i) xacc[i][j] = mfma16(__builtin_bit_cast(s16x8, wpf[i]), of, xacc[i][j]);
     }
-    __syncthreads();  // S3: sO read; the next head's sW / sTB written
+    __syncthreads();  // S3: sO read; the next head's sW written
   }
 
-  // ---- epilogue: x2 = x + s1[n] * (proj + bias)
+  // ---- epilogue: x2 = x + s1[n] * (proj + bias); all loads before the first store (see above)
+  f32x4 biasp[3];
+  uint2 xres[3][4];
+  float scj[4];
+  int64_t pixj[4];
+  bool vj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int n;
+    vj[j] = tok_pix(ptg * 64 + 16 * j + c16, pixj[j], n);
+    scj[j] = (a.rsc && vj[j]) ? a.rsc[n] : 1.f;
+  }
+  const auto xr = make_rsrc(a.x, (uint32_t)((size_t)a.N * a.H * a.W * a.Cp * 2));
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int oc = pog * 48 + 16 * i + 4 * g;
+    biasp[i] = oc < a.Cp ? *(const f32x4*)(sBP + oc) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      xres[i][j] = buf_load8(xr, (oc < a.Cp && vj[j]) ? (uint32_t)(pixj[j] * a.Cp + oc) * 2u : SR_OOB);
+  }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int oc = pog * 48 + 16 * i + 4 * g;
     if (oc >= a.Cp) continue;
-    const f32x4 bias = *(const f32x4*)(a.bp + oc);
+    const f32x4 bias = biasp[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      int64_t pix;
-      int n;
-      if (!tok_pix(ptg * 64 + 16 * j + c16, pix, n)) continue;
-      const float sc = a.rsc ? a.rsc[n] : 1.f;
-      const uint2 xv = *(const uint2*)(a.x + pix * a.Cp + oc);
+      if (!vj[j]) continue;
+      const int64_t pix = pixj[j];
+      const float sc = scj[j];
+      const uint2 xv = xres[i][j];
       uint2 u;
       u.x = pack_bf16x2(bf16_to_f32(xv.x & 0xffff) + sc * (xacc[i][j][0] + bias[0]),
                         bf16_to_f32(xv.x >> 16) + sc * (xacc[i][j][1] + bias[1]));
@@ -418,7 +449,9 @@ struct SmbArgs {
 
 constexpr int SMB_H = 0;                 // [6 cg][128][128 B]: LN(x2) tile (cg 0..2), then h (cg 0..5)
 constexpr int SMB_GB = 6 * 128 * 128;    // float [2][192]
-constexpr int SMB_LDS = SMB_GB + 2 * 192 * 4;
+constexpr int SMB_B1 = SMB_GB + 2 * 192 * 4;  // float [384]: fc1 bias
+constexpr int SMB_B2 = SMB_B1 + 384 * 4;      // float [192]: fc2 bias
+constexpr int SMB_LDS = SMB_B2 + 192 * 4;
 
 __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[SMB_LDS];
@@ -428,9 +461,30 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   const int m0 = (int)xcd_remap(blockIdx.x, gridDim.x) * 128;
   const bool train = a.z != nullptr;
   float* sGB = (float*)(smem + SMB_GB);
+  float* sB1 = (float*)(smem + SMB_B1);
+  float* sB2 = (float*)(smem + SMB_B2);
+  if (tid < 384) sB1[tid] = tid < a.Hp ? a.b1[tid] : 0.f;
+  if (tid < 192) sB2[tid] = tid < a.Cp ? a.b2[tid] : 0.f;
   if (tid < 192) {
     sGB[tid] = tid < a.C ? a.ln_g[tid] : 0.f;
     sGB[192 + tid] = tid < a.C ? a.ln_b[tid] : 0.f;
+  }
+  // fc1's first two K-steps of W1 fragments, issued before the LayerNorm's stores (on gfx9 vmcnt
+  // counts stores too: a load issued after them waits for them)
+  const int ntl = (a.Hp + 15) / 16;
+  const auto w1r = make_rsrc(a.w1, (uint32_t)((size_t)a.Hp * a.Cp * 2));
+  const auto w2r = make_rsrc(a.w2, (uint32_t)((size_t)a.Cp * a.Hp * 2));
+  const auto xr = make_rsrc(a.x, (uint32_t)((size_t)a.M * a.Cp * 2));
+  auto w1_frag = [&](int i, int kk) -> s16x8 {  // buffer loads: no branches around the MFMAs
+    const int row = 16 * (w + 8 * i) + c16, ch = 4 * kk + g;
+    const bool v = w + 8 * i < ntl && row < a.Hp && ch < a.KC;
+    return __builtin_bit_cast(s16x8, buf_load16(w1r, v ? (uint32_t)(row * a.Cp + ch * 8) * 2u : SR_OOB));
+  };
+  s16x8 af[2][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    af[0][i] = w1_frag(i, 0);
+    af[1][i] = w1_frag(i, 1);
   }
   // ---- LayerNorm of the 128 rows: 4 lanes per row
   {
@@ -492,40 +546,57 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   }
   __syncthreads();
 
-  // ---- fc1: hidden tiles t = w, w + 8, w + 16 (< 23) x all 128 tokens
-  const int ntl = (a.Hp + 15) / 16;
+  // ---- fc1: hidden tiles t = w, w + 8, w + 16 (< 23) x all 128 tokens; W1 fragments two K-steps ahead
   f32x4 acc[3][8];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto w1_frag = [&](int i, int kk) -> s16x8 {
-    const int row = 16 * (w + 8 * i) + c16, ch = 4 * kk + g;
-    u32x4 v = u32x4{0u, 0u, 0u, 0u};
-    if (w + 8 * i < ntl && row < a.Hp && ch < a.KC) v = *(const u32x4*)(a.w1 + (size_t)row * a.Cp + ch * 8);
-    return __builtin_bit_cast(s16x8, v);
+  // the wave's tile count (1..3) as a compile-time constant: a run-time guard per MFMA made the
+  // compiler drain every counter before each one
+  auto fc1 = [&](auto nt_) {
+    constexpr int NT = decltype(nt_)::value;
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      s16x8 an[3];
+      if (kk + 2 < 6) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) an[i] = w1_frag(i, kk + 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch here (the scheduler sinks it to its use)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const s16x8 bf = *(const s16x8*)(smem + SMB_H + tile_off(128, 16 * j + c16, 4 * kk + g));
+#pragma unroll
+        for (int i = 0; i < NT; ++i) acc[i][j] = mfma16(af[kk & 1][i], bf, acc[i][j]);
+      }
+      if (kk + 2 < 6) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) af[kk & 1][i] = an[i];
+      }
+    }
   };
-  s16x8 af[3];
+  if (w + 16 < ntl) fc1(std::integral_constant<int, 3>{});
+  else if (w + 8 < ntl) fc1(std::integral_constant<int, 2>{});
+  else if (w < ntl) fc1(std::integral_constant<int, 1>{});
+  // fc2's first W2 fragments and fc1's biases, before the z / h stores
+  const int og = w & 3, tg = w >> 2;
+  auto w2_frag = [&](int i, int kk) -> s16x8 {
+    const int row = og * 48 + 16 * i + c16, ch = 4 * kk + g;
+    const bool v = row < a.Cp && ch < a.HC;
+    return __builtin_bit_cast(s16x8, buf_load16(w2r, v ? (uint32_t)(row * a.Hp + ch * 8) * 2u : SR_OOB));
+  };
+  constexpr int W2LA = 3;  // fc2 K-steps of W2 fragments in flight
+  s16x8 bf2[W2LA][3];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) af[i] = w1_frag(i, 0);
+  for (int u = 0; u < W2LA; ++u)
 #pragma unroll
-  for (int kk = 0; kk < 6; ++kk) {
-    s16x8 an[3];
-    if (kk + 1 < 6) {
+    for (int i = 0; i < 3; ++i) bf2[u][i] = w2_frag(i, u);
+  f32x4 bias1[3];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) an[i] = w1_frag(i, kk + 1);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const s16x8 bf = *(const s16x8*)(smem + SMB_H + tile_off(128, 16 * j + c16, 4 * kk + g));
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (w + 8 * i < ntl) acc[i][j] = mfma16(af[i], bf, acc[i][j]);
-    }
-    if (kk + 1 < 6) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) af[i] = an[i];
-    }
+  for (int i = 0; i < 3; ++i) {
+    const int hr = 16 * (w + 8 * i) + 4 * g;
+    bias1[i] = (w + 8 * i < ntl && hr < a.Hp) ? *(const f32x4*)(sB1 + hr) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();  // every wave done with the LN tile: h overwrites it
   // hidden chunks past the last computed tile read as zeros in fc2 (0 x stale LDS could be NaN)
@@ -537,8 +608,7 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   for (int i = 0; i < 3; ++i) {
     if (w + 8 * i >= ntl) continue;
     const int hr = 16 * (w + 8 * i) + 4 * g;  // 4 consecutive hidden channels
-    f32x4 bias = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (hr < a.Hp) bias = *(const f32x4*)(a.b1 + hr);
+    const f32x4 bias = bias1[i];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int t = 16 * j + c16, m = m0 + t;
@@ -563,51 +633,61 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   __syncthreads();  // h tile complete
 
   // ---- fc2: wave = 48 output channels (og) x 64 tokens (tg), K = 384 hidden (zero past Hp)
-  const int og = w & 3, tg = w >> 2;
   f32x4 acc2[3][4];
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto w2_frag = [&](int i, int kk) -> s16x8 {
-    const int row = og * 48 + 16 * i + c16, ch = 4 * kk + g;
-    u32x4 v = u32x4{0u, 0u, 0u, 0u};
-    if (row < a.Cp && ch < a.HC) v = *(const u32x4*)(a.w2 + (size_t)row * a.Hp + ch * 8);
-    return __builtin_bit_cast(s16x8, v);
-  };
-  s16x8 bf2[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) bf2[i] = w2_frag(i, 0);
 #pragma unroll
   for (int kk = 0; kk < 12; ++kk) {
     s16x8 bn[3];
-    if (kk + 1 < 12) {
+    if (kk + W2LA < 12) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) bn[i] = w2_frag(i, kk + 1);
+      for (int i = 0; i < 3; ++i) bn[i] = w2_frag(i, kk + W2LA);
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const s16x8 hf = *(const s16x8*)(smem + SMB_H + tile_off(128, tg * 64 + 16 * j + c16, 4 * kk + g));
 #pragma unroll
-      for (int i = 0; i < 3; ++i) acc2[i][j] = mfma16(bf2[i], hf, acc2[i][j]);
+      for (int i = 0; i < 3; ++i) acc2[i][j] = mfma16(bf2[kk % W2LA][i], hf, acc2[i][j]);
     }
-    if (kk + 1 < 12) {
+    if (kk + W2LA < 12) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) bf2[i] = bn[i];
+      for (int i = 0; i < 3; ++i) bf2[kk % W2LA][i] = bn[i];
     }
   }
-  // ---- out = x2 + s2[n] * (fc2 + bias)
+  // ---- out = x2 + s2[n] * (fc2 + bias); all loads before the first store
+  f32x4 bias2[3];
+  uint2 xres[3][4];
+  float scj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + tg * 64 + 16 * j + c16;
+    scj[j] = (a.rsc && m < a.M) ? a.rsc[m / a.HW] : 1.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int oc = og * 48 + 16 * i + 4 * g;
+    bias2[i] = oc < a.Cp ? *(const f32x4*)(sB2 + oc) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + tg * 64 + 16 * j + c16;
+      xres[i][j] = buf_load8(xr, (oc < a.Cp && m < a.M) ? (uint32_t)(m * a.Cp + oc) * 2u : SR_OOB);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int oc = og * 48 + 16 * i + 4 * g;
     if (oc >= a.Cp) continue;
-    const f32x4 bias = *(const f32x4*)(a.b2 + oc);
+    const f32x4 bias = bias2[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + tg * 64 + 16 * j + c16;
       if (m >= a.M) continue;
-      const float sc = a.rsc ? a.rsc[m / a.HW] : 1.f;
-      const uint2 xv = *(const uint2*)(a.x + (int64_t)m * a.Cp + oc);
+      const float sc = scj[j];
+      const uint2 xv = xres[i][j];
       uint2 u;
       u.x = pack_bf16x2(bf16_to_f32(xv.x & 0xffff) + sc * (acc2[i][j][0] + bias[0]),
                         bf16_to_f32(xv.x >> 16) + sc * (acc2[i][j][1] + bias[1]));
@@ -639,6 +719,8 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
     return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: training needs ln_out, mean, rstd, qkv, attn_out and lse");
   if (!sr_swin_attn_fused_ok(SR_BF16, N, H, W, 8, nH, 32, 32, C, Cp) || shift < 0 || shift >= 8)
     return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: bf16, window 8, head dim <= 32, nH * 32 <= 192, Cp <= 192");
+  if ((size_t)N * H * W * Cp * 2 >= 0x80000000ull)
+    return sr_fail(SR_ETOOBIG, "swin_attn_fused_fwd: token map >= 2 GiB (split the batch)");
   SabArgs a{};
   a.x = (const bf16_t*)x; a.ln_g = ln_g; a.ln_b = ln_b; a.wq = (const bf16_t*)wqkv; a.bq = bqkv;
   a.table = bias_table; a.wp = (const bf16_t*)wproj; a.bp = bproj; a.rsc = row_scale;
@@ -667,6 +749,8 @@ int sr_swin_mlp_fused_fwd(const void* x, const float* ln_g, const float* ln_b, i
     return sr_fail(SR_EINVAL, "swin_mlp_fused_fwd: training needs ln_out, mean, rstd, z and h");
   if (!sr_swin_mlp_fused_ok(SR_BF16, C, Cp, Hp) || N <= 0 || HW <= 0)
     return sr_fail(SR_EINVAL, "swin_mlp_fused_fwd: bf16, Cp <= 192, hidden <= 368 (multiples of 8)");
+  if ((size_t)N * HW * (Cp > Hp ? Cp : Hp) * 2 >= 0x80000000ull)
+    return sr_fail(SR_ETOOBIG, "swin_mlp_fused_fwd: token map >= 2 GiB (split the batch)");
   SmbArgs a{};
   a.x = (const bf16_t*)x; a.ln_g = ln_g; a.ln_b = ln_b; a.w1 = (const bf16_t*)w1; a.b1 = b1;
   a.w2 = (const bf16_t*)w2; a.b2 = b2; a.rsc = row_scale; a.out = (bf16_t*)out;

@@ -15,11 +15,15 @@ Execution (per call, all images at once instead of the reference's per-image loo
             (``sr_dcn_fwd_fused``), which stores the columns only when a backward will run.
   backward: dcols = dy x W (same GEMM on the transposed weight image), dW / db by the
             split-K wgrad kernel over (dy, cols), ``sr_dcn_col2im`` for grad x (fp32
-            atomics), grad offset and grad mask in one pass.
+            atomics), grad offset and grad mask in one pass; in bf16 with groups 1 and 64
+            input channels (round 4) ``sr_dcn_bwd_fused`` instead of the dcols GEMM and
+            col2im: each tap's dcols tile is formed on MFMA inside the coordinate-gradient and
+            scatter kernels and never stored (``SR_DCN_BWD_FUSED=0`` keeps the dcols path).
 Under ``torch.autocast('cuda')`` samples, columns and GEMMs run in bf16 (fp32 accumulate);
 offsets, masks and all their gradients stay fp32.
 """
 import math
+import os
 
 import torch
 from torch import nn
@@ -158,19 +162,31 @@ def _dcn_forward(x, offset, mask, weight, bias, g, dtype, need_cols=True):
     return C.nhwc_to_nchw(y, g.cout), (xh, off, msk, cols)
 
 
+BWD_FUSED = os.environ.get('SR_DCN_BWD_FUSED') != '0'
+
+
+def bwd_fused_ok(g, dtype):
+    """True when the backward runs without the dcols matrix (``sr_dcn_bwd_fused``: bf16, groups 1,
+    64 input channels, <= 64 outputs)."""
+    return (BWD_FUSED and dtype == torch.bfloat16 and g.G == 1
+            and bool(_lib.load().sr_dcn_bwd_fused_ok(g.desc(dtype), g.cout_gp)))
+
+
 def _dcn_backward(grad_out, saved, weight, bias, g, dtype):
     xh, off, msk, cols = saved
     lib = _lib.load()
     spec = _spec(g)
     images = _prepared(weight, bias, g, spec, dtype)
     dyh = C.nchw_to_nhwc(grad_out.float(), g.ldy, dtype)
-    dcols = torch.empty(g.N, g.Ho, g.Wo, g.L, device=dyh.device, dtype=dtype)
+    fused = bwd_fused_ok(g, dtype)
+    dcols = None if fused else torch.empty(g.N, g.Ho, g.Wo, g.L, device=dyh.device, dtype=dtype)
     ci_map = spec.maps(dyh.device)[3]
     kc = g.K * g.cgp
     dws, dbs = [], []
     for gi, (_, wd, _) in enumerate(images):
-        C.conv_fwd_raw(dyh, wd, None, dcols, g.N, g.Ho, g.Wo, g.cout_gp, kc, kc, ksize=1, ldx=g.ldy,
-                       xcoff=gi * g.cout_gp, ldy=g.L, ycoff=gi * kc)
+        if not fused:
+            C.conv_fwd_raw(dyh, wd, None, dcols, g.N, g.Ho, g.Wo, g.cout_gp, kc, kc, ksize=1, ldx=g.ldy,
+                           xcoff=gi * g.cout_gp, ldy=g.L, ycoff=gi * kc)
         dw, db = C.conv_wgrad_raw(dyh, cols, g.N, g.Ho, g.Wo, kc, g.cg * g.K, g.cout_gp, g.cout_g, ksize=1,
                                   ci_map=ci_map, ldx=g.L, xcoff=gi * kc, ldy=g.ldy, ycoff=gi * g.cout_gp,
                                   need_bias=bias is not None)
@@ -184,6 +200,13 @@ def _dcn_backward(grad_out, saved, weight, bias, g, dtype):
     d = g.desc(dtype)
     wsb = lib.sr_dcn_col2im_workspace(d)
     ws = torch.empty(wsb // 4 + 1, device=dyh.device, dtype=torch.int32)
+    if fused:
+        wd = images[0][1]
+        _lib.check(
+            lib.sr_dcn_bwd_fused(d, _lib.ptr(dyh), g.ldy, _lib.ptr(wd), wd.shape[1], g.cout_gp, _lib.ptr(xh),
+                                 _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx), _lib.ptr(goff), _lib.ptr(gmask),
+                                 _lib.ptr(ws), wsb, _lib.stream()))
+        return C.nhwc_to_nchw(gx, g.C), goff, gmask, grad_weight, grad_bias
     _lib.check(
         lib.sr_dcn_col2im(d, _lib.ptr(dcols), _lib.ptr(xh), _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx),
                           _lib.ptr(goff), _lib.ptr(gmask), _lib.ptr(ws), wsb, _lib.stream()))

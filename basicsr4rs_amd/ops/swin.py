@@ -368,7 +368,7 @@ def swin_mlp_fused(x, n2w, n2b, Creal, f1wf, f1bg, fc1s, f2wf, f2bg, s2, train):
     N, H, W, Cp = x.shape
     lib = _lib.load()
     Hp = fc1s.cout_p
-    if not _SWIN_FUSED or Cp != fc1s.cin_p or fc2s.cin_p != Hp or fc2s.cout_p != Cp or \
+    if not _SWIN_FUSED or Cp != fc1s.cin_p or f2wf.shape[0] != Cp or f2wf.numel() != Cp * Hp or \
             not lib.sr_swin_mlp_fused_ok(_lib.dtype_code(x.dtype), Creal, Cp, Hp):
         return None
     M = N * H * W

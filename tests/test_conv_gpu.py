@@ -400,14 +400,16 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
                                    (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
-@pytest.mark.parametrize('variant', [0, 65, 69])
+@pytest.mark.parametrize('variant', [0, 65, 73, 74, 75])
 def test_wgrad_halo_vs_fp64(cuda, shape, variant):
     """All-taps halo wgrad (Cout <= 64, W % 64 == 0), row-streaming form: channel slices of
     wider buffers (ldx, xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather
     (in_up = 2), splits that cross image boundaries (rows per split not dividing H), several
     64-px column segments per row, ragged last split, against an fp64 CPU reference on the same
-    bf16 operands; variant 0: two row groups per 8-wave block for Cout <= 32 (round 4); 65: the opt-in
-    early-issue schedule (one barrier per step, W 64 only); 69: the 4-wave one-row-group form."""
+    bf16 operands; variant 0: the default 4-wave blocks; 65: the opt-in early-issue schedule (one barrier
+    per step, W 64 only); 73: two co groups per 8-wave block sharing one x ring (Cout 49..64); 74: two
+    row groups per 8-wave block (Cout <= 32); 75: Cout 64 as two 32-channel co-tile blocks over twice the
+    rows -- the round-4 A/B forms."""
     N, H, W, cin, cout, up = shape
     torch.manual_seed(9)
     dt = torch.bfloat16

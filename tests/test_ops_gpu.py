@@ -154,6 +154,60 @@ def test_dcn_fused_forward(cuda, case, need_grad):
             assert rel(tt.grad, gr) < 5e-2, (name, rel(tt.grad, gr))
 
 
+@pytest.mark.parametrize('case', FUSED_CASES)
+def test_dcn_fused_backward_vs_dcols_path(cuda, case):
+    """sr_dcn_bwd_fused (round 4: each tap's dcols tile formed on MFMA inside the coordinate-gradient
+    and scatter kernels, never stored) against the dcols path on the same operands: dcols =
+    bf16(dy x W) by the 1x1 GEMM, then sr_dcn_col2im.  Both sample the same bf16 dcols values (up to
+    the GEMMs' summation order), so grad offset / mask / x agree to fp32 summation-order noise;
+    offsets of std 2 put many samples past the R = 2 windows onto the global paths."""
+    N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
+    x, off, msk, w, b, dy = _dcn_inputs(case, seed=3)
+    lib = _lib.load()
+    bf = torch.bfloat16
+    xt = torch.tensor(x, device=cuda)
+    wt = torch.tensor(w, device=cuda)
+    g = D._Geom(xt, wt, s, p, d, groups, dg)
+    if s > 1:  # a stride-2 tile's scatter footprint exceeds the LDS image: the dcols path runs
+        assert lib.sr_dcn_bwd_fused_ok(g.desc(bf), g.cout_gp) == 0 and not D.bwd_fused_ok(g, bf)
+        return
+    assert lib.sr_dcn_bwd_fused_ok(g.desc(bf), g.cout_gp) == 1 and D.bwd_fused_ok(g, bf)
+    xh = D.C.nchw_to_nhwc(xt, g.Cp, bf)
+    dyh = D.C.nchw_to_nhwc(torch.tensor(dy, device=cuda), g.ldy, bf)
+    offc = torch.tensor(off, device=cuda)
+    mskc = torch.tensor(msk, device=cuda) if modulated else None
+    _, wd, _ = D._prepared(wt, None, g, D._spec(g), bf)[0]
+    kc = g.K * g.cgp
+    dcols = torch.empty(g.N, g.Ho, g.Wo, g.L, device=cuda, dtype=bf)
+    D.C.conv_fwd_raw(dyh, wd, None, dcols, g.N, g.Ho, g.Wo, g.cout_gp, kc, kc, ksize=1, ldx=g.ldy, xcoff=0,
+                     ldy=g.L, ycoff=0)
+    desc = g.desc(bf)
+    wsb = lib.sr_dcn_col2im_workspace(desc)
+    outs = []
+    for fused in (False, True):
+        gx = torch.zeros(g.N, g.H, g.W, g.Cp, device=cuda)
+        goff = torch.full_like(offc, float('nan'))
+        gm = torch.full_like(mskc, float('nan')) if modulated else None
+        ws = torch.empty(wsb // 4 + 1, device=cuda, dtype=torch.int32)
+        if fused:
+            _lib.check(lib.sr_dcn_bwd_fused(desc, _lib.ptr(dyh), g.ldy, _lib.ptr(wd), wd.shape[1], g.cout_gp,
+                                            _lib.ptr(xh), _lib.ptr(offc), _lib.ptr(mskc), _lib.ptr(gx), _lib.ptr(goff),
+                                            _lib.ptr(gm), _lib.ptr(ws), wsb, _lib.stream()))
+        else:
+            _lib.check(lib.sr_dcn_col2im(desc, _lib.ptr(dcols), _lib.ptr(xh), _lib.ptr(offc), _lib.ptr(mskc),
+                                         _lib.ptr(gx), _lib.ptr(goff), _lib.ptr(gm), _lib.ptr(ws), wsb,
+                                         _lib.stream()))
+        outs.append((gx, goff, gm))
+    torch.cuda.synchronize()
+    for name, a_, b_ in zip(('x', 'offset', 'mask'), outs[0], outs[1]):
+        if a_ is None:
+            continue
+        assert torch.isfinite(b_).all(), name
+        err = (a_ - b_).abs().max().item() / max(1e-6, a_.abs().max().item())
+        print(f'{case}: fused bwd vs dcols path, grad {name} rel err {err:.2e}')
+        assert err < 1e-2, (name, err)
+
+
 def test_dcn_fused_ok_query(cuda):
     """Shapes outside the fused kernel keep the unfused path (fp32, C != 64, Cout > 64, groups 2)."""
     mk = lambda C, Co, gr: D._Geom(torch.empty(1, C, 8, 8), torch.empty(Co, C // gr, 3, 3), 1, 1, 1, gr, 1)  # noqa

@@ -5,8 +5,10 @@ basicsr/archs/edvr_arch.py:42) -- the reference's modulated_deform_conv path
 (basicsr/ops/dcn/deform_conv.py:121-188 -> deform_conv_cuda.cpp:490-685).
 
 Times forward and forward + backward in fp32 and bf16 (autocast) with HIP events, reports
-algorithmic FLOPs / bytes (each tensor touched once at the compute dtype: fwd reads x, offset,
-mask and writes y; bwd also reads dy, writes dx, doffset, dmask) and the roofline fraction
+algorithmic FLOPs / bytes -- one definition for every DCN number (round 4): each tensor touched once
+as the kernels store it: x, dy at the compute dtype (bf16 NHWC under autocast), offset, mask, y and
+their gradients and dx in fp32 (the forward: 327 MB at the C5 config in bf16; the backward reads dy,
+x, offset, mask and writes dx, doffset, dmask: 587 MB) -- and the roofline fraction
 against min(2.5 PF, AI x 8 TB/s) (bf16) / min(157 TF, AI x 8 TB/s) (fp32), and times the CPU
 oracle (oracle/ops.py, numpy float64, the restatement of the reference's kernels) on a bounded
 sample (batch 1 of the same per-image shape) on the host cores.
@@ -62,6 +64,7 @@ def main():
     ap.add_argument('--out', default='')
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--iters', type=int, default=20)
+    ap.add_argument('--modes', default='fp32,bf16')
     args = ap.parse_args()
     dev = torch.device('cuda')
     N, C, H, W, dg = args.batch, 64, 128, 128, 8
@@ -73,13 +76,12 @@ def main():
     flops_bwd = 2 * flops_fwd  # dcols = W^T dy and dW = dy cols^T (the coordinate / scatter math not counted)
     res = {'config': 'x[16,64,128,128] offset[16,144,128,128] mask[16,72,128,128] W[64,64,3,3] dg 8, s1 p1 d1 g1',
            'batch': N}
-    for mode in ('fp32', 'bf16'):
+    for mode in args.modes.split(','):
         ac = mode == 'bf16'
         esz = 2 if ac else 4
-        elems_fwd = x.numel() + off.numel() + msk.numel() + dy.numel()  # x, offset, mask in; y out
-        bytes_fwd = esz * elems_fwd
-        bytes_bwd = esz * (x.numel() + off.numel() + msk.numel() + dy.numel()  # re-read inputs + dy
-                           + x.numel() + off.numel() + msk.numel())  # write dx, doffset, dmask
+        om = 4 * (off.numel() + msk.numel())  # offset + mask (or their gradients), fp32
+        bytes_fwd = esz * x.numel() + om + 4 * dy.numel()  # x, offset, mask in; y (fp32) out
+        bytes_bwd = esz * (dy.numel() + x.numel()) + 2 * om + 4 * x.numel()  # dy, x, off, mask in; dx, doff, dmask out
 
         def fwd():
             with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16, enabled=ac):
