@@ -1263,26 +1263,382 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy_kernel(DcnArgs a, int R
   }
 }
 
+// Eight-channel lane layout (round 4b).  The kernels above give a lane 4 channels of ONE pixel per
+// 16-channel MFMA tile, so each bilinear sample (offset / mask reads, corner geometry) served only 4
+// channels.  With two pixel tiles per wave (tile rows 2 w and 2 w + 1) a lane swaps with lane ^ 16 the
+// row it does not keep: afterwards lane (g, pl) holds channels 16 cb + 8 (g >> 1) .. + 7 of pixel pl
+// of row g & 1 -- one 16-B channel vector, one sample per deformable-group vector, as the dcols
+// path's kernels.
+SR_DEV void own8(const f32x4& a0, const f32x4& a1, int g, float (&o)[8]) {
+  const bool odd = g & 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float recv = __shfl_xor(odd ? a0[i] : a1[i], 16);  // the partner's values of my row
+    const float mine = odd ? a1[i] : a0[i];
+    o[i] = bf16_round(odd ? recv : mine);
+    o[4 + i] = bf16_round(odd ? mine : recv);
+  }
+}
+
+constexpr int DC8_NT = 256;  // 4 waves: an 8 x 16 tile, two rows per wave
+
+// dcn_coord_dy_kernel in the eight-channel layout: offsets / masks read per lane a tap ahead (16
+// consecutive pixels of one plane per 16 lanes) and the gradients stored per lane, so no offset
+// staging and ONE barrier per tap (the weight slices are double-buffered in LDS).
+__global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, const bf16_t* __restrict__ dy, int ldy,
+                                                                 const bf16_t* __restrict__ wd, int ldw, int cop,
+                                                                 const bf16_t* __restrict__ x,
+                                                                 const float* __restrict__ off,
+                                                                 const float* __restrict__ msk,
+                                                                 float* __restrict__ goff, float* __restrict__ gmsk,
+                                                                 unsigned* __restrict__ amax, int R, int WH, int WW) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  bf16_t* sW = (bf16_t*)s_raw;                                 // [2][64 ci][DF_RS]: wd rows of taps k, k + 1
+  unsigned char* sX = s_raw + 2 * 64 * DF_RS * 2;             // [WH * WW][8 slots][16 B]
+  const int HWo = a.Ho * a.Wo;
+  const int64_t HWo64 = HWo;
+  const int tw = (a.Wo + DW_TW - 1) / DW_TW, th = (a.Ho + DW_TH - 1) / DW_TH;
+  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / (tw * th), t = bid - n * (tw * th);
+  const int ho0 = (t / tw) * DW_TH, wo0 = (t - (t / tw) * tw) * DW_TW;
+  const int y0 = ho0 * a.sh - a.ph - R, x0 = wo0 * a.sw - a.pw - R;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, pl = lane & 15;
+  const int ho = ho0 + 2 * wv + (g & 1), wo = wo0 + pl;  // this lane's pixel
+  const bool pv = ho < a.Ho && wo < a.Wo;
+  const int p = pv ? ho * a.Wo + wo : 0;
+  const uint32_t pxb = (uint32_t)a.Cp * 2u;
+  const auto xr = make_rsrc(x + (int64_t)n * a.H * a.W * a.Cp, (uint32_t)((size_t)a.H * a.W * a.Cp * 2));
+  const auto dyr = make_rsrc(dy + (int64_t)n * HWo64 * ldy, (uint32_t)((size_t)HWo * ldy * 2));
+  const auto wr = make_rsrc(wd, (uint32_t)((size_t)a.K * 64 * ldw * 2));
+  u32x4 dyf[2][2];  // B fragments of both rows
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int hu = ho0 + 2 * wv + uu;
+    const bool v = hu < a.Ho && wo < a.Wo;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int co = 32 * kk + 8 * g;
+      dyf[uu][kk] = buf_load16(dyr, v && co < cop ? (uint32_t)((hu * a.Wo + wo) * ldy + co) * 2u : SR_OOB);
+    }
+  }
+  auto wload = [&](int k, u32x4 (&wp)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = tid + DC8_NT * j, row = q >> 3, pc = q & 7;
+      wp[j] = buf_load16(wr, 8 * pc < cop ? (uint32_t)((k * 64 + row) * ldw + 8 * pc) * 2u : SR_OOB);
+    }
+  };
+  auto wstore = [&](int buf, const u32x4 (&wp)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = tid + DC8_NT * j, row = q >> 3, pc = q & 7;
+      *(u32x4*)&sW[(buf * 64 + row) * DF_RS + 8 * pc] = wp[j];
+    }
+  };
+  const int64_t obase = (int64_t)n * a.DG * 2 * a.K * HWo64, mbase = (int64_t)n * a.DG * a.K * HWo64;
+  int dgc[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) dgc[cb] = (16 * cb + 8 * (g >> 1)) / a.cpg;
+  auto load_om = [&](int k, float (&o)[4][3]) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int dgi = dgc[cb];
+      o[cb][0] = pv ? off[obase + (int64_t)(dgi * 2 * a.K + 2 * k) * HWo64 + p] : 0.f;
+      o[cb][1] = pv ? off[obase + (int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64 + p] : 0.f;
+      o[cb][2] = pv ? (msk ? msk[mbase + (int64_t)(dgi * a.K + k) * HWo64 + p] : 1.f) : 0.f;
+    }
+  };
+  u32x4 wp[2];
+  wload(0, wp);
+  float om[4][3];
+  load_om(0, om);
+  const int nwin = WH * WW * 8;
+  for (int b0 = 0; b0 < nwin; b0 += 4 * DC8_NT) {
+    u32x4 val[4];
+    int dst[4];
+#pragma unroll
+    for (int uq = 0; uq < 4; ++uq) {
+      const int i = b0 + uq * DC8_NT + tid;
+      const int pix = i >> 3, vv = i & 7;
+      const int wy = pix / WW, wx = pix - wy * WW;
+      const int yy = y0 + wy, xx = x0 + wx;
+      const bool in = i < nwin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      val[uq] = buf_load16(xr, in ? (uint32_t)(yy * a.W + xx) * pxb + (uint32_t)vv * 16u : SR_OOB);
+      dst[uq] = i < nwin ? pix * 128 + ((vv ^ (pix & 7)) << 4) : -1;
+    }
+#pragma unroll
+    for (int uq = 0; uq < 4; ++uq)
+      if (dst[uq] >= 0) *(u32x4*)(sX + dst[uq]) = val[uq];
+  }
+  wstore(0, wp);
+  if (a.K > 1) wload(1, wp);
+  __syncthreads();
+  float vmax = 0.f;
+  const int gv = a.cpg / 8;  // channel vectors per deformable group
+  for (int k = 0; k < a.K; ++k) {
+    float omn[4][3];
+    if (k + 1 < a.K) load_om(k + 1, omn);
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int uu = 0; uu < 2; ++uu)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[uu][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* sWk = sW + (k & 1) * 64 * DF_RS;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const u32x4 af = *(const u32x4*)&sWk[(16 * cb + pl) * DF_RS + 32 * kk + 8 * g];
+        mfma_bf16(af, dyf[0][kk], acc[0][cb]);
+        mfma_bf16(af, dyf[1][kk], acc[1][cb]);
+      }
+    if (k + 1 < a.K) {  // the other buffer's last readers (tap k - 1) are past this tap's barrier
+      wstore((k + 1) & 1, wp);
+      if (k + 2 < a.K) wload(k + 2, wp);
+    }
+    const int ti = k / a.kw, tj = k - ti * a.kw;
+    const float hk = (float)(ho * a.sh - a.ph + ti * a.dh), wk = (float)(wo * a.sw - a.pw + tj * a.dw);
+    float rh[4], rw[4], rm[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      float dc[8];
+      own8(acc[0][cb], acc[1][cb], g, dc);
+      const int v = 2 * cb + (g >> 1);
+      const float m = om[cb][2];
+      const float h = hk + om[cb][0], w = wk + om[cb][1];
+      const Sample s = make_sample(h, w, a.H, a.W);
+      float ah = 0.f, aw = 0.f, am = 0.f;
+      if (pv && s.valid) {
+        const int ly = (int)floorf(h) - y0, lx = (int)floorf(w) - x0;
+        u32x4 cv[4];
+        if (ly >= 0 && ly + 1 < WH && lx >= 0 && lx + 1 < WW) {
+          const int q0 = ly * WW + lx;
+          const int qs[4] = {q0, q0 + 1, q0 + WW, q0 + WW + 1};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cv[q] = *(const u32x4*)(sX + qs[q] * 128 + ((v ^ (qs[q] & 7)) << 4));
+        } else {
+          const uint32_t cb16 = (uint32_t)v * 16u;
+          cv[0] = buf_load16(xr, s.o1 >= 0 ? (uint32_t)s.o1 * pxb + cb16 : SR_OOB);
+          cv[1] = buf_load16(xr, s.o2 >= 0 ? (uint32_t)s.o2 * pxb + cb16 : SR_OOB);
+          cv[2] = buf_load16(xr, s.o3 >= 0 ? (uint32_t)s.o3 * pxb + cb16 : SR_OOB);
+          cv[3] = buf_load16(xr, s.o4 >= 0 ? (uint32_t)s.o4 * pxb + cb16 : SR_OOB);
+        }
+        const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const auto f = [&](uint32_t w32) { return __uint_as_float((e & 1) ? (w32 & 0xffff0000u) : (w32 << 16)); };
+          const float v1 = f(cv[0][e >> 1]), v2 = f(cv[1][e >> 1]), v3 = f(cv[2][e >> 1]), v4 = f(cv[3][e >> 1]);
+          const float wh = -s.hw * v1 - s.lw * v2 + s.hw * v3 + s.lw * v4;
+          const float ww = -s.hh * v1 + s.hh * v2 - s.lh * v3 + s.lh * v4;
+          ah += wh * dc[e] * m;
+          aw += ww * dc[e] * m;
+          am += dc[e] * (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
+          vmax = fmaxf(vmax, fabsf(dc[e] * m));
+          if (!(fabsf(dc[e] * m) <= 3.0e38f)) vmax = __builtin_inff();
+        }
+      }
+      rh[cb] = ah; rw[cb] = aw; rm[cb] = am;
+    }
+    // a group's vectors: cb pairs (cpg 32) or all four (cpg 64) of the lane, then the lanes ^ 32
+    if (gv >= 4) {
+      rh[0] += rh[1]; rw[0] += rw[1]; rm[0] += rm[1];
+      rh[2] += rh[3]; rw[2] += rw[3]; rm[2] += rm[3];
+    }
+    if (gv >= 8) { rh[0] += rh[2]; rw[0] += rw[2]; rm[0] += rm[2]; }
+    if (gv >= 2) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        rh[cb] += __shfl_xor(rh[cb], 32); rw[cb] += __shfl_xor(rw[cb], 32); rm[cb] += __shfl_xor(rm[cb], 32);
+      }
+    }
+    if (pv) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int v = 2 * cb + (g >> 1);
+        if (v % gv == 0) {  // the lane holding the group's first vector
+          const int dgi = dgc[cb];
+          goff[obase + (int64_t)(dgi * 2 * a.K + 2 * k) * HWo64 + p] = rh[cb];
+          goff[obase + (int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64 + p] = rw[cb];
+          if (gmsk) gmsk[mbase + (int64_t)(dgi * a.K + k) * HWo64 + p] = rm[cb];
+        }
+      }
+    }
+    __syncthreads();  // the next tap's weight slice is in LDS
+    if (k + 1 < a.K) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int e = 0; e < 3; ++e) om[cb][e] = omn[cb][e];
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
+  if (lane == 0 && vmax > 0.f) atomicMax(amax + n, __float_as_uint(vmax));
+}
+
+// dcn_gradx_dy_kernel in the eight-channel layout; FX: int64 fixed-point LDS image (exact, order-free
+// within the block) or fp32 LDS atomics (half the LDS bytes and image: a wider halo fits)
+template <bool FX>
+__global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int R, int RH, int RW,
+                                                                 const bf16_t* __restrict__ dy, int ldy,
+                                                                 const bf16_t* __restrict__ wd, int ldw, int cop,
+                                                                 const float* __restrict__ off,
+                                                                 const float* __restrict__ msk,
+                                                                 const unsigned* __restrict__ amax,
+                                                                 float* __restrict__ gx) {
+  extern __shared__ unsigned long long s_acc[];  // [RH * RW][DX_ST]: u64 (FX) or float
+  float* s_accf = (float*)s_acc;
+  const int HWo = a.Ho * a.Wo;
+  const int64_t HWo64 = HWo;
+  const int tw = (a.Wo + DX_TT - 1) / DX_TT, th = (a.Ho + DX_TT - 1) / DX_TT;
+  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int n = bid / (tw * th), t = bid - n * (tw * th);
+  const float mx = __uint_as_float(amax[n]);
+  if (mx == 0.f) return;  // nothing of this image is scattered (uniform per block)
+  const bool direct = FX && !(mx <= 3.0e38f);
+  int ex = 0;
+  frexpf(direct || !FX ? 1.f : mx, &ex);
+  const int e = min(127, 48 - ex);
+  const float sc = ldexpf(1.f, e), isc = ldexpf(1.f, -e);
+  const int ho0 = (t / tw) * DX_TT, wo0 = (t - (t / tw) * tw) * DX_TT;
+  const int ry0 = ho0 * a.sh - a.ph - R, rx0 = wo0 * a.sw - a.pw - R;
+  const int RP = RH * RW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, pl = lane & 15;
+  float* gim = gx + (int64_t)n * a.H * a.W * a.Cp;
+  const auto dyr = make_rsrc(dy + (int64_t)n * HWo64 * ldy, (uint32_t)((size_t)HWo * ldy * 2));
+  const auto wr = make_rsrc(wd, (uint32_t)((size_t)a.K * 64 * ldw * 2));
+  const int ho = ho0 + 2 * wv + (g & 1), wo = wo0 + pl;  // this lane's pixel
+  const bool pv = ho < a.Ho && wo < a.Wo;
+  const int p = pv ? ho * a.Wo + wo : 0;
+  u32x4 dyf[2][2];
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int hu = ho0 + 2 * wv + uu;
+    const bool v = hu < a.Ho && wo < a.Wo;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int co = 32 * kk + 8 * g;
+      dyf[uu][kk] = buf_load16(dyr, v && co < cop ? (uint32_t)((hu * a.Wo + wo) * ldy + co) * 2u : SR_OOB);
+    }
+  }
+  const float* offn = off + (int64_t)n * a.DG * 2 * a.K * HWo64;
+  const float* mskn = msk ? msk + (int64_t)n * a.DG * a.K * HWo64 : nullptr;
+  for (int c0 = 0; c0 < a.C; c0 += DX_CPP) {
+    const int c = c0 + 8 * (g >> 1), dgi = c / a.cpg;  // this lane's 8 channels
+    auto load_w = [&](int k, u32x4 (&wa)[2]) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int co = 32 * kk + 8 * g;
+        wa[kk] = buf_load16(wr, co < cop ? (uint32_t)((k * 64 + c0 + pl) * ldw + co) * 2u : SR_OOB);
+      }
+    };
+    auto load_om = [&](int k, float (&o)[3]) {
+      o[0] = pv ? offn[(int64_t)(dgi * 2 * a.K + 2 * k) * HWo64 + p] : 0.f;
+      o[1] = pv ? offn[(int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64 + p] : 0.f;
+      o[2] = pv ? (mskn ? mskn[(int64_t)(dgi * a.K + k) * HWo64 + p] : 1.f) : 0.f;
+    };
+    u32x4 wa[2];
+    float om[3];
+    load_w(0, wa);
+    load_om(0, om);
+    for (int i = tid; i < RP * DX_ST; i += DW_NT) {
+      if (FX) s_acc[i] = 0ull;
+      else s_accf[i] = 0.f;
+    }
+    __syncthreads();
+    for (int k = 0; k < a.K; ++k) {
+      u32x4 wn[2];
+      float omn[3];
+      if (k + 1 < a.K) {
+        load_w(k + 1, wn);
+        load_om(k + 1, omn);
+      }
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      mfma_bf16(wa[0], dyf[0][0], acc0);
+      mfma_bf16(wa[1], dyf[0][1], acc0);
+      mfma_bf16(wa[0], dyf[1][0], acc1);
+      mfma_bf16(wa[1], dyf[1][1], acc1);
+      float dm[8];
+      own8(acc0, acc1, g, dm);
+      const int ti = k / a.kw, tj = k - ti * a.kw;
+      const float h = (float)(ho * a.sh - a.ph + ti * a.dh) + om[0];
+      const float w = (float)(wo * a.sw - a.pw + tj * a.dw) + om[1];
+      const Sample s = make_sample(h, w, a.H, a.W);
+      if (pv && s.valid) {
+#pragma unroll
+        for (int e2 = 0; e2 < 8; ++e2) dm[e2] *= om[2];
+        const int hl = (int)floorf(h), wl = (int)floorf(w);
+        const float wt[4] = {s.hh * s.hw, s.hh * s.lw, s.lh * s.hw, s.lh * s.lw};
+        const int oo[4] = {s.o1, s.o2, s.o3, s.o4};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (oo[q] < 0) continue;
+          const int ly = hl + (q >> 1) - ry0, lx = wl + (q & 1) - rx0;
+          if (!direct && ly >= 0 && ly < RH && lx >= 0 && lx < RW) {
+            const int base = (ly * RW + lx) * DX_ST + 8 * (g >> 1);
+#pragma unroll
+            for (int e2 = 0; e2 < 8; ++e2) {
+              if (FX) atomicAdd(s_acc + base + e2, (unsigned long long)__float2ll_rn(wt[q] * dm[e2] * sc));
+              else atomicAdd(s_accf + base + e2, wt[q] * dm[e2]);
+            }
+          } else {
+            float* dst = gim + (int64_t)oo[q] * a.Cp + c;
+#pragma unroll
+            for (int e2 = 0; e2 < 8; ++e2) unsafeAtomicAdd(dst + e2, wt[q] * dm[e2]);
+          }
+        }
+      }
+      if (k + 1 < a.K) {
+        wa[0] = wn[0]; wa[1] = wn[1];
+        om[0] = omn[0]; om[1] = omn[1]; om[2] = omn[2];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < RP * DX_CPP; i += DW_NT) {
+      const int pix = i / DX_CPP, ch = i - pix * DX_CPP;
+      const int yy = ry0 + pix / RW, xx = rx0 + pix % RW;
+      if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) continue;
+      const float v = FX ? (float)(long long)s_acc[pix * DX_ST + ch] * isc : s_accf[pix * DX_ST + ch];
+      if (v != 0.f) unsafeAtomicAdd(gim + ((int64_t)yy * a.W + xx) * a.Cp + c0 + ch, v);
+    }
+    __syncthreads();
+  }
+}
+
 // Shapes and geometry of the fused backward: coord_win's shapes with Cout <= 64; the coordinate
 // kernel's LDS (offset tile + weight slice + window, R <= 2) and the scatter image (R <= 2) each
 // within 80 KB, two blocks per CU.  (The op layer's SR_DCN_BWD_FUSED=0 keeps the dcols path.)
 struct BwdGeom {
   int R1, WH, WW, R2, RH, RW;
   size_t lds1, lds2;
+  int v8, fx;  // eight-channel kernels; fixed-point scatter image
 };
+// Kernel forms (A/B; read per call, so one test process runs every form): SR_DCN_BWD8=0 the
+// four-channel kernels; SR_DCN_GX_FX=0 / 1 the scatter image in fp32 / int64 fixed point
+int bwd8_env() {
+  const char* e = getenv("SR_DCN_BWD8");
+  return e ? atoi(e) : 1;
+}
+int gx_fx_env() {
+  const char* e = getenv("SR_DCN_GX_FX");
+  return e ? atoi(e) : 1;
+}
 bool bwd_fused_geom(const sr_dcn_desc* d, const DcnArgs& a, int cop, BwdGeom* bg) {
   if (!coord_win_ok(d, a) || cop < 8 || cop > 64 || cop % 8) return false;
+  bg->v8 = bwd8_env() != 0;
+  bg->fx = bg->v8 ? gx_fx_env() != 0 : 1;
   bool ok1 = false, ok2 = false;
   for (int r = 2; r >= 0 && !ok1; --r) {
     const int wh = (DW_TH - 1) * a.sh + (a.kh - 1) * a.dh + 2 + 2 * r;
     const int ww = (DW_TW - 1) * a.sw + (a.kw - 1) * a.dw + 2 + 2 * r;
-    const size_t l = (size_t)3 * a.DG * DF_TP * 4 + (size_t)64 * DF_RS * 2 + (size_t)wh * ww * 128;
+    const size_t l = bg->v8 ? (size_t)2 * 64 * DF_RS * 2 + (size_t)wh * ww * 128
+                            : (size_t)3 * a.DG * DF_TP * 4 + (size_t)64 * DF_RS * 2 + (size_t)wh * ww * 128;
     if (l <= 80 * 1024) { bg->R1 = r; bg->WH = wh; bg->WW = ww; bg->lds1 = l; ok1 = true; }
   }
-  for (int r = 2; r >= 0 && !ok2; --r) {
+  const size_t esz = bg->fx ? 8 : 4;
+  for (int r = bg->fx ? 2 : 4; r >= 0 && !ok2; --r) {
     const int rh = (DX_TT - 1) * a.sh + (a.kh - 1) * a.dh + 2 * r + 2;
     const int rw = (DX_TT - 1) * a.sw + (a.kw - 1) * a.dw + 2 * r + 2;
-    const size_t l = (size_t)rh * rw * DX_ST * 8;
+    const size_t l = (size_t)rh * rw * DX_ST * esz;
     if (l <= 80 * 1024) { bg->R2 = r; bg->RH = rh; bg->RW = rw; bg->lds2 = l; ok2 = true; }
   }
   return ok1 && ok2;
@@ -1367,21 +1723,32 @@ int sr_dcn_bwd_fused(const sr_dcn_desc* d, const void* dy, int ldy, const void* 
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(amax, 0, (size_t)a.N * sizeof(unsigned), s) != hipSuccess)
     return sr_fail(SR_ELAUNCH, "dcn_bwd_fused: memset failed");
-  if (bg.lds1 > 65536 && hipFuncSetAttribute((const void*)dcn_coord_dy_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bg.lds1) != hipSuccess)
+  const void* k1 = bg.v8 ? (const void*)dcn_coord_dy8_kernel : (const void*)dcn_coord_dy_kernel;
+  const void* k2 = !bg.v8 ? (const void*)dcn_gradx_dy_kernel
+                   : bg.fx ? (const void*)dcn_gradx_dy8_kernel<true> : (const void*)dcn_gradx_dy8_kernel<false>;
+  if (bg.lds1 > 65536 && hipFuncSetAttribute(k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bg.lds1) != hipSuccess)
     return sr_fail(SR_ELAUNCH, "dcn_bwd_fused: LDS attribute");
-  if (bg.lds2 > 65536 && hipFuncSetAttribute((const void*)dcn_gradx_dy_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bg.lds2) != hipSuccess)
+  if (bg.lds2 > 65536 && hipFuncSetAttribute(k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bg.lds2) != hipSuccess)
     return sr_fail(SR_ELAUNCH, "dcn_bwd_fused: LDS attribute");
   const int wt = ((a.Ho + DW_TH - 1) / DW_TH) * ((a.Wo + DW_TW - 1) / DW_TW);
-  hipLaunchKernelGGL(dcn_coord_dy_kernel, dim3((unsigned)(a.N * wt)), dim3(DW_NT), bg.lds1, s, a, (const bf16_t*)dy,
-                     ldy, (const bf16_t*)wd, ldw, cout_p, (const bf16_t*)x, offset, mask, grad_offset, grad_mask, amax,
-                     bg.R1, bg.WH, bg.WW);
+  if (bg.v8)
+    hipLaunchKernelGGL(dcn_coord_dy8_kernel, dim3((unsigned)(a.N * wt)), dim3(DC8_NT), bg.lds1, s, a, (const bf16_t*)dy,
+                       ldy, (const bf16_t*)wd, ldw, cout_p, (const bf16_t*)x, offset, mask, grad_offset, grad_mask,
+                       amax, bg.R1, bg.WH, bg.WW);
+  else
+    hipLaunchKernelGGL(dcn_coord_dy_kernel, dim3((unsigned)(a.N * wt)), dim3(DW_NT), bg.lds1, s, a, (const bf16_t*)dy,
+                       ldy, (const bf16_t*)wd, ldw, cout_p, (const bf16_t*)x, offset, mask, grad_offset, grad_mask,
+                       amax, bg.R1, bg.WH, bg.WW);
   if (hipGetLastError() != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_coord_dy launch");
   const int xt = ((a.Ho + DX_TT - 1) / DX_TT) * ((a.Wo + DX_TT - 1) / DX_TT);
-  hipLaunchKernelGGL(dcn_gradx_dy_kernel, dim3((unsigned)(a.N * xt)), dim3(DW_NT), bg.lds2, s, a, bg.R2, bg.RH, bg.RW,
-                     (const bf16_t*)dy, ldy, (const bf16_t*)wd, ldw, cout_p, offset, mask, (const unsigned*)amax,
-                     grad_x);
+  const dim3 xg((unsigned)(a.N * xt));
+#define SR_GX(KERN)                                                                                            \
+  hipLaunchKernelGGL(KERN, xg, dim3(DW_NT), bg.lds2, s, a, bg.R2, bg.RH, bg.RW, (const bf16_t*)dy, ldy,        \
+                     (const bf16_t*)wd, ldw, cout_p, offset, mask, (const unsigned*)amax, grad_x)
+  if (!bg.v8) SR_GX(dcn_gradx_dy_kernel);
+  else if (bg.fx) SR_GX(dcn_gradx_dy8_kernel<true>);
+  else SR_GX(dcn_gradx_dy8_kernel<false>);
+#undef SR_GX
   return sr_check(hipGetLastError(), "dcn_gradx_dy launch");
 }
 

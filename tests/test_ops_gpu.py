@@ -155,12 +155,16 @@ def test_dcn_fused_forward(cuda, case, need_grad):
 
 
 @pytest.mark.parametrize('case', FUSED_CASES)
-def test_dcn_fused_backward_vs_dcols_path(cuda, case):
+@pytest.mark.parametrize('form', ['v8_fx', 'v8_f32', 'v4'])
+def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, monkeypatch):
     """sr_dcn_bwd_fused (round 4: each tap's dcols tile formed on MFMA inside the coordinate-gradient
     and scatter kernels, never stored) against the dcols path on the same operands: dcols =
     bf16(dy x W) by the 1x1 GEMM, then sr_dcn_col2im.  Both sample the same bf16 dcols values (up to
     the GEMMs' summation order), so grad offset / mask / x agree to fp32 summation-order noise;
-    offsets of std 2 put many samples past the R = 2 windows onto the global paths."""
+    offsets of std 2 put many samples past the R = 2 windows onto the global paths.  Forms: the
+    eight-channel kernels with the fixed-point or the fp32 scatter image, and the four-channel ones."""
+    monkeypatch.setenv('SR_DCN_BWD8', '0' if form == 'v4' else '1')
+    monkeypatch.setenv('SR_DCN_GX_FX', '0' if form == 'v8_f32' else '1')
     N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
     x, off, msk, w, b, dy = _dcn_inputs(case, seed=3)
     lib = _lib.load()
@@ -204,7 +208,7 @@ def test_dcn_fused_backward_vs_dcols_path(cuda, case):
             continue
         assert torch.isfinite(b_).all(), name
         err = (a_ - b_).abs().max().item() / max(1e-6, a_.abs().max().item())
-        print(f'{case}: fused bwd vs dcols path, grad {name} rel err {err:.2e}')
+        print(f'{case} {form}: fused bwd vs dcols path, grad {name} rel err {err:.2e}')
         assert err < 1e-2, (name, err)
 
 
