@@ -123,8 +123,8 @@ SIGNATURES = {
     'sr_dcn_col2im_workspace': (_sz, [ctypes.POINTER(DcnDesc)]),
     'sr_dcn_col2im': (_i, [ctypes.POINTER(DcnDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     'sr_dcn_bwd_fused_ok': (_i, [ctypes.POINTER(DcnDesc), _i]),
-    'sr_dcn_bwd_fused': (_i, [ctypes.POINTER(DcnDesc), _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz,
-                              _vp]),
+    'sr_dcn_bwd_fused': (_i, [ctypes.POINTER(DcnDesc), _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp,
+                              _sz, _vp]),
     'sr_deform_conv_workspace': (_sz, [_i] * 16),
     'sr_deform_conv_forward': (_i, [_vp] * 6 + [_i] * 16 + [_vp, _sz, _vp]),
     'sr_deform_conv_backward_input': (_i, [_vp] * 7 + [_i] * 16 + [_vp, _sz, _vp]),

@@ -948,16 +948,14 @@ bool coord_win_geom(const DcnArgs& a, int* R, int* WH, int* WW, size_t* lds) {
 // dcols = dy . W (the reference's per-image addmm into columns, deform_conv_cuda.cpp:640-660) is
 // never stored.  Both kernels form each tap's dcols tile on MFMA from the dy tile, transposed:
 // dcols^T[ci][px] = sum_co wd[k*64 + ci][co] * dy[px][co] (v_mfma_f32_16x16x32_bf16 with the
-// weight rows as A and the lane's pixel row of dy as B), so a lane ends up holding 4 consecutive
-// channels (16 cb + 4 (lane >> 4) .. + 3) of ONE pixel (lane & 15) per 16-channel tile: exactly
-// the operand of the per-pixel sampling math, no LDS transpose.  The results are rounded to bf16
-// as the unfused path's GEMM stores them, so both paths sample the same values.
-//   dcn_coord_dy_kernel : offset / mask gradients (col2im_coord, deform_conv_cuda_kernel.cu:696-770)
-//                         on dcn_coord_win_kernel's tile, window and staging; the tap's 64 x 64
-//                         weight slice staged in LDS beside them; per-image max |mask * dcols|.
-//   dcn_gradx_dy_kernel : the bilinear scatter (col2im, :635-693) into the fixed-point LDS image
-//                         of a 16 x 16 tile's footprint, 16 channels per pass (one MFMA tile),
-//                         weight fragments from L2 a tap ahead, offsets / masks a tap ahead.
+// weight rows as A and a pixel row of dy as B), rounded to bf16 as the dcols path's GEMM stores it,
+// so both paths sample the same values.
+//   dcn_coord_dy8_kernel : offset / mask gradients (col2im_coord, deform_conv_cuda_kernel.cu:696-770)
+//                          on dcn_coord_win_kernel's 8 x 16 tile and x window, the tap's 64 x 64 weight
+//                          slice double-buffered in LDS; per-image max |mask * dcols|.
+//   dcn_gradx_dy8_kernel : the bilinear scatter (col2im, :635-693) into the fixed-point LDS image of a
+//                          16 x 16 tile's footprint, 16 channels per pass (one MFMA tile), weight
+//                          fragments from L2 a tap ahead, offsets / masks a tap ahead.
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // 4 bf16 channels [c, c + 4) of pixel q of the LDS window (slot layout of dcn_fwd_win_kernel)
@@ -972,303 +970,14 @@ SR_DEV float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 SR_DEV float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 SR_DEV float bf16_round(float v) { return bf16_to_f32(f32_to_bf16(v)); }
 
-__global__ void __launch_bounds__(DW_NT, 2) dcn_coord_dy_kernel(DcnArgs a, const bf16_t* __restrict__ dy, int ldy,
-                                                                const bf16_t* __restrict__ wd, int ldw, int cop,
-                                                                const bf16_t* __restrict__ x,
-                                                                const float* __restrict__ off,
-                                                                const float* __restrict__ msk,
-                                                                float* __restrict__ goff, float* __restrict__ gmsk,
-                                                                unsigned* __restrict__ amax, int R, int WH, int WW) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
-  float* sO = (float*)s_raw;                                           // [3 * DG][DF_TP]
-  bf16_t* sW = (bf16_t*)(s_raw + (size_t)3 * a.DG * DF_TP * 4);        // [64 ci][DF_RS]: wd rows of this tap
-  unsigned char* sX = (unsigned char*)(sW + 64 * DF_RS);               // [WH * WW][8 slots][16 B]
-  const int HWo = a.Ho * a.Wo;
-  const int64_t HWo64 = HWo;
-  const int tw = (a.Wo + DW_TW - 1) / DW_TW, th = (a.Ho + DW_TH - 1) / DW_TH;
-  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
-  const int n = bid / (tw * th), t = bid - n * (tw * th);
-  const int ho0 = (t / tw) * DW_TH, wo0 = (t - (t / tw) * tw) * DW_TW;
-  const int y0 = ho0 * a.sh - a.ph - R, x0 = wo0 * a.sw - a.pw - R;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, pl = lane & 15;
-  const int px = 16 * wv + pl, ho = ho0 + wv, wo = wo0 + pl;  // wave wv = tile row wv
-  const bool pv = ho < a.Ho && wo < a.Wo;
-  const int p = pv ? ho * a.Wo + wo : 0;
-  const uint32_t pxb = (uint32_t)a.Cp * 2u;
-  const auto xr = make_rsrc(x + (int64_t)n * a.H * a.W * a.Cp, (uint32_t)((size_t)a.H * a.W * a.Cp * 2));
-  const auto dyr = make_rsrc(dy + (int64_t)n * HWo64 * ldy, (uint32_t)((size_t)HWo * ldy * 2));
-  const auto wr = make_rsrc(wd, (uint32_t)((size_t)a.K * 64 * ldw * 2));
-  // B fragments (k = output channel, column = this lane's pixel), loaded once
-  u32x4 dyf[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int co = 32 * kk + 8 * g;
-    dyf[kk] = buf_load16(dyr, pv && co < cop ? (uint32_t)(p * ldy + co) * 2u : SR_OOB);
-  }
-  const int nwin = WH * WW * 8;
-  for (int b0 = 0; b0 < nwin; b0 += 4 * DW_NT) {
-    u32x4 val[4];
-    int dst[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = b0 + u * DW_NT + tid;
-      const int pix = i >> 3, vv = i & 7;
-      const int wy = pix / WW, wx = pix - wy * WW;
-      const int yy = y0 + wy, xx = x0 + wx;
-      const bool in = i < nwin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-      val[u] = buf_load16(xr, in ? (uint32_t)(yy * a.W + xx) * pxb + (uint32_t)vv * 16u : SR_OOB);
-      dst[u] = i < nwin ? pix * 128 + ((vv ^ (pix & 7)) << 4) : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (dst[u] >= 0) *(u32x4*)(sX + dst[u]) = val[u];
-  }
-  const int nrow = 3 * a.DG;
-  const int64_t obase = (int64_t)n * a.DG * 2 * a.K * HWo64, mbase = (int64_t)n * a.DG * a.K * HWo64;
-  const int wrow = tid >> 3, wpc = tid & 7;  // this thread's 16-B piece of the weight slice
-  float vmax = 0.f;
-  for (int k = 0; k < a.K; ++k) {
-    const u32x4 wpiece = buf_load16(wr, 8 * wpc < cop ? (uint32_t)((k * 64 + wrow) * ldw + 8 * wpc) * 2u : SR_OOB);
-    for (int i = tid; i < nrow * DF_TP; i += DW_NT) {
-      const int r = i / DF_TP, q = i - r * DF_TP;
-      const int qh = ho0 + (q >> 4), qw = wo0 + (q & 15);
-      float val = 0.f;
-      if (qh < a.Ho && qw < a.Wo) {
-        const int64_t pp = (int64_t)qh * a.Wo + qw;
-        if (r < 2 * a.DG) val = off[obase + (int64_t)((r >> 1) * 2 * a.K + 2 * k + (r & 1)) * HWo64 + pp];
-        else val = msk ? msk[mbase + (int64_t)((r - 2 * a.DG) * a.K + k) * HWo64 + pp] : 1.f;
-      }
-      sO[i] = val;
-    }
-    *(u32x4*)&sW[wrow * DF_RS + 8 * wpc] = wpiece;
-    __syncthreads();
-    // dcols^T tile: acc[cb][i] = dcols[px][16 cb + 4 g + i]
-    f32x4 acc[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        mfma_bf16(*(const u32x4*)&sW[(16 * cb + pl) * DF_RS + 32 * kk + 8 * g], dyf[kk], acc[cb]);
-    const int ti = k / a.kw, tj = k - ti * a.kw;
-    const float hk = (float)(ho * a.sh - a.ph + ti * a.dh), wk = (float)(wo * a.sw - a.pw + tj * a.dw);
-    float rh[4], rw[4], rm[4];
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int c = 16 * cb + 4 * g;
-      const int dgi = c / a.cpg;
-      const float m = sO[(2 * a.DG + dgi) * DF_TP + px];
-      const float h = hk + sO[(2 * dgi) * DF_TP + px], w = wk + sO[(2 * dgi + 1) * DF_TP + px];
-      const Sample s = make_sample(h, w, a.H, a.W);
-      float ah = 0.f, aw = 0.f, am = 0.f;
-      if (pv && s.valid) {
-        const int ly = (int)floorf(h) - y0, lx = (int)floorf(w) - x0;
-        u32x2 cv[4];
-        if (ly >= 0 && ly + 1 < WH && lx >= 0 && lx + 1 < WW) {
-          const int q0 = ly * WW + lx;
-          cv[0] = win_read4(sX, q0, c);
-          cv[1] = win_read4(sX, q0 + 1, c);
-          cv[2] = win_read4(sX, q0 + WW, c);
-          cv[3] = win_read4(sX, q0 + WW + 1, c);
-        } else {
-          cv[0] = glb_read4(xr, s.o1, pxb, c);
-          cv[1] = glb_read4(xr, s.o2, pxb, c);
-          cv[2] = glb_read4(xr, s.o3, pxb, c);
-          cv[3] = glb_read4(xr, s.o4, pxb, c);
-        }
-        const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto f = [&](const u32x2& u) { return (e & 1) ? bf_hi(u[e >> 1]) : bf_lo(u[e >> 1]); };
-          const float v1 = f(cv[0]), v2 = f(cv[1]), v3 = f(cv[2]), v4 = f(cv[3]);
-          const float dc = bf16_round(acc[cb][e]);
-          const float wh = -s.hw * v1 - s.lw * v2 + s.hw * v3 + s.lw * v4;
-          const float ww = -s.hh * v1 + s.hh * v2 - s.lh * v3 + s.lh * v4;
-          ah += wh * dc * m;
-          aw += ww * dc * m;
-          am += dc * (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
-          vmax = fmaxf(vmax, fabsf(dc * m));
-          if (!(fabsf(dc * m) <= 3.0e38f)) vmax = __builtin_inff();
-        }
-      }
-      rh[cb] = ah; rw[cb] = aw; rm[cb] = am;
-    }
-    // group sums: the tiles of one group (cpg >= 32), then its lanes (xor 16: the 8 channels of a
-    // vector; xor 32: cpg >= 16); every lane of a group has read its sO words (same wave)
-    if (a.cpg >= 32) {
-      rh[0] += rh[1]; rw[0] += rw[1]; rm[0] += rm[1];
-      rh[2] += rh[3]; rw[2] += rw[3]; rm[2] += rm[3];
-    }
-    if (a.cpg >= 64) { rh[0] += rh[2]; rw[0] += rw[2]; rm[0] += rm[2]; }
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      rh[cb] += __shfl_xor(rh[cb], 16); rw[cb] += __shfl_xor(rw[cb], 16); rm[cb] += __shfl_xor(rm[cb], 16);
-      if (a.cpg >= 16) {
-        rh[cb] += __shfl_xor(rh[cb], 32); rw[cb] += __shfl_xor(rw[cb], 32); rm[cb] += __shfl_xor(rm[cb], 32);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int c = 16 * cb + 4 * g;
-      if (c % a.cpg == 0) {  // the lane holding the group's first channel
-        const int dgi = c / a.cpg;
-        sO[(2 * dgi) * DF_TP + px] = rh[cb];
-        sO[(2 * dgi + 1) * DF_TP + px] = rw[cb];
-        sO[(2 * a.DG + dgi) * DF_TP + px] = rm[cb];
-      }
-    }
-    __syncthreads();
-    for (int i = tid; i < nrow * DF_TP; i += DW_NT) {
-      const int r = i / DF_TP, q = i - r * DF_TP;
-      const int qh = ho0 + (q >> 4), qw = wo0 + (q & 15);
-      if (qh >= a.Ho || qw >= a.Wo) continue;
-      const int64_t pp = (int64_t)qh * a.Wo + qw;
-      if (r < 2 * a.DG) goff[obase + (int64_t)((r >> 1) * 2 * a.K + 2 * k + (r & 1)) * HWo64 + pp] = sO[i];
-      else if (gmsk) gmsk[mbase + (int64_t)((r - 2 * a.DG) * a.K + k) * HWo64 + pp] = sO[i];
-    }
-    __syncthreads();
-  }
-  for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
-  if (lane == 0 && vmax > 0.f) atomicMax(amax + n, __float_as_uint(vmax));
-}
-
 constexpr int DX_TT = 16, DX_CPP = 16, DX_ST = DX_CPP + 1;  // tile edge, channels per pass, LDS pixel stride (u64)
 
-__global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy_kernel(DcnArgs a, int R, int RH, int RW,
-                                                                const bf16_t* __restrict__ dy, int ldy,
-                                                                const bf16_t* __restrict__ wd, int ldw, int cop,
-                                                                const float* __restrict__ off,
-                                                                const float* __restrict__ msk,
-                                                                const unsigned* __restrict__ amax,
-                                                                float* __restrict__ gx) {
-  extern __shared__ unsigned long long s_acc[];  // [RH * RW][DX_ST]
-  const int HWo = a.Ho * a.Wo;
-  const int64_t HWo64 = HWo;
-  const int tw = (a.Wo + DX_TT - 1) / DX_TT, th = (a.Ho + DX_TT - 1) / DX_TT;
-  const int bid = (int)xcd_remap(blockIdx.x, gridDim.x);
-  const int n = bid / (tw * th), t = bid - n * (tw * th);
-  const float mx = __uint_as_float(amax[n]);
-  if (mx == 0.f) return;  // nothing of this image is scattered (uniform per block)
-  const bool direct = !(mx <= 3.0e38f);
-  int ex = 0;
-  frexpf(direct ? 1.f : mx, &ex);
-  const int e = min(127, 48 - ex);
-  const float sc = ldexpf(1.f, e), isc = ldexpf(1.f, -e);
-  const int ho0 = (t / tw) * DX_TT, wo0 = (t - (t / tw) * tw) * DX_TT;
-  const int ry0 = ho0 * a.sh - a.ph - R, rx0 = wo0 * a.sw - a.pw - R;
-  const int RP = RH * RW;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, pl = lane & 15;
-  float* gim = gx + (int64_t)n * a.H * a.W * a.Cp;
-  const auto dyr = make_rsrc(dy + (int64_t)n * HWo64 * ldy, (uint32_t)((size_t)HWo * ldy * 2));
-  const auto wr = make_rsrc(wd, (uint32_t)((size_t)a.K * 64 * ldw * 2));
-  // this lane's two pixels (tile rows 2 wv, 2 wv + 1; column pl) and their dy fragments
-  int pp[2];
-  bool pv[2];
-  u32x4 dyf[2][2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int ho = ho0 + 2 * wv + u, wo = wo0 + pl;
-    pv[u] = ho < a.Ho && wo < a.Wo;
-    pp[u] = pv[u] ? ho * a.Wo + wo : 0;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int co = 32 * kk + 8 * g;
-      dyf[u][kk] = buf_load16(dyr, pv[u] && co < cop ? (uint32_t)(pp[u] * ldy + co) * 2u : SR_OOB);
-    }
-  }
-  const float* offn = off + (int64_t)n * a.DG * 2 * a.K * HWo64;
-  const float* mskn = msk ? msk + (int64_t)n * a.DG * a.K * HWo64 : nullptr;
-  for (int c0 = 0; c0 < a.C; c0 += DX_CPP) {
-    const int c = c0 + 4 * g, dgi = c / a.cpg;
-    auto load_w = [&](int k, u32x4 (&wa)[2]) {  // A fragments: wd rows k*64 + c0 + pl, k = co
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int co = 32 * kk + 8 * g;
-        wa[kk] = buf_load16(wr, co < cop ? (uint32_t)((k * 64 + c0 + pl) * ldw + co) * 2u : SR_OOB);
-      }
-    };
-    auto load_om = [&](int k, float (&o)[2][3]) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        o[u][0] = pv[u] ? offn[(int64_t)(dgi * 2 * a.K + 2 * k) * HWo64 + pp[u]] : 0.f;
-        o[u][1] = pv[u] ? offn[(int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64 + pp[u]] : 0.f;
-        o[u][2] = pv[u] ? (mskn ? mskn[(int64_t)(dgi * a.K + k) * HWo64 + pp[u]] : 1.f) : 0.f;
-      }
-    };
-    u32x4 wa[2];
-    float om[2][3];
-    load_w(0, wa);
-    load_om(0, om);
-    for (int i = tid; i < RP * DX_ST; i += DW_NT) s_acc[i] = 0ull;
-    __syncthreads();
-    for (int k = 0; k < a.K; ++k) {
-      u32x4 wn[2];
-      float omn[2][3];
-      if (k + 1 < a.K) {
-        load_w(k + 1, wn);
-        load_om(k + 1, omn);
-      }
-      const int ti = k / a.kw, tj = k - ti * a.kw;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        mfma_bf16(wa[0], dyf[u][0], acc);
-        mfma_bf16(wa[1], dyf[u][1], acc);
-        if (!pv[u]) continue;
-        const int ho = ho0 + 2 * wv + u, wo = wo0 + pl;
-        const float h = (float)(ho * a.sh - a.ph + ti * a.dh) + om[u][0];
-        const float w = (float)(wo * a.sw - a.pw + tj * a.dw) + om[u][1];
-        const Sample s = make_sample(h, w, a.H, a.W);
-        if (!s.valid) continue;
-        float dm[4];
-#pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) dm[e2] = bf16_round(acc[e2]) * om[u][2];
-        const int hl = (int)floorf(h), wl = (int)floorf(w);
-        const float wt[4] = {s.hh * s.hw, s.hh * s.lw, s.lh * s.hw, s.lh * s.lw};
-        const int oo[4] = {s.o1, s.o2, s.o3, s.o4};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (oo[q] < 0) continue;
-          const int ly = hl + (q >> 1) - ry0, lx = wl + (q & 1) - rx0;
-          if (!direct && ly >= 0 && ly < RH && lx >= 0 && lx < RW) {
-            unsigned long long* dst = s_acc + (ly * RW + lx) * DX_ST + 4 * g;
-#pragma unroll
-            for (int e2 = 0; e2 < 4; ++e2) atomicAdd(dst + e2, (unsigned long long)__float2ll_rn(wt[q] * dm[e2] * sc));
-          } else {
-            float* dst = gim + (int64_t)oo[q] * a.Cp + c;
-#pragma unroll
-            for (int e2 = 0; e2 < 4; ++e2) unsafeAtomicAdd(dst + e2, wt[q] * dm[e2]);
-          }
-        }
-      }
-      if (k + 1 < a.K) {
-        wa[0] = wn[0]; wa[1] = wn[1];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) om[u][j] = omn[u][j];
-      }
-    }
-    __syncthreads();
-    for (int i = tid; i < RP * DX_CPP; i += DW_NT) {
-      const int pix = i / DX_CPP, ch = i - pix * DX_CPP;
-      const int yy = ry0 + pix / RW, xx = rx0 + pix % RW;
-      if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) continue;
-      const long long v = (long long)s_acc[pix * DX_ST + ch];
-      if (v != 0) unsafeAtomicAdd(gim + ((int64_t)yy * a.W + xx) * a.Cp + c0 + ch, (float)v * isc);
-    }
-    __syncthreads();
-  }
-}
-
-// Eight-channel lane layout (round 4b).  The kernels above give a lane 4 channels of ONE pixel per
-// 16-channel MFMA tile, so each bilinear sample (offset / mask reads, corner geometry) served only 4
-// channels.  With two pixel tiles per wave (tile rows 2 w and 2 w + 1) a lane swaps with lane ^ 16 the
-// row it does not keep: afterwards lane (g, pl) holds channels 16 cb + 8 (g >> 1) .. + 7 of pixel pl
-// of row g & 1 -- one 16-B channel vector, one sample per deformable-group vector, as the dcols
-// path's kernels.
+// Eight-channel lane layout.  The MFMA leaves a lane 4 channels (16 cb + 4 (lane >> 4) .. + 3) of ONE
+// pixel (lane & 15) per 16-channel tile; a bilinear sample (offset / mask reads, corner geometry) for
+// 4 channels measured 438 us for the coordinate kernel (SQ: half the wave time waiting, VALU-heavy).
+// With two pixel tiles per wave (tile rows 2 w and 2 w + 1) a lane swaps with lane ^ 16 the row it does
+// not keep: afterwards lane (g, pl) holds channels 16 cb + 8 (g >> 1) .. + 7 of pixel pl of row g & 1 --
+// one 16-B channel vector, one sample per deformable-group vector (308 us).
 SR_DEV void own8(const f32x4& a0, const f32x4& a1, int g, float (&o)[8]) {
   const bool odd = g & 1;
 #pragma unroll
@@ -1282,16 +991,18 @@ SR_DEV void own8(const f32x4& a0, const f32x4& a1, int g, float (&o)[8]) {
 
 constexpr int DC8_NT = 256;  // 4 waves: an 8 x 16 tile, two rows per wave
 
-// dcn_coord_dy_kernel in the eight-channel layout: offsets / masks read per lane a tap ahead (16
-// consecutive pixels of one plane per 16 lanes) and the gradients stored per lane, so no offset
-// staging and ONE barrier per tap (the weight slices are double-buffered in LDS).
+// Offsets / masks read per lane a tap ahead (16 consecutive pixels of one plane per 16 lanes) and the
+// gradients stored per lane, so no offset staging and ONE barrier per tap (the weight slices are
+// double-buffered in LDS).  gxz (optional): the NCHW grad_x of the call, zeroed by the blocks after
+// their last tap (the scatter kernel that follows accumulates into it).
 __global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, const bf16_t* __restrict__ dy, int ldy,
                                                                  const bf16_t* __restrict__ wd, int ldw, int cop,
                                                                  const bf16_t* __restrict__ x,
                                                                  const float* __restrict__ off,
                                                                  const float* __restrict__ msk,
                                                                  float* __restrict__ goff, float* __restrict__ gmsk,
-                                                                 unsigned* __restrict__ amax, int R, int WH, int WW) {
+                                                                 unsigned* __restrict__ amax, int R, int WH, int WW,
+                                                                 float* __restrict__ gxz, int64_t gxn4) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   bf16_t* sW = (bf16_t*)s_raw;                                 // [2][64 ci][DF_RS]: wd rows of taps k, k + 1
   unsigned char* sX = s_raw + 2 * 64 * DF_RS * 2;             // [WH * WW][8 slots][16 B]
@@ -1473,11 +1184,20 @@ __global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, con
   }
   for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
   if (lane == 0 && vmax > 0.f) atomicMax(amax + n, __float_as_uint(vmax));
+  for (int64_t i = (int64_t)blockIdx.x * DC8_NT + tid; i < gxn4; i += (int64_t)gridDim.x * DC8_NT)
+    ((f32x4*)gxz)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// dcn_gradx_dy_kernel in the eight-channel layout; FX: int64 fixed-point LDS image (exact, order-free
-// within the block) or fp32 LDS atomics (half the LDS bytes and image: a wider halo fits)
-template <bool FX>
+// The scatter kernel.  FXB 64: the int64 fixed-point LDS image of the
+// round-3 kernel (scale 2^(48 - e) for a per-image max |mask * dcols| below 2^e); FXB 32: int32 fixed
+// point, scale 2^(18 - e): a cell sums at most 16 x 16 pixels x 9 taps < 2^12 contributions of at
+// most 2^18 each, so it cannot overflow; the quantum is 2^-18 of the image's max |mask * dcols| (the
+// dcols themselves carry bf16 rounding, 2^-9 of each value).  The float -> int64 conversion is ~12 VALU
+// instructions per corner and channel, the int32 one two -- the kernel is VALU-bound on them -- and
+// the int32 image is half the LDS (a wider halo fits).  fp32 LDS atomics are ~25x slower on gfx950.
+// NCHW: grad_x as fp32 [N][C][H][W] (the op's output layout: no NHWC -> NCHW pass), else NHWC
+// [N][H][W][Cp]; the flush then walks pixels fastest, so the atomics of a wave are row-contiguous.
+template <int FXB, bool NCHW>
 __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int R, int RH, int RW,
                                                                  const bf16_t* __restrict__ dy, int ldy,
                                                                  const bf16_t* __restrict__ wd, int ldw, int cop,
@@ -1485,8 +1205,8 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int 
                                                                  const float* __restrict__ msk,
                                                                  const unsigned* __restrict__ amax,
                                                                  float* __restrict__ gx) {
-  extern __shared__ unsigned long long s_acc[];  // [RH * RW][DX_ST]: u64 (FX) or float
-  float* s_accf = (float*)s_acc;
+  extern __shared__ unsigned long long s_acc[];  // [RH * RW][DX_ST]: u64 (FXB 64) or u32
+  unsigned* s_acc32 = (unsigned*)s_acc;
   const int HWo = a.Ho * a.Wo;
   const int64_t HWo64 = HWo;
   const int tw = (a.Wo + DX_TT - 1) / DX_TT, th = (a.Ho + DX_TT - 1) / DX_TT;
@@ -1494,16 +1214,20 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int 
   const int n = bid / (tw * th), t = bid - n * (tw * th);
   const float mx = __uint_as_float(amax[n]);
   if (mx == 0.f) return;  // nothing of this image is scattered (uniform per block)
-  const bool direct = FX && !(mx <= 3.0e38f);
+  const bool direct = !(mx <= 3.0e38f);
   int ex = 0;
-  frexpf(direct || !FX ? 1.f : mx, &ex);
-  const int e = min(127, 48 - ex);
+  frexpf(direct ? 1.f : mx, &ex);
+  const int e = min(127, (FXB == 64 ? 48 : 18) - ex);
   const float sc = ldexpf(1.f, e), isc = ldexpf(1.f, -e);
   const int ho0 = (t / tw) * DX_TT, wo0 = (t - (t / tw) * tw) * DX_TT;
   const int ry0 = ho0 * a.sh - a.ph - R, rx0 = wo0 * a.sw - a.pw - R;
   const int RP = RH * RW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane >> 4, pl = lane & 15;
-  float* gim = gx + (int64_t)n * a.H * a.W * a.Cp;
+  const int64_t HW64 = (int64_t)a.H * a.W;
+  float* gim = gx + (int64_t)n * HW64 * (NCHW ? a.C : a.Cp);
+  // element (pixel o, channel c) of this image's grad_x, and the step between channels
+  auto gaddr = [&](int64_t o, int c) { return NCHW ? gim + c * HW64 + o : gim + o * a.Cp + c; };
+  const int64_t cstep = NCHW ? HW64 : 1;
   const auto dyr = make_rsrc(dy + (int64_t)n * HWo64 * ldy, (uint32_t)((size_t)HWo * ldy * 2));
   const auto wr = make_rsrc(wd, (uint32_t)((size_t)a.K * 64 * ldw * 2));
   const int ho = ho0 + 2 * wv + (g & 1), wo = wo0 + pl;  // this lane's pixel
@@ -1541,8 +1265,8 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int 
     load_w(0, wa);
     load_om(0, om);
     for (int i = tid; i < RP * DX_ST; i += DW_NT) {
-      if (FX) s_acc[i] = 0ull;
-      else s_accf[i] = 0.f;
+      if (FXB == 64) s_acc[i] = 0ull;
+      else s_acc32[i] = 0u;
     }
     __syncthreads();
     for (int k = 0; k < a.K; ++k) {
@@ -1577,13 +1301,13 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int 
             const int base = (ly * RW + lx) * DX_ST + 8 * (g >> 1);
 #pragma unroll
             for (int e2 = 0; e2 < 8; ++e2) {
-              if (FX) atomicAdd(s_acc + base + e2, (unsigned long long)__float2ll_rn(wt[q] * dm[e2] * sc));
-              else atomicAdd(s_accf + base + e2, wt[q] * dm[e2]);
+              if (FXB == 64) atomicAdd(s_acc + base + e2, (unsigned long long)__float2ll_rn(wt[q] * dm[e2] * sc));
+              else atomicAdd(s_acc32 + base + e2, (unsigned)__float2int_rn(wt[q] * dm[e2] * sc));
             }
           } else {
-            float* dst = gim + (int64_t)oo[q] * a.Cp + c;
+            float* dst = gaddr(oo[q], c);
 #pragma unroll
-            for (int e2 = 0; e2 < 8; ++e2) unsafeAtomicAdd(dst + e2, wt[q] * dm[e2]);
+            for (int e2 = 0; e2 < 8; ++e2) unsafeAtomicAdd(dst + e2 * cstep, wt[q] * dm[e2]);
           }
         }
       }
@@ -1594,11 +1318,11 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int 
     }
     __syncthreads();
     for (int i = tid; i < RP * DX_CPP; i += DW_NT) {
-      const int pix = i / DX_CPP, ch = i - pix * DX_CPP;
+      const int ch = NCHW ? i / RP : i % DX_CPP, pix = NCHW ? i - ch * RP : i / DX_CPP;
       const int yy = ry0 + pix / RW, xx = rx0 + pix % RW;
       if (yy < 0 || yy >= a.H || xx < 0 || xx >= a.W) continue;
-      const float v = FX ? (float)(long long)s_acc[pix * DX_ST + ch] * isc : s_accf[pix * DX_ST + ch];
-      if (v != 0.f) unsafeAtomicAdd(gim + ((int64_t)yy * a.W + xx) * a.Cp + c0 + ch, v);
+      const float v = FXB == 64 ? (float)(long long)s_acc[pix * DX_ST + ch] * isc : (float)(int)s_acc32[pix * DX_ST + ch] * isc;
+      if (v != 0.f) unsafeAtomicAdd(gaddr((int64_t)yy * a.W + xx, c0 + ch), v);
     }
     __syncthreads();
   }
@@ -1610,32 +1334,26 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int 
 struct BwdGeom {
   int R1, WH, WW, R2, RH, RW;
   size_t lds1, lds2;
-  int v8, fx;  // eight-channel kernels; fixed-point scatter image
+  int fx;  // fixed-point bits of the scatter image (64 / 32)
 };
-// Kernel forms (A/B; read per call, so one test process runs every form): SR_DCN_BWD8=0 the
-// four-channel kernels; SR_DCN_GX_FX=0 / 1 the scatter image in fp32 / int64 fixed point
-int bwd8_env() {
-  const char* e = getenv("SR_DCN_BWD8");
-  return e ? atoi(e) : 1;
-}
+// Scatter image (A/B; read per call, so one test process runs both): SR_DCN_GX_FX=64 the int64
+// fixed-point image, else int32
 int gx_fx_env() {
   const char* e = getenv("SR_DCN_GX_FX");
-  return e ? atoi(e) : 1;
+  return e && atoi(e) == 64 ? 64 : 32;
 }
 bool bwd_fused_geom(const sr_dcn_desc* d, const DcnArgs& a, int cop, BwdGeom* bg) {
   if (!coord_win_ok(d, a) || cop < 8 || cop > 64 || cop % 8) return false;
-  bg->v8 = bwd8_env() != 0;
-  bg->fx = bg->v8 ? gx_fx_env() != 0 : 1;
+  bg->fx = gx_fx_env();
   bool ok1 = false, ok2 = false;
   for (int r = 2; r >= 0 && !ok1; --r) {
     const int wh = (DW_TH - 1) * a.sh + (a.kh - 1) * a.dh + 2 + 2 * r;
     const int ww = (DW_TW - 1) * a.sw + (a.kw - 1) * a.dw + 2 + 2 * r;
-    const size_t l = bg->v8 ? (size_t)2 * 64 * DF_RS * 2 + (size_t)wh * ww * 128
-                            : (size_t)3 * a.DG * DF_TP * 4 + (size_t)64 * DF_RS * 2 + (size_t)wh * ww * 128;
+    const size_t l = (size_t)2 * 64 * DF_RS * 2 + (size_t)wh * ww * 128;
     if (l <= 80 * 1024) { bg->R1 = r; bg->WH = wh; bg->WW = ww; bg->lds1 = l; ok1 = true; }
   }
-  const size_t esz = bg->fx ? 8 : 4;
-  for (int r = bg->fx ? 2 : 4; r >= 0 && !ok2; --r) {
+  const size_t esz = bg->fx == 64 ? 8 : 4;
+  for (int r = bg->fx == 64 ? 2 : 4; r >= 0 && !ok2; --r) {
     const int rh = (DX_TT - 1) * a.sh + (a.kh - 1) * a.dh + 2 * r + 2;
     const int rw = (DX_TT - 1) * a.sw + (a.kw - 1) * a.dw + 2 * r + 2;
     const size_t l = (size_t)rh * rw * DX_ST * esz;
@@ -1704,8 +1422,8 @@ int sr_dcn_bwd_fused_ok(const sr_dcn_desc* d, int cout_p) {
 }
 
 int sr_dcn_bwd_fused(const sr_dcn_desc* d, const void* dy, int ldy, const void* wd, int ldw, int cout_p, const void* x,
-                     const float* offset, const float* mask, float* grad_x, float* grad_offset, float* grad_mask,
-                     void* workspace, size_t ws_bytes, void* stream) {
+                     const float* offset, const float* mask, float* grad_x, int grad_x_nchw, float* grad_offset,
+                     float* grad_mask, void* workspace, size_t ws_bytes, void* stream) {
   DcnArgs a;
   int rc = make_args(d, a);
   if (rc) return rc;
@@ -1723,33 +1441,31 @@ int sr_dcn_bwd_fused(const sr_dcn_desc* d, const void* dy, int ldy, const void* 
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(amax, 0, (size_t)a.N * sizeof(unsigned), s) != hipSuccess)
     return sr_fail(SR_ELAUNCH, "dcn_bwd_fused: memset failed");
-  const void* k1 = bg.v8 ? (const void*)dcn_coord_dy8_kernel : (const void*)dcn_coord_dy_kernel;
-  const void* k2 = !bg.v8 ? (const void*)dcn_gradx_dy_kernel
-                   : bg.fx ? (const void*)dcn_gradx_dy8_kernel<true> : (const void*)dcn_gradx_dy8_kernel<false>;
-  if (bg.lds1 > 65536 && hipFuncSetAttribute(k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bg.lds1) != hipSuccess)
+  const bool nchw = grad_x_nchw != 0;
+  const void* k2 = bg.fx == 64 ? (nchw ? (const void*)dcn_gradx_dy8_kernel<64, true> : (const void*)dcn_gradx_dy8_kernel<64, false>)
+                               : (nchw ? (const void*)dcn_gradx_dy8_kernel<32, true> : (const void*)dcn_gradx_dy8_kernel<32, false>);
+  if (bg.lds1 > 65536 && hipFuncSetAttribute((const void*)dcn_coord_dy8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)bg.lds1) != hipSuccess)
     return sr_fail(SR_ELAUNCH, "dcn_bwd_fused: LDS attribute");
   if (bg.lds2 > 65536 && hipFuncSetAttribute(k2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bg.lds2) != hipSuccess)
     return sr_fail(SR_ELAUNCH, "dcn_bwd_fused: LDS attribute");
+  // NCHW grad_x is written in full: the coordinate kernel zeroes it (C H W a multiple of 4: C = 64)
+  const int64_t gxn4 = nchw ? (int64_t)a.N * a.C * a.H * a.W / 4 : 0;
   const int wt = ((a.Ho + DW_TH - 1) / DW_TH) * ((a.Wo + DW_TW - 1) / DW_TW);
-  if (bg.v8)
-    hipLaunchKernelGGL(dcn_coord_dy8_kernel, dim3((unsigned)(a.N * wt)), dim3(DC8_NT), bg.lds1, s, a, (const bf16_t*)dy,
-                       ldy, (const bf16_t*)wd, ldw, cout_p, (const bf16_t*)x, offset, mask, grad_offset, grad_mask,
-                       amax, bg.R1, bg.WH, bg.WW);
-  else
-    hipLaunchKernelGGL(dcn_coord_dy_kernel, dim3((unsigned)(a.N * wt)), dim3(DW_NT), bg.lds1, s, a, (const bf16_t*)dy,
-                       ldy, (const bf16_t*)wd, ldw, cout_p, (const bf16_t*)x, offset, mask, grad_offset, grad_mask,
-                       amax, bg.R1, bg.WH, bg.WW);
-  if (hipGetLastError() != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_coord_dy launch");
+  hipLaunchKernelGGL(dcn_coord_dy8_kernel, dim3((unsigned)(a.N * wt)), dim3(DC8_NT), bg.lds1, s, a, (const bf16_t*)dy,
+                     ldy, (const bf16_t*)wd, ldw, cout_p, (const bf16_t*)x, offset, mask, grad_offset, grad_mask, amax,
+                     bg.R1, bg.WH, bg.WW, nchw ? grad_x : nullptr, gxn4);
+  if (hipGetLastError() != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_coord_dy8 launch");
   const int xt = ((a.Ho + DX_TT - 1) / DX_TT) * ((a.Wo + DX_TT - 1) / DX_TT);
   const dim3 xg((unsigned)(a.N * xt));
-#define SR_GX(KERN)                                                                                            \
-  hipLaunchKernelGGL(KERN, xg, dim3(DW_NT), bg.lds2, s, a, bg.R2, bg.RH, bg.RW, (const bf16_t*)dy, ldy,        \
-                     (const bf16_t*)wd, ldw, cout_p, offset, mask, (const unsigned*)amax, grad_x)
-  if (!bg.v8) SR_GX(dcn_gradx_dy_kernel);
-  else if (bg.fx) SR_GX(dcn_gradx_dy8_kernel<true>);
-  else SR_GX(dcn_gradx_dy8_kernel<false>);
+#define SR_GX(FXB, NC)                                                                                        \
+  hipLaunchKernelGGL((dcn_gradx_dy8_kernel<FXB, NC>), xg, dim3(DW_NT), bg.lds2, s, a, bg.R2, bg.RH, bg.RW,     \
+                     (const bf16_t*)dy, ldy, (const bf16_t*)wd, ldw, cout_p, offset, mask, (const unsigned*)amax, \
+                     grad_x)
+  if (bg.fx == 64) { if (nchw) SR_GX(64, true); else SR_GX(64, false); }
+  else { if (nchw) SR_GX(32, true); else SR_GX(32, false); }
 #undef SR_GX
-  return sr_check(hipGetLastError(), "dcn_gradx_dy launch");
+  return sr_check(hipGetLastError(), "dcn_gradx_dy8 launch");
 }
 
 size_t sr_dcn_col2im_workspace(const sr_dcn_desc* d) { return d ? (size_t)d->N * sizeof(unsigned) : 0; }

@@ -36,8 +36,22 @@
 
 namespace {
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 SR_DEV uint2 buf_load8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+// Global stores of the fused kernels go through buffer resources with out-of-range offsets for the
+// lanes that must not store, and no branch at all around them (inference: the training outputs'
+// resources have size 0, every store drops): on gfx9 stores count in vmcnt, and behind a branch the
+// compiler's bookkeeping takes the no-store path's count, so a later load wait drained every store.
+SR_DEV void buf_store8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+SR_DEV void buf_store16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+SR_DEV void buf_store4f(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
 
 struct SabArgs {
@@ -93,6 +107,14 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   const int g = lane >> 4, c16 = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
   const int blk = (int)xcd_remap(blockIdx.x, gridDim.x);
   const bool train = a.qkv != nullptr;
+  const uint32_t M = (uint32_t)(a.N * a.H * a.W);
+  const auto lnr = make_rsrc(a.ln_out, train ? M * a.Cp * 2u : 0u);
+  const auto mur = make_rsrc(a.mean, train ? M * 4u : 0u);
+  const auto rsr = make_rsrc(a.rstd, train ? M * 4u : 0u);
+  const auto qkvr = make_rsrc(a.qkv, train ? M * a.ldq * 2u : 0u);
+  const auto aor = make_rsrc(a.ao, train ? M * a.ldo * 2u : 0u);
+  const auto lser = make_rsrc(a.lse, train ? (uint32_t)a.nwin_total * a.nH * 64u * 4u : 0u);
+  const auto x2r = make_rsrc(a.x2, M * a.Cp * 2u);
   float* sTB = (float*)(smem + SAB_TB);
   float* sGB = (float*)(smem + SAB_GB);
   float* sBQ = (float*)(smem + SAB_BQ);
@@ -204,14 +226,12 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
-        if (train) *(u32x4*)(a.ln_out + pr * a.Cp + ch * 8) = o4;
       }
+      buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(pr * a.Cp + ch * 8) * 2u : SR_OOB, o4);
       *(u32x4*)(smem + SAB_X + tile_off(128, r, ch)) = o4;
     }
-    if (train && vr && part == 0) {
-      a.mean[pr] = mu;
-      a.rstd[pr] = rs;
-    }
+    buf_store4f(mur, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, mu);
+    buf_store4f(rsr, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, rs);
   }
   w_store();
   __syncthreads();
@@ -263,6 +283,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       wpf[i] = buf_load16(wpr, row < a.Cp ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
     }
     if (h + 1 < a.nH) w_load(h + 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep these loads here, ahead of the head's stores
 
     // ---- A: q / k / v of head h
     f32x4 acc[3][2];
@@ -295,10 +316,10 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         uint2 u;
         u.x = pack_bf16x2(acc[i][j][0] + bias[0], acc[i][j][1] + bias[1]);
         u.y = pack_bf16x2(acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]);
-        if (train && vA[j]) *(uint2*)(a.qkv + pixA[j] * a.ldq + gr) = u;
-        if (which == 0) *(uint2*)(smem + SAB_Q + qk_off(t, d)) = u;
-        else if (which == 1) *(uint2*)(smem + SAB_K + qk_off(t, d)) = u;
-        else *(uint2*)(smem + SAB_V + (t >> 6) * 4096 + sx_byte(t & 63, d)) = u;
+        buf_store8(qkvr, vA[j] ? (uint32_t)(pixA[j] * a.ldq + gr) * 2u : SR_OOB, u);
+        const uint32_t qk = qk_off(t, d);
+        const uint32_t la = which == 0 ? SAB_Q + qk : which == 1 ? SAB_K + qk : SAB_V + (t >> 6) * 4096 + sx_byte(t & 63, d);
+        *(uint2*)(smem + la) = u;
       }
     }
     __syncthreads();  // S1: Q, K, V of head h in LDS
@@ -341,7 +362,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[i][r] *= inv;
-      if (train && vB && g == 0) a.lse[((int64_t)(2 * blk + wi) * a.nH + h) * 64 + qq] = mx + __logf(sm);
+      buf_store4f(lser, (vB && g == 0) ? (uint32_t)(((2 * blk + wi) * a.nH + h) * 64 + qq) * 4u : SR_OOB, mx + __logf(sm));
       f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       const char* sVw = smem + SAB_V + wi * 4096;
 #pragma unroll
@@ -355,7 +376,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         uint2 u;
         u.x = pack_bf16x2(o[d][0], o[d][1]);
         u.y = pack_bf16x2(o[d][2], o[d][3]);
-        if (train && vB) *(uint2*)(a.ao + pixB * a.ldo + h * 32 + 16 * d + 4 * g) = u;
+        buf_store8(aor, vB ? (uint32_t)(pixB * a.ldo + h * 32 + 16 * d + 4 * g) * 2u : SR_OOB, u);
         *(uint2*)(smem + SAB_O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
       }
     }
@@ -397,12 +418,9 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int oc = pog * 48 + 16 * i + 4 * g;
-    if (oc >= a.Cp) continue;
     const f32x4 bias = biasp[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if (!vj[j]) continue;
-      const int64_t pix = pixj[j];
       const float sc = scj[j];
       const uint2 xv = xres[i][j];
       uint2 u;
@@ -410,7 +428,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
                         bf16_to_f32(xv.x >> 16) + sc * (xacc[i][j][1] + bias[1]));
       u.y = pack_bf16x2(bf16_to_f32(xv.y & 0xffff) + sc * (xacc[i][j][2] + bias[2]),
                         bf16_to_f32(xv.y >> 16) + sc * (xacc[i][j][3] + bias[3]));
-      *(uint2*)(a.x2 + pix * a.Cp + oc) = u;
+      buf_store8(x2r, (oc < a.Cp && vj[j]) ? (uint32_t)(pixj[j] * a.Cp + oc) * 2u : SR_OOB, u);
     }
   }
 }
@@ -460,6 +478,13 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   const int g = lane >> 4, c16 = lane & 15;
   const int m0 = (int)xcd_remap(blockIdx.x, gridDim.x) * 128;
   const bool train = a.z != nullptr;
+  const uint32_t Mu = (uint32_t)a.M;
+  const auto lnr = make_rsrc(a.ln_out, train ? Mu * a.Cp * 2u : 0u);  // size 0: every store drops
+  const auto mur = make_rsrc(a.mean, train ? Mu * 4u : 0u);
+  const auto rsr = make_rsrc(a.rstd, train ? Mu * 4u : 0u);
+  const auto zr = make_rsrc(a.z, train ? Mu * a.Hp * 2u : 0u);
+  const auto hr_ = make_rsrc(a.h, train ? Mu * a.Hp * 2u : 0u);
+  const auto outr = make_rsrc(a.out, Mu * a.Cp * 2u);
   float* sGB = (float*)(smem + SMB_GB);
   float* sB1 = (float*)(smem + SMB_B1);
   float* sB2 = (float*)(smem + SMB_B2);
@@ -535,14 +560,12 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
-        if (train) *(u32x4*)(a.ln_out + (int64_t)m * a.Cp + ch * 8) = o4;
       }
+      buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(m * a.Cp + ch * 8) * 2u : SR_OOB, o4);
       *(u32x4*)(smem + SMB_H + tile_off(128, r, ch)) = o4;
     }
-    if (train && vr && part == 0) {
-      a.mean[m] = mu;
-      a.rstd[m] = rs;
-    }
+    buf_store4f(mur, (vr && part == 0) ? (uint32_t)m * 4u : SR_OOB, mu);
+    buf_store4f(rsr, (vr && part == 0) ? (uint32_t)m * 4u : SR_OOB, rs);
   }
   __syncthreads();
 
@@ -623,10 +646,9 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
       uz.y = pack_bf16x2(zv[2], zv[3]);
       uh.x = pack_bf16x2(hv[0], hv[1]);
       uh.y = pack_bf16x2(hv[2], hv[3]);
-      if (train && m < a.M && hr < a.Hp) {
-        *(uint2*)(a.z + (int64_t)m * a.Hp + hr) = uz;
-        *(uint2*)(a.h + (int64_t)m * a.Hp + hr) = uh;
-      }
+      const uint32_t zo = (m < a.M && hr < a.Hp) ? (uint32_t)(m * a.Hp + hr) * 2u : SR_OOB;
+      buf_store8(zr, zo, uz);
+      buf_store8(hr_, zo, uh);
       *(uint2*)(smem + SMB_H + tile_off(128, t, hr >> 3) + (hr & 7) * 2) = uh;
     }
   }
@@ -680,12 +702,10 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int oc = og * 48 + 16 * i + 4 * g;
-    if (oc >= a.Cp) continue;
     const f32x4 bias = bias2[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + tg * 64 + 16 * j + c16;
-      if (m >= a.M) continue;
       const float sc = scj[j];
       const uint2 xv = xres[i][j];
       uint2 u;
@@ -693,7 +713,7 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
                         bf16_to_f32(xv.x >> 16) + sc * (acc2[i][j][1] + bias[1]));
       u.y = pack_bf16x2(bf16_to_f32(xv.y & 0xffff) + sc * (acc2[i][j][2] + bias[2]),
                         bf16_to_f32(xv.y >> 16) + sc * (acc2[i][j][3] + bias[3]));
-      *(uint2*)(a.out + (int64_t)m * a.Cp + oc) = u;
+      buf_store8(outr, (oc < a.Cp && m < a.M) ? (uint32_t)(m * a.Cp + oc) * 2u : SR_OOB, u);
     }
   }
 }
@@ -719,8 +739,8 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
     return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: training needs ln_out, mean, rstd, qkv, attn_out and lse");
   if (!sr_swin_attn_fused_ok(SR_BF16, N, H, W, 8, nH, 32, 32, C, Cp) || shift < 0 || shift >= 8)
     return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: bf16, window 8, head dim <= 32, nH * 32 <= 192, Cp <= 192");
-  if ((size_t)N * H * W * Cp * 2 >= 0x80000000ull)
-    return sr_fail(SR_ETOOBIG, "swin_attn_fused_fwd: token map >= 2 GiB (split the batch)");
+  if ((size_t)N * H * W * 3 * nH * 32 * 2 >= 0x80000000ull || (size_t)N * H * W * Cp * 2 >= 0x80000000ull)
+    return sr_fail(SR_ETOOBIG, "swin_attn_fused_fwd: qkv map >= 2 GiB (split the batch)");
   SabArgs a{};
   a.x = (const bf16_t*)x; a.ln_g = ln_g; a.ln_b = ln_b; a.wq = (const bf16_t*)wqkv; a.bq = bqkv;
   a.table = bias_table; a.wp = (const bf16_t*)wproj; a.bp = bproj; a.rsc = row_scale;

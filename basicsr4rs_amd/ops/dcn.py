@@ -194,19 +194,20 @@ def _dcn_backward(grad_out, saved, weight, bias, g, dtype):
         dbs.append(db)
     grad_weight = torch.cat(dws, 0) if g.G > 1 else dws[0]
     grad_bias = None if bias is None else (torch.cat(dbs, 0) if g.G > 1 else dbs[0])
-    gx = torch.zeros(g.N, g.H, g.W, g.Cp, device=dyh.device, dtype=torch.float32)
     goff = torch.empty_like(off)
     gmask = None if msk is None else torch.empty_like(msk)
     d = g.desc(dtype)
     wsb = lib.sr_dcn_col2im_workspace(d)
     ws = torch.empty(wsb // 4 + 1, device=dyh.device, dtype=torch.int32)
-    if fused:
+    if fused:  # grad x written in full, NCHW
         wd = images[0][1]
+        gx = torch.empty(g.N, g.C, g.H, g.W, device=dyh.device, dtype=torch.float32)
         _lib.check(
             lib.sr_dcn_bwd_fused(d, _lib.ptr(dyh), g.ldy, _lib.ptr(wd), wd.shape[1], g.cout_gp, _lib.ptr(xh),
-                                 _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx), _lib.ptr(goff), _lib.ptr(gmask),
+                                 _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx), 1, _lib.ptr(goff), _lib.ptr(gmask),
                                  _lib.ptr(ws), wsb, _lib.stream()))
-        return C.nhwc_to_nchw(gx, g.C), goff, gmask, grad_weight, grad_bias
+        return gx, goff, gmask, grad_weight, grad_bias
+    gx = torch.zeros(g.N, g.H, g.W, g.Cp, device=dyh.device, dtype=torch.float32)
     _lib.check(
         lib.sr_dcn_col2im(d, _lib.ptr(dcols), _lib.ptr(xh), _lib.ptr(off), _lib.ptr(msk), _lib.ptr(gx),
                           _lib.ptr(goff), _lib.ptr(gmask), _lib.ptr(ws), wsb, _lib.stream()))

@@ -416,13 +416,14 @@ int sr_dcn_col2im(const sr_dcn_desc* d, const void* dcols, const void* x, const 
  * multiple of 8; query sr_dcn_bwd_fused_ok): from dy (bf16 NHWC [N][Ho][Wo][ldy], channels [0, cout_p))
  * and the transposed weight image wd (bf16 [K*64][ldw], row tap*64 + ci, column co -- the GEMM image the
  * dcols path multiplies dy by), each tap's dcols tile is formed on MFMA in registers and consumed at once:
- * grad_offset / grad_mask written in full, grad_x += the bilinear scatter (fp32 NHWC [N][H][W][Cp], caller
- * zeroes it).  Same results as sr_dcn_col2im on dcols = bf16(dy x wd^T).  Workspace as sr_dcn_col2im.
+ * grad_offset / grad_mask written in full; grad_x: grad_x_nchw = 0 -> += the bilinear scatter into fp32
+ * NHWC [N][H][W][Cp] (caller zeroes it, as sr_dcn_col2im), 1 -> fp32 NCHW [N][C][H][W] written in full.
+ * Same results as sr_dcn_col2im on dcols = bf16(dy x wd^T).  Workspace as sr_dcn_col2im.
  * Replaces the addmm into columns + col2im + col2im_coord of deform_conv_cuda.cpp:640-685. */
 int sr_dcn_bwd_fused_ok(const sr_dcn_desc* d, int cout_p);
 int sr_dcn_bwd_fused(const sr_dcn_desc* d, const void* dy, int ldy, const void* wd, int ldw, int cout_p, const void* x,
-                     const float* offset, const float* mask, float* grad_x, float* grad_offset, float* grad_mask,
-                     void* workspace, size_t ws_bytes, void* stream);
+                     const float* offset, const float* mask, float* grad_x, int grad_x_nchw, float* grad_offset,
+                     float* grad_mask, void* workspace, size_t ws_bytes, void* stream);
 
 /* deform_conv_ext-compatible entries (basicsr/ops/dcn/src/deform_conv_ext.cpp:52-163; argument order
  * of :52-57, :70-76, :89-94, :107-113, :127-134): the reference's tensors in its order as fp32 NCHW

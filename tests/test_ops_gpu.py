@@ -155,16 +155,17 @@ def test_dcn_fused_forward(cuda, case, need_grad):
 
 
 @pytest.mark.parametrize('case', FUSED_CASES)
-@pytest.mark.parametrize('form', ['v8_fx', 'v8_f32', 'v4'])
+@pytest.mark.parametrize('form', ['i32_nchw', 'i64_nchw', 'i32_nhwc'])
 def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, monkeypatch):
     """sr_dcn_bwd_fused (round 4: each tap's dcols tile formed on MFMA inside the coordinate-gradient
     and scatter kernels, never stored) against the dcols path on the same operands: dcols =
     bf16(dy x W) by the 1x1 GEMM, then sr_dcn_col2im.  Both sample the same bf16 dcols values (up to
     the GEMMs' summation order), so grad offset / mask / x agree to fp32 summation-order noise;
-    offsets of std 2 put many samples past the R = 2 windows onto the global paths.  Forms: the
-    eight-channel kernels with the fixed-point or the fp32 scatter image, and the four-channel ones."""
-    monkeypatch.setenv('SR_DCN_BWD8', '0' if form == 'v4' else '1')
-    monkeypatch.setenv('SR_DCN_GX_FX', '0' if form == 'v8_f32' else '1')
+    offsets of std 2 put many samples past the R = 2 windows onto the global paths.  Forms: the int32
+    (default) or int64 fixed-point scatter image; grad x written in full as NCHW (the op's form: the
+    coordinate kernel zeroes it -- the buffer starts as NaN here) or accumulated into a zeroed NHWC map."""
+    monkeypatch.setenv('SR_DCN_GX_FX', '64' if form.startswith('i64') else '32')
+    nchw = form.endswith('nchw')
     N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
     x, off, msk, w, b, dy = _dcn_inputs(case, seed=3)
     lib = _lib.load()
@@ -194,9 +195,13 @@ def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, monkeypatch):
         gm = torch.full_like(mskc, float('nan')) if modulated else None
         ws = torch.empty(wsb // 4 + 1, device=cuda, dtype=torch.int32)
         if fused:
+            gxf = torch.full((g.N, g.C, g.H, g.W), float('nan'), device=cuda) if nchw else gx
             _lib.check(lib.sr_dcn_bwd_fused(desc, _lib.ptr(dyh), g.ldy, _lib.ptr(wd), wd.shape[1], g.cout_gp,
-                                            _lib.ptr(xh), _lib.ptr(offc), _lib.ptr(mskc), _lib.ptr(gx), _lib.ptr(goff),
-                                            _lib.ptr(gm), _lib.ptr(ws), wsb, _lib.stream()))
+                                            _lib.ptr(xh), _lib.ptr(offc), _lib.ptr(mskc), _lib.ptr(gxf), int(nchw),
+                                            _lib.ptr(goff), _lib.ptr(gm), _lib.ptr(ws), wsb, _lib.stream()))
+            if nchw:
+                gx = gxf.permute(0, 2, 3, 1)[..., :g.C]
+                outs[0] = (outs[0][0][..., :g.C],) + outs[0][1:]
         else:
             _lib.check(lib.sr_dcn_col2im(desc, _lib.ptr(dcols), _lib.ptr(xh), _lib.ptr(offc), _lib.ptr(mskc),
                                          _lib.ptr(gx), _lib.ptr(goff), _lib.ptr(gm), _lib.ptr(ws), wsb,
