@@ -1197,8 +1197,10 @@ __global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, con
 // the int32 image is half the LDS (a wider halo fits).  fp32 LDS atomics are ~25x slower on gfx950.
 // NCHW: grad_x as fp32 [N][C][H][W] (the op's output layout: no NHWC -> NCHW pass), else NHWC
 // [N][H][W][Cp]; the flush then walks pixels fastest, so the atomics of a wave are row-contiguous.
-template <int FXB, bool NCHW>
-__global__ void __launch_bounds__(DW_NT, 2) dcn_gradx_dy8_kernel(DcnArgs a, int R, int RH, int RW,
+// OCC: 8-wave blocks per CU the registers are budgeted for (launch bounds count waves per SIMD; at 3
+// the int32 kernel spills 22 VGPRs and ran 1.10 vs 1.01 ms for the C5 op fwd + bwd)
+template <int FXB, bool NCHW, int OCC = 2>
+__global__ void __launch_bounds__(DW_NT, 2 * OCC) dcn_gradx_dy8_kernel(DcnArgs a, int R, int RH, int RW,
                                                                  const bf16_t* __restrict__ dy, int ldy,
                                                                  const bf16_t* __restrict__ wd, int ldw, int cop,
                                                                  const float* __restrict__ off,
@@ -1342,6 +1344,7 @@ int gx_fx_env() {
   const char* e = getenv("SR_DCN_GX_FX");
   return e && atoi(e) == 64 ? 64 : 32;
 }
+
 bool bwd_fused_geom(const sr_dcn_desc* d, const DcnArgs& a, int cop, BwdGeom* bg) {
   if (!coord_win_ok(d, a) || cop < 8 || cop > 64 || cop % 8) return false;
   bg->fx = gx_fx_env();
@@ -1353,11 +1356,12 @@ bool bwd_fused_geom(const sr_dcn_desc* d, const DcnArgs& a, int cop, BwdGeom* bg
     if (l <= 80 * 1024) { bg->R1 = r; bg->WH = wh; bg->WW = ww; bg->lds1 = l; ok1 = true; }
   }
   const size_t esz = bg->fx == 64 ? 8 : 4;
+  const size_t lim2 = 80 * 1024;
   for (int r = bg->fx == 64 ? 2 : 4; r >= 0 && !ok2; --r) {
     const int rh = (DX_TT - 1) * a.sh + (a.kh - 1) * a.dh + 2 * r + 2;
     const int rw = (DX_TT - 1) * a.sw + (a.kw - 1) * a.dw + 2 * r + 2;
     const size_t l = (size_t)rh * rw * DX_ST * esz;
-    if (l <= 80 * 1024) { bg->R2 = r; bg->RH = rh; bg->RW = rw; bg->lds2 = l; ok2 = true; }
+    if (l <= lim2) { bg->R2 = r; bg->RH = rh; bg->RW = rw; bg->lds2 = l; ok2 = true; }
   }
   return ok1 && ok2;
 }
@@ -1458,12 +1462,12 @@ int sr_dcn_bwd_fused(const sr_dcn_desc* d, const void* dy, int ldy, const void* 
   if (hipGetLastError() != hipSuccess) return sr_fail(SR_ELAUNCH, "dcn_coord_dy8 launch");
   const int xt = ((a.Ho + DX_TT - 1) / DX_TT) * ((a.Wo + DX_TT - 1) / DX_TT);
   const dim3 xg((unsigned)(a.N * xt));
-#define SR_GX(FXB, NC)                                                                                        \
-  hipLaunchKernelGGL((dcn_gradx_dy8_kernel<FXB, NC>), xg, dim3(DW_NT), bg.lds2, s, a, bg.R2, bg.RH, bg.RW,     \
+#define SR_GX(FXB, NC, OC)                                                                                    \
+  hipLaunchKernelGGL((dcn_gradx_dy8_kernel<FXB, NC, OC>), xg, dim3(DW_NT), bg.lds2, s, a, bg.R2, bg.RH, bg.RW, \
                      (const bf16_t*)dy, ldy, (const bf16_t*)wd, ldw, cout_p, offset, mask, (const unsigned*)amax, \
                      grad_x)
-  if (bg.fx == 64) { if (nchw) SR_GX(64, true); else SR_GX(64, false); }
-  else { if (nchw) SR_GX(32, true); else SR_GX(32, false); }
+  if (bg.fx == 64) { if (nchw) SR_GX(64, true, 2); else SR_GX(64, false, 2); }
+  else { if (nchw) SR_GX(32, true, 2); else SR_GX(32, false, 2); }
 #undef SR_GX
   return sr_check(hipGetLastError(), "dcn_gradx_dy8 launch");
 }

@@ -243,7 +243,7 @@ class DeformConvFunction(Function):
             raise AssertionError('im2col step must divide batchsize')
         dtype = C.feature_dtype()
         g = _Geom(input, weight, stride, padding, dilation, groups, deformable_groups)
-        out, saved = _dcn_forward(input, offset, None, weight, None, g, dtype, any(ctx.needs_input_grad))
+        out, saved = _dcn_forward(input, offset, None, weight, None, g, dtype, _GRAD[0] and any(ctx.needs_input_grad))
         _save(ctx, g, dtype, input, saved, weight, None)
         return out.to(input.dtype)
 
@@ -267,7 +267,7 @@ class ModulatedDeformConvFunction(Function):
         _require_gpu(input, offset, mask, weight)
         dtype = C.feature_dtype()
         g = _Geom(input, weight, stride, padding, dilation, groups, deformable_groups)
-        out, saved = _dcn_forward(input, offset, mask, weight, bias, g, dtype, any(ctx.needs_input_grad))
+        out, saved = _dcn_forward(input, offset, mask, weight, bias, g, dtype, _GRAD[0] and any(ctx.needs_input_grad))
         _save(ctx, g, dtype, input, saved, weight, bias)
         return out.to(input.dtype)
 
@@ -280,8 +280,24 @@ class ModulatedDeformConvFunction(Function):
         return (gx.to(ctx.in_dtype), goff, gmask, gw, gb, None, None, None, None, None)
 
 
-deform_conv = DeformConvFunction.apply
-modulated_deform_conv = ModulatedDeformConvFunction.apply
+# Grad mode at the call: inside Function.forward it is always off, and needs_input_grad holds under
+# torch.no_grad() too (weights still require grad), so an inference call would store the columns.
+_GRAD = [True]
+
+
+def _with_grad_mode(fn):
+    def call(*args):
+        prev, _GRAD[0] = _GRAD[0], torch.is_grad_enabled()
+        try:
+            return fn(*args)
+        finally:
+            _GRAD[0] = prev
+    call.__name__ = fn.__name__ if hasattr(fn, '__name__') else 'apply'
+    return call
+
+
+deform_conv = _with_grad_mode(DeformConvFunction.apply)
+modulated_deform_conv = _with_grad_mode(ModulatedDeformConvFunction.apply)
 
 
 def _offset_conv(conv, x):

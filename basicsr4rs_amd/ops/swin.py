@@ -395,7 +395,8 @@ def swin_mlp_fused(x, n2w, n2b, Creal, f1wf, f1bg, fc1s, f2wf, f2bg, s2, train):
 class _STB(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, x, geom, fc1s, fc2s, scale, dp, n1w, n1b, qw, qb, table, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b):
+    def forward(ctx, x, geom, fc1s, fc2s, scale, dp, train, n1w, n1b, qw, qb, table, pw, pb, n2w, n2b, f1w, f1b, f2w,
+                f2b):
         dtype = x.dtype
         N, H, W, Cp = x.shape
         Cr = geom.dim
@@ -403,7 +404,8 @@ class _STB(torch.autograd.Function):
         tab = table.detach().float().contiguous()
         pwf, _, pbg = prepared_linear(pw, pb, geom.proj, dtype)
         s1, s2 = dp if dp is not None else (None, None)  # per-sample DropPath factors (fp32 [N])
-        fused = swin_attn_fused(x, n1w, n1b, Cr, qwf, qbg, tab, pwf, pbg, s1, geom, scale, any(ctx.needs_input_grad))
+        train = train and any(ctx.needs_input_grad)  # the fused kernels store the backward's inputs only then
+        fused = swin_attn_fused(x, n1w, n1b, Cr, qwf, qbg, tab, pwf, pbg, s1, geom, scale, train)
         if fused is not None:  # LN1 -> qkv -> window attention -> proj + residual in one launch
             x2, ln1, m1, r1, qkv, a, lse = fused
         else:
@@ -417,7 +419,7 @@ class _STB(torch.autograd.Function):
             x2 = linear_fwd(a, pwf, pbg, geom.proj, N, H, W, res=x, beta=1.0, row_scale=s1)
         f1wf, _, f1bg = prepared_linear(f1w, f1b, fc1s, dtype)
         f2wf, _, f2bg = prepared_linear(f2w, f2b, fc2s, dtype)
-        fm = swin_mlp_fused(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, f2wf, f2bg, s2, any(ctx.needs_input_grad))
+        fm = swin_mlp_fused(x2, n2w, n2b, Cr, f1wf, f1bg, fc1s, f2wf, f2bg, s2, train)
         if fm is not None:  # LN2 -> fc1 -> GELU -> fc2 + residual in one launch
             out, ln2, m2, r2, z, h = fm
         else:
@@ -464,13 +466,17 @@ class _STB(torch.autograd.Function):
         dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
         dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W, params=(qw, qb))
         dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2, params=(n1w, n1b))
-        return (dx, None, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w, df2b)
+        return (dx, None, None, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w,
+                df2b)
 
 
 def swin_block(x, blk, geom, fc1s, fc2s, dp=None):
     """dp: None, or the (s1, s2) per-sample DropPath factors of this forward."""
     at = blk.attn
-    return _STB.apply(x, geom, fc1s, fc2s, float(at.scale), dp, blk.norm1.weight, blk.norm1.bias, at.qkv.weight,
+    # grad mode is read here: inside Function.forward it is always off, and needs_input_grad holds under
+    # torch.no_grad() too (parameters still require grad), so validation would store the backward's inputs
+    return _STB.apply(x, geom, fc1s, fc2s, float(at.scale), dp, torch.is_grad_enabled(), blk.norm1.weight,
+                      blk.norm1.bias, at.qkv.weight,
                       at.qkv.bias, at.relative_position_bias_table, at.proj.weight, at.proj.bias, blk.norm2.weight,
                       blk.norm2.bias, blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.mlp.fc2.weight, blk.mlp.fc2.bias)
 

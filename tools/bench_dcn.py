@@ -88,6 +88,8 @@ def main():
                 return D.modulated_deform_conv(x, off, msk, w, b, 1, 1, 1, 1, dg)
 
         def fwdbwd():
+            for t in (x, off, msk, w, b):  # as zero_grad(set_to_none=True): no accumulation kernels timed
+                t.grad = None
             with torch.autocast('cuda', dtype=torch.bfloat16, enabled=ac):
                 y = D.modulated_deform_conv(x, off, msk, w, b, 1, 1, 1, 1, dg)
             y.backward(dy)

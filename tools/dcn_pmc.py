@@ -29,8 +29,8 @@ y_b, dx_b = 4 * px * C, 4 * px * C
 ALG = {
     'dcn_fwd_win_kernel': (x_b + om_b + y_b, 'x bf16 + offset/mask fp32 in, y fp32 out (columns, when stored '
                                               'for the backward, are not algorithmic)'),
-    'dcn_coord_dy_kernel': (x_b + dy_b + 2 * om_b, 'x, dy bf16 + offset/mask fp32 in, their gradients out'),
-    'dcn_gradx_dy_kernel': (dy_b + om_b + dx_b, 'dy bf16 + offset/mask fp32 in, dx fp32 out'),
+    'dcn_coord_dy8_kernel': (x_b + dy_b + 2 * om_b, 'x, dy bf16 + offset/mask fp32 in, their gradients out'),
+    'dcn_gradx_dy8_kernel': (dy_b + om_b + dx_b, 'dy bf16 + offset/mask fp32 in, dx fp32 out'),
     'dcn_coord_win_kernel': (x_b + 2 * om_b, 'dcols path: x + offset/mask in, gradients out (dcols not counted)'),
     'dcn_grad_x_kernel': (om_b + dx_b, 'dcols path: offset/mask in, dx out (dcols not counted)'),
 }

@@ -16,8 +16,7 @@ bd() {  # $1 tag, rest: env
     > $OUT/bench_$tag.log 2>&1 || { tail -5 $OUT/bench_$tag.log; return 1; }
   python3 -c "import json; d=json.load(open('$OUT/dcn_bench_$tag.json'))['bf16']; print('$tag', d['fwd_ms'], d['fwd_bwd_ms'])"
 }
-bd v8i32 X=1 && bd v8i64 SR_DCN_GX_FX=64 && bd v4 SR_DCN_BWD8=0 && bd dcols SR_DCN_BWD_FUSED=0 && bd v8i32_b X=1 && \
-  bd v8i64_b SR_DCN_GX_FX=64 || exit 1
+bd i32 X=1 && bd i64 SR_DCN_GX_FX=64 && bd dcols SR_DCN_BWD_FUSED=0 && bd i32_b X=1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 tools/bench_dcn.py \
   --no-cpu --modes bf16 --iters 10 > $OUT/prof.log 2>&1 || exit 1
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cp "$f" $OUT/dcn_kernel_stats.csv
