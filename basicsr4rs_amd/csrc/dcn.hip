@@ -970,7 +970,8 @@ SR_DEV float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 SR_DEV float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 SR_DEV float bf16_round(float v) { return bf16_to_f32(f32_to_bf16(v)); }
 
-constexpr int DX_TT = 16, DX_CPP = 16, DX_ST = DX_CPP + 1;  // tile edge, channels per pass, LDS pixel stride (u64)
+constexpr int DX_TT = 16, DX_CPP = 16, DX_ST = DX_CPP + 1;
+constexpr int GX_PD = 3;  // taps of operands in flight in the scatter kernel  // tile edge, channels per pass, LDS pixel stride (u64)
 
 // Eight-channel lane layout.  The MFMA leaves a lane 4 channels (16 cb + 4 (lane >> 4) .. + 3) of ONE
 // pixel (lane & 15) per 16-channel tile; a bilinear sample (offset / mask reads, corner geometry) for
@@ -1061,8 +1062,9 @@ __global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, con
   };
   u32x4 wp[2];
   wload(0, wp);
-  float om[4][3];
+  float om[4][3], om1[4][3];  // taps k and k + 1 (the loads run two taps ahead)
   load_om(0, om);
+  if (a.K > 1) load_om(1, om1);
   const int nwin = WH * WW * 8;
   for (int b0 = 0; b0 < nwin; b0 += 4 * DC8_NT) {
     u32x4 val[4];
@@ -1088,7 +1090,7 @@ __global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, con
   const int gv = a.cpg / 8;  // channel vectors per deformable group
   for (int k = 0; k < a.K; ++k) {
     float omn[4][3];
-    if (k + 1 < a.K) load_om(k + 1, omn);
+    if (k + 2 < a.K) load_om(k + 2, omn);
     f32x4 acc[2][4];
 #pragma unroll
     for (int uu = 0; uu < 2; ++uu)
@@ -1179,7 +1181,10 @@ __global__ void __launch_bounds__(DC8_NT, 2) dcn_coord_dy8_kernel(DcnArgs a, con
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-        for (int e = 0; e < 3; ++e) om[cb][e] = omn[cb][e];
+        for (int e = 0; e < 3; ++e) {
+          om[cb][e] = om1[cb][e];
+          om1[cb][e] = omn[cb][e];
+        }
     }
   }
   for (int o = 32; o > 0; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o));
@@ -1262,10 +1267,16 @@ __global__ void __launch_bounds__(DW_NT, 2 * OCC) dcn_gradx_dy8_kernel(DcnArgs a
       o[1] = pv ? offn[(int64_t)(dgi * 2 * a.K + 2 * k + 1) * HWo64 + p] : 0.f;
       o[2] = pv ? (mskn ? mskn[(int64_t)(dgi * a.K + k) * HWo64 + p] : 1.f) : 0.f;
     };
-    u32x4 wa[2];
-    float om[3];
-    load_w(0, wa);
-    load_om(0, om);
+    // operands GX_PD taps ahead (a tap's work is ~0.3 us per wave, an HBM load several times that):
+    // slot d holds tap k + d; the slots shift down one per tap (register moves)
+    u32x4 wa[GX_PD][2];
+    float om[GX_PD][3];
+#pragma unroll
+    for (int d = 0; d < GX_PD; ++d)
+      if (d < a.K) {
+        load_w(d, wa[d]);
+        load_om(d, om[d]);
+      }
     for (int i = tid; i < RP * DX_ST; i += DW_NT) {
       if (FXB == 64) s_acc[i] = 0ull;
       else s_acc32[i] = 0u;
@@ -1274,24 +1285,24 @@ __global__ void __launch_bounds__(DW_NT, 2 * OCC) dcn_gradx_dy8_kernel(DcnArgs a
     for (int k = 0; k < a.K; ++k) {
       u32x4 wn[2];
       float omn[3];
-      if (k + 1 < a.K) {
-        load_w(k + 1, wn);
-        load_om(k + 1, omn);
+      if (k + GX_PD < a.K) {
+        load_w(k + GX_PD, wn);
+        load_om(k + GX_PD, omn);
       }
       f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-      mfma_bf16(wa[0], dyf[0][0], acc0);
-      mfma_bf16(wa[1], dyf[0][1], acc0);
-      mfma_bf16(wa[0], dyf[1][0], acc1);
-      mfma_bf16(wa[1], dyf[1][1], acc1);
+      mfma_bf16(wa[0][0], dyf[0][0], acc0);
+      mfma_bf16(wa[0][1], dyf[0][1], acc0);
+      mfma_bf16(wa[0][0], dyf[1][0], acc1);
+      mfma_bf16(wa[0][1], dyf[1][1], acc1);
       float dm[8];
       own8(acc0, acc1, g, dm);
       const int ti = k / a.kw, tj = k - ti * a.kw;
-      const float h = (float)(ho * a.sh - a.ph + ti * a.dh) + om[0];
-      const float w = (float)(wo * a.sw - a.pw + tj * a.dw) + om[1];
+      const float h = (float)(ho * a.sh - a.ph + ti * a.dh) + om[0][0];
+      const float w = (float)(wo * a.sw - a.pw + tj * a.dw) + om[0][1];
       const Sample s = make_sample(h, w, a.H, a.W);
       if (pv && s.valid) {
 #pragma unroll
-        for (int e2 = 0; e2 < 8; ++e2) dm[e2] *= om[2];
+        for (int e2 = 0; e2 < 8; ++e2) dm[e2] *= om[0][2];
         const int hl = (int)floorf(h), wl = (int)floorf(w);
         const float wt[4] = {s.hh * s.hw, s.hh * s.lw, s.lh * s.hw, s.lh * s.lw};
         const int oo[4] = {s.o1, s.o2, s.o3, s.o4};
@@ -1313,10 +1324,13 @@ __global__ void __launch_bounds__(DW_NT, 2 * OCC) dcn_gradx_dy8_kernel(DcnArgs a
           }
         }
       }
-      if (k + 1 < a.K) {
-        wa[0] = wn[0]; wa[1] = wn[1];
-        om[0] = omn[0]; om[1] = omn[1]; om[2] = omn[2];
+#pragma unroll
+      for (int d = 0; d + 1 < GX_PD; ++d) {
+        wa[d][0] = wa[d + 1][0]; wa[d][1] = wa[d + 1][1];
+        om[d][0] = om[d + 1][0]; om[d][1] = om[d + 1][1]; om[d][2] = om[d + 1][2];
       }
+      wa[GX_PD - 1][0] = wn[0]; wa[GX_PD - 1][1] = wn[1];
+      om[GX_PD - 1][0] = omn[0]; om[GX_PD - 1][1] = omn[1]; om[GX_PD - 1][2] = omn[2];
     }
     __syncthreads();
     for (int i = tid; i < RP * DX_CPP; i += DW_NT) {

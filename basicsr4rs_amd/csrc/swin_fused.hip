@@ -32,6 +32,7 @@
 #include "sr_internal.h"
 #include "swin_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -77,19 +78,26 @@ struct SabArgs {
   int nwx, nwin, nwin_total;
 };
 
-constexpr int SAB_X = 0;                      // [3 cg][128 rows][128 B]
-constexpr int SAB_W = SAB_X + 3 * 128 * 128;  // [3 cg][96 rows][128 B]
-constexpr int SAB_Q = SAB_W + 3 * 96 * 128;   // [128 tokens][64 B]
-constexpr int SAB_K = SAB_Q + 128 * 64;
-constexpr int SAB_V = SAB_K + 128 * 64;  // [2 windows][64][64 B], sx_byte layout (tr reads)
-constexpr int SAB_O = SAB_V + 128 * 64;  // [128 tokens][64 B]
-constexpr int SAB_TB = SAB_O + 128 * 64;  // float [225][nH <= 6]: the relative-position bias table
-constexpr int SAB_GB = SAB_TB + 5408;         // float [2][192]: LayerNorm gamma, beta (table padded to 16 B)
-constexpr int SAB_BQ = SAB_GB + 2 * 192 * 4;  // float [3 nH 32 <= 576]: qkv bias
-constexpr int SAB_BP = SAB_BQ + 576 * 4;      // float [192]: proj bias
-constexpr int SAB_LDS = SAB_BP + 192 * 4;
-constexpr int SAB_WPIECES = 96 * 24;  // 16-B pieces of W_h (K <= 192)
-constexpr int SAB_WREG = (SAB_WPIECES + 511) / 512;
+// LDS layout of a block of NW windows (TOK = 64 NW tokens, 256 NW threads).  O_h overlays Q_h: a
+// wave reads the Q rows of its own queries (step B) before it writes their O rows, and no other wave
+// reads them.  The bias table is staged one head column at a time (the next head's column is loaded
+// at the head's top, with its weights, and written after S2).
+template <int NW> struct SabL {
+  static constexpr int TOK = 64 * NW, NT = 256 * NW;
+  static constexpr int X = 0;                      // [3 cg][TOK rows][128 B]
+  static constexpr int W = X + 3 * TOK * 128;      // [3 cg][96 rows][128 B]
+  static constexpr int Q = W + 3 * 96 * 128;       // [TOK][64 B]; O_h overlays it
+  static constexpr int K = Q + TOK * 64;
+  static constexpr int V = K + TOK * 64;           // [NW windows][64][64 B], sx_byte layout (tr reads)
+  static constexpr int O = Q;
+  static constexpr int TB = V + TOK * 64;          // float [256]: this head's bias-table column
+  static constexpr int GB = TB + 256 * 4;          // float [2][192]: LayerNorm gamma, beta
+  static constexpr int BQ = GB + 2 * 192 * 4;      // float [3 nH 32 <= 576]: qkv bias
+  static constexpr int BP = BQ + 576 * 4;          // float [192]: proj bias
+  static constexpr int LDS = BP + 192 * 4;
+  static constexpr int WREG = (96 * 24 + NT - 1) / NT;  // 16-B pieces of W_h (K <= 192) per thread
+};
+constexpr int SAB_WPIECES = 96 * 24;
 
 // 16-B chunk ch of row r of a [cg][rows][128 B] image (chunk XOR row & 7 within its 128-B group)
 SR_DEV uint32_t tile_off(int rows, int r, int ch) {
@@ -100,8 +108,13 @@ SR_DEV uint32_t tile_off(int rows, int r, int ch) {
 SR_DEV uint32_t qk_off16(int t, int c) { return (uint32_t)(t * 64 + ((c ^ ((t >> 2) & 3)) << 4)); }
 SR_DEV uint32_t qk_off(int t, int d) { return qk_off16(t, d >> 3) + (uint32_t)((d & 7) * 2); }
 
-__global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[SAB_LDS];
+// NW windows per block: 2 (8 waves, one block per CU: 122 KB of LDS) or 1 (4 waves, 77.5 KB: two
+// independent blocks per CU, each one's barrier waits covered by the other's work)
+template <int NW>
+__global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(SabArgs a) {
+  using L = SabL<NW>;
+  constexpr int TOK = L::TOK, NT = L::NT;
+  __shared__ __attribute__((aligned(16))) char smem[L::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c16 = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
@@ -115,21 +128,21 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   const auto aor = make_rsrc(a.ao, train ? M * a.ldo * 2u : 0u);
   const auto lser = make_rsrc(a.lse, train ? (uint32_t)a.nwin_total * a.nH * 64u * 4u : 0u);
   const auto x2r = make_rsrc(a.x2, M * a.Cp * 2u);
-  float* sTB = (float*)(smem + SAB_TB);
-  float* sGB = (float*)(smem + SAB_GB);
-  float* sBQ = (float*)(smem + SAB_BQ);
-  float* sBP = (float*)(smem + SAB_BP);
+  float* sTB = (float*)(smem + L::TB);
+  float* sGB = (float*)(smem + L::GB);
+  float* sBQ = (float*)(smem + L::BQ);
+  float* sBP = (float*)(smem + L::BP);
 
-  // window geometry of the block's two windows
+  // window geometry of the block's windows
   auto win_of = [&](int wi, int& n, int& wy, int& wx) -> bool {
-    const int gw = 2 * blk + wi;
+    const int gw = NW * blk + wi;
     n = gw / a.nwin;
     const int win = gw - n * a.nwin;
     wy = win / a.nwx;
     wx = win - wy * a.nwx;
     return gw < a.nwin_total;
   };
-  // token t (0..127) of the block -> pixel row (through the cyclic shift), image; false past the end
+  // token t (0..TOK-1) of the block -> pixel row (through the cyclic shift), image; false past the end
   auto tok_pix = [&](int t, int64_t& pix, int& n) -> bool {
     int wy, wx;
     const bool v = win_of(t >> 6, n, wy, wx);
@@ -146,11 +159,12 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   // bookkeeping stays exact across them)
   const auto wqr = make_rsrc(a.wq, (uint32_t)((size_t)3 * a.nH * 32 * a.Cp * 2));
   const auto wpr = make_rsrc(a.wp, (uint32_t)((size_t)a.Cp * a.ldo * 2));
-  u32x4 wreg[SAB_WREG];
+  const auto tbr = make_rsrc(a.table, (uint32_t)(225 * a.nH * 4));
+  u32x4 wreg[L::WREG];
   auto w_load = [&](int h) {
 #pragma unroll
-    for (int k = 0; k < SAB_WREG; ++k) {
-      const int p = tid + 512 * k;
+    for (int k = 0; k < L::WREG; ++k) {
+      const int p = tid + NT * k;
       const int rr = p / 24, ch = p - rr * 24;
       const int grow = (rr >> 5) * a.nH * 32 + h * 32 + (rr & 31);
       wreg[k] = buf_load16(wqr, (p < SAB_WPIECES && ch < a.KC) ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB);
@@ -158,24 +172,24 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
   };
   auto w_store = [&]() {
 #pragma unroll
-    for (int k = 0; k < SAB_WREG; ++k) {
-      const int p = tid + 512 * k;
+    for (int k = 0; k < L::WREG; ++k) {
+      const int p = tid + NT * k;
       const int rr = p / 24, ch = p - rr * 24;
-      if (p < SAB_WPIECES) *(u32x4*)(smem + SAB_W + tile_off(96, rr, ch)) = wreg[k];
+      if (p < SAB_WPIECES) *(u32x4*)(smem + L::W + tile_off(96, rr, ch)) = wreg[k];
     }
   };
   w_load(0);
-  // every small operand (bias table, qkv / proj biases) into LDS before the first global store: on
-  // gfx9 vmcnt counts stores too, so a global load issued after stores makes its wait drain them
-  for (int i = tid; i < 225 * a.nH; i += 512) sTB[i] = a.table[i];
-  for (int i = tid; i < 3 * a.nH * 32; i += 512) sBQ[i] = a.bq[i];
+  // every small operand (bias table column, qkv / proj biases) into LDS before the first global store:
+  // on gfx9 vmcnt counts stores too, so a global load issued after stores makes its wait drain them
+  if (tid < 256) sTB[tid] = tid < 225 ? a.table[tid * a.nH] : 0.f;
+  for (int i = tid; i < 3 * a.nH * 32; i += NT) sBQ[i] = a.bq[i];
   if (tid < 192) sBP[tid] = tid < a.Cp ? a.bp[tid] : 0.f;
   if (tid < 192) {
     sGB[tid] = tid < a.C ? a.ln_g[tid] : 0.f;
     sGB[192 + tid] = tid < a.C ? a.ln_b[tid] : 0.f;
   }
 
-  // ---- 0. LayerNorm of the 128 token rows: 4 lanes per row, chunks part, part + 4, ...
+  // ---- 0. LayerNorm of the TOK token rows: 4 lanes per row, chunks part, part + 4, ...
   {
     const int r = tid >> 2, part = tid & 3;
     int64_t pr;
@@ -228,7 +242,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
       }
       buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(pr * a.Cp + ch * 8) * 2u : SR_OOB, o4);
-      *(u32x4*)(smem + SAB_X + tile_off(128, r, ch)) = o4;
+      *(u32x4*)(smem + L::X + tile_off(TOK, r, ch)) = o4;
     }
     buf_store4f(mur, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, mu);
     buf_store4f(rsr, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, rs);
@@ -283,6 +297,8 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       wpf[i] = buf_load16(wpr, row < a.Cp ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
     }
     if (h + 1 < a.nH) w_load(h + 1);
+    const float tbn = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+        tbr, (h + 1 < a.nH && tid < 225) ? (uint32_t)(tid * a.nH + h + 1) * 4u : SR_OOB, 0, 0));  // next column
     __builtin_amdgcn_sched_barrier(0);  // keep these loads here, ahead of the head's stores
 
     // ---- A: q / k / v of head h
@@ -296,9 +312,9 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       const int ch = 4 * kk + g;
       s16x8 af[3], bf[2];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) af[i] = *(const s16x8*)(smem + SAB_W + tile_off(96, og * 48 + 16 * i + c16, ch));
+      for (int i = 0; i < 3; ++i) af[i] = *(const s16x8*)(smem + L::W + tile_off(96, og * 48 + 16 * i + c16, ch));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = *(const s16x8*)(smem + SAB_X + tile_off(128, tg * 32 + 16 * j + c16, ch));
+      for (int j = 0; j < 2; ++j) bf[j] = *(const s16x8*)(smem + L::X + tile_off(TOK, tg * 32 + 16 * j + c16, ch));
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -318,7 +334,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         u.y = pack_bf16x2(acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]);
         buf_store8(qkvr, vA[j] ? (uint32_t)(pixA[j] * a.ldq + gr) * 2u : SR_OOB, u);
         const uint32_t qk = qk_off(t, d);
-        const uint32_t la = which == 0 ? SAB_Q + qk : which == 1 ? SAB_K + qk : SAB_V + (t >> 6) * 4096 + sx_byte(t & 63, d);
+        const uint32_t la = which == 0 ? L::Q + qk : which == 1 ? L::K + qk : L::V + (t >> 6) * 4096 + sx_byte(t & 63, d);
         *(uint2*)(smem + la) = u;
       }
     }
@@ -326,11 +342,11 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
 
     // ---- B: window attention, wave = (window wi, queries 16 jq ..)
     {
-      const s16x8 qf = *(const s16x8*)(smem + SAB_Q + qk_off16(wi * 64 + qq, g));
+      const s16x8 qf = *(const s16x8*)(smem + L::Q + qk_off16(wi * 64 + qq, g));
       f32x4 s[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const s16x8 kf = *(const s16x8*)(smem + SAB_K + qk_off16(wi * 64 + 16 * i + c16, g));
+        const s16x8 kf = *(const s16x8*)(smem + L::K + qk_off16(wi * 64 + 16 * i + c16, g));
         s[i] = mfma16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f});  // S^T[key 16i + 4g + r][query qq]
       }
       float mx = -3.0e38f;
@@ -339,7 +355,7 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int k = 16 * i + 4 * g + r;
-          float v = s[i][r] * a.scale + sTB[bin8(qq, k) * a.nH + h];
+          float v = s[i][r] * a.scale + sTB[bin8(qq, k)];
           if (a.shift && rk[i][r] != rq) v -= 100.f;
           s[i][r] = v;
           mx = fmaxf(mx, v);
@@ -362,9 +378,9 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[i][r] *= inv;
-      buf_store4f(lser, (vB && g == 0) ? (uint32_t)(((2 * blk + wi) * a.nH + h) * 64 + qq) * 4u : SR_OOB, mx + __logf(sm));
+      buf_store4f(lser, (vB && g == 0) ? (uint32_t)(((NW * blk + wi) * a.nH + h) * 64 + qq) * 4u : SR_OOB, mx + __logf(sm));
       f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-      const char* sVw = smem + SAB_V + wi * 4096;
+      const char* sVw = smem + L::V + wi * 4096;
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         const s16x8 pb = frag_c2(s[2 * st], s[2 * st + 1]);
@@ -377,16 +393,19 @@ __global__ __launch_bounds__(512, 1) void swin_attn_block_fwd_kernel(SabArgs a) 
         u.x = pack_bf16x2(o[d][0], o[d][1]);
         u.y = pack_bf16x2(o[d][2], o[d][3]);
         buf_store8(aor, vB ? (uint32_t)(pixB * a.ldo + h * 32 + 16 * d + 4 * g) * 2u : SR_OOB, u);
-        *(uint2*)(smem + SAB_O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
+        *(uint2*)(smem + L::O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
       }
     }
-    __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW)
-    if (h + 1 < a.nH) w_store();
+    __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW) and step B (sTB)
+    if (h + 1 < a.nH) {
+      w_store();
+      if (tid < 256) sTB[tid] = tbn;
+    }
 
     // ---- C: x2acc += Wp[:, head h] . O_h^T
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const s16x8 of = *(const s16x8*)(smem + SAB_O + qk_off16(ptg * 64 + 16 * j + c16, g));
+      const s16x8 of = *(const s16x8*)(smem + L::O + qk_off16(ptg * 64 + 16 * j + c16, g));
 #pragma unroll
       for (int i = 0; i < 3; ++i) xacc[i][j] = mfma16(__builtin_bit_cast(s16x8, wpf[i]), of, xacc[i][j]);
     }
@@ -718,6 +737,12 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   }
 }
 
+// Windows per block of the fused attention half: SR_SWIN_ATTN_NW=1 / 2 (A/B; read per call)
+int attn_nw() {
+  const char* e = getenv("SR_SWIN_ATTN_NW");
+  return e && atoi(e) == 1 ? 1 : 2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -750,8 +775,10 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
   a.ldq = 3 * nH * 32; a.ldo = nH * 32;
   a.eps = eps; a.scale = scale;
   a.nwx = W / 8; a.nwin = (H / 8) * (W / 8); a.nwin_total = N * a.nwin;
-  const int blocks = (a.nwin_total + 1) / 2;
-  hipLaunchKernelGGL(swin_attn_block_fwd_kernel, dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
+  if (attn_nw() == 1)
+    hipLaunchKernelGGL(swin_attn_block_fwd_kernel<1>, dim3(a.nwin_total), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(swin_attn_block_fwd_kernel<2>, dim3((a.nwin_total + 1) / 2), dim3(512), 0, (hipStream_t)stream, a);
   return sr_check(hipGetLastError(), "swin_attn_fused_fwd launch");
 }
 

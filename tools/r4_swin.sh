@@ -16,4 +16,5 @@ import sys,json; d=json.loads(sys.stdin.readline()); r=d['roofline'] or {}; k=r.
 top=sorted(k.items(), key=lambda kv:-kv[1]['ms_per_step'])[:7]
 print('$wl $tag', d['ms_per_step'], r.get('kernel'), r.get('frac'), d.get('swin_fused_attention'), [(n[:30], v['avg_us'], v['ms_per_step'], v.get('tflops')) for n,v in top])"
 }
-ab swinir fused X=1 && ab swinir unfused SR_SWIN_FUSED=0 && ab swinir fused2 X=1 && ab swinir unfused2 SR_SWIN_FUSED=0
+ab swinir nw2 X=1 && ab swinir nw1 SR_SWIN_ATTN_NW=1 && ab swinir unfused SR_SWIN_FUSED=0 && ab swinir nw2b X=1 && \
+  ab swinir nw1b SR_SWIN_ATTN_NW=1
