@@ -270,14 +270,19 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
   }
   const int qq = 16 * jq + c16;  // this lane's query (B)
   const int rq = region(wyB * 8 + (qq >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (qq & 7), a.W, 8, a.shift);
-  int rk[4][4];
+  // head-invariant parts of step B, once per block: the shift mask of this lane's 16 keys as bits, and
+  // the relative-position index bin8(qq, k) of key k = 16 i + 4 g + r, which is tbase - 30 i - r
+  // (k >> 3 = 2 i + (g >> 1), k & 7 = 4 (g & 1) + r), so the table reads take immediate offsets
+  unsigned mbits = 0u;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = 16 * i + 4 * g + r;
-      rk[i][r] = region(wyB * 8 + (k >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (k & 7), a.W, 8, a.shift);
+      const int rk = region(wyB * 8 + (k >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (k & 7), a.W, 8, a.shift);
+      if (a.shift && rk != rq) mbits |= 1u << (4 * i + r);
     }
+  const int tbase = ((qq >> 3) - (g >> 1) + 7) * 15 + (qq & 7) - 4 * (g & 1) + 7;
 
   f32x4 xacc[3][4];
 #pragma unroll
@@ -353,10 +358,9 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * i + 4 * g + r;
-          float v = s[i][r] * a.scale + sTB[bin8(qq, k)];
-          if (a.shift && rk[i][r] != rq) v -= 100.f;
+        for (int r = 0; r < 4; ++r) {  // key k = 16 i + 4 g + r
+          float v = s[i][r] * a.scale + (sTB + tbase - 93)[93 - 30 * i - r];  // = sTB[bin8(qq, k)]
+          if ((mbits >> (4 * i + r)) & 1u) v -= 100.f;
           s[i][r] = v;
           mx = fmaxf(mx, v);
         }
