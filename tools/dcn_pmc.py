@@ -44,9 +44,11 @@ def short(name):
 
 
 def collect(counter):
+    """Per kernel, the counter of each launch in launch order."""
     vals = {}
     for f in glob.glob(os.path.join(out, f'pmc_{counter}', '**', '*counter_collection.csv'), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r['Dispatch_Id']))
+        for r in rows:
             if r['Counter_Name'] != counter:
                 continue
             k = short(r['Kernel_Name'])
@@ -56,6 +58,17 @@ def collect(counter):
 
 
 fetch, write = collect('FETCH_SIZE'), collect('WRITE_SIZE')
+# the forward runs both without (inference: y only) and with the columns stored for the backward
+# (training: + 302 MB); the two passes launch in the same order, so split both by the WRITE size
+k = 'dcn_fwd_win_kernel'
+if k in write and k in fetch and len(write[k]) == len(fetch[k]):
+    tr = [w > 200e6 for w in write[k]]
+    for tag, sel in (('dcn_fwd_win_kernel (training: + columns)', True), ('dcn_fwd_win_kernel (inference)', False)):
+        fetch[tag] = [f for f, t in zip(fetch[k], tr) if t == sel]
+        write[tag] = [w for w, t in zip(write[k], tr) if t == sel]
+    del fetch[k], write[k]
+    ALG['dcn_fwd_win_kernel (training: + columns)'] = (ALG[k][0], ALG[k][1] + '; 302 MB of columns written')
+    ALG['dcn_fwd_win_kernel (inference)'] = ALG[k]
 res = {'config': 'C5 op: x[16,64,128,128] offset[16,144,128,128] mask[16,72,128,128] W[64,64,3,3] dg 8, bf16',
        'correction': __doc__.split('Corrections')[1].split('Usage')[0].strip()}
 for k, (alg, what) in ALG.items():
