@@ -56,6 +56,9 @@ SIGNATURES = {
     'sr_last_error': (ctypes.c_char_p, []),
     'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_linear_ln_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'sr_linear_ln_bwd_parts': (_i, [ctypes.POINTER(ConvDesc), _i]),
+    'sr_linear_ln_bwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp,
+                              _vp, _sz, _vp]),
     'sr_conv3x3_fwd_colsum_parts': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_fwd_dot_ok': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_get_variant': (_i, []),

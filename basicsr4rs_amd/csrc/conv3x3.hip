@@ -74,6 +74,16 @@ struct FwdArgs {
   const void* dot;  // band kernel, with colsum: partial sums of y * dot (sr_conv3x3_desc.dot)
   uint32_t d_bytes;
   int ldd, dcoff;
+  // LayerNorm backward fused into linear_wk_kernel's epilogue (sr_linear_ln_bwd): the GEMM output is
+  // dL/d(LN out); y receives dL/dx (+ res), lb_dxs the same times lb_rsc[image]
+  const void* lb_x;
+  int lb_ldx, lb_C;
+  const float* lb_mean;
+  const float* lb_rstd;
+  const float* lb_gamma;
+  float* lb_part;  // [2 * tiles][2][lb_C]: per (token tile, token half) dgamma / dbeta partials
+  void* lb_dxs;
+  const float* lb_rsc;
 };
 
 // alpha of output row m: a.alpha, times the per-image row_scale when given
@@ -1195,12 +1205,209 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // fc1 forward), 144 (residual + row scale); the bias
 // (GEMM column order), alpha and beta always.
 // ------------------------------------------------------------------------------------
+// LayerNorm backward over the rows linear_wk_kernel just produced (sr_linear_ln_bwd; the reference's
+// norm1 / norm2 autograd, swinir_arch.py:290, 322): with d = bf16(the GEMM output) = dL/d(LN out),
+// xh = (x - mean) rstd and g = d gamma over the C real channels,
+//   dx = rstd (g - mean_c(g) - xh mean_c(g xh)) (+ res),  dgamma += sum_m d xh,  dbeta += sum_m d
+// -- the ln_bwd8_kernel math on the same bf16-rounded d, so the result matches the two-launch path up
+// to fp32 summation order.  The block's one channel tile holds whole rows (Cout <= 192): a token's
+// row sums run over the lane's 24 channels, the 4 lanes of its g group (xor 16 / 32) and the two
+// channel-half waves (through LDS); the column partials over the lane's 4 tokens and the 16 lanes of
+// its c16 group (xor 1..8), one partial row per (token tile, token half).  x is read twice (the
+// second time from L2); dx overwrites nothing the GEMM still reads.
+// sum over the 16 lanes of a DPP row (every lane gets it): rotations by 1, 2, 4, 8 -- VALU DPP moves
+// instead of ds_bpermute (no LDS traffic, no address registers)
+SR_DEV float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
+  return v;
+}
+SR_DEV void lb_unpack8(const u32x4& q, float* o) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(q[i] << 16);
+    o[2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+  }
+}
+SR_DEV u32x4 lb_pack8(const float* v) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+  return r;
+}
+template <bool RES>
+SR_DEV void lnb_epilogue(const FwdArgs& a, const f32x4 (&acc)[6][4], char* smem, int m0, int wr, int wc, int g,
+                         int c16, int tt) {
+  const int C = a.lb_C;
+  const float invC = 1.f / (float)C;
+  const size_t xb = (size_t)a.M * a.lb_ldx * 2, yb = (size_t)a.M * a.ldy * 2;
+  const __amdgpu_buffer_rsrc_t lxr = make_rsrc(a.lb_x, xb < 0x80000000ull ? (uint32_t)xb : 0x7fffffffu);
+  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, yb < 0x80000000ull ? (uint32_t)yb : 0x7fffffffu);
+  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(a.lb_dxs, a.lb_dxs ? (yb < 0x80000000ull ? (uint32_t)yb : 0x7fffffffu) : 0u);
+  // every per-row / per-channel operand through buffer loads with the bound in the descriptor (and
+  // the partial stores through OOB offsets): no branches, so the epilogue stays one scheduling region
+  const __amdgpu_buffer_rsrc_t mur = make_rsrc(a.lb_mean, (uint32_t)a.M * 4u);
+  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(a.lb_rstd, (uint32_t)a.M * 4u);
+  const __amdgpu_buffer_rsrc_t scr = make_rsrc(a.lb_rsc, a.lb_rsc ? (fdiv((uint32_t)a.M - 1u, a.fd_hw) + 1u) * 4u : 0u);
+  const __amdgpu_buffer_rsrc_t gmr = make_rsrc(a.lb_gamma, (uint32_t)C * 4u);
+  const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.lb_part, (uint32_t)(gridDim.x * 2u * 2u * (uint32_t)C * 4u));
+  auto ld1 = [](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  };
+  float mu[4], rsd[4], sc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + wc * 64 + j * 16 + c16;
+    mu[j] = ld1(mur, (uint32_t)m * 4u);
+    rsd[j] = ld1(rsr, (uint32_t)m * 4u);
+    sc[j] = ld1(scr, fdiv((uint32_t)m, a.fd_hw) * 4u);
+  }
+  // d of (P, j): the GEMM output rounded to bf16 as the unfused path stores it, kept packed (48 VGPRs
+  // instead of the 96 accumulators: with both passes' operands live the fp32 form spilled)
+  u32x4 dpk[3][4];
+#pragma unroll
+  for (int P = 0; P < 3; ++P)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        dpk[P][j][r] = pack_bf16x2(acc[2 * P][j][2 * r] * a.alpha, acc[2 * P][j][2 * r + 1] * a.alpha);
+        dpk[P][j][2 + r] = pack_bf16x2(acc[2 * P + 1][j][2 * r] * a.alpha, acc[2 * P + 1][j][2 * r + 1] * a.alpha);
+      }
+  __builtin_amdgcn_sched_barrier(0);  // the accumulators die here
+  auto dval = [&](int P, int j, float (&d)[8]) { lb_unpack8(dpk[P][j], d); };
+  auto gam = [&](int n, float (&gm)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gm[q] = ld1(gmr, (uint32_t)(n + q) * 4u);
+  };
+  auto xoff = [&](int m, int n) -> uint32_t {
+    return (m < a.M && n < a.Cout) ? (uint32_t)(((size_t)m * a.lb_ldx + n) * 2) : SR_OOB;
+  };
+  // x and gamma of the three channel groups in one round trip (72 VGPRs beside the 48 of d; the
+  // residual follows after pass 1) -- issued per pass, the six dependent HBM round trips of a block
+  // ran serially at two waves per SIMD
+  u32x4 xv[3][4], rv[3][4];
+  float gm[3][8];
+#pragma unroll
+  for (int P = 0; P < 3; ++P) {
+    const int n = (3 * wr + P) * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[P][j] = buf_load16(lxr, xoff(m0 + wc * 64 + j * 16 + c16, n));
+    gam(n, gm[P]);
+  }
+  // pass 1: row sums s1 = sum g, s2 = sum g xh; the column partials, written per P
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int P = 0; P < 3; ++P) {
+    const int n = (3 * wr + P) * 32 + 8 * g;
+    float cg[8], cb[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cg[q] = cb[q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d[8], xf[8];
+      dval(P, j, d);
+      lb_unpack8(xv[P][j], xf);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xh = n + q < C ? (xf[q] - mu[j]) * rsd[j] : 0.f;
+        const float gq = d[q] * gm[P][q];
+        s1[j] += gq;
+        s2[j] += gq * xh;
+        cg[q] += d[q] * xh;
+        cb[q] += n + q < C ? d[q] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      cg[q] = row16_sum(cg[q]);
+      cb[q] = row16_sum(cb[q]);
+    }
+    const uint32_t pb = (uint32_t)((tt * 2 + wc) * 2 * C + n) * 4u;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const bool ok = c16 == 0 && n + q < C;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cg[q]), pr, ok ? pb + 4u * q : SR_OOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cb[q]), pr, ok ? pb + 4u * (C + q) : SR_OOB, 0, 0);
+    }
+  }
+  // the residual (pass 2 only) in flight across the row-sum exchange
+  if constexpr (RES) {
+#pragma unroll
+    for (int P = 0; P < 3; ++P) {
+      const int n = (3 * wr + P) * 32 + 8 * g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wc * 64 + j * 16 + c16;
+        rv[P][j] = buf_load16(rr, (m < a.M && n < a.Cout && n < a.rcols) ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s1[j] += __shfl_xor(s1[j], 16);
+    s1[j] += __shfl_xor(s1[j], 32);
+    s2[j] += __shfl_xor(s2[j], 16);
+    s2[j] += __shfl_xor(s2[j], 32);
+  }
+  // the other channel half's sums (both waves add the same two numbers: a + b == b + a)
+  float* red = (float*)smem;  // [2 wr][2 wc][4 j][16][2]
+  __syncthreads();             // every wave is past its last MFMA-operand read of the stages
+  if (g == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[((((wr * 2 + wc) * 4 + j) * 16 + c16) * 2)] = s1[j];
+      red[((((wr * 2 + wc) * 4 + j) * 16 + c16) * 2) + 1] = s2[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s1[j] = (s1[j] + red[(((((1 - wr) * 2 + wc) * 4 + j) * 16 + c16) * 2)]) * invC;
+    s2[j] = (s2[j] + red[(((((1 - wr) * 2 + wc) * 4 + j) * 16 + c16) * 2) + 1]) * invC;
+  }
+  // pass 2: dx = rstd (g - s1 - xh s2) (+ res), and its row-scaled copy
+#pragma unroll
+  for (int P = 0; P < 3; ++P) {
+    const int n = (3 * wr + P) * 32 + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wc * 64 + j * 16 + c16;
+      float d[8], xf[8], o[8];
+      dval(P, j, d);
+      lb_unpack8(xv[P][j], xf);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xh = (xf[q] - mu[j]) * rsd[j];
+        o[q] = n + q < C ? rsd[j] * (d[q] * gm[P][q] - s1[j] - xh * s2[j]) : 0.f;
+      }
+      if constexpr (RES) {
+        float rf[8];
+        lb_unpack8(rv[P][j], rf);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (n + q < C) o[q] += rf[q];
+      }
+      const uint32_t yo = (m < a.M && n < a.Cout) ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(lb_pack8(o), yr, yo, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] *= sc[j];
+      __builtin_amdgcn_raw_buffer_store_b128(lb_pack8(o), sr_, yo, 0, 0);  // size-0 descriptor without row scale
+    }
+  }
+}
+
 template <int E>
 __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   constexpr int XI = 128 * 128, WI = 192 * 128, STAGE = XI + WI;
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
-  constexpr bool RES = (E & 16) != 0, AUX = (E & 64) != 0, RSC = (E & 128) != 0;
-  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 64 | 128)) == 0, "linear_wk: epilogue subset");
+  constexpr bool RES = (E & 16) != 0, AUX = (E & 64) != 0, RSC = (E & 128) != 0, LNB = (E & 256) != 0;
+  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 64 | 128 | 256)) == 0, "linear_wk: epilogue subset");
+  static_assert(!LNB || (E & ~(16 | 256)) == 0, "linear_wk: the LayerNorm-backward epilogue takes a residual only");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1277,6 +1484,10 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
 
   // ---- epilogue: pair P (tiles 2P, 2P + 1) gives channels n = n0 + (3 wr + P) * 32 + 8g .. + 7 of
   // token m0 + 64 wc + 16 j + c16
+  if constexpr (LNB) {
+    lnb_epilogue<RES>(a, acc, smem, m0, wr, wc, g, c16, tt);
+    return;
+  }
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const size_t ybytes = (size_t)a.M * a.ldy * 2;
@@ -5657,6 +5868,49 @@ int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_ga
   }
 #undef SR_LNL
   return sr_check(hipGetLastError(), "linear_ln_fwd launch");
+}
+
+// sr_linear_ln_bwd: shapes it takes (0 otherwise) and the dgamma / dbeta partial rows it writes
+int sr_linear_ln_bwd_parts(const sr_conv3x3_desc* d, int ln_C) {
+  if (!d || d->dtype != SR_BF16 || d->ksize != 1 || d->N <= 0 || d->H <= 0 || d->W <= 0) return 0;
+  // ln_C % 4: the per-lane gamma reads merge into 16-B buffer loads, which the descriptor bound drops whole
+  if (d->Cin % 8 || d->Cout % 8 || d->Cout > 192 || ln_C <= 0 || ln_C % 4 || ln_C > d->Cout || d->ldy != d->Cout || d->ycoff)
+    return 0;
+  FwdArgs a = fwd_shape(d);
+  if (fwd_kind(a, true) != FK_LIN || !lin_use_wk(a)) return 0;
+  return 2 * ((a.M + 127) / 128);
+}
+
+int sr_linear_ln_bwd(const sr_conv3x3_desc* d, const void* dy, const void* wd, const void* x, int ldx,
+                     const float* mean, const float* rstd, const float* gamma, int ln_C, const void* res, int ldr,
+                     void* dx, const float* row_scale, void* dx_scaled, float* partial, size_t part_bytes,
+                     void* stream) {
+  const int nparts = sr_linear_ln_bwd_parts(d, ln_C);
+  if (nparts <= 0) return sr_fail(SR_EINVAL, "linear_ln_bwd: unsupported shape (query sr_linear_ln_bwd_parts)");
+  if (!dy || !wd || !x || !mean || !rstd || !gamma || !dx || !partial)
+    return sr_fail(SR_EINVAL, "linear_ln_bwd: null pointer");
+  if ((dx_scaled != nullptr) != (row_scale != nullptr))
+    return sr_fail(SR_EINVAL, "linear_ln_bwd: dx_scaled and row_scale go together");
+  if (ldx < d->Cout || ldx % 8 || (res && (ldr < d->Cout || ldr % 8)))
+    return sr_fail(SR_EINVAL, "linear_ln_bwd: x / res strides must be >= Cout and multiples of 8");
+  if (part_bytes < (size_t)nparts * 2 * ln_C * sizeof(float)) return sr_fail(SR_EINVAL, "linear_ln_bwd: partial too small");
+  FwdArgs a = fwd_shape(d);
+  const size_t xb = (size_t)a.M * d->ldx * 2, wb = (size_t)d->Cout * d->ldw * 2;
+  if (xb >= 0x80000000ull || wb >= 0x80000000ull || (size_t)a.M * ldx * 2 >= 0x80000000ull ||
+      (res && (size_t)a.M * ldr * 2 >= 0x80000000ull))
+    return sr_fail(SR_ETOOBIG, "linear_ln_bwd: tensor >= 2 GiB");
+  a.x = dy; a.w = wd; a.bias = nullptr; a.y = dx;
+  a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
+  a.res = res; a.ldr = ldr; a.rcoff = 0; a.rcols = d->Cout;
+  a.r_bytes = res ? (uint32_t)((size_t)a.M * ldr * 2) : 0u;
+  a.lb_x = x; a.lb_ldx = ldx; a.lb_C = ln_C; a.lb_mean = mean; a.lb_rstd = rstd; a.lb_gamma = gamma;
+  a.lb_part = partial; a.lb_dxs = dx_scaled; a.lb_rsc = row_scale;
+  a.fd_hw = make_fastdiv((uint32_t)(d->H * d->W));
+  const dim3 grid((unsigned)((a.M + 127) / 128));
+  hipStream_t s = (hipStream_t)stream;
+  if (res) hipLaunchKernelGGL(linear_wk_kernel<256 | 16>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(linear_wk_kernel<256>, grid, dim3(256), 0, s, a);
+  return sr_check(hipGetLastError(), "linear_ln_bwd launch");
 }
 
 // 1 when sr_conv3x3_fwd can fuse the dot partials (d->dot) into this conv with a residual operand:

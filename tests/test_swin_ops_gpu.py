@@ -122,6 +122,51 @@ def test_linear_ln_fused_vs_separate(cuda, which, shape):
         assert (aux.float() - aux_r.float()).abs().max().item() <= 2e-2 * max(1.0, aux_r.float().abs().max().item())
 
 
+@pytest.mark.parametrize('which', ['qkv', 'fc1'])
+@pytest.mark.parametrize('shape', [(2, 16, 16, 180, 6), (1, 7, 19, 180, 6), (3, 5, 13, 120, 4)])
+@pytest.mark.parametrize('rs', [False, True])
+def test_linear_ln_bwd_fused_vs_separate(cuda, which, shape, rs, monkeypatch):
+    """sr_linear_ln_bwd (the LayerNorm backward in the dgrad GEMM's epilogue) against the two-launch
+    path it replaces (linear_dgrad, then layernorm_bwd on its bf16 output): dx (+ residual), its
+    per-image row-scaled copy, dgamma / dbeta; ragged last token tile (M % 128 != 0) included."""
+    N, H, W, C_, nH = shape
+    torch.manual_seed(5)
+    dt = torch.bfloat16
+    Cp = (C_ + 7) // 8 * 8
+    x = torch.zeros(N, H, W, Cp, device=cuda)
+    x[..., :C_] = torch.randn(N, H, W, C_, device=cuda) * 2 + 0.5
+    x = x.to(dt)
+    g = torch.rand(C_, device=cuda) + 0.5
+    b = torch.randn(C_, device=cuda) * 0.1
+    _, mean, rstd = S.layernorm(x, g, b, C_)
+    if which == 'qkv':
+        spec = S.qkv_spec(C_, nH, 32)
+        lin = torch.nn.Linear(C_, 3 * C_).to(cuda)
+    else:
+        spec = S.plain_spec(C_, 2 * C_)
+        lin = torch.nn.Linear(C_, 2 * C_).to(cuda)
+    _, wd, _ = S.prepared_linear(lin.weight, lin.bias, spec, dt)
+    dy = (torch.randn(N, H, W, spec.cout_p, device=cuda) * 0.5).to(dt)
+    res = torch.zeros(N, H, W, Cp, device=cuda)
+    res[..., :C_] = torch.randn(N, H, W, C_, device=cuda)
+    res = res.to(dt)
+    scale = (torch.rand(N, device=cuda) + 0.5) if rs else None
+    monkeypatch.setenv('SR_LN_BWD_FUSED', '1')
+    got = S.linear_ln_bwd(dy, wd, spec, N, H, W, x, mean, rstd, g, C_, res=res, row_scale=scale)
+    assert got is not None, 'shape expected on the fused path'
+    dln = S.linear_dgrad(dy, wd, spec, N, H, W)
+    want = S.layernorm_bwd(dln, x, mean, rstd, g, C_, res=res, row_scale=scale)
+    torch.cuda.synchronize()
+    (dx, dg, db), (dx_r, dg_r, db_r) = got, want
+    pairs = list(zip(dx, dx_r)) if rs else [(dx, dx_r)]
+    for a, r in pairs:
+        a, r = a.float(), r.float()
+        assert (a[..., :C_] - r[..., :C_]).abs().max().item() <= 2e-2 * max(1.0, r.abs().max().item())
+        assert torch.equal(a[..., C_:], torch.zeros_like(a[..., C_:]))
+    assert (dg - dg_r).abs().max().item() <= 1e-2 * max(1.0, dg_r.abs().max().item())
+    assert (db - db_r).abs().max().item() <= 1e-2 * max(1.0, db_r.abs().max().item())
+
+
 @pytest.mark.parametrize('K,Cout', [(360, 184), (576, 184), (200, 96), (256, 304), (384, 40), (184, 184), (184, 360)])
 @pytest.mark.parametrize('epi', ['plain', 'res', 'res_rowscale', 'gate'])
 def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
