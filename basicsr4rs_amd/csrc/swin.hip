@@ -14,6 +14,8 @@
 // heads); out layout [nH][hdp].  bf16 with window 8 and hdp 32 (SwinIR-M/S/light) runs the
 // MFMA kernels; other shapes and the fp32 parity mode run the fp32-FMA kernels (one wave per
 // (image, window, head) unit, lane = query token).
+#include <cstdlib>
+
 #include "sr_common.h"
 #include "sr_internal.h"
 #include "swin_common.h"
@@ -670,6 +672,7 @@ __global__ __launch_bounds__(64) void wattn_fwd_mfma_kernel(AttnArgs a) {
 // base(g, c) + 30 (i - j) + r (bin8), so a lane touches 28 distinct bins: their biases are
 // read once and their dS contributions pre-summed in registers before the LDS adds.
 constexpr int ATT_UPW = 4;  // windows per backward wave
+constexpr int ATT_SLOTS_LANE = 28, ATT_SLOTS = 64 * ATT_SLOTS_LANE;  // per-lane bias-gradient slots
 SR_DEV int bin_base_qk(int g, int c) { return ((g >> 1) - (c >> 3) + 7) * 15 + 4 * (g & 1) - (c & 7) + 7; }
 
 __global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
@@ -887,6 +890,311 @@ __global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
   for (int b = lane; b < 225; b += 64) a.dbias_part[(int64_t)part * 225 + b] = sBin[b];
 }
 
+// The same backward at two waves per SIMD (round 4, default; SR_WATTN_BWD=1 selects the kernel
+// above, which holds a whole window's S / dP tiles, the next window's loads and the bias column in
+// 466 registers at one wave per SIMD, so nothing hides its dependent load -> MFMA -> exp -> MFMA
+// chain).  Here the queries go in two halves of 32 (the K-step of the dV / dK contractions): per
+// half, S and dP for its two 16-query tiles (64 registers), P and dS, the dV^T / dK^T MFMAs, then
+// dS^T of the half into a [64 keys][32 queries] LDS image and dQ of those 32 queries at once; K rows
+// and Q / dO rows come from the LDS images instead of registers, the bias column from LDS per use.
+// 16.2 KB of LDS and <= 256 registers: two 1-wave blocks per SIMD, one's loads under the other's
+// math.  Per element the same arithmetic in the same order as above (bit-identical dQ / dK / dV).
+template <int UPW, int DB>
+__global__ __launch_bounds__(64, 2) void wattn_bwd_mfma2_kernel(AttnArgs a) {
+  // [0, 4K) K image, [4K, 8K) Q, [8K, 12K) dO, [12K, 16K) dS^T of one query half
+  __shared__ __attribute__((aligned(16))) char smem[4 * 4096];
+  __shared__ __attribute__((aligned(16))) float sT[228], sD[64], sL[64];
+  char* sK = smem;
+  char* sQ = smem + 4096;
+  char* sdO = smem + 8192;
+  char* sdS = smem + 12288;
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, c = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int part = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int h = part % a.nH;
+  const int win0 = (part / a.nH) * UPW;
+  const int bb = bin_base_qk(g, c);
+  float dbs[7][4];
+#pragma unroll
+  for (int d = 0; d < 7; ++d)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dbs[d][r] = 0.f;
+  const bf16_t* qkv = (const bf16_t*)a.qkv;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (lane + 64 * k < 225) sT[lane + 64 * k] = a.bias_table[(lane + 64 * k) * a.nH + h];
+  for (int uw = 0; uw < UPW; ++uw) {
+    const int wg = win0 + uw;
+    if (wg >= a.N * a.nwin) break;
+    const int unit = wg * a.nH + h;
+    const int n = wg / a.nwin, win = wg - n * a.nwin;
+    const int wy = win / a.nwx, wx = win - (win / a.nwx) * a.nwx;
+    int64_t pix[4];
+    s16x8 vf[4];
+    {
+      u32x4 qu[4], ku[4], vu[4], du[4], ou[4];
+      f32x4 l4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pix[i] = token_pixel(a, n, wy, wx, 16 * i + c);
+        const bf16_t* row = qkv + pix[i] * a.ldq + g * 8;
+        qu[i] = *(const u32x4*)(row + h * 32);
+        ku[i] = *(const u32x4*)(row + (a.nH + h) * 32);
+        vu[i] = *(const u32x4*)(row + (2 * a.nH + h) * 32);
+        const int64_t orow = pix[i] * a.ldo + h * 32 + g * 8;
+        du[i] = *(const u32x4*)((const bf16_t*)a.dout + orow);
+        ou[i] = *(const u32x4*)((const bf16_t*)a.out + orow);
+        l4[i] = *(const f32x4*)(a.lse + (int64_t)unit * 64 + 16 * i + 4 * g);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        vf[i] = __builtin_bit_cast(s16x8, vu[i]);
+        *(u32x4*)(sQ + sx_off(16 * i + c, g)) = qu[i];
+        *(u32x4*)(sK + sx_off(16 * i + c, g)) = ku[i];
+        *(u32x4*)(sdO + sx_off(16 * i + c, g)) = du[i];
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          t += bf16_to_f32(du[i][e] & 0xffff) * bf16_to_f32(ou[i][e] & 0xffff) +
+               bf16_to_f32(du[i][e] >> 16) * bf16_to_f32(ou[i][e] >> 16);
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        if (g == 0) sD[16 * i + c] = t;
+        if (c == 0) *(f32x4*)(sL + 16 * i + 4 * g) = l4[i];
+      }
+    }
+    __syncthreads();
+    int rk[4];  // shift-mask region of key 16j + c
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      rk[j] = region(wy * 8 + 2 * j + (c >> 3), a.H, 8, a.shift) * 3 + region(wx * 8 + (c & 7), a.W, 8, a.shift);
+    f32x4 dv[2][4], dk[2][4];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dv[d][j] = dk[d][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16_t* gq = (bf16_t*)a.y;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      // S = Q K^T and dP = dO V^T for queries 16i + 4g + r (i = 2s, 2s + 1), keys 16j + c
+      f32x4 pa[2][4], ds[2][4];
+      {
+        s16x8 kf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kf[j] = __builtin_bit_cast(s16x8, *(const u32x4*)(sK + sx_off(16 * j + c, g)));
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int i = 2 * s + ii;
+          const s16x8 qf = __builtin_bit_cast(s16x8, *(const u32x4*)(sQ + sx_off(16 * i + c, g)));
+          const s16x8 df = __builtin_bit_cast(s16x8, *(const u32x4*)(sdO + sx_off(16 * i + c, g)));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pa[ii][j] = mfma16(qf, kf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+            ds[ii][j] = mfma16(df, vf[j], f32x4{0.f, 0.f, 0.f, 0.f});
+          }
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * s + ii;
+        const f32x4 lc = *(const f32x4*)(sL + 16 * i + 4 * g);
+        const f32x4 Dq = *(const f32x4*)(sD + 16 * i + 4 * g);
+        int rq[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          rq[r] = region(wy * 8 + 2 * i + (g >> 1), a.H, 8, a.shift) * 3 + region(wx * 8 + 4 * (g & 1) + r, a.W, 8, a.shift);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = pa[ii][j][r] * a.scale + sT[bb + 30 * (i - j) + r];
+            if (a.shift && rq[r] != rk[j]) v -= 100.f;
+            const float p = __expf(v - lc[r]);
+            const float dsv = p * (ds[ii][j][r] - Dq[r]);
+            pa[ii][j][r] = p;
+            ds[ii][j][r] = dsv;
+            dbs[i - j + 3][r] += dsv;
+          }
+      }
+      // dV^T += dO^T P and dK^T += Q^T dS over this half's 32 queries: [dim 16d + 4g + r][key 16j + c]
+      {
+        s16x8 at[2], qt[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          at[d] = frag_tr64(sdO, s, g, tq, tp, 16 * d);
+          qt[d] = frag_tr64(sQ, s, g, tq, tp, 16 * d);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const s16x8 pb = frag_c2(pa[0][j], pa[1][j]);
+          const s16x8 sb = frag_c2(ds[0][j], ds[1][j]);
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            dv[d][j] = mfma16(at[d], pb, dv[d][j]);
+            dk[d][j] = mfma16(qt[d], sb, dk[d][j]);
+          }
+        }
+      }
+      // dS^T of this half: [key 16j + c][query 16 ii + 4g .. + 3] (bf16, as the one-wave kernel)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint2 w2;
+          w2.x = pack_bf16x2(ds[ii][j][0], ds[ii][j][1]);
+          w2.y = pack_bf16x2(ds[ii][j][2], ds[ii][j][3]);
+          *(uint2*)(sdS + sx_byte(16 * j + c, 16 * ii + 4 * g)) = w2;
+        }
+      __syncthreads();
+      // dQ^T = K^T dS^T for queries 32s + 16jj + c: [dim 16d + 4g + r], keys in two K-steps
+      f32x4 dq[2][2];
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) dq[d][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s16x8 kt[2];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) kt[d] = frag_tr64(sK, ks, g, tq, tp, 16 * d);
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const s16x8 sb = frag_tr64(sdS, ks, g, tq, tp, 16 * jj);
+#pragma unroll
+          for (int d = 0; d < 2; ++d) dq[d][jj] = mfma16(kt[d], sb, dq[d][jj]);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        bf16_t* row = gq + pix[2 * s + jj] * a.ldq + 4 * g;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          uint2 w;
+          w.x = pack_bf16x2(dq[d][jj][0] * a.scale, dq[d][jj][1] * a.scale);
+          w.y = pack_bf16x2(dq[d][jj][2] * a.scale, dq[d][jj][3] * a.scale);
+          *(uint2*)(row + h * 32 + 16 * d) = w;
+        }
+      }
+      __syncthreads();  // dS^T image read: free for the next half
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16_t* row = gq + pix[j] * a.ldq + 4 * g;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        uint2 w;
+        w.x = pack_bf16x2(dk[d][j][0] * a.scale, dk[d][j][1] * a.scale);
+        w.y = pack_bf16x2(dk[d][j][2] * a.scale, dk[d][j][3] * a.scale);
+        *(uint2*)(row + (a.nH + h) * 32 + 16 * d) = w;
+        w.x = pack_bf16x2(dv[d][j][0], dv[d][j][1]);
+        w.y = pack_bf16x2(dv[d][j][2], dv[d][j][3]);
+        *(uint2*)(row + (2 * a.nH + h) * 32 + 16 * d) = w;
+      }
+    }
+    __syncthreads();  // LDS images free for the next window
+  }
+  if constexpr (DB == 2) {
+    // the lane's 28 pre-summed bias gradients as they are (one 1792-float slot row per wave, folded
+    // into the 225 bins by wattn_dbias_slots / _fold in a fixed order): gfx950's fp32 LDS atomics
+    // cost more than the rest of a wave's tail
+    f32x4* dst = (f32x4*)(a.dbias_part + ((int64_t)part * 64 + lane) * ATT_SLOTS_LANE);
+#pragma unroll
+    for (int d = 0; d < 7; ++d) dst[d] = f32x4{dbs[d][0], dbs[d][1], dbs[d][2], dbs[d][3]};
+  } else {
+    float* sBin = (float*)smem;  // over the K image: 225 bins
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane + 64 * k < 225) sBin[lane + 64 * k] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < 7; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(&sBin[bb + 30 * (d - 3) + r], dbs[d][r]);
+    __syncthreads();
+    for (int b = lane; b < 225; b += 64) a.dbias_part[(int64_t)part * 225 + b] = sBin[b];
+  }
+}
+
+// slot rows (DB 2): stage 1 sums each head's rows per slot (block = head x 64 slots, 16 waves over
+// the rows, fixed-order LDS combine); stage 2 folds a head's 1792 slots into its 225 bins: bin b
+// takes slot (lane, d, r) when bin_base_qk(lane) + 30 (d - 3) + r == b, enumerated in a fixed order
+__global__ __launch_bounds__(1024) void wattn_dbias_slots(const float* __restrict__ part, int parts, int nH,
+                                                          float* __restrict__ slots) {
+  __shared__ float red[16][65];
+  const int h = blockIdx.x % nH, chunk = blockIdx.x / nH;
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sl = chunk * 64 + l;
+  float sm = 0.f;
+  for (int p = h + wv * nH; p < parts; p += 16 * nH) sm += part[(int64_t)p * ATT_SLOTS + sl];
+  red[wv][l] = sm;
+  __syncthreads();
+  if (wv == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][l];
+    slots[h * ATT_SLOTS + sl] = t;
+  }
+}
+__global__ __launch_bounds__(256) void wattn_dbias_fold(const float* __restrict__ slots, int nH,
+                                                        float* __restrict__ dbias, int acc) {
+  const int h = blockIdx.x, b = threadIdx.x;
+  if (b >= 225) return;
+  const float* sh = slots + h * ATT_SLOTS;
+  float t = 0.f;
+  for (int d = 0; d < 7; ++d)
+    for (int r = 0; r < 4; ++r) {
+      const int q = b - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
+      if (q < 0 || q >= 225) continue;
+      const int dyp = q / 15, dxp = q - 15 * dyp;  // (g >> 1) - (c >> 3) + 7, 4 (g & 1) - (c & 7) + 7
+      if (dyp < 6 || dyp > 8 || dxp > 11) continue;
+      for (int gh = 0; gh < 2; ++gh) {
+        const int ch = gh - (dyp - 7);
+        if (ch < 0 || ch > 1) continue;
+        for (int g1 = 0; g1 < 2; ++g1) {
+          const int c7 = 4 * g1 - (dxp - 7);
+          if (c7 < 0 || c7 > 7) continue;
+          t += sh[((2 * gh + g1) * 16 + 8 * ch + c7) * ATT_SLOTS_LANE + 4 * d + r];
+        }
+      }
+    }
+  dbias[b * nH + h] = (acc ? dbias[b * nH + h] : 0.f) + t;
+}
+
+__global__ void wattn_dbias_reduce2(const float* __restrict__ part, int units, int nH, int nbins,
+                                    float* __restrict__ dbias, int acc);
+// the table gradient from the partial rows: parts > 0 rows of nbins, parts < 0 -parts slot rows
+// (stage-1 sums after them in the workspace)
+void dbias_reduce(const float* ws, int parts, int nH, int nbins, float* dbias, int acc, hipStream_t s) {
+  if (parts > 0) {
+    hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((nbins + 63) / 64)), dim3(1024), 0, s, ws, parts, nH, nbins,
+                       dbias, acc);
+    return;
+  }
+  float* slots = const_cast<float*>(ws) + (int64_t)(-parts) * ATT_SLOTS;
+  hipLaunchKernelGGL(wattn_dbias_slots, dim3(nH * (ATT_SLOTS / 64)), dim3(1024), 0, s, ws, -parts, nH, slots);
+  hipLaunchKernelGGL(wattn_dbias_fold, dim3(nH), dim3(256), 0, s, (const float*)slots, nH, dbias, acc);
+}
+
+// SR_WATTN_BWD=1: the one-wave-per-SIMD backward (A/B and parity reference); read per call
+bool attn_bwd_v1() {
+  const char* e = getenv("SR_WATTN_BWD");
+  return e && e[0] == '1';
+}
+// the two-wave kernel's bias gradient: per-lane slot rows (default) or SR_WATTN_DBIAS=atomic
+bool attn_dbias_slots() {
+  if (attn_bwd_v1()) return false;
+  const char* e = getenv("SR_WATTN_DBIAS");
+  return !(e && e[0] == 'a');
+}
+// windows per wave of the two-wave kernel (SR_WATTN_UPW 1 / 2 / 4, read per call): the dbias
+// partial rows are per (head, group of UPW windows)
+int attn_bwd_upw() {
+  if (attn_bwd_v1()) return ATT_UPW;
+  const char* e = getenv("SR_WATTN_UPW");
+  const int u = e ? atoi(e) : 4;
+  return (u == 1 || u == 2 || u == 4) ? u : 4;
+}
+
 bool attn_mfma_ok(const AttnArgs& a, int dtype) {
   return dtype == SR_BF16 && a.ws == 8 && a.hdp == 32 && a.ldq % 8 == 0 && a.ldo % 8 == 0;
 }
@@ -1071,7 +1379,9 @@ int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W,
 
 size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH) {
   const int nb = (2 * ws - 1) * (2 * ws - 1);
-  return (size_t)N * (H / ws) * (W / ws) * nH * nb * sizeof(float);
+  const size_t units = (size_t)N * (H / ws) * (W / ws) * nH;
+  const size_t rows = units * nb, slots = ws == 8 ? (units + nH) * ATT_SLOTS : 0;  // slot rows at 1 window per wave
+  return (rows > slots ? rows : slots) * sizeof(float);
 }
 
 int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, const void* dout, int ldo, const float* lse,
@@ -1087,17 +1397,26 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
   a.dbias_part = (float*)workspace; a.ldq = ldq; a.ldo = ldo;
   hipStream_t s = (hipStream_t)stream;
   int parts = a.units;  // dbias partial rows, interleaved by head (row % nH == head)
+  bool slot_rows = false;
   if (attn_mfma_ok(a, dtype)) {
-    parts = nH * ((N * a.nwin + ATT_UPW - 1) / ATT_UPW);
-    hipLaunchKernelGGL(wattn_bwd_mfma_kernel, dim3(parts), dim3(64), 0, s, a);
+    const int upw = attn_bwd_upw();
+    parts = nH * ((N * a.nwin + upw - 1) / upw);
+    const bool sl = attn_dbias_slots();
+    slot_rows = sl;
+    if (attn_bwd_v1()) hipLaunchKernelGGL(wattn_bwd_mfma_kernel, dim3(parts), dim3(64), 0, s, a);
+    else if (sl && upw == 1) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<1, 2>), dim3(parts), dim3(64), 0, s, a);
+    else if (sl && upw == 2) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<2, 2>), dim3(parts), dim3(64), 0, s, a);
+    else if (sl) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<4, 2>), dim3(parts), dim3(64), 0, s, a);
+    else if (upw == 1) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<1, 0>), dim3(parts), dim3(64), 0, s, a);
+    else if (upw == 2) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<2, 0>), dim3(parts), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<4, 0>), dim3(parts), dim3(64), 0, s, a);
   } else if (dtype == SR_BF16) {
     hipLaunchKernelGGL(wattn_bwd_kernel<bf16_t>, dim3(a.units), dim3(64), 0, s, a);
   } else {
     hipLaunchKernelGGL(wattn_bwd_kernel<float>, dim3(a.units), dim3(64), 0, s, a);
   }
   if (!(accumulate & 2))  // bit 1: partials only (sr_window_attn_dbias_reduce later)
-    hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((a.nbins + 63) / 64)), dim3(1024), 0, s,
-                       (const float*)workspace, parts, nH, a.nbins, dbias_table, accumulate & 1);
+    dbias_reduce((const float*)workspace, slot_rows ? -parts : parts, nH, a.nbins, dbias_table, accumulate & 1, s);
   return sr_check(hipGetLastError(), "window_attn_bwd launch");
 }
 
@@ -1106,16 +1425,18 @@ int sr_window_attn_bwd_parts(int dtype, int N, int H, int W, int ws, int nH, int
   AttnArgs a{};
   if (!attn_setup(a, N, H, W, ws, 0, nH, hd, hdp, 1.f)) return 0;
   a.ldq = ldq; a.ldo = ldo;
-  return attn_mfma_ok(a, dtype) ? nH * ((N * a.nwin + ATT_UPW - 1) / ATT_UPW) : a.units;
+  const int upw = attn_bwd_upw();
+  if (!attn_mfma_ok(a, dtype)) return a.units;
+  const int parts = nH * ((N * a.nwin + upw - 1) / upw);
+  return attn_dbias_slots() ? -parts : parts;  // negative: slot rows (see sr_hip.h)
 }
 
 int sr_window_attn_dbias_reduce(const float* workspace, int parts, int nH, int ws, float* dbias_table, int accumulate,
                                 void* stream) {
   const int nbins = (2 * ws - 1) * (2 * ws - 1);
-  if (!workspace || !dbias_table || parts <= 0 || nH <= 0 || ws <= 0)
+  if (!workspace || !dbias_table || parts == 0 || nH <= 0 || ws <= 0 || (parts < 0 && ws != 8))
     return sr_fail(SR_EINVAL, "window_attn_dbias_reduce: bad arguments");
-  hipLaunchKernelGGL(wattn_dbias_reduce2, dim3(nH * ((nbins + 63) / 64)), dim3(1024), 0, (hipStream_t)stream, workspace,
-                     parts, nH, nbins, dbias_table, accumulate & 1);
+  dbias_reduce(workspace, parts, nH, nbins, dbias_table, accumulate & 1, (hipStream_t)stream);
   return sr_check(hipGetLastError(), "window_attn_dbias_reduce launch");
 }
 

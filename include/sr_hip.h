@@ -375,7 +375,9 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
                        float scale, const float* bias_table, void* dqkv, float* dbias_table, void* workspace,
                        size_t ws_bytes, int accumulate, void* stream);
 /* accumulate bit 1 of sr_window_attn_bwd: the relative-bias gradient partial rows (count:
- * sr_window_attn_bwd_parts) stay in the workspace for sr_window_attn_dbias_reduce. */
+ * sr_window_attn_bwd_parts) stay in the workspace for sr_window_attn_dbias_reduce.  A negative
+ * count -P means P per-lane slot rows (the two-wave MFMA backward: 64 lanes x 28 pre-summed bins
+ * per row, folded into the (2ws-1)^2 bins by the reduce); pass it through unchanged. */
 int sr_window_attn_bwd_parts(int dtype, int N, int H, int W, int ws, int nH, int hd, int hdp, int ldq, int ldo);
 int sr_window_attn_dbias_reduce(const float* workspace, int parts, int nH, int ws, float* dbias_table, int accumulate,
                                 void* stream);

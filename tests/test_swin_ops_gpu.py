@@ -82,6 +82,56 @@ def test_window_attention_fwd_bwd(cuda, shift, dtype, geom):
     assert (dtab.double().cpu() - td.grad).abs().max().item() < tol * max(1.0, td.grad.abs().max().item())
 
 
+@pytest.mark.parametrize('shift', [0, 4])
+@pytest.mark.parametrize('geom', [(2, 16, 24, 6, 30), (3, 8, 40, 3, 32), (1, 24, 24, 2, 16)])
+@pytest.mark.parametrize('upw,dbias', [('4', 'slots'), ('4', 'atomic'), ('2', 'slots'), ('1', 'slots'), ('1', 'atomic')])
+def test_window_attention_bwd_two_wave_bitwise(cuda, shift, geom, upw, dbias, monkeypatch):
+    """The two-waves-per-SIMD MFMA backward (wattn_bwd_mfma2_kernel, default) against the one-wave
+    kernel it replaced (SR_WATTN_BWD=1): the same products summed in the same order, so dqkv is
+    bitwise equal; the table gradient is bitwise equal with the same LDS-atomic bin sums at the
+    same 4 windows per wave, and equal to fp32 rounding with the per-lane slot rows (fixed-order
+    fold) or other window counts per wave; window counts not a multiple of the windows per wave;
+    both through the fused reduce and the deferred one (sr_window_attn_dbias_reduce)."""
+    monkeypatch.setenv('SR_WATTN_UPW', upw)
+    monkeypatch.setenv('SR_WATTN_DBIAS', dbias)
+    b, h, w, nH, hd = geom
+    torch.manual_seed(7)
+    C = nH * hd
+    g = S.AttnGeom(C, nH, 8, shift, 32)
+    qkv = _qkv_padded(torch.randn(b, h, w, 3 * C), nH, hd, 32).to(torch.bfloat16).to(cuda).contiguous()
+    table = (torch.randn(225, nH) * 0.5).to(cuda)
+    dout = F.pad(torch.randn(b, h, w, nH, hd), (0, 32 - hd)).reshape(b, h, w, nH * 32).to(torch.bfloat16)
+    dout = dout.to(cuda).contiguous()
+    scale = hd**-0.5
+    out, lse = S.window_attn(qkv, g, b, h, w, scale, table)
+    res = {}
+    for v in ('1', '2'):
+        monkeypatch.setenv('SR_WATTN_BWD', v)
+        res[v] = S.window_attn_bwd(qkv, out, dout, lse, g, b, h, w, scale, table)
+    torch.cuda.synchronize()
+    # the deferred reduce (side-stream path): partial rows left in the workspace, reduced later
+    from basicsr4rs_amd import _lib
+    lib = _lib.load()
+    wsb = lib.sr_window_attn_bwd_workspace(b, h, w, 8, nH)
+    ws = torch.empty(wsb // 4 + 1, device=cuda, dtype=torch.float32)
+    dq2, dt2 = torch.empty_like(qkv), torch.zeros_like(table)
+    _lib.check(lib.sr_window_attn_bwd(_lib.dtype_code(qkv.dtype), _lib.ptr(qkv), qkv.shape[-1], _lib.ptr(out),
+                                      _lib.ptr(dout), out.shape[-1], _lib.ptr(lse), b, h, w, 8, shift, nH, hd, 32,
+                                      float(scale), _lib.ptr(table), _lib.ptr(dq2), _lib.ptr(dt2), _lib.ptr(ws), wsb, 2,
+                                      _lib.stream()))
+    parts = lib.sr_window_attn_bwd_parts(_lib.dtype_code(qkv.dtype), b, h, w, 8, nH, hd, 32, qkv.shape[-1],
+                                         out.shape[-1])
+    assert (parts < 0) == (dbias == 'slots')
+    _lib.check(lib.sr_window_attn_dbias_reduce(_lib.ptr(ws), parts, nH, 8, _lib.ptr(dt2), 1, _lib.stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(res['1'][0], res['2'][0]) and torch.equal(dq2, res['2'][0])
+    assert torch.equal(dt2, res['2'][1])
+    if upw == '4' and dbias == 'atomic':
+        assert torch.equal(res['1'][1], res['2'][1])
+    else:
+        assert torch.allclose(res['1'][1], res['2'][1], rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize('which', ['qkv', 'fc1'])
 @pytest.mark.parametrize('shape', [(2, 16, 16, 180, 6), (1, 8, 24, 60, 6), (3, 5, 13, 96, 3)])
 def test_linear_ln_fused_vs_separate(cuda, which, shape):
