@@ -146,6 +146,13 @@ class _RCAB(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        # the block's three side-stream launches (squeeze-conv gradients, both conv weight
+        # gradients) forked once, after conv1's dgrad (ops.conv.side_batch)
+        with C.side_batch():
+            return _RCAB._backward_body(ctx, dy)
+
+    @staticmethod
+    def _backward_body(ctx, dy):
         x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2 = ctx.saved_tensors
         spec1, spec2 = ctx.specs
         rs = ctx.rs
@@ -189,16 +196,13 @@ class _RCAB(torch.autograd.Function):
                 _lib.ptr(dA2), _lib.ptr(dab2), int(direct))
         side = C.async_side_stream(x.device) if direct else None
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream(x.device))
-            for t_ in (dz2, dz1, h, pool):
-                t_.record_stream(side)
-            with torch.cuda.stream(side):
-                _lib.check(lib.sr_ca_param_grad(*args, _lib.stream()))
+            C.side_launch(side, lambda: _lib.check(lib.sr_ca_param_grad(*args, _lib.stream())), (dz2, dz1, h, pool),
+                          after=tuple((lambda p=p: C.grad_ready(p)) for p in ca))
         else:
             _lib.check(lib.sr_ca_param_grad(*args, _lib.stream()))
-        if direct:
-            for p in ca:
-                C.grad_ready(p)
+            if direct:
+                for p in ca:
+                    C.grad_ready(p)
         _, wd1, _ = C.prepared(w1, b1, spec1, dtype)
         _, wd2, _ = C.prepared(w2, b2, spec2, dtype)
         dz1 = torch.empty_like(t)

@@ -228,12 +228,11 @@ def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None, row_s
                                      _lib.stream()))
     if row_scale is not None:
         dx = (dx, scaled if scaled is not None else row_scale_(dx, row_scale, H * W))
-    if side is not None:
-        side.wait_stream(torch.cuda.current_stream(x.device))
-        ws.record_stream(side)
-        with torch.cuda.stream(side):
-            _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg), _lib.ptr(db), 1,
-                                                   _lib.stream()))
+    if side is not None:  # (direct is not None): the gradient-ready callbacks follow the reduce
+        C.side_launch(side, lambda: _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg),
+                                                                           _lib.ptr(db), 1, _lib.stream())), (ws,),
+                      after=tuple((lambda p=p: C.grad_ready(p)) for p in params))
+        return dx, None, None
     if direct is not None:
         for p in params:
             C.grad_ready(p)
@@ -282,14 +281,12 @@ def linear_ln_bwd(dy, wd, spec, N, H, W, x, mean, rstd, weight, Creal, res=None,
     # the dgamma / dbeta reduce on the weight-gradient side stream, as layernorm_bwd
     side = C.async_side_stream(x.device) if direct is not None and not ktrace.active() and _PARAM_REDUCE_SIDE else None
     if side is not None:
-        side.wait_stream(torch.cuda.current_stream(x.device))
-        ws.record_stream(side)
-        with torch.cuda.stream(side):
-            _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg), _lib.ptr(db), 1,
-                                                   _lib.stream()))
-    else:
-        _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg), _lib.ptr(db),
-                                               int(direct is not None), _lib.stream()))
+        C.side_launch(side, lambda: _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg),
+                                                                           _lib.ptr(db), 1, _lib.stream())), (ws,),
+                      after=tuple((lambda p=p: C.grad_ready(p)) for p in params))
+        return dx, None, None
+    _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg), _lib.ptr(db),
+                                           int(direct is not None), _lib.stream()))
     if direct is not None:
         for p in params:
             C.grad_ready(p)
@@ -366,11 +363,10 @@ def window_attn_bwd(qkv, out, dout, lse, g, N, H, W, scale, table, table_param=N
     if side is not None:
         parts = lib.sr_window_attn_bwd_parts(_lib.dtype_code(qkv.dtype), N, H, W, g.ws, g.nH, g.hd, g.hdp, qkv.shape[-1],
                                              out.shape[-1])
-        side.wait_stream(torch.cuda.current_stream(qkv.device))
-        ws.record_stream(side)
-        with torch.cuda.stream(side):
-            _lib.check(lib.sr_window_attn_dbias_reduce(_lib.ptr(ws), parts, g.nH, g.ws, _lib.ptr(dtable), 1,
-                                                       _lib.stream()))
+        C.side_launch(side, lambda: _lib.check(lib.sr_window_attn_dbias_reduce(_lib.ptr(ws), parts, g.nH, g.ws,
+                                                                               _lib.ptr(dtable), 1, _lib.stream())),
+                      (ws,), after=(lambda: C.grad_ready(table_param),))
+        return dqkv, None
     if direct is not None:
         C.grad_ready(table_param)
         return dqkv, None
@@ -448,6 +444,9 @@ def swin_mlp_fused(x, n2w, n2b, Creal, f1wf, f1bg, fc1s, f2wf, f2bg, s2, train):
     return out, ln2, m2, r2, z, h
 
 
+_STB_SIDE_BATCH = os.environ.get('SR_STB_SIDE_BATCH', '1') != '0'
+
+
 class _STB(torch.autograd.Function):
 
     @staticmethod
@@ -494,6 +493,13 @@ class _STB(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        if _STB_SIDE_BATCH:  # the block's side-stream launches forked once, at its end (ops.conv.side_batch)
+            with C.side_batch():
+                return _STB._backward_body(ctx, dout)
+        return _STB._backward_body(ctx, dout)
+
+    @staticmethod
+    def _backward_body(ctx, dout):
         (x, ln1, m1, r1, qkv, a, lse, x2, ln2, m2, r2, z, h, tab, n1w, qw, qb, pw, pb, n2w, f1w, f1b, f2w,
          f2b, n1b, n2b, table) = ctx.saved_tensors
         g, fc1s, fc2s, scale = ctx.geom, ctx.fc1s, ctx.fc2s, ctx.scale
