@@ -20,7 +20,7 @@ from ..losses import build_loss
 from ..metrics import calculate_metric
 import os
 
-from ..ops.conv import async_wgrad, bump_param_epoch, take_captured_tables
+from ..ops.conv import async_wgrad, bump_param_epoch, set_side_batch, take_captured_tables
 from ..utils.flat import FlatParams
 from ..utils.img_util import imwrite, tensor2img
 from ..utils.logger import get_root_logger
@@ -74,6 +74,9 @@ class SRModel(BaseModel):
                 get_root_logger().warning(f'train.async_wgrad disabled: {world} ranks share '
                                           f'{torch.cuda.device_count()} GPU(s)')
                 self.async_wgrad = False
+        # blocks whose side-stream launches share one fork (train.async_wgrad_blocks, ops.conv.side_batch;
+        # SR_SIDE_BATCH overrides)
+        set_side_batch(int(os.environ.get('SR_SIDE_BATCH', train_opt.get('async_wgrad_blocks', 1))))
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)

@@ -319,6 +319,11 @@ class _RRDB(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        with C.side_batch():  # with side-stream weight gradients: one fork per RRDB (ops.conv.side_batch)
+            return _RRDB._backward_body(ctx, dout)
+
+    @staticmethod
+    def _backward_body(ctx, dout):
         saved = ctx.saved_tensors
         x, bufs, params = saved[0], saved[1:4], saved[4:]
         nf, gc, specs = ctx.nf, ctx.gc, ctx.specs

@@ -84,6 +84,7 @@ class async_wgrad:
 
     def __exit__(self, *exc):
         if self.enabled:
+            side_flush_pending()  # launches still queued by side_batch fork before the join
             _ASYNC['depth'] -= 1
             _ASYNC['mode'] = self._prev_mode  # a nested context must not leak its mode outward
             for st in _ASYNC['streams'].values():
@@ -97,24 +98,49 @@ class async_wgrad:
 # the current stream ONCE at exit (one event wait for all of them instead of one per launch).  A
 # captured step turns every fork into a cross-queue graph edge, and RCAN's 2.5 k-node step spent
 # ~2.6 us per node between short kernels; SR_SIDE_BATCH=0 forks per launch (A/B).
+# SR_SIDE_BATCH=k > 1 forks once per k blocks (the queue is flushed at the latest by the join).
 _SIDE_BATCH = []
-_SIDE_BATCH_ON = os.environ.get('SR_SIDE_BATCH', '1') != '0'
+_SIDE_BATCH_K = max(0, int(os.environ.get('SR_SIDE_BATCH', '1')))
+_SIDE_PENDING = {'items': [], 'blocks': 0}
 
 
 class side_batch:
     """Context: defer the side-stream launches issued inside (side_launch) to one fork at exit."""
 
     def __enter__(self):
-        if _SIDE_BATCH_ON:
+        if _SIDE_BATCH_K:
             _SIDE_BATCH.append([])
         return self
 
     def __exit__(self, exc_type, *exc):
-        if _SIDE_BATCH_ON:
+        if _SIDE_BATCH_K:
             items = _SIDE_BATCH.pop()
-            if items and exc_type is None:
-                _side_flush(items)
+            if exc_type is not None:
+                return False
+            if _SIDE_BATCH:  # nested: hand over to the enclosing batch
+                _SIDE_BATCH[-1].extend(items)
+                return False
+            pend = _SIDE_PENDING
+            pend['items'].extend(items)
+            pend['blocks'] += 1
+            if pend['blocks'] >= _SIDE_BATCH_K:
+                side_flush_pending()
         return False
+
+
+def set_side_batch(k):
+    """Blocks per side-stream fork (0: fork per launch)."""
+    global _SIDE_BATCH_K
+    side_flush_pending()
+    _SIDE_BATCH_K = max(0, int(k))
+
+
+def side_flush_pending():
+    """Fork the queued side-stream launches now (the join calls this before waiting)."""
+    items = _SIDE_PENDING['items']
+    _SIDE_PENDING['items'], _SIDE_PENDING['blocks'] = [], 0
+    if items:
+        _side_flush(items)
 
 
 def side_launch(side, fn, tensors=(), hold=None, after=()):
@@ -125,8 +151,10 @@ def side_launch(side, fn, tensors=(), hold=None, after=()):
     item = (side, fn, tensors, hold, after)
     if _SIDE_BATCH:
         _SIDE_BATCH[-1].append(item)
-    else:
-        _side_flush([item])
+    else:  # with whatever earlier blocks left queued, in issue order
+        items = _SIDE_PENDING['items'] + [item]
+        _SIDE_PENDING['items'], _SIDE_PENDING['blocks'] = [], 0
+        _side_flush(items)
 
 
 def _side_flush(items):
@@ -635,6 +663,11 @@ class _ResBlock(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        with side_batch():  # with side-stream weight gradients: both forked once, after the block
+            return _ResBlock._backward_body(ctx, dy)
+
+    @staticmethod
+    def _backward_body(ctx, dy):
         x, t, w1, b1, w2, b2 = ctx.saved_tensors
         spec1, spec2 = ctx.specs
         rs = ctx.res_scale

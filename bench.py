@@ -64,8 +64,17 @@ WORKLOADS = {
 # runs in one GPU call: RCAN graph 38.9 -> 37.4 ms but eager 54.5 -> 71.5 ms (its eager step is
 # host-bound: 2.7k launches, and the fork / record_stream per weight gradient add host time), so
 # RCAN takes it only with the HIP graph; SwinIR eager 49.1 -> 46.8 ms; EDSR 40.4 -> 41.4 and RRDB
-# 65.6 -> 66.9 ms (two full-chip MFMA kernels interfering), so those stay single-stream
-ASYNC_WGRAD = {'rcan': 'graph', 'swinir': True}
+# 65.6 -> 66.9 ms (two full-chip MFMA kernels interfering), so those stayed single-stream.  Round 4,
+# with one fork per block (ops.conv.side_batch): RRDB under the graph 66.9 -> 64.6 ms, so it takes it;
+# EDSR still does not (box-dependent: -0.2 ms on one box, +0.6..1.2 ms on another)
+ASYNC_WGRAD = {'rcan': 'graph', 'swinir': True, 'rrdb': 'graph'}
+# blocks per side-stream fork (ops.conv.side_batch; RCAB / STB / RRDB / ResBlock): one everywhere
+# (RCAN 2 / 4 / 20: +0.2 / +0.2 / +1.5 ms; EDSR stays single-stream: with the side stream 37.7 vs
+# 37.9 ms on one box, 39.0-39.7 vs 38.4-38.5 on another, profiles/r04/side_batch/)
+ASYNC_BLOCKS = {}
+for _wl in os.environ.get('SR_BENCH_ASYNC', '').split(','):  # A/B: side-stream weight gradients under the graph
+    if _wl:
+        ASYNC_WGRAD[_wl] = 'graph'
 # bf16 parity floor per workload: PSNR (dB) of the bf16 output against the fp32 CPU oracle on one
 # LR tile (parity_check).  Round-2 observations 71.7 / 52.8 / 66.3 / 46.1 dB; the floors sit ~4-6 dB
 # below them (RRDB's level is bf16 storage rounding through 345 chained convs:
@@ -90,6 +99,7 @@ def make_opt(world, batch, workload='edsr', graph=False, ddp=None, shared_gpu=Fa
         model_type=mtype, is_train=True, dist=world > 1 if ddp is None else ddp, num_gpu=1, rank=0, world_size=world,
         network_g=dict(net),
         train=dict(ema_decay=0.999, use_amp=True, cuda_graph=graph, async_wgrad=aw,
+                   async_wgrad_blocks=ASYNC_BLOCKS.get(workload, 1),
                    optim_g=dict(type='Adam', lr=lr, weight_decay=0, betas=[0.9, 0.99]),
                    scheduler=dict(type='MultiStepLR', milestones=[200000], gamma=0.5),
                    pixel_opt=dict(type='L1Loss', loss_weight=1.0, reduction='mean')),
