@@ -2213,8 +2213,13 @@ SR_DEV void vm_wait_dyn(int n) { vm_wait_bs<0, 63>(n < 0 ? 0 : (n > 63 ? 63 : n)
 // gate_slope), 2 pre-residual GELU'(g), 3 post-residual (g > 0 ? 1 : gate_slope) on output
 // channels gcol0..gcol1), 4 res, 5 res2, 6 aux, 7 colsum, 8 row_scale, 9 dot (with 7: the partial
 // sums are of y * dot, the dot operand staged like the residuals).
+// blocks per CU the band kernel is built for: two for the W 64 forms whose ring + staging fit
+// 80 KB of LDS and 256 registers (no second staging operand, no dot), one otherwise
+constexpr int band_occ(int W, int E) {
+  return W == 64 && (E == 0 || E == 1 || E == 2 || E == 4 || E == 16 || E == 128) ? 2 : 1;
+}
 template <int CO, int W, int LA, int KH, int E>
-__global__ __launch_bounds__(256, 1) void conv3x3_fwd_band_kernel(FwdArgs a) {
+__global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(FwdArgs a) {
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
   constexpr bool RES = (E & 16) != 0, RES2 = (E & 32) != 0, AUX = (E & 64) != 0, CS = (E & 128) != 0,
                  RSC = (E & 256) != 0, DOT = (E & 512) != 0;
@@ -5219,11 +5224,22 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
   *nt = k == FK_BIG ? 512 : 256;
 }
 
+// SR_BAND_2PC=1: two bands per CU for the forms built for it (read per call).  Off by default: the
+// kernel alone gains ~4 % (RCAN step trace 21.4 vs 22.3 us) but the RCAN step loses 0.9 ms (36.0 vs
+// 35.1 ms, three pairs): the second band leaves no room for the side-stream weight gradients
+bool band_two_per_cu_env() {
+  const char* e = getenv("SR_BAND_2PC");
+  return e && e[0] == '1';
+}
 hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
-  // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64
-  // blocks (long bands: ring wrap-around and image crossings inside a band, for tests)
+  // one block per CU (one wave per SIMD: the weights live in registers), two for the forms built
+  // for it (band_occ: bands half as long, one block's ring fill / epilogue under the other's
+  // MFMAs); variant 35 forces 64 blocks (long bands: ring wrap-around and image crossings inside a
+  // band, for tests)
   const int rows = a.N * a.H;
-  const int gmax = g_variant == 35 ? 64 : 256;
+  const int e1 = band_epi(a, 256);
+  const int occ = (e1 >= 0 && band_occ(a.W, e1) == 2 && band_two_per_cu_env()) ? 2 : 1;
+  const int gmax = g_variant == 35 ? 64 : 256 * occ;
   FwdArgs ab = a;
   ab.stamps = g_stamps;
   const dim3 grid(rows < gmax ? rows : gmax);
