@@ -262,12 +262,16 @@ def _pmc_traffic(workload, kernel):
     """HBM bytes per launch of ``kernel`` from this round's committed PMC passes
     (tools/profile_round.sh -> profiles/pmc_traffic.json), or None."""
     try:
-        rec = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))).get(workload)
+        recs = json.load(open(os.path.join(ROOT, 'profiles', 'pmc_traffic.json')))
     except (OSError, ValueError):
         return None
-    if not rec or rec.get('hbm_bytes_per_launch') is None or rec.get('bench_kernel') != kernel:
-        return None
-    return rec
+    # the workload's record, or one of its extra kernels' (key '<workload>_<what>'): the dominant
+    # kernel of a step can change between close contenders (SwinIR linear_wk / linear_wgrad)
+    for key, rec in sorted(recs.items()):
+        if (key == workload or key.startswith(workload + '_')) and rec.get('bench_kernel') == kernel and \
+                rec.get('hbm_bytes_per_launch') is not None:
+            return rec
+    return None
 
 
 def _roof(flops, nbytes, sec):

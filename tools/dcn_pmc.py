@@ -63,9 +63,9 @@ fetch, write = collect('FETCH_SIZE'), collect('WRITE_SIZE')
 k = 'dcn_fwd_win_kernel'
 if k in write and k in fetch and len(write[k]) == len(fetch[k]):
     tr = [w > 200e6 for w in write[k]]
-    for tag, sel in (('dcn_fwd_win_kernel (training: + columns)', True), ('dcn_fwd_win_kernel (inference)', False)):
-        fetch[tag] = [f for f, t in zip(fetch[k], tr) if t == sel]
-        write[tag] = [w for w, t in zip(write[k], tr) if t == sel]
+    for name, sel in (('dcn_fwd_win_kernel (training: + columns)', True), ('dcn_fwd_win_kernel (inference)', False)):
+        fetch[name] = [f for f, t in zip(fetch[k], tr) if t == sel]
+        write[name] = [w for w, t in zip(write[k], tr) if t == sel]
     del fetch[k], write[k]
     ALG['dcn_fwd_win_kernel (training: + columns)'] = (ALG[k][0], ALG[k][1] + '; 302 MB of columns written')
     ALG['dcn_fwd_win_kernel (inference)'] = ALG[k]
