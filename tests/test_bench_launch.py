@@ -47,3 +47,16 @@ def test_bench_world_size_mismatch_fails():
     p = _run(['--gpus', '4', '--dry-run'], env_extra={'WORLD_SIZE': '2', 'RANK': '0', 'LOCAL_RANK': '0'})
     assert p.returncode != 0
     assert 'disagrees with WORLD_SIZE' in p.stderr
+
+
+def test_pmc_traffic_record_per_dominant_kernel():
+    """bench.py's roofline.traffic comes from profiles/pmc_traffic.json: the record of the workload
+    whose bench kernel is the dominant one, also an extra record of that workload ('<wl>_<what>')
+    when a close contender dominates (SwinIR: linear_wk_kernel / linear_wgrad_kernel+reduce)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for wl, kernel in (('edsr', 'conv3x3_fwd_pph_kernel'), ('swinir', 'linear_wk_kernel'),
+                       ('swinir', 'linear_wgrad_kernel+reduce'), ('rcan', 'conv3x3_fwd_band_kernel')):
+        rec = bench._pmc_traffic(wl, kernel)
+        assert rec is not None and rec['bench_kernel'] == kernel and rec['hbm_bytes_per_launch'] > 0, (wl, kernel)
+    assert bench._pmc_traffic('edsr', 'linear_wk_kernel') is None  # another workload's record never answers
