@@ -50,21 +50,38 @@ def _event():
     return pool.pop() if pool else torch.cuda.Event(enable_timing=True)
 
 
-@contextlib.contextmanager
+class _Span:
+    """Event pair around one traced launch (see ``span``)."""
+    __slots__ = ('name', 'flops', 'nbytes', 'relaunch', 'launches', 's', 'e')
+
+    def __init__(self, name, flops, nbytes, relaunch, launches):
+        self.name, self.flops, self.nbytes, self.relaunch, self.launches = name, flops, nbytes, relaunch, launches
+
+    def __enter__(self):
+        self.s, self.e = _event(), _event()
+        self.s.record()
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        self.e.record()
+        if exc_type is None:
+            _STATE['records'].append((self.name, float(self.flops), float(self.nbytes), int(self.launches), self.s, self.e))
+            if self.relaunch is not None:
+                _STATE['relaunch'].setdefault(self.name, []).append(self.relaunch)
+        return False
+
+
+_NULL = contextlib.nullcontext()
+
+
 def span(name, flops=0.0, nbytes=0.0, relaunch=None, launches=1):
     """One op call of kernel ``name``: its algorithmic FLOPs and HBM bytes (every operand the call
     reads or writes, once) and the number of kernel launches it makes (``launches``: the per-launch
-    unit of rocprof's --stats, e.g. the 64-channel slices of a sliced band conv)."""
+    unit of rocprof's --stats, e.g. the 64-channel slices of a sliced band conv).  Outside a trace
+    a shared no-op context (every train step enters ~1 k of these on the host)."""
     if not _STATE['active']:
-        yield
-        return
-    s, e = _event(), _event()
-    s.record()
-    yield
-    e.record()
-    _STATE['records'].append((name, float(flops), float(nbytes), int(launches), s, e))
-    if relaunch is not None:
-        _STATE['relaunch'].setdefault(name, []).append(relaunch)
+        return _NULL
+    return _Span(name, flops, nbytes, relaunch, launches)
 
 
 def relaunch_count(name):
