@@ -396,3 +396,26 @@ def test_fused_leaky_relu_module_and_double_backward(cuda, shape):
     assert rel(gg, O.fused_bias_act(w1, w2, ref, 3, 1, 0.2, 2**0.5)) < 1e-5
     # functional form == module
     assert torch.equal(fused_leaky_relu(xt.detach(), m.bias.detach()), y.detach())
+
+
+@pytest.mark.parametrize('shape,cp', [((2, 64, 32, 48), 64), ((3, 64, 16, 16), 64), ((1, 20, 8, 12), 24),
+                                      ((2, 96, 8, 20), 104), ((1, 64, 7, 9), 64)])
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('affine', [False, True])
+def test_nchw_to_nhwc_bitwise(cuda, shape, cp, dtype, affine):
+    """sr_nchw_to_nhwc (the vector tile for HW % 4 == 0 and Cp % 8 == 0 -- the DCN operands -- else
+    the scalar tile) against torch: (x - shift) * scale, channels padded with zeros to Cp, one
+    rounding to the storage type -- bit for bit."""
+    from basicsr4rs_amd.ops import conv as Cv
+    torch.manual_seed(sum(shape) + cp)
+    N, C, H, W = shape
+    x = torch.randn(*shape, device=cuda) * 3
+    shift = (torch.randn(C, device=cuda) if affine else None)
+    scale = (torch.rand(C, device=cuda) + 0.5 if affine else None)
+    y = Cv.nchw_to_nhwc(x, cp, dtype, shift=shift, scale=scale)
+    ref = x
+    if affine:
+        ref = (ref - shift.view(1, C, 1, 1)) * scale.view(1, C, 1, 1)
+    ref = torch.nn.functional.pad(ref.permute(0, 2, 3, 1), (0, cp - C)).to(dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
