@@ -482,18 +482,11 @@ def conv_wgrad_raw(dy, x, N, H, W, cin, cin_real, cout, cout_real, scale=1.0, ou
         _lib.check(lib.sr_conv3x3_wgrad(d, _lib.ptr(dy), _lib.ptr(x), _lib.ptr(ws), ws_bytes, _lib.ptr(tw), _lib.ptr(tb),
                                         _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')), _lib.stream()))
         d.accumulate = 1
-        side.wait_stream(torch.cuda.current_stream(x.device))
-        ws.record_stream(side)
-        for t in (kw.get('co_map'), kw.get('ci_map')):
-            if t is not None:
-                t.record_stream(side)
-        with torch.cuda.stream(side):
-            _lib.check(lib.sr_conv3x3_wgrad_reduce(d, _lib.ptr(ws), ws_bytes, _lib.ptr(tw), _lib.ptr(tb),
-                                                   _lib.ptr(kw.get('co_map')), _lib.ptr(kw.get('ci_map')),
-                                                   _lib.stream()))
-        grad_ready(params[0])
-        if need_bias:
-            grad_ready(params[1])
+        side_launch(side, lambda: _lib.check(lib.sr_conv3x3_wgrad_reduce(d, _lib.ptr(ws), ws_bytes, _lib.ptr(tw),
+                                                                          _lib.ptr(tb), _lib.ptr(kw.get('co_map')),
+                                                                          _lib.ptr(kw.get('ci_map')), _lib.stream())),
+                    (ws, kw.get('co_map'), kw.get('ci_map')),
+                    after=(lambda: grad_ready(params[0]),) + ((lambda: grad_ready(params[1])),) * need_bias)
         return None, None
     if side is not None:  # fork: dy / x are ready on the current stream
         # dy held until the join: no in-place gradient accumulation into it before the side read
