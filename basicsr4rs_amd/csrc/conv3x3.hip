@@ -5083,6 +5083,18 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
 
 // Narrow-conv halo kernel: bf16 3x3, W 64 or 128, whole-row 256-pixel tiles; Cout <= 64 in one
 // block column, Cout 65..255 (RRDB dense-block dgrads) in 64-channel block columns.
+// SR_HALO_W256=1 (read per call): the one-row halo tiles also for W 256 convs with Cout a multiple
+// of 64 (<= 256) and a plain NHWC store (DIRECT epilogue), instead of the 256x256 pp kernel.  Opt-in:
+// measured slower (EDSR conv_last dgrad 1390 vs 550 us, RCAN 170 vs 150 us; profiles/r04/halo256/) --
+// 99 KB of LDS leave one block per CU, and a 64-channel column block re-stages the row halo per tile
+bool halo_w256_wide() {
+  const char* e = getenv("SR_HALO_W256");
+  return e && e[0] == '1';
+}
+bool halo_w256_direct(const FwdArgs& a) {
+  return a.Cout % 64 == 0 && a.Cout <= 256 && !a.out_nchw && a.out_ps == 0 && !a.colsum && !a.aux && !a.gate &&
+         !a.res2 && !a.row_scale && a.in_ps == 0;
+}
 bool fwd_use_halo(const FwdArgs& a, bool bf) {
   static const bool ps_off = [] {
     const char* e = getenv("SR_HALO_PS");
@@ -5092,8 +5104,9 @@ bool fwd_use_halo(const FwdArgs& a, bool bf) {
   // in one shuffle slot; SR_HALO_PS=0 / variant 68: the tile kernel for those (A/B)
   const bool ps_ok = a.in_ps > 0 && a.fd_cps.d % 64 == 0 && a.W != 256 && !ps_off && g_variant != 68;
   if (!bf || a.in_up != 1 || (a.in_ps != 0 && !ps_ok) || a.tap0 != 0 || g_variant == 1) return false;
-  if (a.W == 256)  // HR-resolution tail convs (conv_last, Cout <= 16, NCHW store): one row per tile
-    return a.Cout <= 16 && g_variant != 29;
+  if (a.W == 256)  // HR-resolution tail convs (conv_last, Cout <= 16, NCHW store): one row per tile;
+    // with SR_HALO_W256=1 also the wide plain-NHWC ones (the conv_last dgrads: 3 -> 64 / 256 channels)
+    return (a.Cout <= 16 && g_variant != 29) || (halo_w256_wide() && halo_w256_direct(a));
   return !a.out_nchw && a.Cout < 256 && (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
 }
 
@@ -5103,7 +5116,8 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   a.tiles = a.M / 256;
   const int ct = (a.Cout + 15) / 16;
   const dim3 grid(a.tiles, a.tiles_n);
-  if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
+  if (a.W == 256 && a.Cout > 16) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 0, true, true>), grid, dim3(256), 0, s, a);
+  else if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
   else if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
   else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, grid, dim3(256), 0, s, a);
   else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);

@@ -937,3 +937,41 @@ def test_prepared_images_freed_with_their_weight(cuda):
     C._retire_table(torch.bfloat16)
     gc.collect()
     assert len(C._PREP_ALL) == n0
+
+
+@pytest.mark.parametrize('shape', [(1, 4, 256, 8, 256), (2, 3, 256, 64, 64), (1, 2, 256, 32, 128),
+                                   (1, 3, 256, 3, 64)])
+@pytest.mark.parametrize('epi', ['plain', 'relu_res'])
+def test_fwd_halo_w256_wide_vs_fp64(cuda, shape, epi, monkeypatch):
+    """The one-row halo tiles for W 256 convs with Cout a multiple of 64 (SR_HALO_W256=1: the HR
+    conv_last dgrads, 3 -> 64 / 256 channels, and the RRDB 256^2 dgrad), DIRECT epilogue, against
+    fp64 on the same bf16 operands; the image's top / bottom rows and left / right halo columns."""
+    monkeypatch.setenv('SR_HALO_W256', '1')
+    N, H, W, cin, cout = shape
+    torch.manual_seed(9)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    cin_p = (cin + 7) // 8 * 8
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    spec = C.ConvSpec(cin, cout)
+    wf, wd, bg = C.prepared(conv.weight, conv.bias, spec, dt)
+    x = torch.zeros(N, H, W, cin_p, device=cuda)
+    x[..., :cin] = torch.randn(N, H, W, cin, device=cuda)
+    x = x.to(dt)
+    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
+    kw = {}
+    if epi == 'relu_res':
+        kw.update(act=_lib.ACT_RELU, res=res, beta=1.0)
+    d = C._desc(dt, N, H, W, cin_p, cin_p, cout, cout, cout)
+    if epi == 'relu_res':
+        d.act = _lib.ACT_RELU
+    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_halo_kernel'
+    y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+    C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin_p, cout, cout, **kw)
+    torch.cuda.synchronize()
+    xd = x[..., :cin].permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(xd, bf(conv.weight.detach().cpu()).double(), conv.bias.detach().cpu().double(), padding=1)
+    if epi == 'relu_res':
+        ref = F.relu(ref) + res.permute(0, 3, 1, 2).double().cpu()
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    assert (got - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())
