@@ -20,7 +20,7 @@ from ..losses import build_loss
 from ..metrics import calculate_metric
 import os
 
-from ..ops.conv import async_wgrad, bump_param_epoch, set_side_batch, take_captured_tables
+from ..ops.conv import async_wgrad, bump_param_epoch, take_captured_tables
 from ..utils.flat import FlatParams
 from ..utils.img_util import imwrite, tensor2img
 from ..utils.logger import get_root_logger
@@ -55,6 +55,11 @@ class SRModel(BaseModel):
         self.net_g.train()
         train_opt = self.opt['train']
         self.use_amp = bool(train_opt.get('use_amp', False))
+        if self.use_amp:
+            # the reference's AMP is fp16 autocast + GradScaler (basicsr/models/srrs_model.py:28-31,
+            # 79-82); the HIP kernels compute bf16 (no fp16 path, no loss scaling needed)
+            get_root_logger().warning('train.use_amp: autocast runs in bfloat16 on the HIP kernels '
+                                      '(the reference uses float16 + GradScaler; DESIGN.md §0)')
         self._graph = None
         self._eager_steps = 0
         # HIP-graph capture of the train step (after 2 eager warm-up steps); distributed: a chain of
@@ -75,8 +80,8 @@ class SRModel(BaseModel):
                                           f'{torch.cuda.device_count()} GPU(s)')
                 self.async_wgrad = False
         # blocks whose side-stream launches share one fork (train.async_wgrad_blocks, ops.conv.side_batch;
-        # SR_SIDE_BATCH overrides)
-        set_side_batch(int(os.environ.get('SR_SIDE_BATCH', train_opt.get('async_wgrad_blocks', 1))))
+        # SR_SIDE_BATCH overrides); applied only inside this model's backward (async_wgrad(blocks=))
+        self.async_blocks = int(os.environ.get('SR_SIDE_BATCH', train_opt.get('async_wgrad_blocks', 1)))
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)
@@ -127,7 +132,8 @@ class SRModel(BaseModel):
             loss_dict['l_pix'] = l_pix
         if before_backward is not None:
             l_total = before_backward(l_total)
-        with async_wgrad(self.async_wgrad):  # weight gradients on a side stream, joined here
+        # weight gradients on a side stream, joined here
+        with async_wgrad(self.async_wgrad, blocks=getattr(self, 'async_blocks', None)):
             l_total.backward()
         # drop the autograd graph now: a graph kept alive by self.output would pin this step's
         # AccumulateGrad nodes (and their stream) into the next step / a HIP-graph capture

@@ -52,7 +52,7 @@ class SRRSModel(SRModel):
             # drop this batch and its graph like the reference (srrs_model.py:68-77)
             del self.lq, self.gt, self.output
             return
-        with async_wgrad(self.async_wgrad):
+        with async_wgrad(self.async_wgrad, blocks=getattr(self, 'async_blocks', None)):
             l_total.backward()
         self.sync_gradients()
         if hasattr(self.optimizer_g, 'fp') and self.ema_decay > 0 and self.flat_ema is not None:

@@ -69,22 +69,35 @@ def async_mode():
 class async_wgrad:
     """Context: weight gradients on the side stream, joined into the current stream on exit.
     ``enabled='reduce'`` moves only the split-K slab reduces there (the slab kernel stays on the
-    main stream): a memory-bound reduce then fills the CUs beside the next MFMA-bound conv."""
+    main stream): a memory-bound reduce then fills the CUs beside the next MFMA-bound conv.
+    ``blocks``: blocks whose side-stream launches share one fork inside this context (side_batch;
+    None keeps the enclosing / SR_SIDE_BATCH setting).  It is restored on exit, so one model's
+    setting never leaks into another's backward."""
 
-    def __init__(self, enabled=True):
+    def __init__(self, enabled=True, blocks=None):
         self.enabled = enabled
+        self.blocks = blocks
         self._prev_mode = None
+        self._prev_k = None
 
     def __enter__(self):
         if self.enabled:
             _ASYNC['depth'] += 1
             self._prev_mode = _ASYNC['mode']
             _ASYNC['mode'] = self.enabled
+            if self.blocks is not None:
+                self._prev_k = _SIDE['k']
+                _SIDE['k'] = max(0, int(self.blocks))
         return self
 
-    def __exit__(self, *exc):
+    def __exit__(self, exc_type, *exc):
         if self.enabled:
-            side_flush_pending()  # launches still queued by side_batch fork before the join
+            if exc_type is None:
+                side_flush_pending()  # launches still queued by side_batch fork before the join
+            else:  # backward failed: its queued gradient launches and callbacks are dropped
+                _SIDE['items'], _SIDE['blocks'] = [], 0
+            if self._prev_k is not None:
+                _SIDE['k'], self._prev_k = self._prev_k, None
             _ASYNC['depth'] -= 1
             _ASYNC['mode'] = self._prev_mode  # a nested context must not leak its mode outward
             for st in _ASYNC['streams'].values():
@@ -98,47 +111,50 @@ class async_wgrad:
 # the current stream ONCE at exit (one event wait for all of them instead of one per launch).  A
 # captured step turns every fork into a cross-queue graph edge, and RCAN's 2.5 k-node step spent
 # ~2.6 us per node between short kernels; SR_SIDE_BATCH=0 forks per launch (A/B).
-# SR_SIDE_BATCH=k > 1 forks once per k blocks (the queue is flushed at the latest by the join).
+# k > 1 (async_wgrad(blocks=k), SR_SIDE_BATCH=k) forks once per k blocks (the queue is flushed at
+# the latest by the join).
 _SIDE_BATCH = []
-_SIDE_BATCH_K = max(0, int(os.environ.get('SR_SIDE_BATCH', '1')))
-_SIDE_PENDING = {'items': [], 'blocks': 0}
+_SIDE = {'items': [], 'blocks': 0, 'k': max(0, int(os.environ.get('SR_SIDE_BATCH', '1')))}
 
 
 class side_batch:
     """Context: defer the side-stream launches issued inside (side_launch) to one fork at exit."""
 
     def __enter__(self):
-        if _SIDE_BATCH_K:
+        self._on = bool(_SIDE['k'])
+        if self._on:
             _SIDE_BATCH.append([])
         return self
 
     def __exit__(self, exc_type, *exc):
-        if _SIDE_BATCH_K:
+        if self._on:
             items = _SIDE_BATCH.pop()
             if exc_type is not None:
                 return False
             if _SIDE_BATCH:  # nested: hand over to the enclosing batch
                 _SIDE_BATCH[-1].extend(items)
                 return False
-            pend = _SIDE_PENDING
-            pend['items'].extend(items)
-            pend['blocks'] += 1
-            if pend['blocks'] >= _SIDE_BATCH_K:
+            _SIDE['items'].extend(items)
+            _SIDE['blocks'] += 1
+            if _SIDE['blocks'] >= _SIDE['k']:
                 side_flush_pending()
         return False
 
 
 def set_side_batch(k):
-    """Blocks per side-stream fork (0: fork per launch)."""
-    global _SIDE_BATCH_K
+    """Default blocks per side-stream fork outside any async_wgrad(blocks=...) (0: fork per launch)."""
     side_flush_pending()
-    _SIDE_BATCH_K = max(0, int(k))
+    _SIDE['k'] = max(0, int(k))
+
+
+def side_batch_blocks():
+    return _SIDE['k']
 
 
 def side_flush_pending():
     """Fork the queued side-stream launches now (the join calls this before waiting)."""
-    items = _SIDE_PENDING['items']
-    _SIDE_PENDING['items'], _SIDE_PENDING['blocks'] = [], 0
+    items = _SIDE['items']
+    _SIDE['items'], _SIDE['blocks'] = [], 0
     if items:
         _side_flush(items)
 
@@ -146,18 +162,21 @@ def side_flush_pending():
 def side_launch(side, fn, tensors=(), hold=None, after=()):
     """Run ``fn`` (kernel launches) on ``side`` after the work queued so far on the current stream:
     ``tensors`` are record_stream'ed there, ``hold`` is kept until the join (_ASYNC['hold']) and
-    ``after`` (gradient-ready callbacks) fire once the launch is queued.  Inside side_batch the
-    launch joins the batch's single fork."""
+    ``after`` (gradient-ready callbacks) fire once every launch of the fork is queued.  Inside
+    side_batch the launch joins the batch's single fork."""
     item = (side, fn, tensors, hold, after)
     if _SIDE_BATCH:
         _SIDE_BATCH[-1].append(item)
     else:  # with whatever earlier blocks left queued, in issue order
-        items = _SIDE_PENDING['items'] + [item]
-        _SIDE_PENDING['items'], _SIDE_PENDING['blocks'] = [], 0
+        items = _SIDE['items'] + [item]
+        _SIDE['items'], _SIDE['blocks'] = [], 0
         _side_flush(items)
 
 
 def _side_flush(items):
+    # Every launch of the fork is queued before ANY gradient-ready callback runs: a callback can
+    # complete a bucket, and the segmented DDP capture (utils/step_graph.py) then cuts the graph and
+    # rejoins the side stream -- launches still to come in this fork would run outside the capture.
     for side in {id(it[0]): it[0] for it in items}.values():
         side.wait_stream(torch.cuda.current_stream(side.device))
     for side, fn, tensors, hold, after in items:
@@ -168,7 +187,8 @@ def _side_flush(items):
             _ASYNC['hold'].append(hold)
         with torch.cuda.stream(side):
             fn()
-        for cb in after:
+    for it in items:
+        for cb in it[4]:
             cb()
 
 
@@ -176,9 +196,21 @@ def pad8(c):
     return (c + 7) // 8 * 8
 
 
+_FP16_WARNED = [False]
+
+
 def feature_dtype():
-    """Compute dtype of the HIP kernels for the current context."""
+    """Compute dtype of the HIP kernels for the current context: bf16 under CUDA autocast of any
+    dtype.  The reference's AMP is fp16 + GradScaler (basicsr/models/srrs_model.py:28-31, 79-82);
+    the kernels have no fp16 path, so an fp16 autocast request runs in bf16 (same 16-bit storage,
+    fp32 range: no loss scaling needed) and says so once per process."""
     if torch.is_autocast_enabled('cuda'):
+        if not _FP16_WARNED[0] and torch.get_autocast_dtype('cuda') == torch.float16:
+            _FP16_WARNED[0] = True
+            import warnings
+            warnings.warn('basicsr4rs_amd: autocast asked for float16; the HIP kernels compute in bfloat16 '
+                          '(the documented AMP divergence, DESIGN.md §0 / SURVEY.md §0.7)', RuntimeWarning,
+                          stacklevel=2)
         return torch.bfloat16
     return torch.float32
 

@@ -135,13 +135,33 @@ def _cpu_model():
     return f'{names[0] if names else "unknown"} ({os.cpu_count()} logical CPUs visible)'
 
 
+def _cpu_threads():
+    """Threads for the CPU baseline and why: the host's usable CPUs (affinity mask), capped by the
+    CPU share the GPU box grants this job (OMP_NUM_THREADS, which the harness sets to 16 per GPU:
+    os.cpu_count() there reports the whole 8-GPU host, and more threads than the share only
+    oversubscribe it)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    share = os.environ.get('OMP_NUM_THREADS')
+    if share and share.isdigit() and 0 < int(share) < usable:
+        return int(share), (f'{share} threads = the CPU share granted per GPU job (OMP_NUM_THREADS); '
+                            f'{usable} usable / {os.cpu_count()} logical CPUs on the host')
+    return usable, f'all {usable} usable CPUs (affinity mask; {os.cpu_count()} logical)'
+
+
 def cpu_baseline(workload, seconds=20.0):
     """The oracle train step of ``workload`` (fwd + L1 + bwd + torch Adam) in torch-CPU fp32 at
     batch 1 on the host's cores: ONE image of the benchmarked tile, timed as the median of as
     many steps as fit in ~``seconds`` (at least 1 after a warm-up).  SwinIR runs eval-mode
-    attention (no stochastic depth: its draws only change which samples a branch skips)."""
+    attention (no stochastic depth: its draws only change which samples a branch skips).
+    Threads: _cpu_threads (the job's CPU share, stated with the host's width in the line)."""
     from basicsr4rs_amd.archs import build_network
     from oracle import nets as O
+    nthr, why = _cpu_threads()
+    prev_thr = torch.get_num_threads()
+    torch.set_num_threads(nthr)
     net_cfg, _, lr, _, lr_px = WORKLOADS[workload][:5]
     torch.manual_seed(42)
     net = build_network(dict(net_cfg))
@@ -168,11 +188,12 @@ def cpu_baseline(workload, seconds=20.0):
         times.append(time.time() - t)
     times.sort()
     t_med = times[len(times) // 2]
-    return {'value': (4 * lr_px)**2 / t_med, 'unit': 'HR-pixels/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-            'cpu_model': _cpu_model(),
+    torch.set_num_threads(prev_thr)
+    return {'value': (4 * lr_px)**2 / t_med, 'unit': 'HR-pixels/s', 'cores': nthr, 'kind': 'port',
+            'cpu_model': _cpu_model(), 'cores_note': why,
             'sample': f'oracle {net_cfg["type"]} fp32 train step (fwd + L1 + bwd + Adam), batch 1 '
                       f'({lr_px}x{lr_px} LR -> {4 * lr_px}x{4 * lr_px} HR), median of {len(times)} steps after '
-                      f'1 warm-up, torch CPU threads={torch.get_num_threads()}'}
+                      f'1 warm-up, torch CPU threads={nthr}'}
 
 
 def parity_check(workload, dev):

@@ -38,11 +38,15 @@ def _collect(q, procs, n, timeout=240):
     return out
 
 
-def _opt(dist_, world, rank, bucket_mb, async_wgrad=False, graph=False):
+EDSR_S = dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=2, upscale=4, res_scale=1)
+RCAN_S = dict(type='RCAN', num_in_ch=3, num_out_ch=3, num_feat=64, num_group=2, num_block=2, squeeze_factor=16,
+              upscale=4, res_scale=1)
+
+
+def _opt(dist_, world, rank, bucket_mb, async_wgrad=False, graph=False, net=EDSR_S):
     return dict(model_type='SRModel', is_train=True, dist=dist_, num_gpu=1, world_size=world, rank=rank, path={},
                 bucket_cap_mb=bucket_mb,
-                network_g=dict(type='EDSR', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=2, upscale=4,
-                               res_scale=1),
+                network_g=dict(net),
                 train=dict(ema_decay=0.999, use_amp=False, async_wgrad=async_wgrad, cuda_graph=graph,
                            optim_g=dict(type='Adam', lr=1e-3, weight_decay=0, betas=[0.9, 0.99]),
                            scheduler=dict(type='MultiStepLR', milestones=[100], gamma=0.5),
@@ -59,11 +63,16 @@ def _worker(rank, world, port, bucket_mb, async_wgrad, q, graph=False, steps=2):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     torch.cuda.set_device(0)
+    if async_wgrad:
+        # two ranks share the one card, where SRModel turns the side stream off;
+        # SR_ASYNC_WGRAD=1 keeps it on so this test covers DDP + side streams (eager steps only)
+        os.environ['SR_ASYNC_WGRAD'] = '1'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     import basicsr4rs_amd.archs  # noqa: F401
     from basicsr4rs_amd.models import build_model
     torch.manual_seed(0 + rank)  # different init per rank: the reducer broadcasts rank 0's
     model = build_model(_opt(True, world, rank, bucket_mb, async_wgrad, graph))
+    assert bool(model.async_wgrad) == bool(async_wgrad), 'side-stream mode silently changed'
     for step in range(1, steps + 1):
         lq, gt = _batch(step)
         sl = slice(rank * 2, rank * 2 + 2)
@@ -123,13 +132,13 @@ def test_ddp_two_ranks_match_full_batch(cuda, bucket_mb, async_wgrad):
         assert err < 2e-4, (k, err)
 
 
-@pytest.mark.parametrize('async_wgrad', [False, True])
-def test_ddp_graph_segments_match_full_batch(cuda, async_wgrad):
+def test_ddp_graph_segments_match_full_batch(cuda, async_wgrad=False):
     """train.cuda_graph with DDP: steps 1-2 eager, step 3 captured as graph segments cut at the ready
     buckets (utils/step_graph.py), steps 4-5 replayed with the bucket all-reduces launched between
     segments.  Two gloo ranks on the one card, fp32: both ranks equal, and equal to single-process
     eager training on the full batch (relative 2e-4); every bucket but the flushed tail goes out
-    between backward segments."""
+    between backward segments.  (Side streams under the segmented graph: the RCCL world-1 tests
+    below, where one process owns the card.)"""
     import basicsr4rs_amd.archs  # noqa: F401
     from basicsr4rs_amd.models import build_model
     ctx = mp.get_context('spawn')
@@ -167,7 +176,7 @@ def test_ddp_graph_segments_match_full_batch(cuda, async_wgrad):
         assert err < 2e-4, (k, err)
 
 
-def _nccl_worker(port, q):
+def _nccl_worker(port, q, async_wgrad=False, net=EDSR_S):
     """World 1 over RCCL: the segmented graph's replay issues real RCCL all-reduces."""
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -179,9 +188,13 @@ def _nccl_worker(port, q):
     out = []
     for graph in (False, True):
         torch.manual_seed(0)
-        o = _opt(True, 1, 0, 0.05, False, graph)
+        o = _opt(True, 1, 0, 0.05, async_wgrad, graph, net)
         o['train']['use_amp'] = True
         model = build_model(o)
+        assert bool(model.async_wgrad) == bool(async_wgrad), 'side-stream mode silently changed'
+        if async_wgrad:
+            red = model.net_g.reducer
+            assert len(red.buckets) > 4  # 50 KB buckets: gradient-ready callbacks cut inside a block's fork
         if graph:
             # hold each capture for a while so RCCL's watchdog thread polls its pending work (an event
             # query) during it: in the global capture mode that poll aborts the process
@@ -214,6 +227,26 @@ def test_ddp_graph_segments_rccl_world1_bitwise(cuda):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    ((l0, s0, _), (l1, s1, nseg)), = _collect(q, [p], 1)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert nseg >= 3
+    assert l0 == l1
+    for k in s0:
+        assert (s0[k] == s1[k]).all(), k
+
+
+@pytest.mark.parametrize('net', ['edsr', 'rcan'])
+def test_ddp_graph_segments_async_rccl_world1_bitwise(cuda, net):
+    """Side-stream weight gradients (train.async_wgrad, forks batched per block) under the segmented
+    DDP graph over RCCL, with 50 KB buckets so a gradient-ready callback completes a bucket -- and
+    cuts the capture -- in the middle of a block's batched fork: every launch of the fork must be
+    inside the graph, so the replayed steps equal the eager ones bitwise (a launch left out of the
+    graph would leave its weight gradient stale at replay)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q, True, EDSR_S if net == 'edsr' else RCAN_S))
     p.start()
     ((l0, s0, _), (l1, s1, nseg)), = _collect(q, [p], 1)
     p.join(timeout=60)

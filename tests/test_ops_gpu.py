@@ -214,7 +214,11 @@ def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, monkeypatch):
         assert torch.isfinite(b_).all(), name
         err = (a_ - b_).abs().max().item() / max(1e-6, a_.abs().max().item())
         print(f'{case} {form}: fused bwd vs dcols path, grad {name} rel err {err:.2e}')
-        assert err < 1e-2, (name, err)
+        # ~2x the maxima observed in round 4 (profiles/r04/tests): the int32 scatter image quantises
+        # each contribution to 2^-18 of the per-image max |mask * dcols| (3.3e-5 observed); the int64
+        # image and the offset / mask gradients differ only by fp32 summation order (<= 8.7e-8)
+        tol = 7e-5 if (name == 'x' and form.startswith('i32')) else 2e-7
+        assert err < tol, (name, err, tol)
 
 
 def test_dcn_fused_ok_query(cuda):

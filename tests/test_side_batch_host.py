@@ -50,7 +50,9 @@ def test_batch_forks_once_in_issue_order(stubs):
         _launch(side, log, 'a')
         _launch(side, log, 'b')
         assert log == []  # nothing forked yet
-    assert log == ['fork', 'rec:a', 'run:a', 'ready:a', 'rec:b', 'run:b', 'ready:b']
+    # every launch of the fork is queued before any gradient-ready callback runs (a callback may
+    # cut the segmented DDP capture and rejoin the side stream)
+    assert log == ['fork', 'rec:a', 'run:a', 'rec:b', 'run:b', 'ready:a', 'ready:b']
     assert C._ASYNC['hold'] == ['a', 'b']
 
 
@@ -84,6 +86,43 @@ def test_unbatched_launch_forks_after_queued_ones(stubs):
         _launch(side, log, 'a')
     _launch(side, log, 'b')  # outside any batch: forks now, 'a' first
     assert [x for x in log if x.startswith('run')] == ['run:a', 'run:b'] and log.count('fork') == 1
+
+
+def test_context_blocks_are_scoped(stubs):
+    log, side = stubs
+    assert C.side_batch_blocks() == 1
+    with C.async_wgrad(True, blocks=3):
+        assert C.side_batch_blocks() == 3
+        for name in 'ab':
+            with C.side_batch():
+                _launch(side, log, name)
+        assert log == []  # 2 of 3 blocks queued
+    assert C.side_batch_blocks() == 1  # restored: no leak into other models
+    assert log.count('fork') == 1 and log[-1] == 'ready:b'
+
+
+def test_exception_in_backward_drops_queued_launches(stubs):
+    log, side = stubs
+    with pytest.raises(RuntimeError):
+        with C.async_wgrad(True, blocks=4):
+            with C.side_batch():
+                _launch(side, log, 'a')
+            raise RuntimeError('backward failed')
+    assert log == [] and C._SIDE['items'] == [] and C.side_batch_blocks() == 1
+
+
+def test_callback_cut_does_not_split_a_fork(stubs):
+    log, side = stubs
+    cut = []
+
+    def launch(name):
+        C.side_launch(side, lambda: log.append('run:' + name), (), after=(lambda: cut.append(list(log)),))
+
+    with C.side_batch():
+        launch('a')
+        launch('b')
+    # the first callback (which could end a capture) already sees both launches queued
+    assert cut[0] == ['fork', 'run:a', 'run:b']
 
 
 def test_exception_inside_batch_drops_its_launches(stubs):

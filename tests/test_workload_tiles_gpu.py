@@ -65,7 +65,7 @@ def _bf16_round(t):
     return t.to(torch.bfloat16).float() if t.is_floating_point() else t
 
 
-def _run(cuda, cfg, batch, lr_px, kernels, out_tol, grad_tol, cos_min=0.995, seed=0):
+def _run(cuda, cfg, batch, lr_px, kernels, out_tol, grad_tol, cos_min=0.995, seed=0, l2_tol=0.08):
     from basicsr4rs_amd.archs import build_network
     from basicsr4rs_amd.utils import ktrace
     torch.manual_seed(seed)
@@ -92,19 +92,21 @@ def _run(cuda, cfg, batch, lr_px, kernels, out_tol, grad_tol, cos_min=0.995, see
     d = out.float().detach().cpu().double() - ref.detach()
     err = d.abs().max().item() / rng
     psnr = 10 * math.log10(rng**2 / max(1e-30, (d**2).mean().item()))
-    worst, worst_cos = (0.0, ''), (1.0, '')
+    worst, worst_cos, worst_l2 = (0.0, ''), (1.0, ''), (0.0, '')
     for n, p in gn.named_parameters():
         r = sdg[n].grad
         a = p.grad.detach().cpu().double()
         e = (a - r).abs().max().item() / max(1e-12, r.abs().max().item())
+        l2 = (a - r).norm().item() / max(1e-12, r.norm().item())
         cos = torch.nn.functional.cosine_similarity(a.flatten(), r.flatten(), dim=0).item()
-        worst, worst_cos = max(worst, (e, n)), min(worst_cos, (cos, n))
+        worst, worst_cos, worst_l2 = max(worst, (e, n)), min(worst_cos, (cos, n)), max(worst_l2, (l2, n))
     print(f"{cfg['type']} bf16 B{batch} {lr_px}x{lr_px}: out max err {err:.3e} of range, PSNR {psnr:.1f} dB; "
-          f"worst param-grad err {worst[0]:.3e} ({worst[1]}), lowest cosine {worst_cos[0]:.5f} ({worst_cos[1]}); "
-          f"kernels {sorted(ran)}")
+          f"worst param-grad err {worst[0]:.3e} ({worst[1]}), worst relative L2 {worst_l2[0]:.3e} ({worst_l2[1]}), "
+          f"lowest cosine {worst_cos[0]:.5f} ({worst_cos[1]}); kernels {sorted(ran)}")
     assert err <= out_tol, err
     assert worst_cos[0] >= cos_min, worst_cos
     assert worst[0] <= grad_tol, worst
+    assert worst_l2[0] <= l2_tol, worst_l2
     return stats
 
 
