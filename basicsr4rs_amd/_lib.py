@@ -54,11 +54,10 @@ class DcnDesc(ctypes.Structure):
 SIGNATURES = {
     'sr_version': (ctypes.c_char_p, []),
     'sr_last_error': (ctypes.c_char_p, []),
+    'sr_set_knob': (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_i)]),
+    'sr_get_knob': (_i, [ctypes.c_char_p]),
     'sr_conv3x3_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     'sr_linear_ln_fwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    'sr_linear_ln_bwd_parts': (_i, [ctypes.POINTER(ConvDesc), _i]),
-    'sr_linear_ln_bwd': (_i, [ctypes.POINTER(ConvDesc), _vp, _vp, _vp, _i, _vp, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp,
-                              _vp, _sz, _vp]),
     'sr_conv3x3_fwd_colsum_parts': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_fwd_dot_ok': (_i, [ctypes.POINTER(ConvDesc)]),
     'sr_conv3x3_get_variant': (_i, []),
@@ -163,6 +162,24 @@ def load():
         if v:
             check(lib.sr_conv3x3_set_variant(v))
     return _LIB
+
+
+class knob:
+    """Context: set a library tuning knob (sr_set_knob; the environment variable of the same name
+    read once per process) for the block, restoring the previous value on exit."""
+
+    def __init__(self, name, value):
+        self.name, self.value, self.prev = name.encode(), int(value), None
+
+    def __enter__(self):
+        prev = ctypes.c_int(0)
+        check(load().sr_set_knob(self.name, self.value, ctypes.byref(prev)))
+        self.prev = prev.value
+        return self
+
+    def __exit__(self, *exc):
+        check(load().sr_set_knob(self.name, self.prev, None))
+        return False
 
 
 def check(rc):

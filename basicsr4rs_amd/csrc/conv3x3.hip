@@ -16,6 +16,7 @@
 // bias, activation, ReLU-mask gate, scale, residual, pixel-shuffle / NCHW store with
 // 16-byte coalesced stores.
 #include <cstdlib>
+#include <atomic>
 #include "sr_common.h"
 #include "sr_internal.h"
 
@@ -74,16 +75,6 @@ struct FwdArgs {
   const void* dot;  // band kernel, with colsum: partial sums of y * dot (sr_conv3x3_desc.dot)
   uint32_t d_bytes;
   int ldd, dcoff;
-  // LayerNorm backward fused into linear_wk_kernel's epilogue (sr_linear_ln_bwd): the GEMM output is
-  // dL/d(LN out); y receives dL/dx (+ res), lb_dxs the same times lb_rsc[image]
-  const void* lb_x;
-  int lb_ldx, lb_C;
-  const float* lb_mean;
-  const float* lb_rstd;
-  const float* lb_gamma;
-  float* lb_part;  // [2 * tiles][2][lb_C]: per (token tile, token half) dgamma / dbeta partials
-  void* lb_dxs;
-  const float* lb_rsc;
 };
 
 // alpha of output row m: a.alpha, times the per-image row_scale when given
@@ -1205,209 +1196,12 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 // fc1 forward), 144 (residual + row scale); the bias
 // (GEMM column order), alpha and beta always.
 // ------------------------------------------------------------------------------------
-// LayerNorm backward over the rows linear_wk_kernel just produced (sr_linear_ln_bwd; the reference's
-// norm1 / norm2 autograd, swinir_arch.py:290, 322): with d = bf16(the GEMM output) = dL/d(LN out),
-// xh = (x - mean) rstd and g = d gamma over the C real channels,
-//   dx = rstd (g - mean_c(g) - xh mean_c(g xh)) (+ res),  dgamma += sum_m d xh,  dbeta += sum_m d
-// -- the ln_bwd8_kernel math on the same bf16-rounded d, so the result matches the two-launch path up
-// to fp32 summation order.  The block's one channel tile holds whole rows (Cout <= 192): a token's
-// row sums run over the lane's 24 channels, the 4 lanes of its g group (xor 16 / 32) and the two
-// channel-half waves (through LDS); the column partials over the lane's 4 tokens and the 16 lanes of
-// its c16 group (xor 1..8), one partial row per (token tile, token half).  x is read twice (the
-// second time from L2); dx overwrites nothing the GEMM still reads.
-// sum over the 16 lanes of a DPP row (every lane gets it): rotations by 1, 2, 4, 8 -- VALU DPP moves
-// instead of ds_bpermute (no LDS traffic, no address registers)
-SR_DEV float row16_sum(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x122, 0xf, 0xf, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xf, 0xf, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
-  return v;
-}
-SR_DEV void lb_unpack8(const u32x4& q, float* o) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    o[2 * i] = __uint_as_float(q[i] << 16);
-    o[2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
-  }
-}
-SR_DEV u32x4 lb_pack8(const float* v) {
-  u32x4 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
-  return r;
-}
-template <bool RES>
-SR_DEV void lnb_epilogue(const FwdArgs& a, const f32x4 (&acc)[6][4], char* smem, int m0, int wr, int wc, int g,
-                         int c16, int tt) {
-  const int C = a.lb_C;
-  const float invC = 1.f / (float)C;
-  const size_t xb = (size_t)a.M * a.lb_ldx * 2, yb = (size_t)a.M * a.ldy * 2;
-  const __amdgpu_buffer_rsrc_t lxr = make_rsrc(a.lb_x, xb < 0x80000000ull ? (uint32_t)xb : 0x7fffffffu);
-  const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
-  const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, yb < 0x80000000ull ? (uint32_t)yb : 0x7fffffffu);
-  const __amdgpu_buffer_rsrc_t sr_ = make_rsrc(a.lb_dxs, a.lb_dxs ? (yb < 0x80000000ull ? (uint32_t)yb : 0x7fffffffu) : 0u);
-  // every per-row / per-channel operand through buffer loads with the bound in the descriptor (and
-  // the partial stores through OOB offsets): no branches, so the epilogue stays one scheduling region
-  const __amdgpu_buffer_rsrc_t mur = make_rsrc(a.lb_mean, (uint32_t)a.M * 4u);
-  const __amdgpu_buffer_rsrc_t rsr = make_rsrc(a.lb_rstd, (uint32_t)a.M * 4u);
-  const __amdgpu_buffer_rsrc_t scr = make_rsrc(a.lb_rsc, a.lb_rsc ? (fdiv((uint32_t)a.M - 1u, a.fd_hw) + 1u) * 4u : 0u);
-  const __amdgpu_buffer_rsrc_t gmr = make_rsrc(a.lb_gamma, (uint32_t)C * 4u);
-  const __amdgpu_buffer_rsrc_t pr = make_rsrc(a.lb_part, (uint32_t)(gridDim.x * 2u * 2u * (uint32_t)C * 4u));
-  auto ld1 = [](__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-  };
-  float mu[4], rsd[4], sc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int m = m0 + wc * 64 + j * 16 + c16;
-    mu[j] = ld1(mur, (uint32_t)m * 4u);
-    rsd[j] = ld1(rsr, (uint32_t)m * 4u);
-    sc[j] = ld1(scr, fdiv((uint32_t)m, a.fd_hw) * 4u);
-  }
-  // d of (P, j): the GEMM output rounded to bf16 as the unfused path stores it, kept packed (48 VGPRs
-  // instead of the 96 accumulators: with both passes' operands live the fp32 form spilled)
-  u32x4 dpk[3][4];
-#pragma unroll
-  for (int P = 0; P < 3; ++P)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        dpk[P][j][r] = pack_bf16x2(acc[2 * P][j][2 * r] * a.alpha, acc[2 * P][j][2 * r + 1] * a.alpha);
-        dpk[P][j][2 + r] = pack_bf16x2(acc[2 * P + 1][j][2 * r] * a.alpha, acc[2 * P + 1][j][2 * r + 1] * a.alpha);
-      }
-  __builtin_amdgcn_sched_barrier(0);  // the accumulators die here
-  auto dval = [&](int P, int j, float (&d)[8]) { lb_unpack8(dpk[P][j], d); };
-  auto gam = [&](int n, float (&gm)[8]) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) gm[q] = ld1(gmr, (uint32_t)(n + q) * 4u);
-  };
-  auto xoff = [&](int m, int n) -> uint32_t {
-    return (m < a.M && n < a.Cout) ? (uint32_t)(((size_t)m * a.lb_ldx + n) * 2) : SR_OOB;
-  };
-  // x and gamma of the three channel groups in one round trip (72 VGPRs beside the 48 of d; the
-  // residual follows after pass 1) -- issued per pass, the six dependent HBM round trips of a block
-  // ran serially at two waves per SIMD
-  u32x4 xv[3][4], rv[3][4];
-  float gm[3][8];
-#pragma unroll
-  for (int P = 0; P < 3; ++P) {
-    const int n = (3 * wr + P) * 32 + 8 * g;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xv[P][j] = buf_load16(lxr, xoff(m0 + wc * 64 + j * 16 + c16, n));
-    gam(n, gm[P]);
-  }
-  // pass 1: row sums s1 = sum g, s2 = sum g xh; the column partials, written per P
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int P = 0; P < 3; ++P) {
-    const int n = (3 * wr + P) * 32 + 8 * g;
-    float cg[8], cb[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) cg[q] = cb[q] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float d[8], xf[8];
-      dval(P, j, d);
-      lb_unpack8(xv[P][j], xf);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float xh = n + q < C ? (xf[q] - mu[j]) * rsd[j] : 0.f;
-        const float gq = d[q] * gm[P][q];
-        s1[j] += gq;
-        s2[j] += gq * xh;
-        cg[q] += d[q] * xh;
-        cb[q] += n + q < C ? d[q] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      cg[q] = row16_sum(cg[q]);
-      cb[q] = row16_sum(cb[q]);
-    }
-    const uint32_t pb = (uint32_t)((tt * 2 + wc) * 2 * C + n) * 4u;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const bool ok = c16 == 0 && n + q < C;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cg[q]), pr, ok ? pb + 4u * q : SR_OOB, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cb[q]), pr, ok ? pb + 4u * (C + q) : SR_OOB, 0, 0);
-    }
-  }
-  // the residual (pass 2 only) in flight across the row-sum exchange
-  if constexpr (RES) {
-#pragma unroll
-    for (int P = 0; P < 3; ++P) {
-      const int n = (3 * wr + P) * 32 + 8 * g;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + wc * 64 + j * 16 + c16;
-        rv[P][j] = buf_load16(rr, (m < a.M && n < a.Cout && n < a.rcols) ? (uint32_t)(((size_t)m * a.ldr + a.rcoff + n) * 2) : SR_OOB);
-      }
-    }
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    s1[j] += __shfl_xor(s1[j], 16);
-    s1[j] += __shfl_xor(s1[j], 32);
-    s2[j] += __shfl_xor(s2[j], 16);
-    s2[j] += __shfl_xor(s2[j], 32);
-  }
-  // the other channel half's sums (both waves add the same two numbers: a + b == b + a)
-  float* red = (float*)smem;  // [2 wr][2 wc][4 j][16][2]
-  __syncthreads();             // every wave is past its last MFMA-operand read of the stages
-  if (g == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      red[((((wr * 2 + wc) * 4 + j) * 16 + c16) * 2)] = s1[j];
-      red[((((wr * 2 + wc) * 4 + j) * 16 + c16) * 2) + 1] = s2[j];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    s1[j] = (s1[j] + red[(((((1 - wr) * 2 + wc) * 4 + j) * 16 + c16) * 2)]) * invC;
-    s2[j] = (s2[j] + red[(((((1 - wr) * 2 + wc) * 4 + j) * 16 + c16) * 2) + 1]) * invC;
-  }
-  // pass 2: dx = rstd (g - s1 - xh s2) (+ res), and its row-scaled copy
-#pragma unroll
-  for (int P = 0; P < 3; ++P) {
-    const int n = (3 * wr + P) * 32 + 8 * g;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wc * 64 + j * 16 + c16;
-      float d[8], xf[8], o[8];
-      dval(P, j, d);
-      lb_unpack8(xv[P][j], xf);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float xh = (xf[q] - mu[j]) * rsd[j];
-        o[q] = n + q < C ? rsd[j] * (d[q] * gm[P][q] - s1[j] - xh * s2[j]) : 0.f;
-      }
-      if constexpr (RES) {
-        float rf[8];
-        lb_unpack8(rv[P][j], rf);
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (n + q < C) o[q] += rf[q];
-      }
-      const uint32_t yo = (m < a.M && n < a.Cout) ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB;
-      __builtin_amdgcn_raw_buffer_store_b128(lb_pack8(o), yr, yo, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] *= sc[j];
-      __builtin_amdgcn_raw_buffer_store_b128(lb_pack8(o), sr_, yo, 0, 0);  // size-0 descriptor without row scale
-    }
-  }
-}
-
 template <int E>
 __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
   constexpr int XI = 128 * 128, WI = 192 * 128, STAGE = XI + WI;
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
-  constexpr bool RES = (E & 16) != 0, AUX = (E & 64) != 0, RSC = (E & 128) != 0, LNB = (E & 256) != 0;
-  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 64 | 128 | 256)) == 0, "linear_wk: epilogue subset");
-  static_assert(!LNB || (E & ~(16 | 256)) == 0, "linear_wk: the LayerNorm-backward epilogue takes a residual only");
+  constexpr bool RES = (E & 16) != 0, AUX = (E & 64) != 0, RSC = (E & 128) != 0;
+  static_assert(GATE != 3 && (E & ~(3 | 12 | 16 | 64 | 128)) == 0, "linear_wk: epilogue subset");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1484,10 +1278,6 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
 
   // ---- epilogue: pair P (tiles 2P, 2P + 1) gives channels n = n0 + (3 wr + P) * 32 + 8g .. + 7 of
   // token m0 + 64 wc + 16 j + c16
-  if constexpr (LNB) {
-    lnb_epilogue<RES>(a, acc, smem, m0, wr, wc, g, c16, tt);
-    return;
-  }
   const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
   const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
   const size_t ybytes = (size_t)a.M * a.ldy * 2;
@@ -2756,7 +2546,12 @@ struct WgArgs {
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   int bias_group;  // pp kernel: > 0 = the bias-role blocks come after all tile blocks, each doing this many splits
   int bias_fused;  // pp kernel: no bias-role blocks; the centre-tap, first-ci-tile blocks sum dy as well
-  int ring_early;  // ring kernel: issue step ks + D before step ks's MFMAs (one barrier per step)
+  // ring kernel in-kernel split reduce (red_g > 1): level-2 slab [S / G][9][Cin][Cout] + bias rows,
+  // the counter bank, and the byte sizes of the buffer descriptors
+  int red_g, red_bank;
+  float* red_ws;
+  float* red_wsb;
+  uint32_t ws_bytes, wsb_bytes, red_ws_bytes;
   FastDiv fd_W, fd_H, fd_cps;
   unsigned long long* stamps;  // diagnostics (SR_BAND_STAMPS builds): per-block phase cycles
 };
@@ -3707,611 +3502,50 @@ __global__ __launch_bounds__(512) void linear_wgrad_kernel(WgArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
-// Weight gradient, tap-row form (bf16, Cout and Cin multiples of 128, W % 64 == 0): a block owns
-// one kernel row ty and a 128 (co) x 128 (ci) tile of all THREE taps of that row over a pixel
-// K-range.  A 64-pixel K-step is one image-row segment; per step it DMA's the dy tile [64 px][128
-// co] (16 KB) once for the three taps and ONE x halo row [66 px][128 ci] (17 KB: pixels x0-1 ..
-// x0+64 of input row y+ty-1) whose rows t .. t+63 are tap t's B operand -- 33 KB per 3.1 M MACs
-// against the per-tap pp kernel's 64 KB per 4.2 M (ablation on the EDSR-L body shape: that
-// kernel's MFMA-only and DMA-only runs take 117 / 122 us and 192 us together).  Waves (wr, wc)
-// own co wr*64 .. +64 x ci wc*32 .. +32 of every tap (24 accumulator tiles); a K-step is three
-// phases, one per tap (16 MFMAs each, the A fragments read once in the first), waves 4-7 one
-// barrier behind waves 0-3 as in the pp kernels.  Stages are triple-buffered: step t+2's dy
-// (phase 0) and halo row (phase 1) are issued during step t and a counted wait at phase 2 retires
-// step t+1.  Fragment reads finish (lgkmcnt) before each barrier, so a stage refilled after that
-// barrier has no reader left.  Output: the [S][9][Cout][Cin] slab of the pp kernel (same reduce).
-// ------------------------------------------------------------------------------------
-template <int DBG = 0>  // timing ablations (wrong results): 1 no DMA, 2 no MFMA, 3 no lgkmcnt waits
-__global__ __launch_bounds__(512) void conv3x3_wgrad_tr3_kernel(WgArgs a) {
-  constexpr int DYB = 64 * 256;          // dy image [64 px][256 B], stage s at s * DYB
-  constexpr int XB = 68 * 256;           // x halo image [66 (68) px][256 B], stage s at XOFF + s * XB
-  constexpr int XOFF = 3 * DYB;
-  constexpr int DUMMY = XOFF + 3 * XB;   // target of the padding DMAs
-  constexpr int CSTR = 128 + 4;
-  constexpr int EPI = 128 * CSTR * 4;    // one tap's 128 x 128 fp32 tile
-  constexpr int SMEM = (DUMMY + 1024 > EPI ? DUMMY + 1024 : EPI);
-  static_assert(SMEM >= 2 * 64 * 512, "bias role LDS");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 2, wc = w & 3;
-  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = 3 * a.tiles_co * a.tiles_ci;
-  const int per_split = ntile + (a.wsb ? (a.Cout + 255) / 256 : 0);
-  const int split = (int)b / per_split;
-  int rem = (int)b - split * per_split;
-  if (rem >= ntile) {
-    wgrad_bias_role(a, smem, split, (rem - ntile) * 256);
-    return;
-  }
-  const int ty = rem / (a.tiles_co * a.tiles_ci);
-  rem -= ty * a.tiles_co * a.tiles_ci;
-  const int co0 = (rem / a.tiles_ci) * 128;
-  const int ci0 = (rem % a.tiles_ci) * 128;
-  const int p_begin = split * a.kper;
-  const int p_end = min(a.M, p_begin + a.kper);
-  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
-  const int rps = a.out_ps > 0 ? a.out_ps : 1;
-
-  // DMA lanes: instruction q of an image covers rows 4q .. 4q+3, lane -> row 4q + (lane >> 4),
-  // 16-B slot lane & 15 holding the logical chunk lc of the swizzled 256-B row
-  auto lchunk = [&](int R) {
-    const int f = (R & 3) | (((R >> 3) & 1) << 2);
-    const int sl = lane & 15;
-    return (((sl >> 1) ^ f) << 1) | (sl & 1);
-  };
-  uint32_t la[2];  // dy rows 8w + 4j + (lane >> 4)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int R = 8 * w + 4 * j + (lane >> 4);
-    la[j] = (uint32_t)(R * rps * a.ldy) * 2u + (uint32_t)lchunk(R) * 16u;
-  }
-  int xR[3];       // halo rows of this wave's 3 instructions (q = w, w + 8, w + 16; q > 16: padding)
-  uint32_t lx[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int q = w + 8 * j;
-    const int R = 4 * q + (lane >> 4);
-    xR[j] = q <= 16 && R < 66 ? R : -1000000;
-    lx[j] = (uint32_t)(R * a.ldx) * 2u + (uint32_t)lchunk(R) * 16u;
-  }
-
-  // scalar state of the step being issued
-  int s_ua = 0, s_ub = 0, s_xm1 = 0, s_yv = 0;
-  auto k_eval = [&](int ks) {
-    const int p0s = p_begin + ks * 64;
-    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
-    const int x0 = p0s - q * a.W;
-    const int n = (int)fdiv((uint32_t)q, a.fd_H);
-    const int y = q - n * a.H;
-    int ua;
-    if (a.out_ps == 0) {
-      ua = (p0s * a.ldy + a.ycoff + co0) * 2;
-    } else {
-      const int r = a.out_ps;
-      const int sl = (int)fdiv((uint32_t)co0, a.fd_cps);
-      const int cch = co0 - sl * a.fd_cps.d;
-      const int si = sl / r, sj = sl - si * r;
-      ua = (((q * r + si) * (a.W * r) + x0 * r + sj) * a.ldy + a.ycoff + cch) * 2;
-    }
-    const int yy = y + ty - 1;
-    s_ua = __builtin_amdgcn_readfirstlane(ua);
-    s_ub = __builtin_amdgcn_readfirstlane((((n * a.H + yy) * a.W + x0 - 1) * a.ldx + a.xcoff + ci0) * 2);
-    s_xm1 = __builtin_amdgcn_readfirstlane(x0 - 1);
-    s_yv = __builtin_amdgcn_readfirstlane((unsigned)yy < (unsigned)a.H ? 1 : 0);
-  };
-  auto issue_dy = [&](int ks, bool real) {
-    if (DBG == 1 && ks > 1) real = false;
-    char* dst = smem + (ks % 3) * DYB + w * 2048;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(dyr, real ? dst + j * 1024 : smem + DUMMY, real ? (uint32_t)s_ua + la[j] : SR_OOB);
-  };
-  auto issue_x = [&](int ks, bool real) {
-    if (DBG == 1 && ks > 1) real = false;
-    char* img = smem + XOFF + (ks % 3) * XB;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int q = w + 8 * j;
-      const bool v = real && s_yv && (unsigned)(s_xm1 + xR[j]) < (unsigned)a.W;
-      glds16(xr, (real && q <= 16) ? img + q * 1024 : smem + DUMMY, v ? (uint32_t)s_ub + lx[j] : SR_OOB);
-    }
-  };
-
-  // Fragment reads: per-lane swizzled offsets computed once (kk = 0 rows; kk = 1 is +8192 B, the
-  // stage a compile-time offset), so a read costs no VALU (the per-read swz_tr math doubled the
-  // kernel's VALU count against the pp kernel's)
-  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-  uint32_t offA[4][2], offX[3][2][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) offA[i][hl] = swz_tr(8 * tg + tq + 4 * hl, (wr * 64 + i * 16 + 4 * tp) * 2, 256);
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl)
-        offX[t][j][hl] = XOFF + swz_tr(t + 8 * tg + tq + 4 * hl, (wc * 32 + j * 16 + 4 * tp) * 2, 256);
-  auto lds_tr = [&](uint32_t off) -> s16x4 {
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(smem + off));
-  };
-  auto cat8 = [](s16x4 lo, s16x4 hi) { return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}; };
-  s16x8 fa[2][4], fb[2][2];
-  auto read_a = [&](int st) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        fa[kk][i] = cat8(lds_tr(offA[i][0] + st * DYB + kk * 8192), lds_tr(offA[i][1] + st * DYB + kk * 8192));
-  };
-  auto read_b = [&](int st, int t) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[kk][j] = cat8(lds_tr(offX[t][j][0] + st * XB + kk * 8192), lds_tr(offX[t][j][1] + st * XB + kk * 8192));
-  };
-  f32x4 acc[3][4][2];
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](int t) {
-    if constexpr (DBG == 2) return;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][i], fb[kk][j], acc[t][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int nk = (p_end - p_begin) / 64;  // >= 1 (whole 64-px row segments)
-  k_eval(0);
-  issue_dy(0, true);
-  issue_x(0, true);
-  if (nk > 1) k_eval(1);
-  issue_dy(1, nk > 1);
-  issue_x(1, nk > 1);
-  asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // step 0 landed (step 1's 5 in flight)
-  pp_barrier();
-  if (wr) pp_barrier();  // stagger: waves 4-7 run one barrier behind
-  auto step = [&](int t, const int st) {
-    const bool more = t + 2 < nk;
-    // phase 0: tap 0, A fragments; issue dy(t + 2)
-    read_a(st);
-    read_b(st, 0);
-    if (more) k_eval(t + 2);
-    issue_dy(t + 2, more);
-    if (DBG != 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pp_barrier();
-    mma(0);
-    pp_barrier();
-    // phase 1: tap 1; issue the halo row of step t + 2
-    read_b(st, 1);
-    issue_x(t + 2, more);
-    if (DBG != 3) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pp_barrier();
-    mma(1);
-    pp_barrier();
-    // phase 2: tap 2; retire step t + 1 (step t + 2's 5 DMAs stay in flight)
-    read_b(st, 2);
-    if (DBG != 3) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    pp_barrier();
-    mma(2);
-    pp_barrier();
-  };
-#pragma unroll 1
-  for (int t = 0; t < nk; ++t) step(t, t % 3);  // (a 3-way unrolled stage loop spilled)
-  if (!wr) pp_barrier();  // balance the stagger
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  float* Cs = (float*)smem;
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CSTR + wc * 32 + j * 16 + (lane & 15)] = acc[t][i][j][r];
-    __syncthreads();
-    float* ws = a.ws + ((size_t)split * 9 + ty * 3 + t) * a.Cout * a.Cin;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = tid + k * 512;
-      const int row = idx >> 5, c4 = (idx & 31) * 4;
-      *(f32x4*)(ws + (size_t)(co0 + row) * a.Cin + ci0 + c4) = *(const f32x4*)(Cs + row * CSTR + c4);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Tap-row weight gradient over 12 waves (round 4): a block owns kernel row ty (taps 3 ty + tx),
-// a 128 (co) x 128 (ci) tile and a pixel K-range of whole 64-px row segments.  Per K-step it DMAs
-// the dy tile [64 px][128 co] and ONE x halo row [66 px][128 ci] (x row y + ty - 1, columns
-// x0 - 1 .. x0 + 64) -- 33 KB for 3 x 128 x 128 x 64 MACs, against the pp kernel's 64 KB for
-// 256 x 256 x 64: 1.5x fewer L2 -> LDS bytes per MAC (the pp kernel is bound by them: DMA-only
-// 121 us, MFMA-only 116 us, both 184 us on the EDSR-L body, DESIGN.md note 2c).  Wave w = (tap
-// tx = w / 4, co half, ci half) owns 64 x 64 of one tap (16 accumulator tiles, 64 registers), so
-// the three taps' MFMAs run on different waves at once instead of in three barrier-separated
-// phases (conv3x3_wgrad_tr3_kernel: six barriers per step, 172 us MFMA + LDS only).  Three stages,
-// two steps in flight, ONE barrier per step; every wave issues exactly three 1-KB LDS-DMAs per
-// step (dy pieces, x pieces, padding to a dummy slot), so its vmcnt waits are constants.  Bias
-// gradient by grouped bias-role blocks (the pp kernel's, 8 waves of 12).  Slab and reduce: the pp
-// kernel's [split][tap][co][ci].  DBG (timing ablations, wrong results): 1 no DMA after the
-// prologue, 2 no MFMA.
-// ------------------------------------------------------------------------------------
-template <int DBG = 0>
-__global__ __launch_bounds__(768, 1) void conv3x3_wgrad_tw_kernel(WgArgs a) {
-  constexpr int DYB = 64 * 256;          // dy image [64 px][256 B], stage s at s * DYB
-  constexpr int XB = 68 * 256;           // x halo image [66 (68) px][256 B], stage s at XOFF + s * XB
-  constexpr int XOFF = 3 * DYB;
-  constexpr int DUMMY = XOFF + 3 * XB;   // target of the padding DMAs
-  constexpr int SMEM = DUMMY + 1024;
-  static_assert(SMEM >= 64 * 1024 + 32 * 1024, "bias role LDS");
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int ntile = 3 * a.tiles_co * a.tiles_ci;
-  if ((int)b >= a.splits * ntile) {  // bias role: bias_group splits of one 256-co tile (8 waves)
-    if (w >= 8) return;
-    const int bb = (int)b - a.splits * ntile;
-    const int t256 = (a.Cout + 255) / 256;
-    const int grp = bb / t256, co_t = bb - grp * t256;
-    const int s1 = min(a.splits, (grp + 1) * a.bias_group);
-    for (int sp = grp * a.bias_group; sp < s1; ++sp) {
-      if (sp > grp * a.bias_group) __syncthreads();
-      wgrad_bias_role(a, smem, sp, co_t * 256);
-    }
-    return;
-  }
-  const int split = (int)b / ntile;
-  int rem = (int)b - split * ntile;
-  const int ty = rem / (a.tiles_co * a.tiles_ci);
-  rem -= ty * a.tiles_co * a.tiles_ci;
-  const int co0 = (rem / a.tiles_ci) * 128;
-  const int ci0 = (rem % a.tiles_ci) * 128;
-  const int p_begin = split * a.kper;
-  const int p_end = min(a.M, p_begin + a.kper);
-  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
-
-  // DMA slots m = 0..2 of this wave: slot s = w + 12 m < 16: dy piece s (rows 4s ..); < 33: x piece
-  // s - 16 (halo rows 4(s - 16) ..); else the dummy target.  Lane -> row base + (lane >> 4), 16-B
-  // slot lane & 15 holding the logical chunk lc of the swizzled 256-B row.
-  auto lchunk = [&](int R) {
-    const int f = (R & 3) | (((R >> 3) & 1) << 2);
-    const int sl = lane & 15;
-    return (((sl >> 1) ^ f) << 1) | (sl & 1);
-  };
-  int kind[3], lrow[3];
-  uint32_t loff[3];
-#pragma unroll
-  for (int m = 0; m < 3; ++m) {
-    const int sl = w + 12 * m;
-    kind[m] = sl < 16 ? 0 : (sl < 33 ? 1 : 2);
-    const int R = (kind[m] == 0 ? 4 * sl : 4 * (sl - 16)) + (lane >> 4);
-    lrow[m] = kind[m] == 1 ? (R < 66 ? R : -1000000) : R;
-    loff[m] = kind[m] == 0 ? (uint32_t)(R * a.ldy) * 2u + (uint32_t)lchunk(R) * 16u
-                           : (uint32_t)(R * a.ldx) * 2u + (uint32_t)lchunk(R) * 16u;
-  }
-  int s_ua = 0, s_ub = 0, s_xm1 = 0, s_yv = 0;
-  auto k_eval = [&](int ks) {
-    const int p0s = p_begin + ks * 64;
-    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
-    const int x0 = p0s - q * a.W;
-    const int n = (int)fdiv((uint32_t)q, a.fd_H);
-    const int y = q - n * a.H;
-    const int yy = y + ty - 1;
-    s_ua = __builtin_amdgcn_readfirstlane((p0s * a.ldy + a.ycoff + co0) * 2);
-    s_ub = __builtin_amdgcn_readfirstlane((((n * a.H + yy) * a.W + x0 - 1) * a.ldx + a.xcoff + ci0) * 2);
-    s_xm1 = __builtin_amdgcn_readfirstlane(x0 - 1);
-    s_yv = __builtin_amdgcn_readfirstlane((unsigned)yy < (unsigned)a.H ? 1 : 0);
-  };
-  auto issue = [&](int ks, bool real) {
-    if (DBG == 1 && ks > 1) real = false;
-    const int st = ks % 3;
-#pragma unroll
-    for (int m = 0; m < 3; ++m) {
-      const int sl = w + 12 * m;
-      if (kind[m] == 0) {
-        glds16(dyr, real ? smem + st * DYB + sl * 1024 : smem + DUMMY, real ? (uint32_t)s_ua + loff[m] : SR_OOB);
-      } else if (kind[m] == 1) {
-        const bool v = real && s_yv && (unsigned)(s_xm1 + lrow[m]) < (unsigned)a.W;
-        glds16(xr, real ? smem + XOFF + st * XB + (sl - 16) * 1024 : smem + DUMMY, v ? (uint32_t)s_ub + loff[m] : SR_OOB);
-      } else {
-        glds16(xr, smem + DUMMY, SR_OOB);
-      }
-    }
-  };
-
-  // fragment offsets (kk = 0 rows; kk = 1 is +8192 B), computed once
-  const int tx = w >> 2, wco = (w >> 1) & 1, wci = w & 1;
-  const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-  uint32_t offA[4][2], offB[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) {
-      offA[i][hl] = swz_tr(8 * tg + tq + 4 * hl, (wco * 64 + i * 16 + 4 * tp) * 2, 256);
-      offB[i][hl] = XOFF + swz_tr(tx + 8 * tg + tq + 4 * hl, (wci * 64 + i * 16 + 4 * tp) * 2, 256);
-    }
-  auto lds_tr = [&](uint32_t off) -> s16x4 {
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(smem + off));
-  };
-  auto cat8 = [](s16x4 lo, s16x4 hi) { return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]}; };
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (p_end - p_begin) / 64;  // >= 1 (whole 64-px row segments)
-  k_eval(0);
-  issue(0, true);
-  if (nk > 1) k_eval(1);
-  issue(1, nk > 1);
-  for (int ks = 0; ks < nk; ++ks) {
-    if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // step ks + 1's 3 DMAs stay in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-    // stage (ks + 2) % 3 was last read in step ks - 1, finished by every wave before this barrier
-    if (ks + 2 < nk) {
-      k_eval(ks + 2);
-      issue(ks + 2, true);
-    } else {
-      issue(ks + 2, false);  // keep the per-step DMA count (vmcnt arithmetic) constant
-    }
-    const int st = ks % 3;
-    const uint32_t sa = st * DYB, sb = st * XB;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      s16x8 fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = cat8(lds_tr(offA[i][0] + sa + kk * 8192), lds_tr(offA[i][1] + sa + kk * 8192));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = cat8(lds_tr(offB[j][0] + sb + kk * 8192), lds_tr(offB[j][1] + sb + kk * 8192));
-      if constexpr (DBG != 2) {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // slab [split][tap][co][ci]: 16 lanes store 64 consecutive bytes of a co row
-  const int tap = 3 * ty + tx;
-  float* ws = a.ws + ((size_t)split * 9 + tap) * a.Cout * a.Cin;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * 64 + 16 * i + 4 * tg + r;
-        const int ci = ci0 + wci * 64 + 16 * j + (lane & 15);
-        ws[(size_t)co * a.Cin + ci] = acc[i][j][r];
-      }
-}
-
-// ------------------------------------------------------------------------------------
-// Weight gradient for narrow convs (Cout <= 64: RCAN / RRDB / SRResNet bodies), all nine
-// taps in one block.  A 64-pixel K-step is one image-row segment (W % 64 == 0); the block
-// stages dy[64 px][Cout] once and the x halo rows y-1..y+1, cols x0-1..x0+64 of its
-// 64-channel chunk once, and forms every tap's GEMM from LDS (the x bytes are read from
-// L2 once per step instead of once per tap).  Wave w owns ci tile w (16 channels) x all co
-// tiles x 9 taps (36*CO_T accumulators); operands by ds_read_b64_tr_b16.  LDS images are
-// [tile][row][32 B] with row r stored at r ^ ((r >> 3) & 1) << 2: the rows a 32-lane half
-// reads ({b..b+3} u {b+8..b+11}, any base b) hit distinct 32-B bank slots.  Both images are
-// filled by LDS-DMA, two stages in flight.  Nearest-neighbour input upsampling (in_up 2,
-// RRDBNet conv_up*) is folded into the halo gather.
+// Weight gradient for narrow convs (Cout <= 64: RCAN / RRDB / SRResNet bodies; or 64-channel output
+// tiles of a wider conv, wg_ring_wide), all nine taps in one block, whole image rows per split
+// (W % 64 == 0).  The block walks each 64-px column segment of its rows top to bottom, so a K-step
+// loads ONE new x halo row (66 px of a 16-ci tile per wave) into a ring and dy[64 px][Cout] once;
+// rows above / below an image read a zero slot (x read ~once per pass instead of ~3x).  Every tap's
+// GEMM is formed from LDS.  Wave w owns ci tile w (16 channels) x all co tiles x 9 taps (36 * CO_T
+// accumulator tiles, pinned to AGPRs); operands by ds_read_b64_tr_b16.  LDS images are
+// [tile][row][32 B] with row r stored at r ^ ((r >> 3) & 1) << 2: the rows a 32-lane half reads
+// ({b..b+3} u {b+8..b+11}, any base b) hit distinct 32-B bank slots.  Both images are filled by
+// LDS-DMA, two steps in flight.  Nearest-neighbour input upsampling (in_up 2, RRDBNet conv_up*) is
+// folded into the halo gather; pixel-shuffled dy (the wide form) into the dy gather.  The first
+// step of a segment loads its three rows itself, after the previous segment's last step (its slots
+// may still be read), so a block has nseg - 1 one-step bubbles.
+// (Round 4's variants -- two row groups or two co groups per 8-wave block, co split over blocks,
+// early DMA issue, deeper pipelines -- all measured slower and were removed in round 5.)
+//
+// Output: the block's [tap][ci][co] partial sums (co fastest: a lane's 4 accumulator rows are 4
+// consecutive co, one 16-B store per (tap, co tile)) into slab row `split` of [S][9][Cin][Cout].
+// In-kernel split reduce (a.red_g = G > 1, round 5): the slab rows are stored write-through (sc1),
+// every wave drains them, and one lane takes a ticket on the (group of G splits, tile) counter; the
+// block that draws the group's last ticket sums the group's rows IN SPLIT ORDER (its own from its
+// registers, the others by sc1 loads: the hand-off of cdna_hip_programming.md §6 Guideline 16, R1 --
+// no fence, correct for any XCD placement), writes the sum into row `group` of the level-2 slab
+// (a.red_ws / a.red_wsb) and resets the counter for the next launch.  The standalone reduce then
+// reads S / G rows instead of S.  Deterministic: the order is fixed whichever block arrives last.
 // ------------------------------------------------------------------------------------
 SR_DEV int hrow(int r) { return r ^ (((r >> 3) & 1) << 2); }
 
+constexpr int RING_CNT_BANKS = 64, RING_CNT_PER = 2048;  // ticket counters: a bank per launch (cycled)
+__device__ unsigned g_ring_cnt[RING_CNT_BANKS * RING_CNT_PER];  // zero at load; last arrivers reset theirs
+
 template <int CO_T>
-__global__ __launch_bounds__(256) void conv3x3_wgrad_halo_kernel(WgArgs a) {
-  constexpr int HT = 7 * 1024;      // halo image of one 16-ci tile: 224 rows x 32 B (198 used)
-  constexpr int HALO = 4 * HT;
-  constexpr int DYB = CO_T * 2048;  // dy image: CO_T tiles x 64 rows x 32 B
-  constexpr int STAGE = HALO + DYB + 1024;  // + 1 KB target for padding DMAs
-  constexpr int DYI = (CO_T * 2 + 3) / 4;   // dy DMAs per wave
-  constexpr int NDMA = 7 + DYI;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = (int)b / a.tiles_ci;
-  const int chunk = (int)b - split * a.tiles_ci;
-  const int ci0 = chunk * 64;
-  const int p_begin = split * a.kper;
-  const int p_end = min(a.M, p_begin + a.kper);
-  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
-  const int sh = a.in_up > 1 ? 1 : 0;  // in_up is 1 or 2 here
-  const int Hs = a.H >> sh, Ws = a.W >> sh;
-
-  // halo rows of this lane's 7 DMAs: physical row 32i + (lane >> 1), channel half lane & 1
-  int hty[7], htx[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int hr = hrow(32 * i + (lane >> 1));
-    hty[i] = hr < 198 ? hr / 66 : -100000;
-    htx[i] = hr < 198 ? hr - (hr / 66) * 66 : 0;
-  }
-  const int cil = ci0 + w * 16 + (lane & 1) * 8;
-  const bool civ = cil < a.Cin;
-
-  f32x4 acc[9][CO_T], accb[CO_T];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int c = 0; c < CO_T; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < CO_T; ++c) accb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = a.wsb != nullptr && chunk == 0 && w == 0;
-
-  auto issue = [&](int ks, int buf) {
-    const int p0s = p_begin + ks * 64;
-    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
-    const int x0 = p0s - q * a.W;
-    const int n = (int)fdiv((uint32_t)q, a.fd_H);
-    const int y = q - n * a.H;
-    char* hd = smem + buf * STAGE + w * HT;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int yy = y - 1 + hty[i], xx = x0 - 1 + htx[i];
-      const bool v = civ && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
-      const uint32_t off = (uint32_t)((((n * Hs + (yy >> sh)) * Ws + (xx >> sh)) * a.ldx + a.xcoff + cil) * 2);
-      glds16(xr, hd + i * 1024, v ? off : SR_OOB);
-    }
-    const int left = p_end - p0s;
-#pragma unroll
-    for (int i = 0; i < DYI; ++i) {
-      const int k = w + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
-      char* dst = smem + buf * STAGE + HALO + DYB;
-      uint32_t off = SR_OOB;
-      if (k < CO_T * 2) {
-        const int pr = hrow((k & 1) * 32 + (lane >> 1));
-        const int co = (k >> 1) * 16 + (lane & 1) * 8;
-        dst = smem + buf * STAGE + HALO + k * 1024;
-        if (pr < left && co < a.Cout) off = (uint32_t)(((p0s + pr) * a.ldy + a.ycoff + co) * 2);
-      }
-      glds16(dyr, dst, off);
-    }
-  };
-
-  const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-  auto tr2 = [&](const char* img, int r0) -> s16x8 {  // rows r0 + tq (K 0..3), r0 + 4 + tq (K 4..7)
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0 + tq) * 32 + tp * 8));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0 + 4 + tq) * 32 + tp * 8));
-    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
-  auto compute = [&](int buf) {
-    const char* hs = smem + buf * STAGE + w * HT;
-    const char* ds = smem + buf * STAGE + HALO;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      s16x8 fa[CO_T];
-#pragma unroll
-      for (int c = 0; c < CO_T; ++c) fa[c] = tr2(ds + c * 2048, kk * 32 + 8 * g);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const s16x8 fb = tr2(hs, (t / 3) * 66 + (t % 3) + kk * 32 + 8 * g);
-#pragma unroll
-        for (int c = 0; c < CO_T; ++c) acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c], fb, acc[t][c], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      if (do_bias) {
-#pragma unroll
-        for (int c = 0; c < CO_T; ++c) accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c], ones, accb[c], 0, 0, 0);
-      }
-    }
-  };
-
-  const int nk = (p_end - p_begin + 63) / 64;  // >= 1
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
-  for (int ks = 0; ks < nk; ++ks) {
-    if (ks + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    compute(ks & 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (ks + 2 < nk) issue(ks + 2, ks & 1);
-  }
-
-  const int c16 = lane & 15;
-  const int ci = ci0 + w * 16 + c16;
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    float* ws = a.ws + ((size_t)split * 9 + t) * a.Cout * a.Cin;
-#pragma unroll
-    for (int c = 0; c < CO_T; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = c * 16 + g * 4 + r;
-        if (co < a.Cout && ci < a.Cin) ws[(size_t)co * a.Cin + ci] = acc[t][c][r];
-      }
-  }
-  if (do_bias && c16 == 0) {
-#pragma unroll
-    for (int c = 0; c < CO_T; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = c * 16 + g * 4 + r;
-        if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
-      }
-  }
-}
-
-// Row-streaming form of the halo wgrad (whole image rows per split, W % 64 == 0): the block walks
-// each 64-px column segment of its rows top to bottom, so a K-step loads ONE new x halo row (66 px
-// of a 16-ci tile) into a ring instead of three rows; the rows above / below an image read a zero
-// slot (x read ~once per pass instead of ~3x).  Wave w owns ci tile w and all co tiles (9 x CO_T
-// accumulator tiles, pinned to AGPRs).  (An 8-wave form, two waves per SIMD over halves of the co
-// tiles, ran its two groups in lock-step between the per-step barriers and was slower.)  The
-// first step of a segment loads its three rows itself, after the previous segment's last step
-// (its slots may still be read), so a block has nseg - 1 one-step bubbles.
-// EARLY (opt-in, SR_RING_EARLY=1, one image-row segment per block row): step ks + D is issued right
-// after step ks's barrier, before its MFMAs, into a slot / dy stage nobody reads in step ks (one more
-// ring slot and dy stage), so a step needs ONE barrier; otherwise the issue waits for a second barrier
-// after the MFMAs.  Measured slower: the extra LDS (RCAN 78 -> 99 KB, RRDB 70 -> 87 KB) costs the
-// second block per CU (RRDB 65.5 -> 73 ms).  LA: fragment reads in flight ahead of the MFMA group.
-// VB = 2 (round 4): an 8-wave block of two 4-wave row groups, each with its own ring and dy stages
-// (2 x 78 KB of LDS), walking the two halves of the split's rows in lock-step (same barriers; a
-// group with fewer rows idles through the extra steps); at the end group 1 hands its accumulators
-// to group 0 through LDS and group 0 writes ONE slab for the block.  Against two 4-wave blocks per
-// CU (VB = 1) it halves the slab written per CU (and read by the reduce) at the same occupancy.
-// CS = 2 (round 4): an 8-wave block of two 4-wave CO groups over the same rows: both read one x ring
-// (loaded by group 0), group c multiplies the c-th half of the dy tiles.  Against two 4-wave blocks
-// per CU it halves the slab (and the reduce) and the x DMAs per pixel at the same MFMA work per
-// SIMD, with half the accumulators per wave (no spill at CO_T 4).
-template <int CO_T, int D = 2, int LA = 3, bool EARLY = false, int VB = 1, int CS = 1>  // D: steps in flight
-__global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
-  static_assert(VB == 1 || (VB == 2 && !EARLY), "two row groups: the two-barrier schedule only");
-  static_assert(CS == 1 || (CS == 2 && VB == 1 && !EARLY && CO_T % 2 == 0), "co split: even co tiles, one row group");
-  constexpr int CW = CO_T / CS;  // co tiles per wave
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
+  constexpr int D = 2;              // steps in flight
+  constexpr int LA = 3;             // fragment reads ahead of the MFMA group that needs them
   constexpr int RS = 3 * 1024;      // one halo row of one 16-ci tile: 96 rows x 32 B (66 used)
-  constexpr int RSL = D + (EARLY ? 3 : 2);  // ring slots: rows q-1 .. q+1 read, D - 1 in flight (+1 being issued)
+  constexpr int RSL = D + 2;        // ring slots: rows q-1 .. q+1 read, D - 1 in flight (+1 being issued)
   constexpr int RING = (RSL + 1) * RS;  // + the zero slot, per ci tile
   constexpr int DYB = CO_T * 2048;  // dy image: CO_T tiles x 64 rows x 32 B
   constexpr int DYS = DYB + 1024;   // + 1 KB target for padding DMAs
-  constexpr int NWD = 4 * CS;  // waves sharing the dy DMAs of a step
-  constexpr int DYI = (CO_T * 2 + NWD - 1) / NWD;  // dy DMAs per wave
-  constexpr int DST = D + (EARLY ? 1 : 0);  // dy stages
-  constexpr int GRP = 4 * RING + DST * DYS;  // LDS of one row group
-  static_assert(VB == 1 || GRP * VB >= (4 * 9 * CW + CW) * 64 * 16, "LDS hand-over of group 1's accumulators");
-  __shared__ __attribute__((aligned(16))) char smem[VB * GRP];
+  constexpr int DYI = (CO_T * 2 + 3) / 4;  // dy DMAs per wave
+  __shared__ __attribute__((aligned(16))) char smem[4 * RING + D * DYS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wl = w & 3;  // wave within its row group
-  const int vb = VB > 1 ? w >> 2 : 0;  // row group
-  const int cs = CS > 1 ? w >> 2 : 0;  // co group
-  const int wd = CS > 1 ? w : wl;  // index among the waves sharing the dy DMAs
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
   // block = (split, co tile, ci chunk), ci fastest: the tiles of one split (the same x / dy rows)
   // are consecutive, so xcd_remap keeps them on one XCD's L2
@@ -4327,20 +3561,15 @@ __global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(Wg
   const int ps_si = a.out_ps > 0 ? ps_sl / a.out_ps : 0, ps_sj = a.out_ps > 0 ? ps_sl - ps_si * a.out_ps : 0;
   const int rows_total = a.N * a.H;
   const int rps = a.kper / a.W;  // image rows per split
-  const int rs0 = split * rps, rs1 = min(rows_total, rs0 + rps);
-  // this row group's rows: the first ceil(n / VB) of the split's n rows, or the rest
-  const int rhalf = (rs1 - rs0 + VB - 1) / VB;
-  const int r0 = min(rs1, rs0 + vb * rhalf), r1 = min(rs1, r0 + rhalf);
+  const int r0 = split * rps, r1 = min(rows_total, r0 + rps);
   const int nrows = r1 - r0, nseg = a.W >> 6, nk = nrows * nseg;
-  const int nk_all = rhalf * nseg;  // steps of the block (group 0 has the most rows)
   const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const int sh = a.in_up > 1 ? 1 : 0;  // in_up is 1 or 2 here
   const int Hs = a.H >> sh, Ws = a.W >> sh;
-  char* ring = smem + vb * GRP + wl * RING;
-  char* dys = smem + vb * GRP + 4 * RING;
+  char* ring = smem + w * RING;
+  char* dys = smem + 4 * RING;
   auto slot = [](int q) { return (q + RSL) % RSL; };  // q >= -1
-  const bool xdma = cs == 0;  // the (first co group's) waves load their ci tile's x rows; all load some dy
 
   // this lane's halo pixels of its 3 DMAs per row: physical row 32i + (lane >> 1) holds pixel
   // hrow(.) (x0 - 1 + that), channel half lane & 1
@@ -4350,21 +3579,18 @@ __global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(Wg
     const int hr = hrow(32 * i + (lane >> 1));
     hpx[i] = hr < 66 ? hr : -100000;
   }
-  const int cil = ci0 + wl * 16 + (lane & 1) * 8;
+  const int cil = ci0 + w * 16 + (lane & 1) * 8;
   const bool civ = cil < a.Cin;
-  if (xdma)
-    for (int i = lane; i < RS / 16; i += 64) *(u32x4*)(ring + RSL * RS + i * 16) = u32x4{0u, 0u, 0u, 0u};
+  for (int i = lane; i < RS / 16; i += 64) *(u32x4*)(ring + RSL * RS + i * 16) = u32x4{0u, 0u, 0u, 0u};
 
-  f32x4 acc[9][CW], accb[CW];
+  f32x4 acc[9][CO_T], accb[CO_T];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int c = 0; c < CW; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < CO_T; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < CW; ++c) accb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int ct0 = cs * CW;
-  constexpr int ncw = CW;
-  const bool do_bias = a.wsb != nullptr && chunk == 0 && wl == 0;
+  for (int c = 0; c < CO_T; ++c) accb[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.wsb != nullptr && chunk == 0 && w == 0;
 
   // x halo row q (global image row; outside [0, rows_total) -> zeros), column segment seg
   auto issue_row = [&](int q, int seg) {
@@ -4383,22 +3609,20 @@ __global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(Wg
   // step j = (segment j / nrows, row r0 + j % nrows); the first step of a segment loads its
   // three rows and is issued after the previous segment's last step (whose slots it reuses)
   auto first = [&](int j) { return j % nrows == 0; };
-  auto nops = [&](int j) { return DYI + (xdma ? (first(j) ? 9 : 3) : 0); };
+  auto nops = [&](int j) { return DYI + (first(j) ? 9 : 3); };
   auto issue_iter = [&](int j) { const int f = j - j % nrows - 1, e = j - D; return f > e ? f : e; };
   auto issue = [&](int j) {
     const int seg = j / nrows, q = r0 + (j - seg * nrows);
-    if (xdma) {
-      if (first(j)) {
-        issue_row(q - 1, seg);
-        issue_row(q, seg);
-      }
-      issue_row(q + 1, seg);
+    if (first(j)) {
+      issue_row(q - 1, seg);
+      issue_row(q, seg);
     }
+    issue_row(q + 1, seg);
     const int p0s = q * a.W + seg * 64;
-    char* st = dys + (j % DST) * DYS;
+    char* st = dys + (j % D) * DYS;
 #pragma unroll
     for (int i = 0; i < DYI; ++i) {
-      const int k = wd + NWD * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
+      const int k = w + 4 * i;  // dy DMA index: co tile k >> 1, rows 32 (k & 1) ..
       char* dst = st + DYB;
       uint32_t off = SR_OOB;
       if (k < CO_T * 2) {
@@ -4433,22 +3657,22 @@ __global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(Wg
     const int y = q - (int)fdiv((uint32_t)q, a.fd_H) * a.H;
     const char* rows3[3] = {ring + (y == 0 ? RSL : slot(q - 1)) * RS, ring + slot(q) * RS,
                             ring + (y == a.H - 1 ? RSL : slot(q + 1)) * RS};
-    const char* ds = dys + (j % DST) * DYS + ct0 * 2048;
+    const char* ds = dys + (j % D) * DYS;
     // Fragment reads (per K half: this wave's dy tiles, then the 9 taps' x tiles) run LA reads
-    // ahead of the MFMA group (one tap x CW co tiles) that needs them, in program order fixed by
+    // ahead of the MFMA group (one tap x CO_T co tiles) that needs them, in program order fixed by
     // scheduling barriers (the compiler otherwise sinks each read to just before its MFMAs); at
     // most ~2 (LA + 1) reads are in flight, within what lgkmcnt counts, so its waits stay exact.
-    constexpr int NR = CW + 9;
+    constexpr int NR = CO_T + 9;
     s16x8 fr[2 * NR];
     auto rd = [&](int r) {
       const int kk = r / NR, i = r - kk * NR;
-      fr[r] = i < CW ? tr2(ds + i * 2048, kk * 32 + 8 * g) : tr2(rows3[(i - CW) / 3], ((i - CW) % 3) + kk * 32 + 8 * g);
+      fr[r] = i < CO_T ? tr2(ds + i * 2048, kk * 32 + 8 * g) : tr2(rows3[(i - CO_T) / 3], ((i - CO_T) % 3) + kk * 32 + 8 * g);
     };
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int need = kk * NR + CW + t;
+        const int need = kk * NR + CO_T + t;
         // reads not yet issued up to need + LA (the previous group issued up to its need + LA)
         const int lo = (kk == 0 && t == 0) ? 0 : (t > 0 ? need + LA : NR + LA);
 #pragma unroll
@@ -4457,135 +3681,165 @@ __global__ __launch_bounds__(256 * VB * CS, 1) void conv3x3_wgrad_ring_kernel(Wg
         // accumulators pinned to AGPRs (inline asm): with this many of them the compiler
         // otherwise moves every one between AGPRs and VGPRs once per step
 #pragma unroll
-        for (int c = 0; c < CW; ++c)
-          if (CW == 1 || c < ncw)
-            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[t][c]) : "v"(fr[kk * NR + c]), "v"(fr[need]));
+        for (int c = 0; c < CO_T; ++c)
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[t][c]) : "v"(fr[kk * NR + c]), "v"(fr[need]));
         __builtin_amdgcn_sched_barrier(0);
       }
       if (do_bias) {  // builtin: the compiler pads the VALU write of `ones` before its read
 #pragma unroll
-        for (int c = 0; c < CW; ++c)
-          if (c < ncw) accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kk * NR + c], ones, accb[c], 0, 0, 0);
+        for (int c = 0; c < CO_T; ++c) accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[kk * NR + c], ones, accb[c], 0, 0, 0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
   };
 
-#ifdef SR_BAND_STAMPS
-  unsigned long long ph[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
-  const unsigned long long t_start = __builtin_readcyclecounter();
-#endif
   __syncthreads();  // zero slots written
-  const bool early = EARLY && nseg == 1;
   int next = 0;  // steps issued so far, in step order (issue_iter is non-decreasing)
   while (next < nk && issue_iter(next) < 0) issue(next++);
-  for (int ks = 0; ks < nk_all; ++ks) {
-    if (VB > 1 && ks >= nk) {  // a group out of rows keeps the block's barriers
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_barrier();
-      continue;
-    }
-#ifdef SR_BAND_STAMPS
-    const unsigned long long t0 = __builtin_readcyclecounter();
-#endif
+  for (int ks = 0; ks < nk; ++ks) {
     // step ks's DMAs landed; the steps issued after it may stay in flight
     if (next == ks + D && (ks + 1) % nrows != 0 && (ks + 1) / nrows == (next - 1) / nrows) {
       // steady state: the D - 1 steps after ks, none of them a segment's first
-      if (xdma)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (DYI + 3)) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * DYI) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * (DYI + 3)) : "memory");
     } else {
       int younger = 0;
       for (int j = ks + 1; j < next; ++j) younger += nops(j);
       vm_wait_dyn(younger);
     }
-#ifdef SR_BAND_STAMPS
-    const unsigned long long t1 = __builtin_readcyclecounter();
-#endif
     __builtin_amdgcn_s_barrier();
-    if (early)  // step ks + D: its slot / stage were last read in step ks - 1, finished by every wave
-      while (next < nk && issue_iter(next) <= ks) issue(next++);
-#ifdef SR_BAND_STAMPS
-    const unsigned long long t2 = __builtin_readcyclecounter();
-#endif
     compute(ks);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifdef SR_BAND_STAMPS
-    const unsigned long long t3 = __builtin_readcyclecounter();
-#endif
-    if (!early) {
-      __builtin_amdgcn_s_barrier();
-      while (next < nk && issue_iter(next) <= ks) issue(next++);
-    }
-#ifdef SR_BAND_STAMPS
-    const unsigned long long t4 = __builtin_readcyclecounter();
-    ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
-#endif
+    __builtin_amdgcn_s_barrier();
+    while (next < nk && issue_iter(next) <= ks) issue(next++);
   }
-#ifdef SR_BAND_STAMPS
-  const unsigned long long t_loop = __builtin_readcyclecounter();
-#endif
 
   // the last MFMAs' results are read below (inline-asm MFMAs: the hazard wait is ours)
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (VB > 1) {
-    // every wave passed the last step's second barrier after its LDS reads (lgkmcnt(0)) and no
-    // DMA is in flight: the rings are free.  Group 1 stores its accumulators (and wave 0's bias
-    // sums), group 0 adds them in a fixed order (deterministic).
-    f32x4* hand = (f32x4*)smem;
-    f32x4* handb = hand + 4 * 9 * CW * 64;
-    if (vb == 1) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int c = 0; c < CW; ++c) hand[((wl * 9 + t) * CW + c) * 64 + lane] = acc[t][c];
-      if (do_bias)
-#pragma unroll
-        for (int c = 0; c < CW; ++c) handb[c * 64 + lane] = accb[c];
-    }
-    __syncthreads();
-    if (vb == 1) return;
-    if (do_bias)
-#pragma unroll
-      for (int c = 0; c < CW; ++c) accb[c] += handb[c * 64 + lane];
-  }
-  // slab [split][tap][ci][co] (co fastest): a lane's 4 accumulator rows are 4 consecutive co,
-  // so one 16-B store per (tap, co tile) per lane (a [co][ci] slab takes four 4-B ones)
   const int c16 = lane & 15;
-  const int ci = ci0 + wl * 16 + c16;
-  if (ci < a.Cin) {
+  const int ci = ci0 + w * 16 + c16;
+  const int G = a.red_g;
+  if (G <= 1) {  // slab row `split`; the standalone reduce sums the S rows
+    if (ci < a.Cin) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      float* ws = a.ws + (((size_t)split * 9 + t) * a.Cin + ci) * a.Cout;
+      for (int t = 0; t < 9; ++t) {
+        float* ws = a.ws + (((size_t)split * 9 + t) * a.Cin + ci) * a.Cout;
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        const int co = co0 + (ct0 + c) * 16 + g * 4;
-        f32x4 v = acc[t][c];
-        if constexpr (VB > 1) v += ((const f32x4*)smem)[((wl * 9 + t) * CW + c) * 64 + lane];  // group 1's sums
-        if (c < ncw && co < a.Cout) *(f32x4*)(ws + co) = v;
+        for (int c = 0; c < CO_T; ++c) {
+          const int co = co0 + c * 16 + g * 4;
+          if (co < a.Cout) *(f32x4*)(ws + co) = acc[t][c];
+        }
       }
-      // one tap at a time: the hand-over reads must not be hoisted next to 36 live accumulators
-      if constexpr (VB > 1) __builtin_amdgcn_sched_barrier(0);
     }
+    if (do_bias && c16 == 0) {
+#pragma unroll
+      for (int c = 0; c < CO_T; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = co0 + c * 16 + g * 4 + r;
+          if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
+        }
+    }
+    return;
   }
-#ifdef SR_BAND_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.stamps && tid == 0) {
-    unsigned long long* st = a.stamps + (size_t)blockIdx.x * 16;
-    st[0] = t_start; st[1] = t_loop; st[2] = __builtin_readcyclecounter(); st[3] = nk;
-    st[4] = ph[0]; st[5] = ph[1]; st[6] = ph[2]; st[7] = ph[3];
-  }
-#endif
+
+  // ---- in-kernel reduce over the group's G splits (see the header comment) ----
+  const size_t row_f = (size_t)9 * a.Cin * a.Cout;  // floats per slab row
+  const __amdgpu_buffer_rsrc_t wsr = make_rsrc(a.ws, a.ws_bytes);
+  const __amdgpu_buffer_rsrc_t wbr = make_rsrc(a.wsb, a.wsb ? a.wsb_bytes : 0u);
+  // this lane's element offset inside a slab row for (tap t, co tile c); SR_OOB-style masking
+  // through the descriptor: an offset past ws_bytes stores / loads nothing
+  auto eoff = [&](int t, int c) -> uint32_t {
+    const int co = co0 + c * 16 + g * 4;
+    return (ci < a.Cin && co < a.Cout) ? (uint32_t)((((size_t)t * a.Cin + ci) * a.Cout + co) * 4) : SR_OOB;
+  };
+  const uint32_t my_row = (uint32_t)((size_t)split * row_f * 4);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c) {
+      const uint32_t o = eoff(t, c);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][c]), wsr, o == SR_OOB ? SR_OOB : my_row + o,
+                                             0, 16);  // aux 16: sc1 (write-through)
+    }
   if (do_bias && c16 == 0) {
 #pragma unroll
-    for (int c = 0; c < CW; ++c)
+    for (int c = 0; c < CO_T; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + (ct0 + c) * 16 + g * 4 + r;
-        if (c < ncw && co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
+        const int co = co0 + c * 16 + g * 4 + r;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(accb[c][r]), wbr,
+                                              co < a.Cout ? (uint32_t)(((size_t)split * a.Cout + co) * 4) : SR_OOB, 0, 16);
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  const int grp = split / G, g0 = grp * G;
+  const int gs = min(G, a.splits - g0);
+  unsigned* flag = (unsigned*)smem;  // the rings are free: every wave passed the last step's barriers
+  if (tid == 0) {
+    unsigned* cnt = g_ring_cnt + a.red_bank * RING_CNT_PER + grp * per_split + rem_;
+    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = t == (unsigned)(gs - 1);
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+    *flag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*flag == 0u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the ticket
+  const __amdgpu_buffer_rsrc_t w2r = make_rsrc(a.red_ws, a.red_ws_bytes);
+  const uint32_t out_row = (uint32_t)((size_t)grp * row_f * 4);
+  // three taps at a time: the other rows' loads of those taps in flight together (<= 3 x 12 x 16 B
+  // per lane), then the sum in split order
+#pragma unroll
+  for (int t0 = 0; t0 < 9; t0 += 3) {
+    f32x4 ld[3][3][CO_T];  // [other row k][tap][co tile]
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int sk = g0 + k + (g0 + k >= split ? 1 : 0);  // the k-th row of the group other than ours
+      const bool v = k < gs - 1;
+      const uint32_t rowb = (uint32_t)((size_t)sk * row_f * 4);
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int c = 0; c < CO_T; ++c) {
+          const uint32_t o = eoff(t0 + t, c);
+          ld[k][t][c] = v ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          wsr, o == SR_OOB ? SR_OOB : rowb + o, 0, 16))
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int c = 0; c < CO_T; ++c) {
+        // rows g0 .. g0 + gs - 1 in order: ours (registers) at position split - g0
+        f32x4 s = split == g0 ? acc[t0 + t][c] : ld[0][t][c];
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+          if (j < gs) {
+            const int k = j - (split < g0 + j ? 1 : 0);  // index among the other rows
+            s += (g0 + j == split) ? acc[t0 + t][c] : ld[k][t][c];
+          }
+        const uint32_t o = eoff(t0 + t, c);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, s), w2r, o == SR_OOB ? SR_OOB : out_row + o, 0, 0);
+      }
+  }
+  if (do_bias && c16 == 0) {
+#pragma unroll
+    for (int c = 0; c < CO_T; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + c * 16 + g * 4 + r;
+        if (co < a.Cout) {
+          float s = 0.f;
+          for (int j = 0; j < gs; ++j)
+            s = (j == 0 ? 0.f : s) + ((g0 + j == split) ? accb[c][r]
+                                                          : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                                                wbr, (uint32_t)(((size_t)(g0 + j) * a.Cout + co) * 4), 0, 16)));
+          a.red_wsb[(size_t)grp * a.Cout + co] = s;
+        }
       }
   }
 }
@@ -5082,31 +4336,16 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
 }
 
 // Narrow-conv halo kernel: bf16 3x3, W 64 or 128, whole-row 256-pixel tiles; Cout <= 64 in one
-// block column, Cout 65..255 (RRDB dense-block dgrads) in 64-channel block columns.
-// SR_HALO_W256=1 (read per call): the one-row halo tiles also for W 256 convs with Cout a multiple
-// of 64 (<= 256) and a plain NHWC store (DIRECT epilogue), instead of the 256x256 pp kernel.  Opt-in:
-// measured slower (EDSR conv_last dgrad 1390 vs 550 us, RCAN 170 vs 150 us; profiles/r04/halo256/) --
-// 99 KB of LDS leave one block per CU, and a 64-channel column block re-stages the row halo per tile
-bool halo_w256_wide() {
-  const char* e = getenv("SR_HALO_W256");
-  return e && e[0] == '1';
-}
-bool halo_w256_direct(const FwdArgs& a) {
-  return a.Cout % 64 == 0 && a.Cout <= 256 && !a.out_nchw && a.out_ps == 0 && !a.colsum && !a.aux && !a.gate &&
-         !a.res2 && !a.row_scale && a.in_ps == 0;
-}
+// block column, Cout 65..255 (RRDB dense-block dgrads) in 64-channel block columns.  (Round 4's
+// one-row tiles for the wide W-256 convs measured slower than the pp / tile kernels and were removed
+// in round 5: EDSR conv_last dgrad 1390 vs 550 us, profiles/r04/halo256/.)
 bool fwd_use_halo(const FwdArgs& a, bool bf) {
-  static const bool ps_off = [] {
-    const char* e = getenv("SR_HALO_PS");
-    return e && atoi(e) == 0;
-  }();
   // pixel-shuffled input (the upsample convs' dgrads into 64 channels) when each 64-channel chunk lies
-  // in one shuffle slot; SR_HALO_PS=0 / variant 68: the tile kernel for those (A/B)
-  const bool ps_ok = a.in_ps > 0 && a.fd_cps.d % 64 == 0 && a.W != 256 && !ps_off && g_variant != 68;
+  // in one shuffle slot; variant 68: the tile kernel for those (A/B)
+  const bool ps_ok = a.in_ps > 0 && a.fd_cps.d % 64 == 0 && a.W != 256 && g_variant != 68;
   if (!bf || a.in_up != 1 || (a.in_ps != 0 && !ps_ok) || a.tap0 != 0 || g_variant == 1) return false;
-  if (a.W == 256)  // HR-resolution tail convs (conv_last, Cout <= 16, NCHW store): one row per tile;
-    // with SR_HALO_W256=1 also the wide plain-NHWC ones (the conv_last dgrads: 3 -> 64 / 256 channels)
-    return (a.Cout <= 16 && g_variant != 29) || (halo_w256_wide() && halo_w256_direct(a));
+  if (a.W == 256)  // HR-resolution tail convs (conv_last, Cout <= 16, NCHW store): one row per tile
+    return a.Cout <= 16 && g_variant != 29;
   return !a.out_nchw && a.Cout < 256 && (a.W == 64 || a.W == 128) && a.H % (256 / a.W) == 0;
 }
 
@@ -5116,8 +4355,7 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   a.tiles = a.M / 256;
   const int ct = (a.Cout + 15) / 16;
   const dim3 grid(a.tiles, a.tiles_n);
-  if (a.W == 256 && a.Cout > 16) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 0, true, true>), grid, dim3(256), 0, s, a);
-  else if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
+  if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
   else if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
   else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, grid, dim3(256), 0, s, a);
   else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);
@@ -5198,14 +4436,9 @@ bool fwd_use_lin(const FwdArgs& a, bool bf) {
 }
 // linear_wk_kernel for the linears with K > SR_LWK_MINK (default 0: all; 192: only the wide-K ones,
 // which the 64-token lin kernel took), K <= 576, 96 < Cout <= 576 and a plain / GELU' gate / GELU +
-// pre-activation / residual / residual + row-scale epilogue; SR_LWK=0 (read once) or variant 64: the lin kernel (A/B, tests)
+// pre-activation / residual / residual + row-scale epilogue; knob SR_LWK=0 or variant 64: the lin kernel (A/B, tests)
 bool lin_use_wk(const FwdArgs& a) {
-  static const int mink = [] {
-    const char* e = getenv("SR_LWK");
-    if (e && atoi(e) == 0) return 1 << 30;
-    const char* k = getenv("SR_LWK_MINK");
-    return k ? atoi(k) : 0;
-  }();
+  const int mink = sr_knob(K_LWK) == 0 ? (1 << 30) : (sr_knob(K_LWK_MINK) > 0 ? sr_knob(K_LWK_MINK) : 0);
   if (g_variant == 64 || a.Cin <= mink || a.Cin > 576 || a.Cout > 576 || a.Cout <= 96) return false;
   const int e = lin_epi(a);
   return e == 0 || e == 8 || e == 16 || e == 67 || e == 144;
@@ -5238,22 +4471,13 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
   *nt = k == FK_BIG ? 512 : 256;
 }
 
-// SR_BAND_2PC=1: two bands per CU for the forms built for it (read per call).  Off by default: the
-// kernel alone gains ~4 % (RCAN step trace 21.4 vs 22.3 us) but the RCAN step loses 0.9 ms (36.0 vs
-// 35.1 ms, three pairs): the second band leaves no room for the side-stream weight gradients
-bool band_two_per_cu_env() {
-  const char* e = getenv("SR_BAND_2PC");
-  return e && e[0] == '1';
-}
 hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
-  // one block per CU (one wave per SIMD: the weights live in registers), two for the forms built
-  // for it (band_occ: bands half as long, one block's ring fill / epilogue under the other's
-  // MFMAs); variant 35 forces 64 blocks (long bands: ring wrap-around and image crossings inside a
-  // band, for tests)
+  // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64 blocks
+  // (long bands: ring wrap-around and image crossings inside a band, for tests).  (Two bands per CU
+  // for the band_occ forms measured faster alone but slower in the RCAN step beside the side-stream
+  // weight gradients; the switch was removed in round 5.)
   const int rows = a.N * a.H;
-  const int e1 = band_epi(a, 256);
-  const int occ = (e1 >= 0 && band_occ(a.W, e1) == 2 && band_two_per_cu_env()) ? 2 : 1;
-  const int gmax = g_variant == 35 ? 64 : 256 * occ;
+  const int gmax = g_variant == 35 ? 64 : 256;
   FwdArgs ab = a;
   ab.stamps = g_stamps;
   const dim3 grid(rows < gmax ? rows : gmax);
@@ -5446,41 +4670,6 @@ bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
   return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
 }
 
-// Tap-row wgrad (three taps of a kernel row per block, one x halo row per K-step): bf16 3x3,
-// Cout / Cin (and the shuffle slot width) multiples of 128, W % 64 == 0.  Opt-in (variant 46; 47-49
-// its ablations): on the EDSR-L body shape it measured 236 us against the pp kernel's 184 us --
-// its DMA-only run is faster (99 vs 121 us) but its MFMA + fragment-read run is not (172 vs 116 us).
-bool wg_use_tr3(const sr_conv3x3_wgrad_desc* d) {
-  if (d->dtype != SR_BF16 || d->ksize == 1 || d->in_up > 1 || g_variant < 46 || g_variant > 49) return false;
-  const int cps = d->out_ps > 0 ? d->Cout / (d->out_ps * d->out_ps) : 128;
-  return d->W % 64 == 0 && d->Cout % 128 == 0 && d->Cin % 128 == 0 && cps % 128 == 0;
-}
-
-// 12-wave tap-row wgrad (conv3x3_wgrad_tw_kernel): bf16 3x3, no pixel shuffle / upsample,
-// Cout, Cin multiples of 128, W % 64 == 0 (the EDSR-L body shape).  Opt-in while it is measured:
-// SR_WG_TW=1 (read once) or variant 70; variants 71 / 72 are its DBG ablations (wrong results).
-bool wg_use_tw(const sr_conv3x3_wgrad_desc* d) {
-  static const bool on = [] {
-    const char* e = getenv("SR_WG_TW");
-    return e && atoi(e) == 1;
-  }();
-  if (!(on || (g_variant >= 70 && g_variant <= 72))) return false;
-  return d->dtype == SR_BF16 && d->ksize == 3 && d->in_up <= 1 && d->out_ps == 0 && d->W % 64 == 0 &&
-         d->Cout % 128 == 0 && d->Cin % 128 == 0 && (size_t)d->N * d->H * d->W * d->Cin * 2 < 0x80000000ull;
-}
-
-// Splits per bias-role block of the tw kernel: 1, or SR_TW_BG (read once).  A bias block streams
-// dy at ~60 GB/s (one block per CU, two stages in flight), so at the tw plan's ~100 K-steps per split
-// a group of 3 splits (the pp kernel's) made the bias blocks the critical path (190 vs 186 us).
-int tw_bias_group() {
-  static const int v = [] {
-    const char* e = getenv("SR_TW_BG");
-    const int x = e ? atoi(e) : 1;
-    return x >= 1 && x <= 8 ? x : 1;
-  }();
-  return v;
-}
-
 // Splits per bias-role block of the pp kernel (0: one bias block per split, interleaved with the
 // tile blocks).  The bias role reads dy only, so a third of the CUs' worth of bias blocks can take
 // three splits each and the tile blocks get more, shorter splits (EDSR-L body wgrad, 247 blocks:
@@ -5501,23 +4690,17 @@ bool wg_bias_fused(const sr_conv3x3_wgrad_desc* d) {
   return g_variant == 54 || d->Cout > 256;
 }
 
-// the row-streaming form of it (variant 37: the tile-row form, for A/B)
-bool wg_use_ring() { return g_variant != 37; }
 // Row-streaming wgrad over 64-channel output tiles of a wider conv (Cout above 64, the last tile
 // partial): a block is (split, co tile, 64-ci chunk); at 80 KB of LDS two blocks share a CU, so the
 // plan targets 512 blocks.  Taken where the 256x256 pp kernel is not at home -- channel counts that
 // are not multiples of 128 (SwinIR's 184-channel convs: 164 -> 116 us at B 32, 64^2) or Cin < 128
 // (the head convs); on the EDSR-L body shape it ties the pp kernel (193 vs 189 us; 256 blocks 256 us,
 // 3 / 4 steps in flight 250-280 us: LDS for one block per CU), which stays there.
-// SR_RING_WIDE (read once): 0 = off, > 0 = on for every Cout > 64 shape with that block target (A/B);
+// knob SR_RING_WIDE: 0 = off, > 0 = on for every Cout > 64 shape with that block target (A/B);
 // variant 62: on everywhere (parity tests).
 int ring_wide_env() {
-  static int v = [] {
-    const char* e = getenv("SR_RING_WIDE");
-    const int x = e ? atoi(e) : -1;
-    return x >= -1 && x <= 4096 ? x : -1;
-  }();
-  return v;
+  const int x = sr_knob(K_RING_WIDE);
+  return x >= -1 && x <= 4096 ? x : -1;
 }
 int ring_wide_target() {
   if (g_variant == 62) return 512;
@@ -5525,131 +4708,48 @@ int ring_wide_target() {
   return v < 0 ? 512 : v;
 }
 bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d) {
-  if (ring_wide_target() <= 0 || !wg_use_ring() || g_variant == 1 || d->dtype != SR_BF16 || d->ksize == 1 ||
-      d->Cout <= 64 || d->W % 64 || d->in_up > 2)
+  if (ring_wide_target() <= 0 || g_variant == 1 || d->dtype != SR_BF16 || d->ksize == 1 || d->Cout <= 64 ||
+      d->W % 64 || d->in_up > 2)
     return false;
-  static const bool ps_off = [] {
-    const char* e = getenv("SR_RING_PS");
-    return e && atoi(e) == 0;
-  }();
+  const bool ps_off = sr_knob(K_RING_PS) == 0;
   if (d->out_ps > 0 && (d->in_up > 1 || (d->Cout / (d->out_ps * d->out_ps)) % 64 != 0 || g_variant == 67 || ps_off))
-    return false;  // pixel-shuffled dy: each 64-wide co tile inside one shuffle slot; variant 67 / SR_RING_PS=0: off (A/B)
+    return false;  // pixel-shuffled dy: each 64-wide co tile inside one shuffle slot; variant 67 / knob SR_RING_PS=0: off (A/B)
   if (g_variant == 62 || ring_wide_env() > 0) return true;
   return d->Cout % 128 != 0 || d->Cin % 128 != 0;
 }
 // 1x1 weight gradient on linear_wgrad_kernel (192x192 tiles): bf16 dense token rows, no pixel
-// shuffle / upsample.  SR_LWG=0 (read once) or variant 63: off (the pp kernel, A/B and tests).
+// shuffle / upsample.  Knob SR_LWG=0 or variant 63: off (the pp kernel, A/B and tests).
 bool wg_use_lin(const sr_conv3x3_wgrad_desc* d) {
-  static const bool off = [] {
-    const char* e = getenv("SR_LWG");
-    return e && atoi(e) == 0;
-  }();
+  const bool off = sr_knob(K_LWG) == 0;
   return !off && g_variant != 63 && g_variant != 1 && d->dtype == SR_BF16 && d->ksize == 1 && d->in_up <= 1 &&
          d->out_ps == 0 && d->Cout >= 64 && d->Cin >= 64;
 }
-// Block target of its split plan: 256 (one 144-KB block per CU), or SR_LWG_T (A/B; read once)
+// Block target of its split plan: 256 (one 144-KB block per CU), or knob SR_LWG_T (A/B)
 int lin_wg_target() {
-  static int v = [] {
-    const char* e = getenv("SR_LWG_T");
-    const int x = e ? atoi(e) : 0;
-    return x >= 16 && x <= 4096 ? x : 256;
-  }();
-  return v;
+  const int x = sr_knob(K_LWG_T);
+  return x >= 16 && x <= 4096 ? x : 256;
 }
-// All-taps halo wgrad kernel: bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample <= 2 (or the
-// row-streaming form over 64-channel output tiles, wg_ring_wide).
+// Row-streaming wgrad (conv3x3_wgrad_ring_kernel): bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample
+// <= 2 (or over 64-channel output tiles, wg_ring_wide).
 bool wg_use_halo(const sr_conv3x3_wgrad_desc* d) {
   if (wg_ring_wide(d)) return true;
   return d->dtype == SR_BF16 && d->ksize != 1 && d->Cout <= 64 && d->W % 64 == 0 && d->in_up <= 2 && d->out_ps == 0 &&
          g_variant != 1;
 }
 
-// Block target of the narrow (ring / halo) wgrad split plan: 512, or SR_RING_SPLITS (A/B sweeps; read
-// once per process)
+// Block target of the narrow ring wgrad split plan: 512, or knob SR_RING_SPLITS (A/B sweeps)
 int ring_split_target() {
-  static int v = [] {
-    const char* e = getenv("SR_RING_SPLITS");
-    const int x = e ? atoi(e) : 0;
-    return x >= 16 && x <= 4096 ? x : 512;
-  }();
-  return v;
+  const int x = sr_knob(K_RING_SPLITS);
+  return x >= 16 && x <= 4096 ? x : 512;
 }
-
-// Steps in flight of the ring wgrad kernel: 2, or SR_RING_D = 3 / 4 (A/B; read once per process)
-int ring_depth() {
-  static int v = [] {
-    const char* e = getenv("SR_RING_D");
-    const int x = e ? atoi(e) : 0;
-    return x == 3 || x == 4 ? x : 2;
-  }();
-  return v;
-}
-
-bool ring_early();
-int ring_depth();
-int ring_la();
-bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d);
-// Co split of the narrow ring wgrad (opt-in SR_RING_COSPLIT=1 / variant 75; A/B): Cout 64 (or 48 / 40 ..,
-// a multiple of 32 above 32) as two 32-channel co tiles of separate blocks over twice the rows each:
-// the same block count, half the slab (and reduce) per block and in total, x read by both co
-// tiles (the second time from L2: the tiles of one split are consecutive blocks on one XCD).
-bool ring_cosplit(const sr_conv3x3_wgrad_desc* d) {
-  static const bool v = [] {
-    const char* e = getenv("SR_RING_COSPLIT");
-    return e && atoi(e) == 1;
-  }();
-  return (v || g_variant == 75) && wg_use_ring() && !wg_ring_wide(d) && d->Cout > 32 && d->Cout % 32 == 0;
-}
-// 16-channel co tiles per wave of the ring / halo wgrad
-int ring_ct(const sr_conv3x3_wgrad_desc* d) {
-  return wg_ring_wide(d) ? 4 : ring_cosplit(d) ? 2 : (d->Cout + 15) / 16;
-}
-int ring_tiles_co(const sr_conv3x3_wgrad_desc* d) {
-  return wg_ring_wide(d) ? (d->Cout + 63) / 64 : ring_cosplit(d) ? d->Cout / 32 : 1;
-}
-// Row groups per ring-wgrad block: 1 (4-wave blocks, two per CU), or SR_RING_VB=2 (A/B; CO_T <= 2:
-// 8-wave blocks, one per CU, one slab per block -- at 3 / 4 co tiles per wave the two-waves-per-SIMD
-// register budget spills: 12 / 132 VGPRs, with fragment lookahead 3 or 1 alike).  Measured on RRDB
-// (profiles/r04/ab/): 66.6 ms at 1 vs 68.0 ms at 2 (ring + reduce 60.3 vs 64.7 us per call): two
-// independent 4-wave blocks overlap each other's barriers, one 8-wave block does not, and that
-// costs more than the halved slab saves.  Variant 69: the 4-wave form; 0 keeps the default.
-// The early-issue and deeper-pipeline A/B forms are 4-wave only.
-int ring_vb() {
-  static const int v = [] {
-    const char* e = getenv("SR_RING_VB");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  return (g_variant == 69 || ring_early() || ring_depth() != 2 || ring_la() != 3) ? 1 : (g_variant == 74 ? 2 : v);
-}
-
-// Co groups per ring-wgrad block (CO_T 4, 4-wave form otherwise): 2 with SR_RING_CS=1 (A/B) or
-// variant 73 (parity tests): one 8-wave block per CU over twice the rows, half the slab.  Measured
-// on RCAN (profiles/r04/ab/): ring + reduce 39.1 vs 38.8 us per call, step 40.1 vs 37.9 ms -- the
-// halved slab is paid back by the lost overlap of two independent blocks, as for SR_RING_VB=2.
-int ring_cs(int ct) {
-  static const int v = [] {
-    const char* e = getenv("SR_RING_CS");
-    return e && atoi(e) == 1 ? 2 : 1;
-  }();
-  if (ct != 4 || ring_early() || ring_depth() != 2 || ring_la() != 3) return 1;
-  return g_variant == 73 ? 2 : (g_variant == 69 ? 1 : v);
-}
-
-// Early DMA issue in the ring wgrad (one barrier per step, one more LDS slot): SR_RING_EARLY=1 (A/B; read once)
-bool ring_early() {
-  static const bool v = [] {
-    const char* e = getenv("SR_RING_EARLY");
-    return e && atoi(e) == 1;
-  }();
-  return v || g_variant == 65;  // variant 65: on (parity tests)
-}
-// Fragment-read lookahead of the ring wgrad (D = 2): 3, or SR_RING_LA=5 (A/B; read once)
-int ring_la() {
-  static const int v = [] {
-    const char* e = getenv("SR_RING_LA");
-    return e && atoi(e) == 5 ? 5 : 3;
-  }();
-  return v;
+// 16-channel co tiles per wave of the ring wgrad and its output-channel tiles
+int ring_ct(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? 4 : (d->Cout + 15) / 16; }
+int ring_tiles_co(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? (d->Cout + 63) / 64 : 1; }
+// Splits per in-kernel reduce group of the ring wgrad (conv3x3_wgrad_ring_kernel, round 5): knob
+// SR_RING_RED = G in 2..4 (0 / 1 / unset: the standalone slab reduce over all splits)
+int ring_red_group() {
+  const int g = sr_knob(K_RING_RED);
+  return g >= 2 && g <= 4 ? g : 0;
 }
 
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
@@ -5662,54 +4762,21 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     // ~2 blocks per CU, but at least 8 K-steps per block (the slab costs 8 B per tap-MAC row)
     // (A/B on RCAN / RRDB: twice or half as many splits are 6-12 % slower per step)
     const int chunks = (d->Cin + 63) / 64;
-    // (an 8-wave two-row-group block takes a CU alone: half the block target)
-    const int vbdiv = !wg_use_ring() ? 1 : ring_ct(d) <= 2 ? ring_vb() : ring_cs(ring_ct(d));
-    int S = (wg_ring_wide(d) ? ring_wide_target() : ring_split_target()) / (chunks * ring_tiles_co(d)) / vbdiv;
+    int S = (wg_ring_wide(d) ? ring_wide_target() : ring_split_target()) / (chunks * ring_tiles_co(d));
     const int maxS = M / 512 > 1 ? M / 512 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
-    if (wg_use_ring()) {  // whole image rows per split
-      const int rows = d->N * d->H;
-      const int rps = (rows + S - 1) / S;
-      *splits = (rows + rps - 1) / rps;
-      *kper = rps * d->W;
-      return;
-    }
-    int kp = (M + S - 1) / S;
-    kp = (kp + 63) / 64 * 64;
-    *splits = (M + kp - 1) / kp;
-    *kper = kp;
+    // whole image rows per split
+    const int rows = d->N * d->H;
+    const int rps = (rows + S - 1) / S;
+    *splits = (rows + rps - 1) / rps;
+    *kper = rps * d->W;
     return;
   }
   if (wg_use_lin(d)) {
     const int tiles = ((d->Cout + 191) / 192) * ((d->Cin + 191) / 192);
     int S = lin_wg_target() / tiles;
     const int maxS = (M + 63) / 64;
-    if (S > maxS) S = maxS;
-    if (S < 1) S = 1;
-    int kp = (M + S - 1) / S;
-    kp = (kp + 63) / 64 * 64;
-    *splits = (M + kp - 1) / kp;
-    *kper = kp;
-    return;
-  }
-  if (wg_use_tw(d)) {  // one 12-wave block per CU, bias-role blocks of tw_bias_group() splits
-    const int tco = (d->Cout + 255) / 256, ntile = 3 * (d->Cout / 128) * (d->Cin / 128), bg = tw_bias_group();
-    int S = (int)(256.0 / (ntile + (double)tco / bg));
-    while (S > 1 && S * ntile + (S + bg - 1) / bg * tco > 256) --S;
-    const int maxS = (M + 255) / 256;
-    if (S > maxS) S = maxS;
-    if (S < 1) S = 1;
-    int kp = (M + S - 1) / S;
-    kp = (kp + 63) / 64 * 64;
-    *splits = (M + kp - 1) / kp;
-    *kper = kp;
-    return;
-  }
-  if (wg_use_tr3(d)) {
-    const int tiles = 3 * (d->Cout / 128) * (d->Cin / 128) + (d->Cout + 255) / 256;
-    int S = 256 / tiles;
-    const int maxS = M / 256 > 1 ? M / 256 : 1;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
     int kp = (M + S - 1) / S;
@@ -5900,49 +4967,6 @@ int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_ga
   return sr_check(hipGetLastError(), "linear_ln_fwd launch");
 }
 
-// sr_linear_ln_bwd: shapes it takes (0 otherwise) and the dgamma / dbeta partial rows it writes
-int sr_linear_ln_bwd_parts(const sr_conv3x3_desc* d, int ln_C) {
-  if (!d || d->dtype != SR_BF16 || d->ksize != 1 || d->N <= 0 || d->H <= 0 || d->W <= 0) return 0;
-  // ln_C % 4: the per-lane gamma reads merge into 16-B buffer loads, which the descriptor bound drops whole
-  if (d->Cin % 8 || d->Cout % 8 || d->Cout > 192 || ln_C <= 0 || ln_C % 4 || ln_C > d->Cout || d->ldy != d->Cout || d->ycoff)
-    return 0;
-  FwdArgs a = fwd_shape(d);
-  if (fwd_kind(a, true) != FK_LIN || !lin_use_wk(a)) return 0;
-  return 2 * ((a.M + 127) / 128);
-}
-
-int sr_linear_ln_bwd(const sr_conv3x3_desc* d, const void* dy, const void* wd, const void* x, int ldx,
-                     const float* mean, const float* rstd, const float* gamma, int ln_C, const void* res, int ldr,
-                     void* dx, const float* row_scale, void* dx_scaled, float* partial, size_t part_bytes,
-                     void* stream) {
-  const int nparts = sr_linear_ln_bwd_parts(d, ln_C);
-  if (nparts <= 0) return sr_fail(SR_EINVAL, "linear_ln_bwd: unsupported shape (query sr_linear_ln_bwd_parts)");
-  if (!dy || !wd || !x || !mean || !rstd || !gamma || !dx || !partial)
-    return sr_fail(SR_EINVAL, "linear_ln_bwd: null pointer");
-  if ((dx_scaled != nullptr) != (row_scale != nullptr))
-    return sr_fail(SR_EINVAL, "linear_ln_bwd: dx_scaled and row_scale go together");
-  if (ldx < d->Cout || ldx % 8 || (res && (ldr < d->Cout || ldr % 8)))
-    return sr_fail(SR_EINVAL, "linear_ln_bwd: x / res strides must be >= Cout and multiples of 8");
-  if (part_bytes < (size_t)nparts * 2 * ln_C * sizeof(float)) return sr_fail(SR_EINVAL, "linear_ln_bwd: partial too small");
-  FwdArgs a = fwd_shape(d);
-  const size_t xb = (size_t)a.M * d->ldx * 2, wb = (size_t)d->Cout * d->ldw * 2;
-  if (xb >= 0x80000000ull || wb >= 0x80000000ull || (size_t)a.M * ldx * 2 >= 0x80000000ull ||
-      (res && (size_t)a.M * ldr * 2 >= 0x80000000ull))
-    return sr_fail(SR_ETOOBIG, "linear_ln_bwd: tensor >= 2 GiB");
-  a.x = dy; a.w = wd; a.bias = nullptr; a.y = dx;
-  a.x_bytes = (uint32_t)xb; a.w_bytes = (uint32_t)wb;
-  a.res = res; a.ldr = ldr; a.rcoff = 0; a.rcols = d->Cout;
-  a.r_bytes = res ? (uint32_t)((size_t)a.M * ldr * 2) : 0u;
-  a.lb_x = x; a.lb_ldx = ldx; a.lb_C = ln_C; a.lb_mean = mean; a.lb_rstd = rstd; a.lb_gamma = gamma;
-  a.lb_part = partial; a.lb_dxs = dx_scaled; a.lb_rsc = row_scale;
-  a.fd_hw = make_fastdiv((uint32_t)(d->H * d->W));
-  const dim3 grid((unsigned)((a.M + 127) / 128));
-  hipStream_t s = (hipStream_t)stream;
-  if (res) hipLaunchKernelGGL(linear_wk_kernel<256 | 16>, grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(linear_wk_kernel<256>, grid, dim3(256), 0, s, a);
-  return sr_check(hipGetLastError(), "linear_ln_bwd launch");
-}
-
 // 1 when sr_conv3x3_fwd can fuse the dot partials (d->dot) into this conv with a residual operand:
 // the band kernel's residual + colsum + dot epilogue (RCAB conv1 dgrad shapes).
 int sr_conv3x3_fwd_dot_ok(const sr_conv3x3_desc* d) {
@@ -5990,10 +5014,8 @@ int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d) {
 }
 
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
-  if (wg_use_halo(d)) return wg_use_ring() ? "conv3x3_wgrad_ring_kernel" : "conv3x3_wgrad_halo_kernel";
+  if (wg_use_halo(d)) return "conv3x3_wgrad_ring_kernel";
   if (wg_use_lin(d)) return "linear_wgrad_kernel";
-  if (wg_use_tw(d)) return "conv3x3_wgrad_tw_kernel";
-  if (wg_use_tr3(d)) return "conv3x3_wgrad_tr3_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
@@ -6022,7 +5044,10 @@ size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d) {
   int S, kp;
   wgrad_plan(d, &S, &kp);
   const int taps = d->ksize == 1 ? 1 : 9;
-  return ((size_t)S * taps * d->Cout * d->Cin + (size_t)S * d->Cout) * sizeof(float) + 256;
+  size_t rows = S;
+  const int G = wg_use_halo(d) ? ring_red_group() : 0;
+  if (G > 1) rows += (S + G - 1) / G;  // + the level-2 slab of the in-kernel reduce
+  return (rows * taps * d->Cout * d->Cin + rows * d->Cout) * sizeof(float) + 256;
 }
 
 }  // extern "C"
@@ -6036,7 +5061,7 @@ int wgrad_reduce_launch(const sr_conv3x3_wgrad_desc* d, int S, int taps, const f
   const int Cin_real = d->Cin_real > 0 ? d->Cin_real : d->Cin;
   const int64_t total = (int64_t)Cout_real * Cin_real;
   const int64_t work = total > Cout_real ? total : Cout_real;
-  const bool tr = wg_use_halo(d) && wg_use_ring();
+  const bool tr = wg_use_halo(d);
   // (the row-streaming slab keeps wgrad_reduce_tr_kernel: 32-group blocks measured slower on RCAN / RRDB)
   if (g_variant != 40 && !tr && Cin_real % 4 == 0 && !ci_map) {
     // split phases P ~ S / 8 (pow2 <= 32), group width GPW so that the grid covers the chip
@@ -6125,57 +5150,42 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   a.stamps = g_stamps;
+  int S_red = S;  // slab rows the standalone reduce sums
+  float* ws_red = a.ws;
+  float* wsb_red = a.wsb;
   if (wg_use_halo(d)) {
     a.tiles_co = ring_tiles_co(d);
     a.tiles_ci = (a.Cin + 63) / 64;
     const int ct = ring_ct(d);
     const dim3 grid(S * a.tiles_ci * a.tiles_co);
-    if (wg_use_ring()) {
-      const int D = ring_depth();
-      a.ring_early = ring_early() ? 1 : 0;
-      const int la = ring_la();
-      const int vbn = ct <= 2 ? ring_vb() : 1;
-#define SR_RING(CT_)                                                                                     \
-  if (vbn == 2 && CT_ <= 2) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<(CT_ <= 2 ? CT_ : 2), 2, 3, false, 2>), grid, dim3(512), 0, s, a); \
-  else if (CT_ == 4 && ring_cs(4) == 2) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<4, 2, 3, false, 1, 2>), grid, dim3(512), 0, s, a); \
-  else if (D == 4) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 4>), grid, dim3(256), 0, s, a);   \
-  else if (D == 3) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 3>), grid, dim3(256), 0, s, a);   \
-  else if (la == 5) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 5>), grid, dim3(256), 0, s, a); \
-  else if (a.ring_early) hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2, 3, true>), grid, dim3(256), 0, s, a); \
-  else hipLaunchKernelGGL((conv3x3_wgrad_ring_kernel<CT_, 2>), grid, dim3(256), 0, s, a);
-      if (ct == 1) { SR_RING(1) }
-      else if (ct == 2) { SR_RING(2) }
-      else if (ct == 3) { SR_RING(3) }
-      else { SR_RING(4) }
-#undef SR_RING
-    } else if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<1>, grid, dim3(256), 0, s, a);
-    else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<2>, grid, dim3(256), 0, s, a);
-    else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<3>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(conv3x3_wgrad_halo_kernel<4>, grid, dim3(256), 0, s, a);
+    // in-kernel reduce over groups of G splits (not in the slab-only mode: sr_conv3x3_wgrad_reduce
+    // then reads all S rows); the ticket counters of one launch must fit a bank
+    const int G = ring_red_group();
+    const int S2 = G > 1 ? (S + G - 1) / G : S;
+    const size_t row_f = (size_t)taps * d->Cout * d->Cin;
+    if (G > 1 && !(d->accumulate & 2) && S2 * a.tiles_ci * a.tiles_co <= RING_CNT_PER && S > G &&
+        (size_t)S * row_f * 4 < 0x80000000ull) {
+      static std::atomic<unsigned> bank{0};
+      a.red_g = G;
+      a.red_bank = (int)(bank.fetch_add(1u, std::memory_order_relaxed) % RING_CNT_BANKS);
+      a.red_ws = a.ws + (size_t)S * row_f + (size_t)S * d->Cout;  // after the level-1 slab and bias rows
+      a.red_wsb = db ? a.red_ws + (size_t)S2 * row_f : nullptr;
+      a.ws_bytes = (uint32_t)((size_t)S * row_f * 4);
+      a.wsb_bytes = db ? (uint32_t)((size_t)S * d->Cout * 4) : 0u;
+      a.red_ws_bytes = (uint32_t)((size_t)S2 * row_f * 4);
+      S_red = S2;
+      ws_red = a.red_ws;
+      wsb_red = a.red_wsb;
+    }
+    if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<1>, grid, dim3(256), 0, s, a);
+    else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<2>, grid, dim3(256), 0, s, a);
+    else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<3>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<4>, grid, dim3(256), 0, s, a);
     e = hipGetLastError();
   } else if (wg_use_lin(d)) {
     a.tiles_co = (a.Cout + 191) / 192;
     a.tiles_ci = (a.Cin + 191) / 192;
     hipLaunchKernelGGL(linear_wgrad_kernel, dim3(S * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
-    e = hipGetLastError();
-  } else if (wg_use_tw(d)) {
-    a.tiles_co = a.Cout / 128;
-    a.tiles_ci = a.Cin / 128;
-    a.bias_group = tw_bias_group();
-    const int nb = S * 3 * a.tiles_co * a.tiles_ci +
-                   (a.wsb ? (S + a.bias_group - 1) / a.bias_group * ((a.Cout + 255) / 256) : 0);
-    if (g_variant == 71) hipLaunchKernelGGL(conv3x3_wgrad_tw_kernel<1>, dim3(nb), dim3(768), 0, s, a);
-    else if (g_variant == 72) hipLaunchKernelGGL(conv3x3_wgrad_tw_kernel<2>, dim3(nb), dim3(768), 0, s, a);
-    else hipLaunchKernelGGL(conv3x3_wgrad_tw_kernel<0>, dim3(nb), dim3(768), 0, s, a);
-    e = hipGetLastError();
-  } else if (wg_use_tr3(d)) {
-    a.tiles_co = a.Cout / 128;
-    a.tiles_ci = a.Cin / 128;
-    const int per_split = 3 * a.tiles_co * a.tiles_ci + (a.wsb ? (a.Cout + 255) / 256 : 0);
-    if (g_variant == 47) hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<1>, dim3(S * per_split), dim3(512), 0, s, a);
-    else if (g_variant == 48) hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<2>, dim3(S * per_split), dim3(512), 0, s, a);
-    else if (g_variant == 49) hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<3>, dim3(S * per_split), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL(conv3x3_wgrad_tr3_kernel<0>, dim3(S * per_split), dim3(512), 0, s, a);
     e = hipGetLastError();
   } else if (wg_use_big(d)) {
     a.tiles_co = (a.Cout + 255) / 256;
@@ -6209,7 +5219,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   }
   if (e != hipSuccess) return sr_check(e, "conv3x3_wgrad launch");
   if (d->accumulate & 2) return SR_OK;  // bit 1: slab only (sr_conv3x3_wgrad_reduce later, e.g. on another stream)
-  return wgrad_reduce_launch(d, S, taps, a.ws, a.wsb, dw, db, co_map, ci_map, s);
+  return wgrad_reduce_launch(d, S_red, taps, ws_red, wsb_red, dw, db, co_map, ci_map, s);
 }
 
 int sr_conv3x3_wgrad_reduce(const sr_conv3x3_wgrad_desc* d, void* workspace, size_t ws_bytes, float* dw, float* db,

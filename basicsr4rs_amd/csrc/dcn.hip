@@ -520,12 +520,8 @@ XGeom grad_x_geom(const DcnArgs& a) {
   // largest (tile, halo) whose LDS footprint fits 64 KB; halo 0 still covers the
   // undeformed footprint, anything outside goes to global atomics
   static const int cfg[][2] = {{16, 4}, {16, 2}, {8, 4}, {8, 2}, {8, 0}, {4, 0}};
-  // channels per pass: 8, or SR_DCN_CPP = 16 / 32 (A/B: fewer passes over dcols, a larger LDS image)
-  static const int cpp = [] {
-    const char* e = getenv("SR_DCN_CPP");
-    const int v = e ? atoi(e) : 8;
-    return v == 16 || v == 32 ? v : 8;
-  }();
+  // channels per pass: 8, or knob SR_DCN_CPP = 16 / 32 (A/B: fewer passes over dcols, a larger LDS image)
+  const int cpp = sr_knob(K_DCN_CPP) == 16 || sr_knob(K_DCN_CPP) == 32 ? sr_knob(K_DCN_CPP) : 8;
   XGeom g;
   g.CPP = cpp;
   const size_t lim = cpp == 8 ? 65536 : 160 * 1024;
@@ -744,15 +740,12 @@ __global__ void __launch_bounds__(DW_NT, 4) dcn_fwd_win_kernel(DcnArgs a, const 
 // Ablation mask of dcn_fwd_win_kernel (SR_DCN_DBG, read per call; tools/dcn_ablate.py): 1 no global
 // fallback, 2 constant offsets (no offset / mask reads), 4 no MFMA, 8 no window staging.  Results are
 // wrong under any of them; 0 (unset) is the kernel.
-int dcn_dbg() {
-  const char* e = getenv("SR_DCN_DBG");
-  return e ? atoi(e) : 0;
-}
+int dcn_dbg() { return sr_knob(K_DCN_DBG) > 0 ? sr_knob(K_DCN_DBG) : 0; }
 
 // Window geometry of dcn_fwd_win_kernel: the largest R <= 2 whose LDS (A tile + window) fits 64 KB.
 bool win_geom(const DcnArgs& a, int* R, int* WH, int* WW, size_t* lds) {
-  const char* e = getenv("SR_DCN_R");
-  const int r0 = e && atoi(e) >= 0 && atoi(e) <= 6 ? atoi(e) : 2;
+  const int rk = sr_knob(K_DCN_R);
+  const int r0 = rk >= 0 && rk <= 6 ? rk : 2;
   for (int r = r0; r >= 0; --r) {
     const int wh = (DW_TH - 1) * a.sh + (a.kh - 1) * a.dh + 2 + 2 * r;
     const int ww = (DW_TW - 1) * a.sw + (a.kw - 1) * a.dw + 2 + 2 * r;
@@ -767,10 +760,7 @@ bool win_geom(const DcnArgs& a, int* R, int* WH, int* WW, size_t* lds) {
 
 // Shapes the fused forward takes (see dcn_fwd_mfma_kernel); SR_DCN_FUSED=0 turns it off (A/B).
 bool dcn_fused_ok(const sr_dcn_desc* d, const DcnArgs& a, int cout) {
-  static const bool off = [] {
-    const char* e = getenv("SR_DCN_FUSED");
-    return e && atoi(e) == 0;
-  }();
+  const bool off = sr_knob(K_DCN_FUSED) == 0;
   return !off && d->dtype == SR_BF16 && a.G == 1 && a.C == 64 && a.Cp == 64 && a.cgp == 64 && cout >= 1 &&
          cout <= 64 && a.cpg % 8 == 0 && (size_t)a.H * a.W * a.Cp * 2 < 0x80000000ull;
 }
@@ -923,10 +913,7 @@ __global__ void __launch_bounds__(DW_NT, 2) dcn_coord_win_kernel(DcnArgs a, cons
 // dcn_coord_win_kernel's shapes (as the fused forward's, any Cout) and window (R <= 2, LDS <= 80 KB
 // so two blocks share a CU); SR_DCN_COORD_WIN=0 keeps dcn_coord_grad_kernel (A/B).
 bool coord_win_ok(const sr_dcn_desc* d, const DcnArgs& a) {
-  static const bool off = [] {
-    const char* e = getenv("SR_DCN_COORD_WIN");
-    return e && atoi(e) == 0;
-  }();
+  const bool off = sr_knob(K_DCN_COORD_WIN) == 0;
   return !off && d->dtype == SR_BF16 && a.G == 1 && a.C == 64 && a.Cp == 64 && a.cgp == 64 && a.cpg % 8 == 0 &&
          (size_t)a.H * a.W * a.Cp * 2 < 0x80000000ull;
 }
@@ -1352,12 +1339,8 @@ struct BwdGeom {
   size_t lds1, lds2;
   int fx;  // fixed-point bits of the scatter image (64 / 32)
 };
-// Scatter image (A/B; read per call, so one test process runs both): SR_DCN_GX_FX=64 the int64
-// fixed-point image, else int32
-int gx_fx_env() {
-  const char* e = getenv("SR_DCN_GX_FX");
-  return e && atoi(e) == 64 ? 64 : 32;
-}
+// Scatter image (A/B): knob SR_DCN_GX_FX=64 the int64 fixed-point image, else int32
+int gx_fx_env() { return sr_knob(K_DCN_GX_FX) == 64 ? 64 : 32; }
 
 bool bwd_fused_geom(const sr_dcn_desc* d, const DcnArgs& a, int cop, BwdGeom* bg) {
   if (!coord_win_ok(d, a) || cop < 8 || cop > 64 || cop % 8) return false;

@@ -675,231 +675,16 @@ constexpr int ATT_UPW = 4;  // windows per backward wave
 constexpr int ATT_SLOTS_LANE = 28, ATT_SLOTS = 64 * ATT_SLOTS_LANE;  // per-lane bias-gradient slots
 SR_DEV int bin_base_qk(int g, int c) { return ((g >> 1) - (c >> 3) + 7) * 15 + 4 * (g & 1) - (c & 7) + 7; }
 
-__global__ __launch_bounds__(64) void wattn_bwd_mfma_kernel(AttnArgs a) {
-  // [0, 4K) K image; [4K, 8K) Q, [8K, 12K) dO -- both later overlaid by the 8 KB dS^T image
-  __shared__ __attribute__((aligned(16))) char smem[3 * 4096];
-  __shared__ float sT[225], sBin[225], sD[64];
-  char* sK = smem;
-  char* sQ = smem + 4096;
-  char* sdO = smem + 8192;
-  char* sdST = smem + 4096;
-  const int lane = threadIdx.x;
-  const int g = lane >> 4, c = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
-  // this wave: head h of ATT_UPW consecutive windows (dbias pre-sums stay in registers)
-  const int part = (int)xcd_remap(blockIdx.x, gridDim.x);  // heads of a window group on one XCD
-  const int h = part % a.nH;
-  const int win0 = (part / a.nH) * ATT_UPW;
-  const int bb = bin_base_qk(g, c);
-  float dbs[7][4];
-#pragma unroll
-  for (int d = 0; d < 7; ++d)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dbs[d][r] = 0.f;
-  const bf16_t* qkv = (const bf16_t*)a.qkv;
-  // the head's bias table once per wave (the same for its ATT_UPW windows)
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (lane + 64 * k < 225) {
-      sT[lane + 64 * k] = a.bias_table[(lane + 64 * k) * a.nH + h];
-      sBin[lane + 64 * k] = 0.f;
-    }
-  // global loads of window uw: issued one window ahead (wave occupancy is 1 per SIMD: nothing
-  // else hides their latency), consumed by the next iteration
-  int64_t pix[4];
-  u32x4 qu[4], ku[4], vu[4], du[4], ou[4];
-  f32x4 l4[4];
-  auto fetch = [&](int uw, int64_t* px, u32x4* q_, u32x4* k_, u32x4* v_, u32x4* d_, u32x4* o_, f32x4* l_) {
-    const int wg = win0 + uw;
-    if (uw >= ATT_UPW || wg >= a.N * a.nwin) return;
-    const int unit = wg * a.nH + h;
-    const int n = wg / a.nwin, win = wg - n * a.nwin;
-    const int wy = win / a.nwx, wx = win - (win / a.nwx) * a.nwx;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      px[i] = token_pixel(a, n, wy, wx, 16 * i + c);
-      const bf16_t* row = qkv + px[i] * a.ldq + g * 8;
-      q_[i] = *(const u32x4*)(row + h * 32);
-      k_[i] = *(const u32x4*)(row + (a.nH + h) * 32);
-      v_[i] = *(const u32x4*)(row + (2 * a.nH + h) * 32);
-      const int64_t orow = px[i] * a.ldo + h * 32 + g * 8;
-      d_[i] = *(const u32x4*)((const bf16_t*)a.dout + orow);
-      o_[i] = *(const u32x4*)((const bf16_t*)a.out + orow);
-      l_[i] = *(const f32x4*)(a.lse + (int64_t)unit * 64 + 16 * i + 4 * g);
-    }
-  };
-  fetch(0, pix, qu, ku, vu, du, ou, l4);
-  for (int uw = 0; uw < ATT_UPW; ++uw) {
-  const int wg = win0 + uw;  // global window index n * nwin + win
-  if (wg >= a.N * a.nwin) break;
-  const int n = wg / a.nwin, win = wg - n * a.nwin;
-  const int wy = win / a.nwx, wx = win - (win / a.nwx) * a.nwx;
-  s16x8 qf[4], kf[4], vf[4], df[4];
-  float dd[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    qf[i] = __builtin_bit_cast(s16x8, qu[i]);
-    kf[i] = __builtin_bit_cast(s16x8, ku[i]);
-    vf[i] = __builtin_bit_cast(s16x8, vu[i]);
-    df[i] = __builtin_bit_cast(s16x8, du[i]);
-    *(u32x4*)(sQ + sx_off(16 * i + c, g)) = qu[i];
-    *(u32x4*)(sK + sx_off(16 * i + c, g)) = ku[i];
-    *(u32x4*)(sdO + sx_off(16 * i + c, g)) = du[i];
-    float t = 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      t += bf16_to_f32(du[i][e] & 0xffff) * bf16_to_f32(ou[i][e] & 0xffff) +
-           bf16_to_f32(du[i][e] >> 16) * bf16_to_f32(ou[i][e] >> 16);
-    dd[i] = t;
-  }
-  f32x4 lc4[4];
-  int64_t pxc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    lc4[i] = l4[i];
-    pxc[i] = pix[i];
-  }
-  // the next window's loads, in flight under this window's work
-  fetch(uw + 1, pix, qu, ku, vu, du, ou, l4);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    dd[i] += __shfl_xor(dd[i], 16);
-    dd[i] += __shfl_xor(dd[i], 32);
-    if (g == 0) sD[16 * i + c] = dd[i];
-  }
-  __syncthreads();
-
-  // S = Q K^T and dP = dO V^T: [query 16i + 4g + r][key 16j + c]
-  f32x4 pa[4][4], ds[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pa[i][j] = mfma16(qf[i], kf[j], f32x4{0.f, 0.f, 0.f, 0.f});
-      ds[i][j] = mfma16(df[i], vf[j], f32x4{0.f, 0.f, 0.f, 0.f});
-    }
-  float bt[7][4];
-#pragma unroll
-  for (int d = 0; d < 7; ++d)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bt[d][r] = sT[bb + 30 * (d - 3) + r];
-  // shift-mask regions: query (i, r) and key j of this lane
-  int rq[4][4], rk[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rk[i] = region(wy * 8 + 2 * i + (c >> 3), a.H, 8, a.shift) * 3 + region(wx * 8 + (c & 7), a.W, 8, a.shift);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      rq[i][r] = region(wy * 8 + 2 * i + (g >> 1), a.H, 8, a.shift) * 3 + region(wx * 8 + 4 * (g & 1) + r, a.W, 8, a.shift);
-  }
-  float Dq[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x4 d4 = *(const f32x4*)(sD + 16 * i + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Dq[i][r] = d4[r];
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = pa[i][j][r] * a.scale + bt[i - j + 3][r];
-        if (a.shift && rq[i][r] != rk[j]) v -= 100.f;
-        const float p = __expf(v - lc4[i][r]);
-        const float dsv = p * (ds[i][j][r] - Dq[i][r]);
-        pa[i][j][r] = p;
-        ds[i][j][r] = dsv;
-        dbs[i - j + 3][r] += dsv;
-      }
-
-  // dV^T = dO^T P and dK^T = Q^T dS: [dim 16d + 4g + r][key 16j + c]
-  f32x4 dv[2][4], dk[2][4], dq[2][4];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dv[d][j] = dk[d][j] = dq[d][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    s16x8 at[2], qt[2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      at[d] = frag_tr64(sdO, s, g, tq, tp, 16 * d);
-      qt[d] = frag_tr64(sQ, s, g, tq, tp, 16 * d);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const s16x8 pb = frag_c2(pa[2 * s][j], pa[2 * s + 1][j]);
-      const s16x8 sb = frag_c2(ds[2 * s][j], ds[2 * s + 1][j]);
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        dv[d][j] = mfma16(at[d], pb, dv[d][j]);
-        dk[d][j] = mfma16(qt[d], sb, dk[d][j]);
-      }
-    }
-  }
-  __syncthreads();  // Q / dO images consumed: overlay dS^T
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint2 w2;
-      w2.x = pack_bf16x2(ds[i][j][0], ds[i][j][1]);
-      w2.y = pack_bf16x2(ds[i][j][2], ds[i][j][3]);
-      *(uint2*)(sdST + st_byte(16 * j + c, 16 * i + 4 * g)) = w2;
-    }
-  __syncthreads();
-  // dQ^T = K^T dS^T: [dim 16d + 4g + r][query 16j + c]
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    s16x8 kt[2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d) kt[d] = frag_tr64(sK, s, g, tq, tp, 16 * d);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const s16x8 sb = frag_trST(sdST, s, g, tq, tp, 16 * j);
-#pragma unroll
-      for (int d = 0; d < 2; ++d) dq[d][j] = mfma16(kt[d], sb, dq[d][j]);
-    }
-  }
-  bf16_t* gq = (bf16_t*)a.y;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    bf16_t* row = gq + pxc[j] * a.ldq + 4 * g;
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      uint2 w;
-      w.x = pack_bf16x2(dq[d][j][0] * a.scale, dq[d][j][1] * a.scale);
-      w.y = pack_bf16x2(dq[d][j][2] * a.scale, dq[d][j][3] * a.scale);
-      *(uint2*)(row + h * 32 + 16 * d) = w;
-      w.x = pack_bf16x2(dk[d][j][0] * a.scale, dk[d][j][1] * a.scale);
-      w.y = pack_bf16x2(dk[d][j][2] * a.scale, dk[d][j][3] * a.scale);
-      *(uint2*)(row + (a.nH + h) * 32 + 16 * d) = w;
-      w.x = pack_bf16x2(dv[d][j][0], dv[d][j][1]);
-      w.y = pack_bf16x2(dv[d][j][2], dv[d][j][3]);
-      *(uint2*)(row + (2 * a.nH + h) * 32 + 16 * d) = w;
-    }
-  }
-  __syncthreads();  // LDS images free for the next unit
-  }
-#pragma unroll
-  for (int d = 0; d < 7; ++d)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) atomicAdd(&sBin[bb + 30 * (d - 3) + r], dbs[d][r]);
-  __syncthreads();
-  for (int b = lane; b < 225; b += 64) a.dbias_part[(int64_t)part * 225 + b] = sBin[b];
-}
-
-// The same backward at two waves per SIMD (round 4, default; SR_WATTN_BWD=1 selects the kernel
-// above, which holds a whole window's S / dP tiles, the next window's loads and the bias column in
-// 466 registers at one wave per SIMD, so nothing hides its dependent load -> MFMA -> exp -> MFMA
-// chain).  Here the queries go in two halves of 32 (the K-step of the dV / dK contractions): per
+// Window-attention backward at two waves per SIMD (round 4; round 2's kernel held a whole window's
+// S / dP tiles, the next window's loads and the bias column in 466 registers at one wave per SIMD,
+// so nothing hid its dependent load -> MFMA -> exp -> MFMA chain; it was removed in round 5 with its
+// LDS-atomic bias-gradient form and the 1 / 2 windows-per-wave forms, all measured slower).  Here the queries go in two halves of 32 (the K-step of the dV / dK contractions): per
 // half, S and dP for its two 16-query tiles (64 registers), P and dS, the dV^T / dK^T MFMAs, then
 // dS^T of the half into a [64 keys][32 queries] LDS image and dQ of those 32 queries at once; K rows
 // and Q / dO rows come from the LDS images instead of registers, the bias column from LDS per use.
 // 16.2 KB of LDS and <= 256 registers: two 1-wave blocks per SIMD, one's loads under the other's
-// math.  Per element the same arithmetic in the same order as above (bit-identical dQ / dK / dV).
-template <int UPW, int DB>
+// math.  Per element the same arithmetic in the same order as round 2's kernel (bit-identical dQ / dK / dV).
+template <int UPW>
 __global__ __launch_bounds__(64, 2) void wattn_bwd_mfma2_kernel(AttnArgs a) {
   // [0, 4K) K image, [4K, 8K) Q, [8K, 12K) dO, [12K, 16K) dS^T of one query half
   __shared__ __attribute__((aligned(16))) char smem[4 * 4096];
@@ -1093,71 +878,77 @@ __global__ __launch_bounds__(64, 2) void wattn_bwd_mfma2_kernel(AttnArgs a) {
     }
     __syncthreads();  // LDS images free for the next window
   }
-  if constexpr (DB == 2) {
-    // the lane's 28 pre-summed bias gradients as they are (one 1792-float slot row per wave, folded
-    // into the 225 bins by wattn_dbias_slots / _fold in a fixed order): gfx950's fp32 LDS atomics
-    // cost more than the rest of a wave's tail
-    f32x4* dst = (f32x4*)(a.dbias_part + ((int64_t)part * 64 + lane) * ATT_SLOTS_LANE);
+  // the lane's 28 pre-summed bias gradients as they are (one 1792-float slot row per wave, folded
+  // into the 225 bins by wattn_dbias_slots / _fold in a fixed order): gfx950's fp32 LDS atomics
+  // cost more than the rest of a wave's tail
+  f32x4* dst = (f32x4*)(a.dbias_part + ((int64_t)part * 64 + lane) * ATT_SLOTS_LANE);
 #pragma unroll
-    for (int d = 0; d < 7; ++d) dst[d] = f32x4{dbs[d][0], dbs[d][1], dbs[d][2], dbs[d][3]};
-  } else {
-    float* sBin = (float*)smem;  // over the K image: 225 bins
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (lane + 64 * k < 225) sBin[lane + 64 * k] = 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int d = 0; d < 7; ++d)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(&sBin[bb + 30 * (d - 3) + r], dbs[d][r]);
-    __syncthreads();
-    for (int b = lane; b < 225; b += 64) a.dbias_part[(int64_t)part * 225 + b] = sBin[b];
-  }
+  for (int d = 0; d < 7; ++d) dst[d] = f32x4{dbs[d][0], dbs[d][1], dbs[d][2], dbs[d][3]};
 }
 
-// slot rows (DB 2): stage 1 sums each head's rows per slot (block = head x 64 slots, 16 waves over
-// the rows, fixed-order LDS combine); stage 2 folds a head's 1792 slots into its 225 bins: bin b
-// takes slot (lane, d, r) when bin_base_qk(lane) + 30 (d - 3) + r == b, enumerated in a fixed order
+// slot rows, folded into the table gradient in two fixed-order stages (deterministic):
+// stage 1 (wattn_dbias_slots): block = (head, 256-slot chunk, quarter of the head's rows); a lane
+// sums 4 consecutive slots with 16-B loads over rows j = q + 4 (wave + 16 k) of the head (4 loads in
+// flight), the 16 waves combine through LDS in a fixed order -> slots[q][h][1792];
+// stage 2 (wattn_dbias_fold): one wave per (head, bin): its 64 lanes take the 112 candidate slots
+// (d, r, gh, g1) of the bin two each, sum the 4 quarters, and a fixed xor tree adds the lanes.
+// (Round 4 ran stage 2 as nH blocks of branchy scalar loops: 70 us per call for 225 x 6 values.)
+constexpr int DB_Q = 4;  // quarters of each head's rows in stage 1
 __global__ __launch_bounds__(1024) void wattn_dbias_slots(const float* __restrict__ part, int parts, int nH,
                                                           float* __restrict__ slots) {
-  __shared__ float red[16][65];
-  const int h = blockIdx.x % nH, chunk = blockIdx.x / nH;
+  __shared__ f32x4 red[16][64];
+  constexpr int NCH = ATT_SLOTS / 256;  // 7 chunks of 256 slots
+  const int b = blockIdx.x;
+  const int q = b % DB_Q, ch = (b / DB_Q) % NCH, h = b / (DB_Q * NCH);
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int sl = chunk * 64 + l;
-  float sm = 0.f;
-  for (int p = h + wv * nH; p < parts; p += 16 * nH) sm += part[(int64_t)p * ATT_SLOTS + sl];
+  const int sl = ch * 256 + 4 * l;
+  const int rows = parts / nH;  // rows of head h: p = h + nH j
+  f32x4 sm = {0.f, 0.f, 0.f, 0.f};
+  int j = q + DB_Q * wv;
+  constexpr int STEP = DB_Q * 16;
+  for (; j + 3 * STEP < rows; j += 4 * STEP) {
+    const f32x4 v0 = *(const f32x4*)(part + (int64_t)(h + nH * j) * ATT_SLOTS + sl);
+    const f32x4 v1 = *(const f32x4*)(part + (int64_t)(h + nH * (j + STEP)) * ATT_SLOTS + sl);
+    const f32x4 v2 = *(const f32x4*)(part + (int64_t)(h + nH * (j + 2 * STEP)) * ATT_SLOTS + sl);
+    const f32x4 v3 = *(const f32x4*)(part + (int64_t)(h + nH * (j + 3 * STEP)) * ATT_SLOTS + sl);
+    sm += v0; sm += v1; sm += v2; sm += v3;
+  }
+  for (; j < rows; j += STEP) sm += *(const f32x4*)(part + (int64_t)(h + nH * j) * ATT_SLOTS + sl);
   red[wv][l] = sm;
   __syncthreads();
   if (wv == 0) {
-    float t = 0.f;
+    f32x4 t = red[0][l];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][l];
-    slots[h * ATT_SLOTS + sl] = t;
+    for (int k = 1; k < 16; ++k) t += red[k][l];
+    *(f32x4*)(slots + ((int64_t)q * nH + h) * ATT_SLOTS + sl) = t;
   }
 }
 __global__ __launch_bounds__(256) void wattn_dbias_fold(const float* __restrict__ slots, int nH,
                                                         float* __restrict__ dbias, int acc) {
-  const int h = blockIdx.x, b = threadIdx.x;
-  if (b >= 225) return;
-  const float* sh = slots + h * ATT_SLOTS;
+  const int wid = (int)blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid >= 225 * nH) return;
+  const int h = wid % nH, bin = wid / nH;
   float t = 0.f;
-  for (int d = 0; d < 7; ++d)
-    for (int r = 0; r < 4; ++r) {
-      const int q = b - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
-      if (q < 0 || q >= 225) continue;
-      const int dyp = q / 15, dxp = q - 15 * dyp;  // (g >> 1) - (c >> 3) + 7, 4 (g & 1) - (c & 7) + 7
-      if (dyp < 6 || dyp > 8 || dxp > 11) continue;
-      for (int gh = 0; gh < 2; ++gh) {
-        const int ch = gh - (dyp - 7);
-        if (ch < 0 || ch > 1) continue;
-        for (int g1 = 0; g1 < 2; ++g1) {
-          const int c7 = 4 * g1 - (dxp - 7);
-          if (c7 < 0 || c7 > 7) continue;
-          t += sh[((2 * gh + g1) * 16 + 8 * ch + c7) * ATT_SLOTS_LANE + 4 * d + r];
-        }
-      }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int e = lane + 64 * c;  // candidate (d, r, gh, g1); 112 of them
+    const int d = e >> 4, r = (e >> 2) & 3, gh = (e >> 1) & 1, g1 = e & 1;
+    const int qq = bin - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
+    const int dyp = qq / 15, dxp = qq - 15 * dyp;  // (g >> 1) - (c >> 3) + 7, 4 (g & 1) - (c & 7) + 7
+    const int chh = gh - (dyp - 7), c7 = 4 * g1 - (dxp - 7);
+    const bool v = e < 112 && qq >= 0 && qq < 225 && dyp >= 6 && dyp <= 8 && dxp <= 11 && chh >= 0 && chh <= 1 &&
+                   c7 >= 0 && c7 <= 7;
+    if (v) {
+      const int64_t off = (int64_t)h * ATT_SLOTS + ((2 * gh + g1) * 16 + 8 * chh + c7) * ATT_SLOTS_LANE + 4 * d + r;
+      float u = 0.f;
+#pragma unroll
+      for (int q = 0; q < DB_Q; ++q) u += slots[(int64_t)q * nH * ATT_SLOTS + off];
+      t += u;
     }
-  dbias[b * nH + h] = (acc ? dbias[b * nH + h] : 0.f) + t;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+  if (lane == 0) dbias[bin * nH + h] = (acc ? dbias[bin * nH + h] : 0.f) + t;
 }
 
 __global__ void wattn_dbias_reduce2(const float* __restrict__ part, int units, int nH, int nbins,
@@ -1171,28 +962,8 @@ void dbias_reduce(const float* ws, int parts, int nH, int nbins, float* dbias, i
     return;
   }
   float* slots = const_cast<float*>(ws) + (int64_t)(-parts) * ATT_SLOTS;
-  hipLaunchKernelGGL(wattn_dbias_slots, dim3(nH * (ATT_SLOTS / 64)), dim3(1024), 0, s, ws, -parts, nH, slots);
-  hipLaunchKernelGGL(wattn_dbias_fold, dim3(nH), dim3(256), 0, s, (const float*)slots, nH, dbias, acc);
-}
-
-// SR_WATTN_BWD=1: the one-wave-per-SIMD backward (A/B and parity reference); read per call
-bool attn_bwd_v1() {
-  const char* e = getenv("SR_WATTN_BWD");
-  return e && e[0] == '1';
-}
-// the two-wave kernel's bias gradient: per-lane slot rows (default) or SR_WATTN_DBIAS=atomic
-bool attn_dbias_slots() {
-  if (attn_bwd_v1()) return false;
-  const char* e = getenv("SR_WATTN_DBIAS");
-  return !(e && e[0] == 'a');
-}
-// windows per wave of the two-wave kernel (SR_WATTN_UPW 1 / 2 / 4, read per call): the dbias
-// partial rows are per (head, group of UPW windows)
-int attn_bwd_upw() {
-  if (attn_bwd_v1()) return ATT_UPW;
-  const char* e = getenv("SR_WATTN_UPW");
-  const int u = e ? atoi(e) : 4;
-  return (u == 1 || u == 2 || u == 4) ? u : 4;
+  hipLaunchKernelGGL(wattn_dbias_slots, dim3(nH * (ATT_SLOTS / 256) * DB_Q), dim3(1024), 0, s, ws, -parts, nH, slots);
+  hipLaunchKernelGGL(wattn_dbias_fold, dim3((225 * nH + 3) / 4), dim3(256), 0, s, (const float*)slots, nH, dbias, acc);
 }
 
 bool attn_mfma_ok(const AttnArgs& a, int dtype) {
@@ -1380,7 +1151,8 @@ int sr_window_attn_fwd(int dtype, const void* qkv, int ldq, int N, int H, int W,
 size_t sr_window_attn_bwd_workspace(int N, int H, int W, int ws, int nH) {
   const int nb = (2 * ws - 1) * (2 * ws - 1);
   const size_t units = (size_t)N * (H / ws) * (W / ws) * nH;
-  const size_t rows = units * nb, slots = ws == 8 ? (units + nH) * ATT_SLOTS : 0;  // slot rows at 1 window per wave
+  // slot rows at 1 window per wave + the quarter sums of wattn_dbias_slots
+  const size_t rows = units * nb, slots = ws == 8 ? (units + (size_t)DB_Q * nH) * ATT_SLOTS : 0;
   return (rows > slots ? rows : slots) * sizeof(float);
 }
 
@@ -1399,17 +1171,9 @@ int sr_window_attn_bwd(int dtype, const void* qkv, int ldq, const void* out, con
   int parts = a.units;  // dbias partial rows, interleaved by head (row % nH == head)
   bool slot_rows = false;
   if (attn_mfma_ok(a, dtype)) {
-    const int upw = attn_bwd_upw();
-    parts = nH * ((N * a.nwin + upw - 1) / upw);
-    const bool sl = attn_dbias_slots();
-    slot_rows = sl;
-    if (attn_bwd_v1()) hipLaunchKernelGGL(wattn_bwd_mfma_kernel, dim3(parts), dim3(64), 0, s, a);
-    else if (sl && upw == 1) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<1, 2>), dim3(parts), dim3(64), 0, s, a);
-    else if (sl && upw == 2) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<2, 2>), dim3(parts), dim3(64), 0, s, a);
-    else if (sl) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<4, 2>), dim3(parts), dim3(64), 0, s, a);
-    else if (upw == 1) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<1, 0>), dim3(parts), dim3(64), 0, s, a);
-    else if (upw == 2) hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<2, 0>), dim3(parts), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<4, 0>), dim3(parts), dim3(64), 0, s, a);
+    parts = nH * ((N * a.nwin + ATT_UPW - 1) / ATT_UPW);
+    slot_rows = true;
+    hipLaunchKernelGGL((wattn_bwd_mfma2_kernel<ATT_UPW>), dim3(parts), dim3(64), 0, s, a);
   } else if (dtype == SR_BF16) {
     hipLaunchKernelGGL(wattn_bwd_kernel<bf16_t>, dim3(a.units), dim3(64), 0, s, a);
   } else {
@@ -1425,10 +1189,9 @@ int sr_window_attn_bwd_parts(int dtype, int N, int H, int W, int ws, int nH, int
   AttnArgs a{};
   if (!attn_setup(a, N, H, W, ws, 0, nH, hd, hdp, 1.f)) return 0;
   a.ldq = ldq; a.ldo = ldo;
-  const int upw = attn_bwd_upw();
   if (!attn_mfma_ok(a, dtype)) return a.units;
-  const int parts = nH * ((N * a.nwin + upw - 1) / upw);
-  return attn_dbias_slots() ? -parts : parts;  // negative: slot rows (see sr_hip.h)
+  const int parts = nH * ((N * a.nwin + ATT_UPW - 1) / ATT_UPW);
+  return -parts;  // negative: slot rows (see sr_hip.h)
 }
 
 int sr_window_attn_dbias_reduce(const float* workspace, int parts, int nH, int ws, float* dbias_table, int accumulate,

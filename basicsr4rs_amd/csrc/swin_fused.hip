@@ -741,11 +741,8 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   }
 }
 
-// Windows per block of the fused attention half: SR_SWIN_ATTN_NW=1 / 2 (A/B; read per call)
-int attn_nw() {
-  const char* e = getenv("SR_SWIN_ATTN_NW");
-  return e && atoi(e) == 1 ? 1 : 2;
-}
+// Windows per block of the fused attention half: 2, or knob SR_SWIN_ATTN_NW=1 (A/B)
+int attn_nw() { return sr_knob(K_SWIN_ATTN_NW) == 1 ? 1 : 2; }
 
 }  // namespace
 

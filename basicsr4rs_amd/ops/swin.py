@@ -240,60 +240,6 @@ def layernorm_bwd(dy, x, mean, rstd, weight, Creal, res=None, params=None, row_s
     return dx, dg, db
 
 
-def linear_ln_bwd(dy, wd, spec, N, H, W, x, mean, rstd, weight, Creal, res=None, params=None, row_scale=None):
-    """layernorm_bwd(linear_dgrad(dy, wd, spec, N, H, W), x, mean, rstd, weight, Creal, ...) with the
-    LayerNorm backward in the dgrad GEMM's epilogue (sr_linear_ln_bwd: one launch, the LN input
-    gradient never round-trips HBM), returning what layernorm_bwd returns; None when the call is
-    not on that path (fp32 parity mode, shapes past the wide-K lin kernel) or not asked for.
-
-    Opt-in (``SR_LN_BWD_FUSED=1``): the fused kernel is faster than its two launches (89 vs 51 + 54
-    us at SwinIR-M, B 32) but the step is slower (39.5 vs 38.6 ms, DESIGN note 20) -- its 80 KB of
-    LDS per block leaves no room for the side-stream weight gradients the LayerNorm backward hides."""
-    if x.dtype != torch.bfloat16 or os.environ.get('SR_LN_BWD_FUSED') != '1':
-        return None
-    N_, H_, W_, Cp = x.shape
-    if Cp != spec.cin_p or dy.shape[-1] < spec.cout_p or (res is not None and res.shape[-1] < Cp):
-        return None
-    d = C._desc(x.dtype, N, H, W, spec.cout_p, dy.shape[-1], spec.cin_p, spec.cin_p, spec.cin_p, ksize=1)
-    lib = _lib.load()
-    nparts = lib.sr_linear_ln_bwd_parts(d, Creal)
-    if nparts <= 0:
-        return None
-    M = N * H * W
-    dx = torch.empty_like(x)
-    scaled = torch.empty_like(x) if row_scale is not None else None
-    direct = _direct(params)
-    if direct is not None:
-        dg, db = direct
-    else:
-        dg = torch.empty(Creal, device=x.device, dtype=torch.float32)
-        db = torch.empty(Creal, device=x.device, dtype=torch.float32)
-    ws = torch.empty(nparts * 2 * Creal, device=x.device, dtype=torch.float32)
-    ldr = res.shape[-1] if res is not None else 0
-    nbytes = x.element_size() * M * (spec.cout_p + Cp * (2 + (res is not None) + (scaled is not None)))
-    with ktrace.span('linear_wk_kernel+ln_bwd', 2.0 * M * spec.cin * spec.cout, nbytes):
-        _lib.check(
-            lib.sr_linear_ln_bwd(d, _lib.ptr(dy), _lib.ptr(wd), _lib.ptr(x), Cp, _lib.ptr(mean), _lib.ptr(rstd),
-                                 _lib.ptr(weight.detach()), Creal, _lib.ptr(res), ldr, _lib.ptr(dx), _lib.ptr(row_scale),
-                                 _lib.ptr(scaled), _lib.ptr(ws), ws.numel() * 4, _lib.stream()))
-    if row_scale is not None:
-        dx = (dx, scaled)
-    # the dgamma / dbeta reduce on the weight-gradient side stream, as layernorm_bwd
-    side = C.async_side_stream(x.device) if direct is not None and not ktrace.active() and _PARAM_REDUCE_SIDE else None
-    if side is not None:
-        C.side_launch(side, lambda: _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg),
-                                                                           _lib.ptr(db), 1, _lib.stream())), (ws,),
-                      after=tuple((lambda p=p: C.grad_ready(p)) for p in params))
-        return dx, None, None
-    _lib.check(lib.sr_layernorm_bwd_reduce(_lib.ptr(ws), nparts, Creal, _lib.ptr(dg), _lib.ptr(db),
-                                           int(direct is not None), _lib.stream()))
-    if direct is not None:
-        for p in params:
-            C.grad_ready(p)
-        return dx, None, None
-    return dx, dg, db
-
-
 class _LayerNorm(torch.autograd.Function):
     """Standalone token LayerNorm (PatchEmbed norm / final norm)."""
 
@@ -513,14 +459,9 @@ class _STB(torch.autograd.Function):
         dz = linear_dgrad(g2, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)
         df2w, df2b = linear_wgrad(g2, h, fc2s, N, H, W, params=(f2w, f2b))
         _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
-        # fc1 dgrad + LN2 backward in one launch when the shape allows, else the two ops
-        fb = linear_ln_bwd(dz, f1wd, fc1s, N, H, W, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b), row_scale=s1)
         df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W, params=(f1w, f1b))
-        if fb is not None:
-            dx2, dn2w, dn2b = fb
-        else:
-            dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
-            dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b), row_scale=s1)
+        dln2 = linear_dgrad(dz, f1wd, fc1s, N, H, W)
+        dx2, dn2w, dn2b = layernorm_bwd(dln2, x2, m2, r2, n2w, Cr, res=dout, params=(n2w, n2b), row_scale=s1)
         if s1 is not None:
             dx2, g1 = dx2  # g1 = the proj-branch gradient s1 * dx2, written by the same kernel
         else:
@@ -530,13 +471,9 @@ class _STB(torch.autograd.Function):
         dpw, dpb = linear_wgrad(g1, a, g.proj, N, H, W, params=(pw, pb))
         dqkv, dtab = window_attn_bwd(qkv, a, da, lse, g, N, H, W, scale, tab, table_param=table)
         _, qwd, _ = prepared_linear(qw, qb, g.qkv, dtype)
-        fb = linear_ln_bwd(dqkv, qwd, g.qkv, N, H, W, x, m1, r1, n1w, Cr, res=dx2, params=(n1w, n1b))
         dqw, dqb = linear_wgrad(dqkv, ln1, g.qkv, N, H, W, params=(qw, qb))
-        if fb is not None:
-            dx, dn1w, dn1b = fb
-        else:
-            dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
-            dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2, params=(n1w, n1b))
+        dln1 = linear_dgrad(dqkv, qwd, g.qkv, N, H, W)
+        dx, dn1w, dn1b = layernorm_bwd(dln1, x, m1, r1, n1w, Cr, res=dx2, params=(n1w, n1b))
         return (dx, None, None, None, None, None, None, dn1w, dn1b, dqw, dqb, dtab, dpw, dpb, dn2w, dn2b, df1w, df1b, df2w,
                 df2b)
 

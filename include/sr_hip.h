@@ -39,6 +39,13 @@ enum sr_act { SR_ACT_NONE = 0, SR_ACT_RELU = 1, SR_ACT_LRELU = 2 };
 /* Library identity / error reporting. */
 const char* sr_version(void);
 const char* sr_last_error(void);
+/* Tuning knobs (A/B switches and split-plan targets, not part of the reference interface).  Each
+ * knob is its environment variable of the same name (SR_RING_RED, SR_LWK, SR_DCN_GX_FX, ...), read
+ * once per process; sr_set_knob overrides it at run time (value < 0: back to the built-in default)
+ * and stores the previous value in *previous when non-NULL.  sr_get_knob returns the current value
+ * (-1 unset, -2 unknown name). */
+int sr_set_knob(const char* name, int value, int* previous);
+int sr_get_knob(const char* name);
 
 /* ---------------------------------------------------------------------------------
  * 3x3 convolution, stride 1, zero padding 1 (implicit GEMM on MFMA).
@@ -100,19 +107,6 @@ typedef struct sr_conv3x3_desc {
 int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_gamma, const float* ln_beta, int ln_C,
                      float eps, void* ln_out, float* ln_mean, float* ln_rstd, const void* w, const float* bias, void* y,
                      void* aux, void* stream);
-/* LayerNorm backward fused into the dgrad GEMM that produces its input (round 4; the reference's
- * norm1 / norm2 autograd, swinir_arch.py:290, 322): dy (bf16 rows [M][Cin]) x wd (the GEMM image of the
- * linear whose input was the LayerNorm output) gives d = dL/d(LN out) (rounded to bf16, not stored);
- * dx = rstd (d gamma - mean_c(d gamma) - xh mean_c(d gamma xh)) (+ res) with xh = (x - mean) rstd over
- * the ln_C real channels, written to dx (bf16 [M][Cout], padded channels zero) and, with row_scale,
- * dx * row_scale[m / (H W)] to dx_scaled; the dgamma / dbeta partial rows go to partial
- * ([sr_linear_ln_bwd_parts][2][ln_C] floats), summed by sr_layernorm_bwd_reduce.  bf16, ksize 1,
- * Cout <= 192 (one output tile holds whole rows), dense output rows; 0 parts = not supported. */
-int sr_linear_ln_bwd_parts(const sr_conv3x3_desc* d, int ln_C);
-int sr_linear_ln_bwd(const sr_conv3x3_desc* d, const void* dy, const void* wd, const void* x, int ldx,
-                     const float* mean, const float* rstd, const float* gamma, int ln_C, const void* res, int ldr,
-                     void* dx, const float* row_scale, void* dx_scaled, float* partial, size_t part_bytes,
-                     void* stream);
 
 
 /* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.

@@ -243,81 +243,6 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize('shape', [(2, 6, 64, 128, 128), (1, 4, 192, 256, 128), (32, 8, 64, 256, 256),
-                                   (1, 5, 64, 384, 256), (1, 1, 64, 128, 256), (4, 64, 64, 256, 256)])
-def test_wgrad_tw_vs_fp64(cuda, shape):
-    """12-wave tap-row wgrad (round 4, conv3x3_wgrad_tw_kernel: a kernel row's three taps on
-    different waves, one x halo row per K-step): image top / bottom rows, the left / right halo
-    columns, several 64-px segments per row, multi-image splits, the EDSR-L body shape, against
-    fp64 on the same bf16 operands and against the per-tap pp kernel (variant 0); opt-in (variant 70)."""
-    N, H, W, cin, cout = shape
-    torch.manual_seed(13)
-    dt = torch.bfloat16
-    lib = _lib.load()
-    x = torch.randn(N, H, W, cin).to(dt)
-    dy = torch.randn(N, H, W, cout).to(dt)
-    d = _lib.WgradDesc()
-    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
-    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, cout, 0, 3
-    outs = []
-    try:
-        _lib.check(lib.sr_conv3x3_set_variant(70))
-        assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_tw_kernel'
-        for variant in (70, 0):
-            _lib.check(lib.sr_conv3x3_set_variant(variant))
-            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0))
-    finally:
-        _lib.check(lib.sr_conv3x3_set_variant(0))
-    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
-    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
-    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
-    torch.cuda.synchronize()
-    dw, db = outs[0]
-    assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
-    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
-    assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
-
-
-@pytest.mark.parametrize('shape', [(2, 6, 64, 128, 128, 0), (1, 4, 192, 256, 128, 0), (32, 8, 64, 256, 256, 0),
-                                   (2, 2, 128, 128, 512, 2), (1, 5, 64, 384, 256, 0), (3, 3, 128, 256, 1024, 2),
-                                   (1, 1, 64, 128, 256, 0)])
-def test_wgrad_tr3_vs_fp64(cuda, shape):
-    """Tap-row wgrad kernel (three taps of a kernel row per block from one x halo row per K-step;
-    image top / bottom rows, the left / right halo columns, multi-image splits, pixel-shuffled dy)
-    against fp64 on the same bf16 operands and against the per-tap pp kernel (variant 0); opt-in (variant 46)."""
-    N, H, W, cin, cout, ps = shape
-    torch.manual_seed(12)
-    dt = torch.bfloat16
-    lib = _lib.load()
-    x = torch.randn(N, H, W, cin).to(dt)
-    if ps:
-        dy = torch.randn(N, H * ps, W * ps, cout // (ps * ps)).to(dt)
-        dy_gemm = O.pixel_unshuffle(dy.permute(0, 3, 1, 2).double(), ps)
-    else:
-        dy = torch.randn(N, H, W, cout).to(dt)
-        dy_gemm = dy.permute(0, 3, 1, 2).double()
-    d = _lib.WgradDesc()
-    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
-    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.out_ps, d.ksize = cin, cin, cin, cout, cout, dy.shape[-1], ps, 3
-    outs = []
-    try:
-        _lib.check(lib.sr_conv3x3_set_variant(46))  # the tap-row kernel is opt-in
-        assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_tr3_kernel'
-        for variant in (46, 0):
-            _lib.check(lib.sr_conv3x3_set_variant(variant))
-            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
-    finally:
-        _lib.check(lib.sr_conv3x3_set_variant(0))
-    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
-    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
-    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy_gemm).sum().backward()
-    torch.cuda.synchronize()
-    dw, db = outs[0]
-    assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
-    assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
-    assert (dw - outs[1][0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
-
-
 @pytest.mark.parametrize('shape', [(2, 64, 64, 184, 576), (1, 64, 64, 192, 184), (3, 8, 64, 184, 360),
                                    (1, 8, 64, 360, 184), (1, 5, 13, 64, 64), (1, 3, 7, 200, 72),
                                    (4, 32, 32, 384, 384), (1, 1, 1, 64, 64)])
@@ -383,6 +308,9 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
         for variant in (62, 0, 67):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
             outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
+        _lib.check(lib.sr_conv3x3_set_variant(62))
+        with _lib.knob('SR_RING_RED', 4):  # the in-kernel group reduce over the output tiles' splits
+            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
     w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
@@ -392,24 +320,25 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
     dw, db = outs[0]
     assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
-    for other in outs[1:]:  # the automatic choice, and variant 67 (no shuffled-dy ring)
+    for other in outs[1:]:  # the automatic choice, variant 67 (no shuffled-dy ring), the in-kernel reduce
         assert (dw - other[0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
         assert (db - other[1]).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
 
 
 @pytest.mark.parametrize('shape', [(2, 3, 64, 64, 64, 1), (1, 2, 128, 192, 32, 1), (1, 5, 64, 160, 48, 1),
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
-                                   (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2)])
-@pytest.mark.parametrize('variant', [0, 65, 73, 74, 75])
-def test_wgrad_halo_vs_fp64(cuda, shape, variant):
+                                   (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2),
+                                   (16, 16, 64, 64, 64, 1), (6, 22, 64, 192, 32, 1), (4, 32, 128, 64, 64, 2)])
+@pytest.mark.parametrize('red', [0, 2, 3, 4])
+def test_wgrad_halo_vs_fp64(cuda, shape, red):
     """All-taps halo wgrad (Cout <= 64, W % 64 == 0), row-streaming form: channel slices of
     wider buffers (ldx, xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather
     (in_up = 2), splits that cross image boundaries (rows per split not dividing H), several
     64-px column segments per row, ragged last split, against an fp64 CPU reference on the same
-    bf16 operands; variant 0: the default 4-wave blocks; 65: the opt-in early-issue schedule (one barrier
-    per step, W 64 only); 73: two co groups per 8-wave block sharing one x ring (Cout 49..64); 74: two
-    row groups per 8-wave block (Cout <= 32); 75: Cout 64 as two 32-channel co-tile blocks over twice the
-    rows -- the round-4 A/B forms."""
+    bf16 operands.  red: splits per in-kernel reduce group (knob SR_RING_RED; 0 = the standalone slab
+    reduce over all splits): the last-arriving block of each group sums the group's slab rows in split
+    order (ragged last groups: 7 splits in groups of 4 + 3, etc.), the standalone reduce then sums the
+    group rows."""
     N, H, W, cin, cout, up = shape
     torch.manual_seed(9)
     dt = torch.bfloat16
@@ -430,13 +359,13 @@ def test_wgrad_halo_vs_fp64(cuda, shape, variant):
     d.Cout = d.Cout_real = cout
     d.ldx, d.xcoff, d.ldy, d.ycoff = cin + 24, 8, cout + 16, 16
     assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_ring_kernel'
-    _lib.check(lib.sr_conv3x3_set_variant(variant))
-    try:
-        dw, db = C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
-                                  xcoff=8, ldy=cout + 16, ycoff=16, in_up=up)
+    with _lib.knob('SR_RING_RED', red):
+        runs = [C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
+                                 xcoff=8, ldy=cout + 16, ycoff=16, in_up=up) for _ in range(2)]
         torch.cuda.synchronize()
-    finally:
-        _lib.check(lib.sr_conv3x3_set_variant(0))
+    dw, db = runs[0]
+    # deterministic: the group sums are in split order whichever block arrives last
+    assert torch.equal(dw, runs[1][0]) and torch.equal(db, runs[1][1])
     tol = 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (dw.cpu().double() - w.grad).abs().max().item() <= tol
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
@@ -937,41 +866,3 @@ def test_prepared_images_freed_with_their_weight(cuda):
     C._retire_table(torch.bfloat16)
     gc.collect()
     assert len(C._PREP_ALL) == n0
-
-
-@pytest.mark.parametrize('shape', [(1, 4, 256, 8, 256), (2, 3, 256, 64, 64), (1, 2, 256, 32, 128),
-                                   (1, 3, 256, 3, 64)])
-@pytest.mark.parametrize('epi', ['plain', 'relu_res'])
-def test_fwd_halo_w256_wide_vs_fp64(cuda, shape, epi, monkeypatch):
-    """The one-row halo tiles for W 256 convs with Cout a multiple of 64 (SR_HALO_W256=1: the HR
-    conv_last dgrads, 3 -> 64 / 256 channels, and the RRDB 256^2 dgrad), DIRECT epilogue, against
-    fp64 on the same bf16 operands; the image's top / bottom rows and left / right halo columns."""
-    monkeypatch.setenv('SR_HALO_W256', '1')
-    N, H, W, cin, cout = shape
-    torch.manual_seed(9)
-    dt = torch.bfloat16
-    lib = _lib.load()
-    cin_p = (cin + 7) // 8 * 8
-    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
-    spec = C.ConvSpec(cin, cout)
-    wf, wd, bg = C.prepared(conv.weight, conv.bias, spec, dt)
-    x = torch.zeros(N, H, W, cin_p, device=cuda)
-    x[..., :cin] = torch.randn(N, H, W, cin, device=cuda)
-    x = x.to(dt)
-    res = torch.randn(N, H, W, cout, device=cuda).to(dt)
-    kw = {}
-    if epi == 'relu_res':
-        kw.update(act=_lib.ACT_RELU, res=res, beta=1.0)
-    d = C._desc(dt, N, H, W, cin_p, cin_p, cout, cout, cout)
-    if epi == 'relu_res':
-        d.act = _lib.ACT_RELU
-    assert lib.sr_conv3x3_fwd_kernel_name(d) == b'conv3x3_fwd_halo_kernel'
-    y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
-    C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin_p, cout, cout, **kw)
-    torch.cuda.synchronize()
-    xd = x[..., :cin].permute(0, 3, 1, 2).double().cpu()
-    ref = F.conv2d(xd, bf(conv.weight.detach().cpu()).double(), conv.bias.detach().cpu().double(), padding=1)
-    if epi == 'relu_res':
-        ref = F.relu(ref) + res.permute(0, 3, 1, 2).double().cpu()
-    got = y.permute(0, 3, 1, 2).double().cpu()
-    assert (got - ref).abs().max().item() <= 2e-2 * max(1.0, ref.abs().max().item())

@@ -176,7 +176,7 @@ def test_ddp_graph_segments_match_full_batch(cuda, async_wgrad=False):
         assert err < 2e-4, (k, err)
 
 
-def _nccl_worker(port, q, async_wgrad=False, net=EDSR_S):
+def _nccl_worker(port, q, async_wgrad=False, netcfg=EDSR_S):
     """World 1 over RCCL: the segmented graph's replay issues real RCCL all-reduces."""
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
@@ -188,7 +188,7 @@ def _nccl_worker(port, q, async_wgrad=False, net=EDSR_S):
     out = []
     for graph in (False, True):
         torch.manual_seed(0)
-        o = _opt(True, 1, 0, 0.05, async_wgrad, graph, net)
+        o = _opt(True, 1, 0, 0.05, async_wgrad, graph, netcfg)
         o['train']['use_amp'] = True
         model = build_model(o)
         assert bool(model.async_wgrad) == bool(async_wgrad), 'side-stream mode silently changed'

@@ -156,7 +156,7 @@ def test_dcn_fused_forward(cuda, case, need_grad):
 
 @pytest.mark.parametrize('case', FUSED_CASES)
 @pytest.mark.parametrize('form', ['i32_nchw', 'i64_nchw', 'i32_nhwc'])
-def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, monkeypatch):
+def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, knob):
     """sr_dcn_bwd_fused (round 4: each tap's dcols tile formed on MFMA inside the coordinate-gradient
     and scatter kernels, never stored) against the dcols path on the same operands: dcols =
     bf16(dy x W) by the 1x1 GEMM, then sr_dcn_col2im.  Both sample the same bf16 dcols values (up to
@@ -164,7 +164,7 @@ def test_dcn_fused_backward_vs_dcols_path(cuda, case, form, monkeypatch):
     offsets of std 2 put many samples past the R = 2 windows onto the global paths.  Forms: the int32
     (default) or int64 fixed-point scatter image; grad x written in full as NCHW (the op's form: the
     coordinate kernel zeroes it -- the buffer starts as NaN here) or accumulated into a zeroed NHWC map."""
-    monkeypatch.setenv('SR_DCN_GX_FX', '64' if form.startswith('i64') else '32')
+    knob('SR_DCN_GX_FX', 64 if form.startswith('i64') else 32)
     nchw = form.endswith('nchw')
     N, C, H, W, Cout, k, s, p, d, groups, dg, modulated = case
     x, off, msk, w, b, dy = _dcn_inputs(case, seed=3)

@@ -11,7 +11,7 @@ x2 = x + s1 * proj(WindowAttention(qkv(LN1(x)))) in one launch
 * geometries: SwinIR-M (C 180, 6 heads, hd 30), shifted and not, an odd window count (the block's
   second window past the end), SwinIR-light (C 60, hd 10), 3 heads of 32 with a DropPath row scale;
   inference mode (no saved tensors) writes the same x2;
-* both block shapes: two windows per 8-wave block and one window per 4-wave block (SR_SWIN_ATTN_NW).
+* both block shapes: two windows per 8-wave block and one window per 4-wave block (knob SR_SWIN_ATTN_NW).
 """
 import pytest
 import torch
@@ -93,8 +93,8 @@ def _unpad_heads(t, g):
 
 @pytest.mark.parametrize('geom', GEOMS)
 @pytest.mark.parametrize('nw', ['1', '2'])
-def test_swin_attn_fused_vs_unfused_and_fp64(cuda, geom, nw, monkeypatch):
-    monkeypatch.setenv('SR_SWIN_ATTN_NW', nw)  # windows per block (read per call)
+def test_swin_attn_fused_vs_unfused_and_fp64(cuda, geom, nw, knob):
+    knob('SR_SWIN_ATTN_NW', int(nw))  # windows per block
     N, H, W, C, nH, shift, rsc = geom
     S, g, x, p = _setup(cuda, N, H, W, C, nH, shift, rsc)
     n1w, n1b, qw, qb, pw, pb, table, s1, qwf, qbg, pwf, pbg, scale = p

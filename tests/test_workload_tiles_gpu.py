@@ -24,7 +24,10 @@ Tolerances: bf16 keeps 8 mantissa bits, so every stored activation and gradient 
 rounding error up to 2^-9.  The per-parameter max-error bounds are ~2x the maxima observed in round 4
 (printed by each test; profiles/r04/tests): RCAN B 8 0.062 -> 0.12, RCAN B 32 0.036 -> 0.07, EDSR
 0.068 -> 0.13; RRDB (0.105) and SwinIR (0.117) keep 0.15 (~1.4x) -- their worst tensors are biases
-of 32-channel convs / the qkv weight, whose gradients sum many bf16-rounded terms.  A defect in a kernel (a wrong tap, a missed row, a race) shows up as a
+of 32-channel convs / the qkv weight, whose gradients sum many bf16-rounded terms.  Round 5 adds the
+per-parameter relative L2 error ||g - g_ref|| / ||g_ref|| at ~1.5x its observed maximum (RCAN B 8
+0.049, B 32 0.039, RRDB 0.075, EDSR 0.056, SwinIR 0.097 on a LayerNorm weight): the worst tensors
+are short vectors (biases, LayerNorm weights), so it sits close to the max error.  A defect in a kernel (a wrong tap, a missed row, a race) shows up as a
 cosine far below 0.99 on the affected tensors, not as a few percent of max error.
 
 ``test_rrdb_full_depth_error_is_bf16_storage_rounding`` explains the bench's RRDB bf16 parity
@@ -113,17 +116,17 @@ def _run(cuda, cfg, batch, lr_px, kernels, out_tol, grad_tol, cos_min=0.995, see
 def test_rcan_workload_tile_bf16(cuda):
     # B 8: 512 LR rows over 256 band blocks, two rows per band (the bench's B 32 has eight)
     _run(cuda, RCAN, 8, 64, ['conv3x3_fwd_band_kernel', 'conv3x3_wgrad_ring_kernel+reduce', 'conv3x3_fwd_pph_kernel',
-                             'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.12)
+                             'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.12, l2_tol=0.075)
 
 
 def test_rrdb_workload_tile_bf16(cuda):
     _run(cuda, RRDB, 2, 128, ['conv3x3_fwd_band_kernel', 'conv3x3_fwd_halo_kernel', 'conv3x3_wgrad_ring_kernel+reduce',
-                              'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.15)
+                              'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.15, l2_tol=0.11)
 
 
 def test_edsr_l_workload_tile_bf16_fwd_bwd(cuda):
     _run(cuda, EDSR_L4, 2, 64, ['conv3x3_fwd_pph_kernel', 'conv3x3_fwd_tail_kernel', 'conv3x3_wgrad_pp_kernel+reduce'],
-         out_tol=5e-3, grad_tol=0.13)
+         out_tol=5e-3, grad_tol=0.13, l2_tol=0.085)
 
 
 def test_swinir_m_workload_tile_bf16(cuda):
@@ -131,7 +134,7 @@ def test_swinir_m_workload_tile_bf16(cuda):
     # round 4); the backward keeps its kernels
     _run(cuda, SWINIR_M2, 2, 64, ['swin_attn_block_fwd_kernel', 'swin_mlp_block_fwd_kernel', 'wattn_bwd_kernel',
                                   'linear_wgrad_kernel+reduce', 'linear_wk_kernel', 'conv3x3_wgrad_ring_kernel+reduce'],
-         out_tol=5e-3, grad_tol=0.15)
+         out_tol=5e-3, grad_tol=0.15, l2_tol=0.145)
 
 
 def test_rcan_b32_bench_geometry_bf16(cuda):
@@ -140,7 +143,7 @@ def test_rcan_b32_bench_geometry_bf16(cuda):
     a quarter of them), checked against fp64 instead of only graph == eager."""
     _run(cuda, dict(RCAN, num_group=1, num_block=1), 32, 64,
          ['conv3x3_fwd_band_kernel', 'conv3x3_wgrad_ring_kernel+reduce', 'conv3x3_fwd_pph_kernel',
-          'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.07)
+          'conv3x3_fwd_tail_kernel'], out_tol=5e-3, grad_tol=0.07, l2_tol=0.06)
 
 
 def test_rrdb_full_depth_error_is_bf16_storage_rounding(cuda):
