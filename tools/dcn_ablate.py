@@ -1,5 +1,5 @@
 """Ablations of the windowed fused DCN forward at the C5 op config (GPU box): kernel-only time
-(HIP events around back-to-back sr_dcn_fwd_fused calls) for SR_DCN_DBG masks / SR_DCN_R radii,
+(HIP events around back-to-back sr_dcn_fwd_fused calls) for the SR_DCN_DBG masks / SR_DCN_R radii knobs,
 then the op's fwd time.  Usage: python tools/dcn_ablate.py"""
 import os
 import sys
@@ -42,14 +42,12 @@ def main():
     if os.environ.get('RS') == 'none':  # the plain kernel only (PMC passes): fwd, then fwd + cols
         print(f'fwd {t(it=5):.1f} us, with cols {t(cols, it=5):.1f} us')
         return
+    from basicsr4rs_amd import _lib
     for r in (os.environ.get('RS') or '2 3 4 1 0').split():
-        os.environ['SR_DCN_R'] = r
         for dbg in (0, 1, 2, 4, 8, 3, 7, 15):
-            os.environ['SR_DCN_DBG'] = str(dbg)
-            print(f'R {r} dbg {dbg:2d}: {t():7.1f} us' + (f'   with cols {t(cols):7.1f} us' if dbg == 0 else ''),
-                  flush=True)
-    os.environ['SR_DCN_DBG'] = '0'
-    os.environ['SR_DCN_R'] = '2'
+            with _lib.knob('SR_DCN_R', int(r)), _lib.knob('SR_DCN_DBG', dbg):  # library knobs (sr_set_knob)
+                print(f'R {r} dbg {dbg:2d}: {t():7.1f} us' + (f'   with cols {t(cols):7.1f} us' if dbg == 0 else ''),
+                      flush=True)
 
 
 if __name__ == '__main__':

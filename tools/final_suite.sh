@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 4 final A: the whole GPU test suite, smoke(), and the bench line of every workload (default
-# configuration, as the driver runs it) -> gpurun_out/r4final/
+# Closing evidence: the whole GPU test suite, smoke(), and the bench line of every workload (default
+# configuration, as the driver runs it): bash tools/final_suite.sh <tag> -> gpurun_out/<tag>/
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r4final
+OUT=gpurun_out/${1:-final}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider \
   > $OUT/gpu_tests.log 2>&1; rc=$?; tail -4 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit 1

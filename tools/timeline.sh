@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 WL=${1:-swinir}
 TAG=${2:-}
 shift 2 2>/dev/null || shift $#
-OUT=gpurun_out/r4tl_$WL$TAG
+OUT=gpurun_out/tl_$WL$TAG
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof -o run -- python3 bench.py --workload $WL \
   --steps 10 --warmup 3 --no-cpu-baseline --no-parity "$@" > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
