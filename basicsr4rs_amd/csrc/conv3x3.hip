@@ -16,7 +16,6 @@
 // bias, activation, ReLU-mask gate, scale, residual, pixel-shuffle / NCHW store with
 // 16-byte coalesced stores.
 #include <cstdlib>
-#include <atomic>
 #include "sr_common.h"
 #include "sr_internal.h"
 
@@ -2546,12 +2545,6 @@ struct WgArgs {
   int tiles_co, tiles_ci, splits, kper;  // kper: pixels per split (multiple of KSTEP)
   int bias_group;  // pp kernel: > 0 = the bias-role blocks come after all tile blocks, each doing this many splits
   int bias_fused;  // pp kernel: no bias-role blocks; the centre-tap, first-ci-tile blocks sum dy as well
-  // ring kernel in-kernel split reduce (red_g > 1): level-2 slab [S / G][9][Cin][Cout] + bias rows,
-  // the counter bank, and the byte sizes of the buffer descriptors
-  int red_g, red_bank;
-  float* red_ws;
-  float* red_wsb;
-  uint32_t ws_bytes, wsb_bytes, red_ws_bytes;
   FastDiv fd_W, fd_H, fd_cps;
   unsigned long long* stamps;  // diagnostics (SR_BAND_STAMPS builds): per-block phase cycles
 };
@@ -3520,18 +3513,13 @@ __global__ __launch_bounds__(512) void linear_wgrad_kernel(WgArgs a) {
 //
 // Output: the block's [tap][ci][co] partial sums (co fastest: a lane's 4 accumulator rows are 4
 // consecutive co, one 16-B store per (tap, co tile)) into slab row `split` of [S][9][Cin][Cout].
-// In-kernel split reduce (a.red_g = G > 1, round 5): the slab rows are stored write-through (sc1),
-// every wave drains them, and one lane takes a ticket on the (group of G splits, tile) counter; the
-// block that draws the group's last ticket sums the group's rows IN SPLIT ORDER (its own from its
-// registers, the others by sc1 loads: the hand-off of cdna_hip_programming.md §6 Guideline 16, R1 --
-// no fence, correct for any XCD placement), writes the sum into row `group` of the level-2 slab
-// (a.red_ws / a.red_wsb) and resets the counter for the next launch.  The standalone reduce then
-// reads S / G rows instead of S.  Deterministic: the order is fixed whichever block arrives last.
+// (Round 5 tried an in-kernel reduce: write-through slab rows, a ticket per group of G splits, the
+// last arriver summing the group's rows in split order into a level-2 slab for the standalone reduce.
+// Measured in the step it lost badly -- RCAN 38.1 -> 51.0 / 60.6 ms at G 2 / 4, RRDB 67.3 -> 77.6 /
+// 80.7 ms: each group's tail reads (G - 1) x 147 KB at a few GB/s per block while the chip-wide reduce
+// it replaces reads the whole slab in ~11 us -- and it was removed)
 // ------------------------------------------------------------------------------------
 SR_DEV int hrow(int r) { return r ^ (((r >> 3) & 1) << 2); }
-
-constexpr int RING_CNT_BANKS = 64, RING_CNT_PER = 2048;  // ticket counters: a bank per launch (cycled)
-__device__ unsigned g_ring_cnt[RING_CNT_BANKS * RING_CNT_PER];  // zero at load; last arrivers reset theirs
 
 template <int CO_T>
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
@@ -3719,112 +3707,17 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   const int c16 = lane & 15;
   const int ci = ci0 + w * 16 + c16;
-  const int G = a.red_g;
-  if (G <= 1) {  // slab row `split`; the standalone reduce sums the S rows
-    if (ci < a.Cin) {
+  // slab row `split`; the standalone reduce sums the S rows
+  if (ci < a.Cin) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        float* ws = a.ws + (((size_t)split * 9 + t) * a.Cin + ci) * a.Cout;
-#pragma unroll
-        for (int c = 0; c < CO_T; ++c) {
-          const int co = co0 + c * 16 + g * 4;
-          if (co < a.Cout) *(f32x4*)(ws + co) = acc[t][c];
-        }
-      }
-    }
-    if (do_bias && c16 == 0) {
-#pragma unroll
-      for (int c = 0; c < CO_T; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = co0 + c * 16 + g * 4 + r;
-          if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
-        }
-    }
-    return;
-  }
-
-  // ---- in-kernel reduce over the group's G splits (see the header comment) ----
-  const size_t row_f = (size_t)9 * a.Cin * a.Cout;  // floats per slab row
-  const __amdgpu_buffer_rsrc_t wsr = make_rsrc(a.ws, a.ws_bytes);
-  const __amdgpu_buffer_rsrc_t wbr = make_rsrc(a.wsb, a.wsb ? a.wsb_bytes : 0u);
-  // this lane's element offset inside a slab row for (tap t, co tile c); SR_OOB-style masking
-  // through the descriptor: an offset past ws_bytes stores / loads nothing
-  auto eoff = [&](int t, int c) -> uint32_t {
-    const int co = co0 + c * 16 + g * 4;
-    return (ci < a.Cin && co < a.Cout) ? (uint32_t)((((size_t)t * a.Cin + ci) * a.Cout + co) * 4) : SR_OOB;
-  };
-  const uint32_t my_row = (uint32_t)((size_t)split * row_f * 4);
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int c = 0; c < CO_T; ++c) {
-      const uint32_t o = eoff(t, c);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[t][c]), wsr, o == SR_OOB ? SR_OOB : my_row + o,
-                                             0, 16);  // aux 16: sc1 (write-through)
-    }
-  if (do_bias && c16 == 0) {
-#pragma unroll
-    for (int c = 0; c < CO_T; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + c * 16 + g * 4 + r;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(accb[c][r]), wbr,
-                                              co < a.Cout ? (uint32_t)(((size_t)split * a.Cout + co) * 4) : SR_OOB, 0, 16);
-      }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  const int grp = split / G, g0 = grp * G;
-  const int gs = min(G, a.splits - g0);
-  unsigned* flag = (unsigned*)smem;  // the rings are free: every wave passed the last step's barriers
-  if (tid == 0) {
-    unsigned* cnt = g_ring_cnt + a.red_bank * RING_CNT_PER + grp * per_split + rem_;
-    const unsigned t = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = t == (unsigned)(gs - 1);
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
-    *flag = last ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*flag == 0u) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the ticket
-  const __amdgpu_buffer_rsrc_t w2r = make_rsrc(a.red_ws, a.red_ws_bytes);
-  const uint32_t out_row = (uint32_t)((size_t)grp * row_f * 4);
-  // three taps at a time: the other rows' loads of those taps in flight together (<= 3 x 12 x 16 B
-  // per lane), then the sum in split order
-#pragma unroll
-  for (int t0 = 0; t0 < 9; t0 += 3) {
-    f32x4 ld[3][3][CO_T];  // [other row k][tap][co tile]
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int sk = g0 + k + (g0 + k >= split ? 1 : 0);  // the k-th row of the group other than ours
-      const bool v = k < gs - 1;
-      const uint32_t rowb = (uint32_t)((size_t)sk * row_f * 4);
-#pragma unroll
-      for (int t = 0; t < 3; ++t)
-#pragma unroll
-        for (int c = 0; c < CO_T; ++c) {
-          const uint32_t o = eoff(t0 + t, c);
-          ld[k][t][c] = v ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          wsr, o == SR_OOB ? SR_OOB : rowb + o, 0, 16))
-                          : f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < 9; ++t) {
+      float* ws = a.ws + (((size_t)split * 9 + t) * a.Cin + ci) * a.Cout;
 #pragma unroll
       for (int c = 0; c < CO_T; ++c) {
-        // rows g0 .. g0 + gs - 1 in order: ours (registers) at position split - g0
-        f32x4 s = split == g0 ? acc[t0 + t][c] : ld[0][t][c];
-#pragma unroll
-        for (int j = 1; j < 4; ++j)
-          if (j < gs) {
-            const int k = j - (split < g0 + j ? 1 : 0);  // index among the other rows
-            s += (g0 + j == split) ? acc[t0 + t][c] : ld[k][t][c];
-          }
-        const uint32_t o = eoff(t0 + t, c);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, s), w2r, o == SR_OOB ? SR_OOB : out_row + o, 0, 0);
+        const int co = co0 + c * 16 + g * 4;
+        if (co < a.Cout) *(f32x4*)(ws + co) = acc[t][c];
       }
+    }
   }
   if (do_bias && c16 == 0) {
 #pragma unroll
@@ -3832,14 +3725,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + c * 16 + g * 4 + r;
-        if (co < a.Cout) {
-          float s = 0.f;
-          for (int j = 0; j < gs; ++j)
-            s = (j == 0 ? 0.f : s) + ((g0 + j == split) ? accb[c][r]
-                                                          : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                                                wbr, (uint32_t)(((size_t)(g0 + j) * a.Cout + co) * 4), 0, 16)));
-          a.red_wsb[(size_t)grp * a.Cout + co] = s;
-        }
+        if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[c][r];
       }
   }
 }
@@ -4745,12 +4631,6 @@ int ring_split_target() {
 // 16-channel co tiles per wave of the ring wgrad and its output-channel tiles
 int ring_ct(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? 4 : (d->Cout + 15) / 16; }
 int ring_tiles_co(const sr_conv3x3_wgrad_desc* d) { return wg_ring_wide(d) ? (d->Cout + 63) / 64 : 1; }
-// Splits per in-kernel reduce group of the ring wgrad (conv3x3_wgrad_ring_kernel, round 5): knob
-// SR_RING_RED = G in 2..4 (0 / 1 / unset: the standalone slab reduce over all splits)
-int ring_red_group() {
-  const int g = sr_knob(K_RING_RED);
-  return g >= 2 && g <= 4 ? g : 0;
-}
 
 // Split-K factor: enough blocks to cover the chip (~1 round of 256 one-per-CU blocks for the
 // 256x256 kernel, ~2 rounds for the small ones), pixels per split a multiple of 64.
@@ -5044,10 +4924,7 @@ size_t sr_conv3x3_wgrad_workspace(const sr_conv3x3_wgrad_desc* d) {
   int S, kp;
   wgrad_plan(d, &S, &kp);
   const int taps = d->ksize == 1 ? 1 : 9;
-  size_t rows = S;
-  const int G = wg_use_halo(d) ? ring_red_group() : 0;
-  if (G > 1) rows += (S + G - 1) / G;  // + the level-2 slab of the in-kernel reduce
-  return (rows * taps * d->Cout * d->Cin + rows * d->Cout) * sizeof(float) + 256;
+  return ((size_t)S * taps * d->Cout * d->Cin + (size_t)S * d->Cout) * sizeof(float) + 256;
 }
 
 }  // extern "C"
@@ -5150,33 +5027,11 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   a.stamps = g_stamps;
-  int S_red = S;  // slab rows the standalone reduce sums
-  float* ws_red = a.ws;
-  float* wsb_red = a.wsb;
   if (wg_use_halo(d)) {
     a.tiles_co = ring_tiles_co(d);
     a.tiles_ci = (a.Cin + 63) / 64;
     const int ct = ring_ct(d);
     const dim3 grid(S * a.tiles_ci * a.tiles_co);
-    // in-kernel reduce over groups of G splits (not in the slab-only mode: sr_conv3x3_wgrad_reduce
-    // then reads all S rows); the ticket counters of one launch must fit a bank
-    const int G = ring_red_group();
-    const int S2 = G > 1 ? (S + G - 1) / G : S;
-    const size_t row_f = (size_t)taps * d->Cout * d->Cin;
-    if (G > 1 && !(d->accumulate & 2) && S2 * a.tiles_ci * a.tiles_co <= RING_CNT_PER && S > G &&
-        (size_t)S * row_f * 4 < 0x80000000ull) {
-      static std::atomic<unsigned> bank{0};
-      a.red_g = G;
-      a.red_bank = (int)(bank.fetch_add(1u, std::memory_order_relaxed) % RING_CNT_BANKS);
-      a.red_ws = a.ws + (size_t)S * row_f + (size_t)S * d->Cout;  // after the level-1 slab and bias rows
-      a.red_wsb = db ? a.red_ws + (size_t)S2 * row_f : nullptr;
-      a.ws_bytes = (uint32_t)((size_t)S * row_f * 4);
-      a.wsb_bytes = db ? (uint32_t)((size_t)S * d->Cout * 4) : 0u;
-      a.red_ws_bytes = (uint32_t)((size_t)S2 * row_f * 4);
-      S_red = S2;
-      ws_red = a.red_ws;
-      wsb_red = a.red_wsb;
-    }
     if (ct == 1) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<1>, grid, dim3(256), 0, s, a);
     else if (ct == 2) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<2>, grid, dim3(256), 0, s, a);
     else if (ct == 3) hipLaunchKernelGGL(conv3x3_wgrad_ring_kernel<3>, grid, dim3(256), 0, s, a);
@@ -5219,7 +5074,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   }
   if (e != hipSuccess) return sr_check(e, "conv3x3_wgrad launch");
   if (d->accumulate & 2) return SR_OK;  // bit 1: slab only (sr_conv3x3_wgrad_reduce later, e.g. on another stream)
-  return wgrad_reduce_launch(d, S_red, taps, ws_red, wsb_red, dw, db, co_map, ci_map, s);
+  return wgrad_reduce_launch(d, S, taps, a.ws, a.wsb, dw, db, co_map, ci_map, s);
 }
 
 int sr_conv3x3_wgrad_reduce(const sr_conv3x3_wgrad_desc* d, void* workspace, size_t ws_bytes, float* dw, float* db,

@@ -24,7 +24,7 @@ int sr_check(hipError_t e, const char* what) {
 // kernels read the cached value (no per-call environment lookups).  -1 = unset (the built-in default).
 static const char* const kKnobNames[K_COUNT] = {
     "SR_LWK", "SR_LWK_MINK", "SR_RING_WIDE", "SR_RING_PS", "SR_LWG", "SR_LWG_T", "SR_RING_SPLITS",
-    "SR_RING_RED", "SR_DCN_CPP", "SR_DCN_DBG", "SR_DCN_R", "SR_DCN_FUSED", "SR_DCN_COORD_WIN",
+    "SR_DCN_CPP", "SR_DCN_DBG", "SR_DCN_R", "SR_DCN_FUSED", "SR_DCN_COORD_WIN",
     "SR_DCN_GX_FX", "SR_SWIN_ATTN_NW"};
 static std::atomic<int> g_knob[K_COUNT];
 static std::once_flag g_knob_once;

@@ -16,7 +16,6 @@ enum SrKnob {
   K_LWG,            // SR_LWG=0: 1x1 wgrads on the pp kernel instead of linear_wgrad_kernel (A/B)
   K_LWG_T,          // SR_LWG_T: block target of the linear_wgrad split plan
   K_RING_SPLITS,    // SR_RING_SPLITS: block target of the narrow ring wgrad split plan
-  K_RING_RED,       // SR_RING_RED: splits per in-kernel reduce group of the ring wgrad (0/1 off)
   K_DCN_CPP,        // SR_DCN_CPP: channels per pass of the DCN scatter
   K_DCN_DBG,        // SR_DCN_DBG: DCN forward timing ablations (wrong results)
   K_DCN_R,          // SR_DCN_R: x-window margin of the fused DCN forward

@@ -40,7 +40,7 @@ enum sr_act { SR_ACT_NONE = 0, SR_ACT_RELU = 1, SR_ACT_LRELU = 2 };
 const char* sr_version(void);
 const char* sr_last_error(void);
 /* Tuning knobs (A/B switches and split-plan targets, not part of the reference interface).  Each
- * knob is its environment variable of the same name (SR_RING_RED, SR_LWK, SR_DCN_GX_FX, ...), read
+ * knob is its environment variable of the same name (SR_RING_SPLITS, SR_LWK, SR_DCN_GX_FX, ...), read
  * once per process; sr_set_knob overrides it at run time (value < 0: back to the built-in default)
  * and stores the previous value in *previous when non-NULL.  sr_get_knob returns the current value
  * (-1 unset, -2 unknown name). */

@@ -308,9 +308,6 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
         for variant in (62, 0, 67):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
             outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
-        _lib.check(lib.sr_conv3x3_set_variant(62))
-        with _lib.knob('SR_RING_RED', 4):  # the in-kernel group reduce over the output tiles' splits
-            outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
     w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
@@ -320,7 +317,7 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
     dw, db = outs[0]
     assert (dw.cpu().double() - w.grad).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
-    for other in outs[1:]:  # the automatic choice, variant 67 (no shuffled-dy ring), the in-kernel reduce
+    for other in outs[1:]:  # the automatic choice, and variant 67 (no shuffled-dy ring)
         assert (dw - other[0]).abs().max().item() <= 1e-3 * w.grad.abs().max().item() + 1e-3
         assert (db - other[1]).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
 
@@ -329,16 +326,12 @@ def test_wgrad_ring_wide_vs_fp64(cuda, shape):
                                    (1, 3, 64, 64, 16, 1), (1, 2, 128, 64, 64, 2), (3, 1, 64, 96, 8, 1),
                                    (3, 20, 64, 64, 32, 1), (2, 10, 256, 64, 64, 1), (4, 12, 128, 96, 32, 2),
                                    (16, 16, 64, 64, 64, 1), (6, 22, 64, 192, 32, 1), (4, 32, 128, 64, 64, 2)])
-@pytest.mark.parametrize('red', [0, 2, 3, 4])
-def test_wgrad_halo_vs_fp64(cuda, shape, red):
+def test_wgrad_halo_vs_fp64(cuda, shape):
     """All-taps halo wgrad (Cout <= 64, W % 64 == 0), row-streaming form: channel slices of
     wider buffers (ldx, xcoff, ldy, ycoff as in RRDB dense blocks), nearest-x2 input gather
     (in_up = 2), splits that cross image boundaries (rows per split not dividing H), several
     64-px column segments per row, ragged last split, against an fp64 CPU reference on the same
-    bf16 operands.  red: splits per in-kernel reduce group (knob SR_RING_RED; 0 = the standalone slab
-    reduce over all splits): the last-arriving block of each group sums the group's slab rows in split
-    order (ragged last groups: 7 splits in groups of 4 + 3, etc.), the standalone reduce then sums the
-    group rows."""
+    bf16 operands; a repeat call is bitwise equal (the split slab reduce is in a fixed order)."""
     N, H, W, cin, cout, up = shape
     torch.manual_seed(9)
     dt = torch.bfloat16
@@ -359,12 +352,10 @@ def test_wgrad_halo_vs_fp64(cuda, shape, red):
     d.Cout = d.Cout_real = cout
     d.ldx, d.xcoff, d.ldy, d.ycoff = cin + 24, 8, cout + 16, 16
     assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_ring_kernel'
-    with _lib.knob('SR_RING_RED', red):
-        runs = [C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
-                                 xcoff=8, ldy=cout + 16, ycoff=16, in_up=up) for _ in range(2)]
-        torch.cuda.synchronize()
+    runs = [C.conv_wgrad_raw(dyw.to(cuda), xw.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0, ldx=cin + 24,
+                             xcoff=8, ldy=cout + 16, ycoff=16, in_up=up) for _ in range(2)]
+    torch.cuda.synchronize()
     dw, db = runs[0]
-    # deterministic: the group sums are in split order whichever block arrives last
     assert torch.equal(dw, runs[1][0]) and torch.equal(db, runs[1][1])
     tol = 1e-3 * w.grad.abs().max().item() + 1e-3
     assert (dw.cpu().double() - w.grad).abs().max().item() <= tol
