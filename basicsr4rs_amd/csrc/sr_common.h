@@ -15,9 +15,11 @@
 #define SR_DEV __device__ __forceinline__
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 // Offset that is guaranteed to fail the buffer range check (load returns 0).
@@ -25,8 +27,31 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 SR_DEV float bf16_to_f32(unsigned short u) { return __uint_as_float(((unsigned)u) << 16); }
 SR_DEV unsigned short f32_to_bf16(float f) { return __builtin_bit_cast(unsigned short, (__bf16)f); }
+// one v_cvt_pk_bf16_f32 (the two-scalar form compiled to two conversions, a shift and an OR);
+// the same round-to-nearest-even result
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 SR_DEV unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
+}
+// cross-lane sums / maxima over the 16-lane rows (xor 16) and the two wave halves (xor 32) by the
+// gfx950 permlane swaps (VALU, no LDS round trip like ds_bpermute); every lane gets the same value
+// from the same two operands in the same order
+SR_DEV float xsum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+SR_DEV float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+SR_DEV float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+SR_DEV float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 // Element traits: the kernels are written once over "16-byte chunks"; T decides how

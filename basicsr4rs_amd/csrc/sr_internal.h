@@ -22,7 +22,7 @@ enum SrKnob {
   K_DCN_FUSED,      // SR_DCN_FUSED=0: unfused DCN forward (A/B)
   K_DCN_COORD_WIN,  // SR_DCN_COORD_WIN=0: global-memory coordinate gradients (A/B)
   K_DCN_GX_FX,      // SR_DCN_GX_FX: 32 / 64-bit fixed-point scatter image
-  K_SWIN_ATTN_NW,   // SR_SWIN_ATTN_NW: windows per fused attention block (1 / 2)
+  K_SWIN_ATTN_DBG,  // SR_SWIN_ATTN_DBG: fused attention timing ablations (wrong results)
   K_COUNT
 };
 int sr_knob(SrKnob k);

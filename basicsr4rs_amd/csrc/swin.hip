@@ -890,9 +890,10 @@ __global__ __launch_bounds__(64, 2) void wattn_bwd_mfma2_kernel(AttnArgs a) {
 // stage 1 (wattn_dbias_slots): block = (head, 256-slot chunk, quarter of the head's rows); a lane
 // sums 4 consecutive slots with 16-B loads over rows j = q + 4 (wave + 16 k) of the head (4 loads in
 // flight), the 16 waves combine through LDS in a fixed order -> slots[q][h][1792];
-// stage 2 (wattn_dbias_fold): one wave per (head, bin): its 64 lanes take the 112 candidate slots
-// (d, r, gh, g1) of the bin two each, sum the 4 quarters, and a fixed xor tree adds the lanes.
-// (Round 4 ran stage 2 as nH blocks of branchy scalar loops: 70 us per call for 225 x 6 values.)
+// stage 2 (wattn_dbias_fold): one block per head stages the head's slot row (4 quarters summed) in
+// LDS and thread b folds bin b's candidate slots (d, r, gh, g1) in a fixed order.  (Round 4 ran
+// stage 2 as nH blocks of branchy scalar loops over global memory: 70 us per call; a wave per
+// (head, bin) gathering from global memory: 27 us.)
 constexpr int DB_Q = 4;  // quarters of each head's rows in stage 1
 __global__ __launch_bounds__(1024) void wattn_dbias_slots(const float* __restrict__ part, int parts, int nH,
                                                           float* __restrict__ slots) {
@@ -925,30 +926,33 @@ __global__ __launch_bounds__(1024) void wattn_dbias_slots(const float* __restric
 }
 __global__ __launch_bounds__(256) void wattn_dbias_fold(const float* __restrict__ slots, int nH,
                                                         float* __restrict__ dbias, int acc) {
-  const int wid = (int)blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (wid >= 225 * nH) return;
-  const int h = wid % nH, bin = wid / nH;
-  float t = 0.f;
+  // one block per head: the head's 4 quarter rows summed into an LDS slot row with coalesced 16-B
+  // loads (scattered 4-B global reads of other XCDs' freshly written lines were the cost: 27 us in
+  // the step), then thread b folds bin b's candidate slots from LDS in a fixed order
+  __shared__ f32x4 sl4[ATT_SLOTS / 4];
+  const int h = blockIdx.x, t = threadIdx.x;
+  for (int i = t; i < ATT_SLOTS / 4; i += 256) {
+    f32x4 v = ((const f32x4*)(slots + (int64_t)h * ATT_SLOTS))[i];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int e = lane + 64 * c;  // candidate (d, r, gh, g1); 112 of them
+    for (int q = 1; q < DB_Q; ++q) v += ((const f32x4*)(slots + ((int64_t)q * nH + h) * ATT_SLOTS))[i];
+    sl4[i] = v;
+  }
+  __syncthreads();
+  const float* sl = (const float*)sl4;
+  const int b = t;
+  if (b >= 225) return;
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 112; ++e) {  // candidate (d, r, gh, g1)
     const int d = e >> 4, r = (e >> 2) & 3, gh = (e >> 1) & 1, g1 = e & 1;
-    const int qq = bin - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
+    const int qq = b - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
     const int dyp = qq / 15, dxp = qq - 15 * dyp;  // (g >> 1) - (c >> 3) + 7, 4 (g & 1) - (c & 7) + 7
     const int chh = gh - (dyp - 7), c7 = 4 * g1 - (dxp - 7);
-    const bool v = e < 112 && qq >= 0 && qq < 225 && dyp >= 6 && dyp <= 8 && dxp <= 11 && chh >= 0 && chh <= 1 &&
-                   c7 >= 0 && c7 <= 7;
-    if (v) {
-      const int64_t off = (int64_t)h * ATT_SLOTS + ((2 * gh + g1) * 16 + 8 * chh + c7) * ATT_SLOTS_LANE + 4 * d + r;
-      float u = 0.f;
-#pragma unroll
-      for (int q = 0; q < DB_Q; ++q) u += slots[(int64_t)q * nH * ATT_SLOTS + off];
-      t += u;
-    }
+    const bool v = qq >= 0 && qq < 225 && dyp >= 6 && dyp <= 8 && dxp <= 11 && chh >= 0 && chh <= 1 && c7 >= 0 && c7 <= 7;
+    const int idx = ((2 * gh + g1) * 16 + 8 * chh + c7) * ATT_SLOTS_LANE + 4 * d + r;
+    s += v ? sl[v ? idx : 0] : 0.f;
   }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
-  if (lane == 0) dbias[bin * nH + h] = (acc ? dbias[bin * nH + h] : 0.f) + t;
+  dbias[b * nH + h] = (acc ? dbias[b * nH + h] : 0.f) + s;
 }
 
 __global__ void wattn_dbias_reduce2(const float* __restrict__ part, int units, int nH, int nbins,
@@ -963,7 +967,7 @@ void dbias_reduce(const float* ws, int parts, int nH, int nbins, float* dbias, i
   }
   float* slots = const_cast<float*>(ws) + (int64_t)(-parts) * ATT_SLOTS;
   hipLaunchKernelGGL(wattn_dbias_slots, dim3(nH * (ATT_SLOTS / 256) * DB_Q), dim3(1024), 0, s, ws, -parts, nH, slots);
-  hipLaunchKernelGGL(wattn_dbias_fold, dim3((225 * nH + 3) / 4), dim3(256), 0, s, (const float*)slots, nH, dbias, acc);
+  hipLaunchKernelGGL(wattn_dbias_fold, dim3(nH), dim3(256), 0, s, (const float*)slots, nH, dbias, acc);
 }
 
 bool attn_mfma_ok(const AttnArgs& a, int dtype) {

@@ -108,9 +108,17 @@ SR_DEV uint32_t tile_off(int rows, int r, int ch) {
 SR_DEV uint32_t qk_off16(int t, int c) { return (uint32_t)(t * 64 + ((c ^ ((t >> 2) & 3)) << 4)); }
 SR_DEV uint32_t qk_off(int t, int d) { return qk_off16(t, d >> 3) + (uint32_t)((d & 7) * 2); }
 
-// NW windows per block: 2 (8 waves, one block per CU: 122 KB of LDS) or 1 (4 waves, 77.5 KB: two
-// independent blocks per CU, each one's barrier waits covered by the other's work)
-template <int NW>
+// NW windows per block: 2 (8 waves, one block per CU: 122 KB of LDS).  (One-window blocks, two per
+// CU at 77.5 KB, measured the same in round 4 and were removed in round 5.)
+// SH: the shifted-window block (the mask arithmetic is compiled only there).
+// DBG (timing ablations, wrong results; knob SR_SWIN_ATTN_DBG): 1 no step-A MFMAs, 2 no softmax
+// VALU, 4 no step-C MFMAs, 8 no LayerNorm arithmetic, 16 no per-head weight staging.
+// Round 5 (VALU per wave was the bound: ablations put 30-36 us of a 148 us inference launch each in
+// the softmax, the LayerNorm and the per-head weight staging): head-invariant addresses hoisted out
+// of the head loop (weight pieces: one offset per piece + the head as the buffer soffset; the step-A /
+// B store offsets), the softmax in base 2 (table column and scale pre-multiplied by log2 e: one fma
+// per score, v_exp_f32 directly), the mask only in shifted blocks.
+template <int NW, int DBG = 0, bool SH = true>
 __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(SabArgs a) {
   using L = SabL<NW>;
   constexpr int TOK = L::TOK, NT = L::NT;
@@ -161,27 +169,33 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
   const auto wpr = make_rsrc(a.wp, (uint32_t)((size_t)a.Cp * a.ldo * 2));
   const auto tbr = make_rsrc(a.table, (uint32_t)(225 * a.nH * 4));
   u32x4 wreg[L::WREG];
-  auto w_load = [&](int h) {
+  // piece p = (row rr of the head's 96, 16-B chunk ch): its global offset at head 0 (the head adds
+  // 64 Cp bytes, passed as the buffer soffset) and its LDS offset, computed once
+  uint32_t wgo[L::WREG], wlo[L::WREG];
 #pragma unroll
-    for (int k = 0; k < L::WREG; ++k) {
-      const int p = tid + NT * k;
-      const int rr = p / 24, ch = p - rr * 24;
-      const int grow = (rr >> 5) * a.nH * 32 + h * 32 + (rr & 31);
-      wreg[k] = buf_load16(wqr, (p < SAB_WPIECES && ch < a.KC) ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB);
-    }
+  for (int k = 0; k < L::WREG; ++k) {
+    const int p = tid + NT * k;
+    const int rr = p / 24, ch = p - rr * 24;
+    const int grow = (rr >> 5) * a.nH * 32 + (rr & 31);
+    wgo[k] = (p < SAB_WPIECES && ch < a.KC) ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB;
+    wlo[k] = L::W + tile_off(96, rr, ch);
+  }
+  auto w_load = [&](int h) {
+    const uint32_t so = (uint32_t)(h * 64 * a.Cp);
+#pragma unroll
+    for (int k = 0; k < L::WREG; ++k)
+      wreg[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wqr, wgo[k], so, 0));
   };
   auto w_store = [&]() {
 #pragma unroll
-    for (int k = 0; k < L::WREG; ++k) {
-      const int p = tid + NT * k;
-      const int rr = p / 24, ch = p - rr * 24;
-      if (p < SAB_WPIECES) *(u32x4*)(smem + L::W + tile_off(96, rr, ch)) = wreg[k];
-    }
+    for (int k = 0; k < L::WREG; ++k)
+      if (tid + NT * k < SAB_WPIECES) *(u32x4*)(smem + wlo[k]) = wreg[k];
   };
   w_load(0);
   // every small operand (bias table column, qkv / proj biases) into LDS before the first global store:
   // on gfx9 vmcnt counts stores too, so a global load issued after stores makes its wait drain them
-  if (tid < 256) sTB[tid] = tid < 225 ? a.table[tid * a.nH] : 0.f;
+  constexpr float LOG2E = 1.4426950408889634f;
+  if (tid < 256) sTB[tid] = tid < 225 ? a.table[tid * a.nH] * LOG2E : 0.f;
   for (int i = tid; i < 3 * a.nH * 32; i += NT) sBQ[i] = a.bq[i];
   if (tid < 192) sBP[tid] = tid < a.Cp ? a.bp[tid] : 0.f;
   if (tid < 192) {
@@ -196,50 +210,55 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
     int nr;
     const bool vr = tok_pix(r, pr, nr);
     u32x4 raw[6];
-    float sm = 0.f;
+    // padded channels of x are exactly zero (the NHWC invariant) and chunks past KC load zeros, so
+    // the sum needs no mask; the 192 - C zero values add exactly mu^2 each to the squared
+    // deviations, subtracted once after the row reduction (no per-element select)
+    f32x2 sm2 = {0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int ch = part + 4 * q;
       raw[q] = (vr && ch < a.KC) ? *(const u32x4*)(a.x + pr * a.Cp + ch * 8) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = ch * 8 + 2 * j;
-        sm += (c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) : 0.f) + (c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) : 0.f);
-      }
+      for (int j = 0; j < 4; ++j) sm2 += f32x2{__uint_as_float(raw[q][j] << 16), __uint_as_float(raw[q][j] & 0xffff0000u)};
     }
+    float sm = sm2[0] + sm2[1];
     sm += __shfl_xor(sm, 1);
     sm += __shfl_xor(sm, 2);
     const float mu = sm / a.C;
-    float sq = 0.f;
+    f32x2 sq2 = {0.f, 0.f};
+    const f32x2 mu2 = {mu, mu};
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int ch = part + 4 * q;
+    for (int q = 0; q < 6; ++q)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = ch * 8 + 2 * j;
-        const float d0 = c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) - mu : 0.f;
-        const float d1 = c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) - mu : 0.f;
-        sq += d0 * d0 + d1 * d1;
+        const f32x2 d = f32x2{__uint_as_float(raw[q][j] << 16), __uint_as_float(raw[q][j] & 0xffff0000u)} - mu2;
+        sq2 += d * d;
       }
-    }
+    float sq = sq2[0] + sq2[1];
     sq += __shfl_xor(sq, 1);
     sq += __shfl_xor(sq, 2);
+    sq = fmaxf(sq - (float)(192 - a.C) * mu * mu, 0.f);
     const float rs = rsqrtf(sq / a.C + a.eps);
-    __syncthreads();  // gamma / beta staged
+    __syncthreads();  // gamma / beta staged (zero past C: padded outputs come out exactly 0)
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int ch = part + 4 * q;
       u32x4 o4 = u32x4{0u, 0u, 0u, 0u};
       if (vr && ch < a.KC) {
-        float o[8];
+        // o = x A + B with A = rs gamma, B = beta - mu A: packed fp32 pairs
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int c = ch * 8 + j;
-          const float xv = bf16_to_f32((raw[q][j >> 1] >> (16 * (j & 1))) & 0xffff);
-          o[j] = c < a.C ? (xv - mu) * rs * sGB[c] + sGB[192 + c] : 0.f;
+        for (int j = 0; j < 4; ++j) {
+          const int c = ch * 8 + 2 * j;
+          const f32x2 xv = {__uint_as_float(raw[q][j] << 16), __uint_as_float(raw[q][j] & 0xffff0000u)};
+          if constexpr ((DBG & 8) != 0) {
+            o4[j] = pack_bf16x2(xv[0], xv[1]);
+          } else {
+            const f32x2 A = f32x2{sGB[c], sGB[c + 1]} * f32x2{rs, rs};
+            const f32x2 B = f32x2{sGB[192 + c], sGB[192 + c + 1]} - mu2 * A;
+            const f32x2 o = xv * A + B;
+            o4[j] = pack_bf16x2(o[0], o[1]);
+          }
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
       }
       buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(pr * a.Cp + ch * 8) * 2u : SR_OOB, o4);
       *(u32x4*)(smem + L::X + tile_off(TOK, r, ch)) = o4;
@@ -273,15 +292,26 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
   // head-invariant parts of step B, once per block: the shift mask of this lane's 16 keys as bits, and
   // the relative-position index bin8(qq, k) of key k = 16 i + 4 g + r, which is tbase - 30 i - r
   // (k >> 3 = 2 i + (g >> 1), k & 7 = 4 (g & 1) + r), so the table reads take immediate offsets
-  unsigned mbits = 0u;
+  // (shifted blocks) the mask of this lane's 16 keys as additive base-2 scores: -100 nats
+  float mk[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = 16 * i + 4 * g + r;
-      const int rk = region(wyB * 8 + (k >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (k & 7), a.W, 8, a.shift);
-      if (a.shift && rk != rq) mbits |= 1u << (4 * i + r);
+      mk[4 * i + r] = 0.f;
+      if constexpr (SH) {
+        const int rk = region(wyB * 8 + (k >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (k & 7), a.W, 8, a.shift);
+        if (rk != rq) mk[4 * i + r] = -100.f * LOG2E;
+      }
     }
+  // head-invariant store offsets (the head adds h * 64 bytes, folded into the per-head base)
+  uint32_t qkvo[2], lao;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) qkvo[j] = vA[j] ? (uint32_t)(pixA[j] * a.ldq) * 2u : SR_OOB;
+  lao = vB ? (uint32_t)(pixB * a.ldo) * 2u : SR_OOB;
+  const uint32_t lseo = (vB && g == 0) ? (uint32_t)((NW * blk + wi) * a.nH * 64 + qq) * 4u : SR_OOB;
+  const float scale2 = a.scale * LOG2E;
   const int tbase = ((qq >> 3) - (g >> 1) + 7) * 15 + (qq & 7) - 4 * (g & 1) + 7;
 
   f32x4 xacc[3][4];
@@ -301,10 +331,21 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
       const int row = pog * 48 + 16 * i + c16;
       wpf[i] = buf_load16(wpr, row < a.Cp ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
     }
-    if (h + 1 < a.nH) w_load(h + 1);
+    if (h + 1 < a.nH && (DBG & 16) == 0) w_load(h + 1);
     const float tbn = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
         tbr, (h + 1 < a.nH && tid < 225) ? (uint32_t)(tid * a.nH + h + 1) * 4u : SR_OOB, 0, 0));  // next column
     __builtin_amdgcn_sched_barrier(0);  // keep these loads here, ahead of the head's stores
+    // step B's 16 bias-table values of this lane (+ the shift mask), read now: their LDS latency hides
+    // under step A instead of 8 dependent ds_read round trips in the softmax (the column was staged
+    // before the previous head's S3 barrier)
+    float tbv[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        tbv[4 * i + r] = (sTB + tbase - 93)[93 - 30 * i - r];
+        if constexpr (SH) tbv[4 * i + r] += mk[4 * i + r];
+      }
 
     // ---- A: q / k / v of head h
     f32x4 acc[3][2];
@@ -323,7 +364,10 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr ((DBG & 1) == 0) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+          else acc[i][j][0] += __builtin_bit_cast(float, (int)(af[i][0] ^ bf[j][1]));
+        }
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -337,7 +381,10 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
         uint2 u;
         u.x = pack_bf16x2(acc[i][j][0] + bias[0], acc[i][j][1] + bias[1]);
         u.y = pack_bf16x2(acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]);
-        buf_store8(qkvr, vA[j] ? (uint32_t)(pixA[j] * a.ldq + gr) * 2u : SR_OOB, u);
+        // lane part of the offset in voffset, the head (uniform) as soffset: a lane-varying soffset
+        // makes the compiler wrap the store in a waterfall loop
+        const uint32_t vo = qkvo[j] == SR_OOB ? SR_OOB : qkvo[j] + (uint32_t)(which * a.nH * 32 + d) * 2u;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, u), qkvr, vo, (uint32_t)h * 64u, 0);
         const uint32_t qk = qk_off(t, d);
         const uint32_t la = which == 0 ? L::Q + qk : which == 1 ? L::K + qk : L::V + (t >> 6) * 4096 + sx_byte(t & 63, d);
         *(uint2*)(smem + la) = u;
@@ -354,35 +401,32 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
         const s16x8 kf = *(const s16x8*)(smem + L::K + qk_off16(wi * 64 + 16 * i + c16, g));
         s[i] = mfma16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f});  // S^T[key 16i + 4g + r][query qq]
       }
-      float mx = -3.0e38f;
+      float mx = -3.0e38f, inv = 1.f;
+      if constexpr ((DBG & 2) == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {  // key k = 16 i + 4 g + r
-          float v = s[i][r] * a.scale + (sTB + tbase - 93)[93 - 30 * i - r];  // = sTB[bin8(qq, k)]
-          if ((mbits >> (4 * i + r)) & 1u) v -= 100.f;
+          // base 2: scores and table scaled by log2 e (the mask: -100 nats)
+          const float v = fmaf(s[i][r], scale2, tbv[4 * i + r]);  // + sTB[bin8(qq, k)] + mask
           s[i][r] = v;
           mx = fmaxf(mx, v);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = xmax32(xmax16(mx));
       float sm = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(s[i][r] - mx);
+          const float e = __builtin_amdgcn_exp2f(s[i][r] - mx);
           s[i][r] = e;
           sm += e;
         }
-      sm += __shfl_xor(sm, 16);
-      sm += __shfl_xor(sm, 32);
-      const float inv = 1.f / sm;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[i][r] *= inv;
-      buf_store4f(lser, (vB && g == 0) ? (uint32_t)(((NW * blk + wi) * a.nH + h) * 64 + qq) * 4u : SR_OOB, mx + __logf(sm));
+      sm = xsum32(xsum16(sm));
+      inv = __builtin_amdgcn_rcpf(sm);  // applied to O (8 values per lane) instead of P (16)
+      mx = (mx + __log2f(sm)) * 0.6931471805599453f;  // natural-log LSE for the backward
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mx), lser, lseo, (uint32_t)h * 256u, 0);
       f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
       const char* sVw = smem + L::V + wi * 4096;
 #pragma unroll
@@ -394,16 +438,17 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
 #pragma unroll
       for (int d = 0; d < 2; ++d) {  // O^T[dim 16d + 4g + r][query qq]
         uint2 u;
-        u.x = pack_bf16x2(o[d][0], o[d][1]);
-        u.y = pack_bf16x2(o[d][2], o[d][3]);
-        buf_store8(aor, vB ? (uint32_t)(pixB * a.ldo + h * 32 + 16 * d + 4 * g) * 2u : SR_OOB, u);
+        u.x = pack_bf16x2(o[d][0] * inv, o[d][1] * inv);
+        u.y = pack_bf16x2(o[d][2] * inv, o[d][3] * inv);
+        const uint32_t vo = lao == SR_OOB ? SR_OOB : lao + (uint32_t)(16 * d + 4 * g) * 2u;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, u), aor, vo, (uint32_t)h * 64u, 0);
         *(uint2*)(smem + L::O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
       }
     }
     __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW) and step B (sTB)
     if (h + 1 < a.nH) {
-      w_store();
-      if (tid < 256) sTB[tid] = tbn;
+      if constexpr ((DBG & 16) == 0) w_store();
+      if (tid < 256) sTB[tid] = tbn * LOG2E;  // (scaled here: a multiply next to the load would wait for it)
     }
 
     // ---- C: x2acc += Wp[:, head h] . O_h^T
@@ -411,7 +456,10 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
     for (int j = 0; j < 4; ++j) {
       const s16x8 of = *(const s16x8*)(smem + L::O + qk_off16(ptg * 64 + 16 * j + c16, g));
 #pragma unroll
-      for (int i = 0; i < 3; ++i) xacc[i][j] = mfma16(__builtin_bit_cast(s16x8, wpf[i]), of, xacc[i][j]);
+      for (int i = 0; i < 3; ++i) {
+        if constexpr ((DBG & 4) == 0) xacc[i][j] = mfma16(__builtin_bit_cast(s16x8, wpf[i]), of, xacc[i][j]);
+        else xacc[i][j][0] += __builtin_bit_cast(float, (int)(wpf[i][0] ^ (unsigned)of[1]));
+      }
     }
     __syncthreads();  // S3: sO read; the next head's sW written
   }
@@ -741,8 +789,6 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
   }
 }
 
-// Windows per block of the fused attention half: 2, or knob SR_SWIN_ATTN_NW=1 (A/B)
-int attn_nw() { return sr_knob(K_SWIN_ATTN_NW) == 1 ? 1 : 2; }
 
 }  // namespace
 
@@ -776,10 +822,24 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
   a.ldq = 3 * nH * 32; a.ldo = nH * 32;
   a.eps = eps; a.scale = scale;
   a.nwx = W / 8; a.nwin = (H / 8) * (W / 8); a.nwin_total = N * a.nwin;
-  if (attn_nw() == 1)
-    hipLaunchKernelGGL(swin_attn_block_fwd_kernel<1>, dim3(a.nwin_total), dim3(256), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(swin_attn_block_fwd_kernel<2>, dim3((a.nwin_total + 1) / 2), dim3(512), 0, (hipStream_t)stream, a);
+  const dim3 g2((a.nwin_total + 1) / 2);
+  hipStream_t s = (hipStream_t)stream;
+  const int dbg = sr_knob(K_SWIN_ATTN_DBG);
+  if (dbg <= 0) {  // the kernel, specialised for unshifted / shifted blocks
+    if (shift) hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 0, true>), g2, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 0, false>), g2, dim3(512), 0, s, a);
+    return sr_check(hipGetLastError(), "swin_attn_fused_fwd launch");
+  }
+  switch (dbg) {  // timing ablations (wrong results)
+    case 1: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 1>), g2, dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 2>), g2, dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 4>), g2, dim3(512), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 8>), g2, dim3(512), 0, s, a); break;
+    case 16: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 16>), g2, dim3(512), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 7>), g2, dim3(512), 0, s, a); break;
+    case 31: hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 31>), g2, dim3(512), 0, s, a); break;
+    default: return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: unknown SR_SWIN_ATTN_DBG ablation");
+  }
   return sr_check(hipGetLastError(), "swin_attn_fused_fwd launch");
 }
 
