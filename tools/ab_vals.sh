@@ -10,9 +10,10 @@ for w in ${WORKLOADS:-rcan}; do
   for r in $(seq ${ROUNDS:-2}); do
     for v in ${VALS:-0 1}; do
       if [ "$v" = unset ]; then unset $VAR; else export $VAR=$v; fi
+      f=$OUT/ab_${w}_$(basename $v)_$r.log
       timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-trace --no-parity --workload $w --steps ${STEPS:-20} \
-        --warmup 5 > $OUT/ab_${w}_${v}_$r.log 2>&1 || { tail -20 $OUT/ab_${w}_${v}_$r.log; exit 1; }
-      python3 -c "import json; d=json.loads([l for l in open('$OUT/ab_${w}_${v}_$r.log') if l.startswith('{\"metric')][-1]); print('$w $VAR=$v round $r', d['ms_per_step'])"
+        --warmup 5 > $f 2>&1 || { tail -20 $f; exit 1; }
+      python3 -c "import json; d=json.loads([l for l in open('$f') if l.startswith('{\"metric')][-1]); print('$w $VAR=$v round $r', d['ms_per_step'])"
     done
   done
 done
