@@ -262,32 +262,23 @@ __global__ __launch_bounds__(1024) void ca_mlp_bwd_kernel(const float* __restric
 // latency-bound kernel (ca_mlp_fwd 5 us, ca_mlp_bwd 17.6 us on one block) ahead of an elementwise
 // pass over the image (nc_affine 8.5 us, HBM-bound).  Here every block of the elementwise pass
 // recomputes its image's MLP from the partial sums (fixed summation order, so every block gets
-// bit-identical s / dpool) and applies it to its pixel range: the block first issues the loads of
-// its map vectors (CA_VPT 16-B vectors per thread per map, held in registers) and of the MLP
-// operands (partial rows, weights, per-image state: all loads up front, staged in LDS), so the
-// MLP's latency chain runs under the map traffic instead of ahead of it.  Block 0 of each image
-// also writes the MLP state the backward / the parameter gradients need.  Grid (K, N), 256 threads,
+// bit-identical s / dpool) and applies it to its pixel range.  The block issues the loads of the MLP
+// operands first (partial rows straight into registers, weights staged in LDS) and then its map
+// vectors (CA_VPT 16-B vectors per thread per map): loads retire in order, so the MLP waits for its
+// own operands only and its chain runs while the map traffic is in flight.  The chain is kept short:
+// the partial rows are summed by 16 row groups per channel quad in parallel, the C-long dot products
+// of the 1x1 convs are wave reductions (one output per wave, C % 64 == 0; a per-thread loop
+// otherwise), so a block spends ~1 us in it instead of ~5 us of serial LDS loops (RCAN x4 B 32:
+// ca_fwd_apply 14.9 us, ca_bwd_apply 9.7 us with the serial chain).  Block 0 of each image also
+// writes the MLP state the backward / the parameter gradients need.  Grid (K, N), 256 threads,
 // C % 8 == 0, C <= CA_FMAXC, Cr <= CA_FMAXR, C * Cr <= CA_FMAXW, P * C <= CA_FMAXP.
 constexpr int CA_FMAXC = 256, CA_FMAXR = 64, CA_FMAXW = 2048, CA_FMAXP = 8192, CA_FNT = 256, CA_VPT = 8;
+constexpr int CA_RPT = CA_FMAXP / 4 / CA_FNT;  // partial-row vectors per thread (8)
 
 // Staging into LDS with every load of the thread issued before the first LDS store (a load/store
 // loop waits one global-memory round trip per iteration: 17 iterations made ca_param_grad 9 us).
-// Up to U 16-B vectors (f4: float4) or U floats per thread; the caller guarantees n <= U * CA_FNT.
-template <int U>
-SR_DEV void ca_stage_f4(const float* __restrict__ src, int n4, float* __restrict__ dst) {
-  f32x4 v[U];
-#pragma unroll
-  for (int j = 0; j < U; ++j) {
-    const int i = threadIdx.x + j * CA_FNT;
-    v[j] = ((const f32x4*)src)[i < n4 ? i : 0];
-  }
-#pragma unroll
-  for (int j = 0; j < U; ++j) {
-    const int i = threadIdx.x + j * CA_FNT;
-    if (i < n4) ((f32x4*)dst)[i] = v[j];
-  }
-}
-
+// Up to U floats per thread; the caller guarantees n <= U * CA_FNT.  Loads are unconditional
+// (clamped): a branch around a load makes the compiler drain every load in flight at the join.
 template <int U>
 SR_DEV void ca_stage_f1(const float* __restrict__ src, int n, float* __restrict__ dst) {
   float v[U];
@@ -303,6 +294,23 @@ SR_DEV void ca_stage_f1(const float* __restrict__ src, int n, float* __restrict_
   }
 }
 
+// the same in two halves, so that other loads can be issued in between: ca_fetch_f1 loads U floats
+// per thread into registers, ca_put_f1 stores all of them to an LDS array of U * CA_FNT floats
+// (slots past n hold clamped copies nobody reads)
+template <int U>
+SR_DEV void ca_fetch_f1(const float* __restrict__ src, int n, float (&v)[U]) {
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const int i = threadIdx.x + j * CA_FNT;
+    v[j] = src[i < n ? i : 0];
+  }
+}
+template <int U>
+SR_DEV void ca_put_f1(float* __restrict__ dst, const float (&v)[U]) {
+#pragma unroll
+  for (int j = 0; j < U; ++j) dst[threadIdx.x + j * CA_FNT] = v[j];
+}
+
 // this thread's map vectors of pixels [p0, p1) of image n: vector i = p0 * cv + t + j * CA_FNT
 template <typename T>
 SR_DEV void ca_load_vec(const T* __restrict__ m, size_t base, int i0, int i1, u32x4 (&v)[CA_VPT]) {
@@ -311,6 +319,46 @@ SR_DEV void ca_load_vec(const T* __restrict__ m, size_t base, int i0, int i1, u3
     const int i = i0 + threadIdx.x + j * CA_FNT;
     v[j] = ((const u32x4*)m)[base + (i < i1 ? i : i0)];  // unconditional (clamped) load: no branch per load
   }
+}
+
+// The partial rows [P][C] of one image, thread (q, g) = (t % C4, t / C4): channel quad q, rows
+// g, g + RG, ... (RG = CA_FNT / C4 row groups; the host checks P <= CA_RPT * RG, which P * C <= CA_FMAXP
+// implies when C4 divides CA_FNT).  ca_rows_issue loads them, ca_rows_sum adds them in
+// row order and then the RG group sums in group order into out[c] (LDS), times scale.
+SR_DEV void ca_rows_issue(const float* __restrict__ pn, int P, int C, f32x4 (&v)[CA_RPT]) {
+  const int C4 = C >> 2, RG = CA_FNT / C4, t = threadIdx.x;
+  const int q = t % C4, g = t / C4 < RG ? t / C4 : 0;
+#pragma unroll
+  for (int j = 0; j < CA_RPT; ++j) {
+    const int p = g + j * RG;
+    v[j] = ((const f32x4*)pn)[(size_t)(p < P ? p : 0) * C4 + q];  // clamped, masked in ca_rows_sum
+  }
+}
+
+SR_DEV void ca_rows_sum(const f32x4 (&v)[CA_RPT], int P, int C, f32x4* __restrict__ red, float scale,
+                        float* __restrict__ out) {
+  const int C4 = C >> 2, RG = CA_FNT / C4, t = threadIdx.x;
+  const int g = t / C4;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc = z;
+#pragma unroll
+  for (int j = 0; j < CA_RPT; ++j) acc += (g < RG && g + j * RG < P) ? v[j] : z;
+  red[t] = acc;  // = red[g * C4 + q]; the slots past RG * C4 are never read (unconditional: a branch
+                 // here lets the compiler sink the row loads behind the map loads)
+  __syncthreads();
+  for (int c = t; c < C; c += CA_FNT) {
+    const float* rf = (const float*)red;
+    float s = 0.f;
+    for (int k = 0; k < RG; ++k) s += rf[k * C + c];
+    out[c] = s * scale;
+  }
+}
+
+// sum over the 64 lanes of a wave (every lane gets the same, fixed-order result)
+SR_DEV float ca_wave_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+  return xsum32(xsum16(v));
 }
 
 // y = x + alpha * u * s[n, c] over pixels [k * ppb, (k + 1) * ppb) of image n
@@ -323,45 +371,52 @@ __global__ __launch_bounds__(256) void ca_fwd_apply_kernel(const float* __restri
                                                            float* __restrict__ pool, float* __restrict__ h,
                                                            float* __restrict__ s) {
   constexpr int PER = Elt<T>::PER16;
-  __shared__ __attribute__((aligned(16))) float pr[CA_FMAXP];
-  __shared__ float W1[CA_FMAXW], W2[CA_FMAXW], B1[CA_FMAXR], B2[CA_FMAXC], red[CA_FNT], pl[CA_FMAXC], hr[CA_FMAXR],
-      sl[CA_FMAXC];
-  const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x;
+  __shared__ f32x4 red[CA_FNT];
+  __shared__ float W1[CA_FMAXW], W2[CA_FMAXW], B1[CA_FNT], B2[CA_FNT], pl[CA_FMAXC], hr[CA_FMAXR], sl[CA_FMAXC];
+  const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int cv = C / PER;
   const int i0 = k * ppb * cv, i1 = min(HW, (k + 1) * ppb) * cv;
   const size_t base = ((size_t)n * HW) * cv;
+  const float* pn = parts + (size_t)n * P * C;
+  // the MLP operands first, then the map vectors (loads retire in order)
+  f32x4 rv[CA_RPT];
+  float w1v[CA_FMAXW / CA_FNT], w2v[CA_FMAXW / CA_FNT], b1v[1], b2v[1];
+  ca_rows_issue(pn, P, C, rv);
+  ca_fetch_f1(w1, C * Cr, w1v);
+  ca_fetch_f1(w2, C * Cr, w2v);
+  ca_fetch_f1(b1 ? b1 : w1, b1 ? Cr : 1, b1v);
+  ca_fetch_f1(b2 ? b2 : w2, b2 ? C : 1, b2v);
+  __builtin_amdgcn_sched_barrier(0);  // issue order: MLP operands, then the maps (loads retire in order)
   u32x4 vx[CA_VPT], vu[CA_VPT];
   ca_load_vec(x, base, i0, i1, vx);
   ca_load_vec(u, base, i0, i1, vu);
-  ca_stage_f4<CA_FMAXP / 4 / CA_FNT>(parts + (size_t)n * P * C, P * C / 4, pr);
-  ca_stage_f1<CA_FMAXW / CA_FNT>(w1, C * Cr, W1);
-  ca_stage_f1<CA_FMAXW / CA_FNT>(w2, C * Cr, W2);
-  if (b1) ca_stage_f1<1>(b1, Cr, B1);
-  if (b2) ca_stage_f1<1>(b2, C, B2);
+  __builtin_amdgcn_sched_barrier(0);  // the map loads stay ahead of the first wait on the MLP operands
+  ca_put_f1(W1, w1v);
+  ca_put_f1(W2, w2v);
+  b1v[0] = b1 ? b1v[0] : 0.f;
+  b2v[0] = b2 ? b2v[0] : 0.f;
+  ca_put_f1(B1, b1v);
+  ca_put_f1(B2, b2v);
+  ca_rows_sum(rv, P, C, red, scale, pl);
   __syncthreads();
-  // pool: G groups of rows per channel in a fixed order, then their sum
-  const int G = CA_FNT / C > 0 ? CA_FNT / C : 1;
-  for (int i = t; i < C * G; i += CA_FNT) {
-    const int c = i % C, g = i / C;
-    float acc = 0.f;
-    for (int p = g; p < P; p += G) acc += pr[p * C + c];
-    red[g * C + c] = acc;
+  if (C % 64 == 0) {  // h[r] = relu(b1 + W1[r] . pool): one wave per output
+    for (int r = wv; r < Cr; r += CA_FNT / 64) {
+      float acc = 0.f;
+      for (int c = lane; c < C; c += 64) acc += W1[r * C + c] * pl[c];
+      acc = ca_wave_sum(acc) + B1[r];
+      if (lane == 0) hr[r] = acc > 0.f ? acc : 0.f;
+    }
+  } else {
+    for (int r = t; r < Cr; r += CA_FNT) {
+      float acc = 0.f;
+      for (int c = 0; c < C; ++c) acc += W1[r * C + c] * pl[c];
+      acc += B1[r];
+      hr[r] = acc > 0.f ? acc : 0.f;
+    }
   }
   __syncthreads();
   for (int c = t; c < C; c += CA_FNT) {
-    float acc = 0.f;
-    for (int g = 0; g < G; ++g) acc += red[g * C + c];
-    pl[c] = acc * scale;
-  }
-  __syncthreads();
-  for (int r = t; r < Cr; r += CA_FNT) {
-    float acc = b1 ? B1[r] : 0.f;
-    for (int c = 0; c < C; ++c) acc += W1[r * C + c] * pl[c];
-    hr[r] = acc > 0.f ? acc : 0.f;
-  }
-  __syncthreads();
-  for (int c = t; c < C; c += CA_FNT) {
-    float acc = b2 ? B2[c] : 0.f;
+    float acc = B2[c];
     for (int r = 0; r < Cr; ++r) acc += W2[c * Cr + r] * hr[r];
     sl[c] = 1.f / (1.f + expf(-acc));
   }
@@ -377,23 +432,26 @@ __global__ __launch_bounds__(256) void ca_fwd_apply_kernel(const float* __restri
     const int c0 = (i % cv) * PER;
     u32x4 o;
     if constexpr (PER == 8) {
+      const f32x4 s0 = *(const f32x4*)(sl + c0), s1 = *(const f32x4*)(sl + c0 + 4);
+      const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float u0 = bf16_to_f32(vu[j][q] & 0xffff), u1 = bf16_to_f32(vu[j][q] >> 16);
         const float x0 = bf16_to_f32(vx[j][q] & 0xffff), x1 = bf16_to_f32(vx[j][q] >> 16);
-        o[q] = pack_bf16x2(1.f * x0 + alpha * u0 * sl[c0 + 2 * q], 1.f * x1 + alpha * u1 * sl[c0 + 2 * q + 1]);
+        o[q] = pack_bf16x2(x0 + alpha * u0 * sv[2 * q], x1 + alpha * u1 * sv[2 * q + 1]);
       }
     } else {
+      const f32x4 s0 = *(const f32x4*)(sl + c0);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        o[q] = __float_as_uint(1.f * __uint_as_float(vx[j][q]) + alpha * __uint_as_float(vu[j][q]) * sl[c0 + q]);
+        o[q] = __float_as_uint(__uint_as_float(vx[j][q]) + alpha * __uint_as_float(vu[j][q]) * s0[q]);
     }
     ((u32x4*)y)[base + i] = o;
   }
 }
 
 // du = alpha * dy * s[n, c] + dpool[n, c] / HW, with ds = alpha * sum_p parts (dL/ds), dz2 = ds s (1 - s),
-// dz1 = relu'(h) (W2^T dz2), dpool = W1^T dz1 recomputed per block (the order of ca_mlp_bwd_kernel)
+// dz1 = relu'(h) (W2^T dz2), dpool = W1^T dz1 recomputed per block
 template <typename T>
 __global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restrict__ parts, int P, float alpha,
                                                            const float* __restrict__ s, const float* __restrict__ h,
@@ -402,41 +460,50 @@ __global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restri
                                                            T* __restrict__ du, float* __restrict__ dz2_out,
                                                            float* __restrict__ dz1_out) {
   constexpr int PER = Elt<T>::PER16;
-  __shared__ __attribute__((aligned(16))) float pr[CA_FMAXP];
-  __shared__ float W1[CA_FMAXW], W2[CA_FMAXW], sl[CA_FMAXC], hh[CA_FMAXR], dz2[CA_FMAXC], dz1[CA_FMAXR],
-      tp[CA_FMAXC];
-  const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x;
+  __shared__ f32x4 red[CA_FNT];
+  __shared__ float W1[CA_FMAXW], W2[CA_FMAXW], sl[CA_FNT], hh[CA_FNT], ds[CA_FMAXC], dz2[CA_FMAXC],
+      dz1[CA_FMAXR], tp[CA_FMAXC];
+  const int n = blockIdx.y, k = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int cv = C / PER;
   const int i0 = k * ppb * cv, i1 = min(HW, (k + 1) * ppb) * cv;
   const size_t base = ((size_t)n * HW) * cv;
+  const float* pn = parts + (size_t)n * P * C;
+  // the MLP operands first, then the map vectors (loads retire in order)
+  f32x4 rv[CA_RPT];
+  float w1v[CA_FMAXW / CA_FNT], w2v[CA_FMAXW / CA_FNT], sv1[1], hv1[1];
+  ca_rows_issue(pn, P, C, rv);
+  ca_fetch_f1(w1, C * Cr, w1v);
+  ca_fetch_f1(w2, C * Cr, w2v);
+  ca_fetch_f1(s + n * C, C, sv1);
+  ca_fetch_f1(h + n * Cr, Cr, hv1);
+  __builtin_amdgcn_sched_barrier(0);  // issue order: MLP operands, then the map (loads retire in order)
   u32x4 vd[CA_VPT];
   ca_load_vec(dy, base, i0, i1, vd);
-  ca_stage_f4<CA_FMAXP / 4 / CA_FNT>(parts + (size_t)n * P * C, P * C / 4, pr);
-  ca_stage_f1<CA_FMAXW / CA_FNT>(w1, C * Cr, W1);
-  ca_stage_f1<CA_FMAXW / CA_FNT>(w2, C * Cr, W2);
-  ca_stage_f1<1>(s + n * C, C, sl);
-  ca_stage_f1<1>(h + n * Cr, Cr, hh);
+  __builtin_amdgcn_sched_barrier(0);  // the map loads stay ahead of the first wait on the MLP operands
+  ca_put_f1(W1, w1v);
+  ca_put_f1(W2, w2v);
+  ca_put_f1(sl, sv1);
+  ca_put_f1(hh, hv1);
+  ca_rows_sum(rv, P, C, red, alpha, ds);
   __syncthreads();
   for (int c = t; c < C; c += CA_FNT) {
-    // the summation order of strided_sum (G = 1): batches of 8 rows, then the tail
-    float acc = 0.f;
-    int p = 0;
-    for (; p + 7 < P; p += 8) {
-      float v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = pr[(p + q) * C + c];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc += v[q];
-    }
-    for (; p < P; ++p) acc += pr[p * C + c];
     const float si = sl[c];
-    dz2[c] = acc * alpha * si * (1.f - si);
+    dz2[c] = ds[c] * si * (1.f - si);
   }
   __syncthreads();
-  for (int r = t; r < Cr; r += CA_FNT) {
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc += W2[c * Cr + r] * dz2[c];
-    dz1[r] = hh[r] > 0.f ? acc : 0.f;
+  if (C % 64 == 0) {  // dz1[r] = relu'(h) W2[:, r] . dz2: one wave per output
+    for (int r = wv; r < Cr; r += CA_FNT / 64) {
+      float acc = 0.f;
+      for (int c = lane; c < C; c += 64) acc += W2[c * Cr + r] * dz2[c];
+      acc = ca_wave_sum(acc);
+      if (lane == 0) dz1[r] = hh[r] > 0.f ? acc : 0.f;
+    }
+  } else {
+    for (int r = t; r < Cr; r += CA_FNT) {
+      float acc = 0.f;
+      for (int c = 0; c < C; ++c) acc += W2[c * Cr + r] * dz2[c];
+      dz1[r] = hh[r] > 0.f ? acc : 0.f;
+    }
   }
   __syncthreads();
   const float inv_hw = 1.f / (float)HW;
@@ -457,16 +524,19 @@ __global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restri
     const int c0 = (i % cv) * PER;
     u32x4 o;
     if constexpr (PER == 8) {
+      const f32x4 s0 = *(const f32x4*)(sl + c0), s1 = *(const f32x4*)(sl + c0 + 4);
+      const f32x4 t0 = *(const f32x4*)(tp + c0), t1 = *(const f32x4*)(tp + c0 + 4);
+      const float sv[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      const float tv[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float d0 = bf16_to_f32(vd[j][q] & 0xffff), d1 = bf16_to_f32(vd[j][q] >> 16);
-        o[q] = pack_bf16x2(0.f * 0.f + alpha * d0 * sl[c0 + 2 * q] + tp[c0 + 2 * q],
-                           0.f * 0.f + alpha * d1 * sl[c0 + 2 * q + 1] + tp[c0 + 2 * q + 1]);
+        o[q] = pack_bf16x2(alpha * d0 * sv[2 * q] + tv[2 * q], alpha * d1 * sv[2 * q + 1] + tv[2 * q + 1]);
       }
     } else {
+      const f32x4 s0 = *(const f32x4*)(sl + c0), t0 = *(const f32x4*)(tp + c0);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        o[q] = __float_as_uint(0.f * 0.f + alpha * __uint_as_float(vd[j][q]) * sl[c0 + q] + tp[c0 + q]);
+      for (int q = 0; q < 4; ++q) o[q] = __float_as_uint(alpha * __uint_as_float(vd[j][q]) * s0[q] + t0[q]);
     }
     ((u32x4*)du)[base + i] = o;
   }
@@ -474,7 +544,7 @@ __global__ __launch_bounds__(256) void ca_bwd_apply_kernel(const float* __restri
 
 // squeeze-conv parameter gradients from the per-image dz2 / dz1 (same loop order as ca_mlp_bwd_kernel);
 // one block, the operands staged in LDS first (the per-n loop over global memory was a 25 us
-// latency chain)
+// latency chain), the n loops in batches of 8 independent LDS loads
 __global__ __launch_bounds__(256) void ca_param_grad_kernel(const float* __restrict__ dz2, const float* __restrict__ dz1,
                                                             const float* __restrict__ h, const float* __restrict__ pool,
                                                             int N, int C, int Cr, float* __restrict__ dw1,
@@ -494,7 +564,23 @@ __global__ __launch_bounds__(256) void ca_param_grad_kernel(const float* __restr
   for (int i = t; i < C * Cr; i += CA_FNT) {
     const int c = i / Cr, r = i - c * Cr;
     float a2 = 0.f, a1 = 0.f;
-    for (int n = 0; n < N; ++n) {
+    int n = 0;
+    for (; n + 7 < N; n += 8) {
+      float z2[8], hv[8], z1[8], pv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        z2[q] = Z2[(n + q) * C + c];
+        hv[q] = HH[(n + q) * Cr + r];
+        z1[q] = Z1[(n + q) * Cr + r];
+        pv[q] = PL[(n + q) * C + c];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        a2 += z2[q] * hv[q];
+        a1 += z1[q] * pv[q];
+      }
+    }
+    for (; n < N; ++n) {
       a2 += Z2[n * C + c] * HH[n * Cr + r];
       a1 += Z1[n * Cr + r] * PL[n * C + c];
     }
@@ -502,14 +588,10 @@ __global__ __launch_bounds__(256) void ca_param_grad_kernel(const float* __restr
     dw1[r * C + c] = (accumulate ? dw1[r * C + c] : 0.f) + a1;
   }
   for (int c = t; c < C; c += CA_FNT) {
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += Z2[n * C + c];
-    if (db2) db2[c] = (accumulate ? db2[c] : 0.f) + acc;
+    if (db2) db2[c] = (accumulate ? db2[c] : 0.f) + strided_sum(Z2 + c, 0, N, 1, C);
   }
   for (int r = t; r < Cr; r += CA_FNT) {
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += Z1[n * Cr + r];
-    if (db1) db1[r] = (accumulate ? db1[r] : 0.f) + acc;
+    if (db1) db1[r] = (accumulate ? db1[r] : 0.f) + strided_sum(Z1 + r, 0, N, 1, Cr);
   }
 }
 
@@ -758,7 +840,7 @@ static int ca_ppb(int HW, int C, int PER) {
 
 static bool ca_shapes_ok(int C, int Cr, int P) {
   return C % 8 == 0 && C <= CA_FMAXC && Cr >= 1 && Cr <= CA_FMAXR && C * Cr <= CA_FMAXW && P >= 1 &&
-         (int64_t)P * C <= CA_FMAXP;
+         (int64_t)P * C <= CA_FMAXP && P <= CA_RPT * (CA_FNT / (C / 4));
 }
 
 int sr_ca_fwd_apply(int dtype, const float* parts, int P, float scale, const float* w1, const float* b1,

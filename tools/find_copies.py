@@ -29,8 +29,8 @@ def main():
     for it in (1, 2):
         model.optimize_parameters(it)
     torch.cuda.synchronize()
-    acts = [torch.profiler.ProfilerActivity.CPU]
-    with torch.profiler.profile(activities=acts, with_stack=True) as prof:
+    acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+    with torch.profiler.profile(activities=acts, with_stack=True, record_shapes=True) as prof:
         model.optimize_parameters(3)
         torch.cuda.synchronize()
     cnt = collections.Counter()
@@ -38,9 +38,19 @@ def main():
         if ev.name in ('aten::copy_', 'aten::clone', 'aten::contiguous', 'aten::to', 'aten::_to_copy', 'aten::cat',
                        'aten::zeros', 'aten::zero_', 'aten::fill_', 'aten::add_', 'aten::add', 'aten::mul'):
             st = [f for f in (ev.stack or []) if 'basicsr4rs_amd' in f or 'bench' in f]
-            cnt[(ev.name, st[0] if st else '(no repo frame: ' + ((ev.stack or ['?'])[0]) + ')')] += 1
+            where = st[0] if st else '(no repo frame: ' + ' <- '.join((ev.stack or ['?'])[:3]) + ')'
+            cnt[(ev.name, where + f' shapes={ev.input_shapes} types={getattr(ev, "input_types", None)}')] += 1
     for (name, where), c in cnt.most_common(40):
         print(f'{c:5d}  {name:18s} {where}')
+    # device-side copies / fills and the CPU op that issued them
+    dev = collections.Counter()
+    for ev in prof.events():
+        for k in getattr(ev, 'kernels', []) or []:
+            if any(t in k.name for t in ('opy', 'emcpy', 'ill')):
+                st = [f for f in (ev.stack or []) if 'basicsr4rs_amd' in f or 'bench' in f]
+                dev[(k.name[:60], ev.name, st[0] if st else '?', str(ev.input_shapes)[:80])] += 1
+    for (kn, op, where, sh), c in dev.most_common(30):
+        print(f'{c:5d}  {kn:40s} <- {op} {where} {sh}')
 
 
 if __name__ == '__main__':
