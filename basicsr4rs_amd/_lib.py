@@ -96,6 +96,7 @@ SIGNATURES = {
     'sr_ca_param_grad': (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     'sr_act_backward_nhwc': (_i, [_i, _i64, _i, _vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _f, _f, _vp]),
     'sr_nearest_up_backward': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    'sr_nearest_up_backward_gate': (_i, [_i, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _f, _vp, _i, _i, _vp]),
     'sr_copy_channels': (_i, [_i, _vp, _i, _i, _vp, _i, _i, _i64, _i, _vp]),
     'sr_layernorm_fwd': (_i, [_i, _vp, _i, _vp, _vp, _i64, _i, _i, _f, _vp, _i, _vp, _vp, _vp]),
     'sr_layernorm_bwd_workspace': (_sz, [_i64, _i]),

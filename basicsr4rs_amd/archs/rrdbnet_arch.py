@@ -73,7 +73,7 @@ class RRDBNet(nn.Module):
         feat = C.conv3x3(h, self.conv_first)
         feat = C.conv3x3(self.body(feat), self.conv_body, res=feat)
         lr = dict(act=_lib.ACT_LRELU, slope=0.2)
-        feat = C.conv3x3(feat, self.conv_up1, in_up=2, **lr)
-        feat = C.conv3x3(feat, self.conv_up2, in_up=2, **lr)
-        feat = C.conv3x3(feat, self.conv_hr, **lr)
-        return C.conv3x3(feat, self.conv_last, out_nchw=True)
+        # upsampling tail (rrdbnet_arch.py:112-119) as one chain: each lrelu backward fused into the
+        # next conv's dgrad (ops/conv.py _ConvChain; RRDB x4 64.43 -> 64.29 ms, A/B 2 rounds)
+        return C.conv_chain(feat, (self.conv_up1, self.conv_up2, self.conv_hr, self.conv_last),
+                            (dict(in_up=2, **lr), dict(in_up=2, **lr), lr, dict(out_nchw=True)))

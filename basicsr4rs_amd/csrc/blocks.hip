@@ -14,7 +14,8 @@
 //   sr_ca_param_grad     the squeeze convs' parameter gradients (off the critical path)
 //   sr_act_backward_nhwc strided (channel-slice) ReLU/LeakyReLU backward (RRDB dense slices)
 //   sr_nearest_up_backward  sum of each 2x2 (s x s) block: backward of F.interpolate(
-//                        scale_factor=s, mode='nearest') (rrdbnet_arch.py:116-117)
+//                        scale_factor=s, mode='nearest') (rrdbnet_arch.py:116-117); _gate: times the
+//                        LeakyReLU derivative of the upsampled map (conv_up1 / conv_up2 activations)
 //   sr_copy_channels     strided channel-slice copy (RRDB dense buffers)
 #include "sr_common.h"
 #include "sr_internal.h"
@@ -678,10 +679,13 @@ __global__ void act_backward_nhwc_kernel(const T* __restrict__ dy, int ldd, int 
   }
 }
 
-// out[n,y,x,c] (+)= sum_{i,j<s} d[n, y*s+i, x*s+j, c]
+// out[n,y,x,c] (+)= sum_{i,j<s} d[n, y*s+i, x*s+j, c]; with a gate (the LR map the upsample read, itself
+// a LeakyReLU / ReLU output): out = that sum * (gate > 0 ? 1 : slope), the activation backward of the
+// conv that produced the gate fused in (RRDBNet HR tail, ops/conv.py conv_chain)
 template <typename T>
 __global__ void nearest_up_backward_kernel(const T* __restrict__ d, int ldd, int N, int H, int W, int C, int s,
-                                           T* __restrict__ out, int ldo, int accumulate) {
+                                           const T* __restrict__ gate, int ldg, float slope, T* __restrict__ out,
+                                           int ldo, int accumulate) {
   constexpr int PER = Elt<T>::PER16;
   const int groups = C / PER;
   const int64_t nv = (int64_t)N * H * W * groups;
@@ -708,6 +712,19 @@ __global__ void nearest_up_backward_kernel(const T* __restrict__ d, int ldd, int
           for (int k = 0; k < 4; ++k) acc[k] += __uint_as_float(v[k]);
         }
       }
+    if (gate) {
+      const u32x4 v = *(const u32x4*)(gate + p * ldg + g * PER);
+      if constexpr (PER == 8) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          acc[2 * k] *= bf16_to_f32(v[k] & 0xffff) > 0.f ? 1.f : slope;
+          acc[2 * k + 1] *= bf16_to_f32(v[k] >> 16) > 0.f ? 1.f : slope;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] *= __uint_as_float(v[k]) > 0.f ? 1.f : slope;
+      }
+    }
     T* dst = out + p * ldo + g * PER;
     if (accumulate) {
       const u32x4 v = *(const u32x4*)dst;
@@ -933,19 +950,25 @@ int sr_act_backward_nhwc(int dtype, int64_t P, int C, const void* dy, int ldd, i
   return sr_check(hipGetLastError(), "act_backward_nhwc launch");
 }
 
-int sr_nearest_up_backward(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s, void* out, int ldo,
-                           int accumulate, void* stream) {
+int sr_nearest_up_backward_gate(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s, const void* gate,
+                                int ldg, float slope, void* out, int ldo, int accumulate, void* stream) {
   const int PER = dtype == SR_BF16 ? 8 : 4;
-  if (!d || !out || C % PER || ldd % PER || ldo % PER || s < 1) return sr_fail(SR_EINVAL, "nearest_up_backward: bad arguments");
+  if (!d || !out || C % PER || ldd % PER || ldo % PER || s < 1 || (gate && (ldg % PER || ldg < C)))
+    return sr_fail(SR_EINVAL, "nearest_up_backward: bad arguments");
   const int64_t nv = (int64_t)N * H * W * (C / PER);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == SR_BF16)
     hipLaunchKernelGGL(nearest_up_backward_kernel<bf16_t>, dim3(grid_for(nv)), dim3(256), 0, st, (const bf16_t*)d, ldd,
-                       N, H, W, C, s, (bf16_t*)out, ldo, accumulate);
+                       N, H, W, C, s, (const bf16_t*)gate, ldg, slope, (bf16_t*)out, ldo, accumulate);
   else
     hipLaunchKernelGGL(nearest_up_backward_kernel<float>, dim3(grid_for(nv)), dim3(256), 0, st, (const float*)d, ldd, N,
-                       H, W, C, s, (float*)out, ldo, accumulate);
+                       H, W, C, s, (const float*)gate, ldg, slope, (float*)out, ldo, accumulate);
   return sr_check(hipGetLastError(), "nearest_up_backward launch");
+}
+
+int sr_nearest_up_backward(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s, void* out, int ldo,
+                           int accumulate, void* stream) {
+  return sr_nearest_up_backward_gate(dtype, d, ldd, N, H, W, C, s, nullptr, 0, 1.f, out, ldo, accumulate, stream);
 }
 
 int sr_copy_channels(int dtype, const void* src, int lds_, int scoff, void* dst, int ldd, int dcoff, int64_t P, int C,

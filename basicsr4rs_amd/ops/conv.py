@@ -663,6 +663,96 @@ def conv3x3(x, conv, res=None, **kw):
     return _Conv3x3.apply(x, res, conv.weight, conv.bias, spec)
 
 
+class _ConvChain(torch.autograd.Function):
+    """A chain of 3x3 convs, each activation read only by the next conv: the RRDBNet HR tail
+    conv_up1 -> lrelu -> conv_up2 -> lrelu -> conv_hr -> lrelu -> conv_last (rrdbnet_arch.py:112-119),
+    with the nearest x2 upsamples folded into conv_up1 / conv_up2's input gather (in_up).
+
+    Forward = the convs of _Conv3x3 back to back.  Backward: a conv's dgrad applies the activation
+    derivative of the conv before it in its epilogue (gate = that conv's output, which is this conv's
+    input), or -- behind an upsample -- the gated 2x2-sum kernel (sr_nearest_up_backward_gate) does, so
+    the chain has no act_backward pass over the HR maps (RRDB x4: 3 per step, 1.1 ms of a 64.5 ms step
+    in round 4); each wgrad reads the gated gradient its dgrad also reads.  The activation outputs are
+    saved as the next conv's inputs anyway (for its wgrad), so the gates cost no extra memory."""
+
+    @staticmethod
+    def forward(ctx, x, specs, *params):
+        cur = x
+        ins = []
+        for i, spec in enumerate(specs):
+            w, b = params[2 * i], params[2 * i + 1]
+            dtype = cur.dtype
+            N, H, W = _grid(spec, cur)
+            wf, _, bg = prepared(w, b, spec, dtype)
+            y = torch.empty(_out_shape(spec, N, H, W), device=cur.device,
+                            dtype=torch.float32 if spec.out_nchw else dtype)
+            conv_fwd_raw(cur, wf, bg, y, N, H, W, spec.cin_p, spec.cout_p, spec.cout, aff_scale=spec.aff_scale,
+                         aff_shift=spec.aff_shift, act=spec.act, slope=spec.slope, alpha=spec.alpha, beta=spec.beta,
+                         out_ps=spec.out_ps, out_nchw=spec.out_nchw, in_up=spec.in_up)
+            ins.append(cur)
+            cur = y
+        ctx.specs = specs
+        ctx.save_for_backward(*ins, cur if specs[-1].act else None, *params)
+        return cur
+
+    @staticmethod
+    def backward(ctx, dy):
+        specs = ctx.specs
+        L = len(specs)
+        saved = ctx.saved_tensors
+        ins, y_last, params = saved[:L], saved[L], saved[L + 1:]
+        grads = [None] * (2 * L)
+        d = dy
+        for i in reversed(range(L)):
+            spec, xi = specs[i], ins[i]
+            w, b = params[2 * i], params[2 * i + 1]
+            N, H, W = _grid(spec, xi)
+            dtype = xi.dtype
+            alpha = spec.alpha
+            if spec.out_nchw:
+                scale = spec.aff_scale * alpha if spec.aff_scale is not None else None
+                if scale is None and alpha != 1.0:
+                    scale = torch.full((spec.cout, ), alpha, device=d.device)
+                dY = nchw_to_nhwc(d, spec.cout_p, dtype, scale=scale)
+                alpha = 1.0
+            else:
+                dY = d.to(dtype).contiguous()
+                if i == L - 1 and spec.act:  # the chain's own output activation: not gated by a successor
+                    dY = act_backward(dY, y_last, spec.act, spec.slope, alpha)
+                    alpha = 1.0
+            _, wd, _ = prepared(w, b, spec, dtype)
+            if i > 0 or ctx.needs_input_grad[0]:
+                # the previous conv's activation output is this conv's input xi: its derivative gates dx
+                gated = i > 0 and bool(specs[i - 1].act)
+                pslope = specs[i - 1].slope if gated else 0.0
+                dx = torch.empty(N, H, W, spec.cin_p, device=xi.device, dtype=dtype)
+                up = spec.in_up and spec.in_up > 1
+                conv_fwd_raw(dY, wd, None, dx, N, H, W, spec.cout_p, spec.cin_p, spec.cin_p, alpha=alpha,
+                             in_ps=spec.out_ps, ldx=dY.shape[-1], gate=xi if gated and not up else None,
+                             gate_slope=pslope)
+                if up:
+                    dx = nearest_up_backward(dx, spec.in_up, gate=xi if gated else None, slope=pslope)
+                d = dx
+            grads[2 * i], grads[2 * i + 1] = conv_wgrad_raw(dY, xi, N, H, W, spec.cin_p, spec.cin, spec.cout_p,
+                                                            spec.cout, scale=alpha, out_ps=spec.out_ps,
+                                                            need_bias=params[2 * i + 1] is not None,
+                                                            in_up=spec.in_up, params=(w, b))
+        return (d if ctx.needs_input_grad[0] else None, None, *grads)
+
+
+def conv_chain(x, convs, kws):
+    """Apply nn.Conv2d(., ., 3, 1, 1) modules ``convs`` in sequence (keyword sets ``kws``: ConvSpec
+    arguments), as one autograd node whose backward fuses each activation derivative into the next
+    conv's dgrad (_ConvChain).  Only for chains whose intermediate maps feed nothing else."""
+    specs = tuple(ConvSpec(c.in_channels, c.out_channels, **kw) for c, kw in zip(convs, kws))
+    if any(sp.out_ps for sp in specs):
+        raise ValueError('conv_chain: no pixel-shuffle convs')
+    params = []
+    for c in convs:
+        params += [c.weight, c.bias]
+    return _ConvChain.apply(x, specs, *params)
+
+
 class _ResBlock(torch.autograd.Function):
     """ResidualBlockNoBN (basicsr/archs/arch_util.py:64-88): x + rs * conv2(relu(conv1(x))).
 
@@ -774,15 +864,20 @@ def upsample_specs(scale):
     raise ValueError(f'scale {scale} is not supported. Supported scales: 2^n and 3.')
 
 
-def nearest_up_backward(d, s, out=None, accumulate=False):
-    """Sum of each s x s block of an NHWC map (backward of nearest upsampling by s)."""
+def nearest_up_backward(d, s, out=None, accumulate=False, gate=None, slope=0.0):
+    """Sum of each s x s block of an NHWC map (backward of nearest upsampling by s); with ``gate`` (the
+    upsampled H x W map, a ReLU / LeakyReLU output) times its activation derivative (gate > 0 ? 1 : slope)."""
     N, Hs, Ws, C = d.shape
     H, W = Hs // s, Ws // s
     if out is None:
         out = torch.empty(N, H, W, C, device=d.device, dtype=d.dtype)
+    if gate is not None and (tuple(gate.shape[:3]) != (N, H, W) or gate.shape[-1] < C or gate.dtype != d.dtype
+                             or not gate.is_contiguous()):
+        raise ValueError(f'nearest_up_backward: gate {tuple(gate.shape)} {gate.dtype} for {(N, H, W, C)} {d.dtype}')
     lib = _lib.load()
-    _lib.check(lib.sr_nearest_up_backward(_lib.dtype_code(d.dtype), _lib.ptr(d), C, N, H, W, C, s, _lib.ptr(out),
-                                          out.shape[-1], int(accumulate), _lib.stream()))
+    _lib.check(lib.sr_nearest_up_backward_gate(_lib.dtype_code(d.dtype), _lib.ptr(d), C, N, H, W, C, s, _lib.ptr(gate),
+                                               gate.shape[-1] if gate is not None else 0, float(slope), _lib.ptr(out),
+                                               out.shape[-1], int(accumulate), _lib.stream()))
     return out
 
 

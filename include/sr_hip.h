@@ -299,6 +299,12 @@ int sr_act_backward_nhwc(int dtype, int64_t P, int C, const void* dy, int ldd, i
  * (rrdbnet_arch.py:116-117); out has H x W pixels, d has sH x sW. */
 int sr_nearest_up_backward(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s, void* out,
                            int ldo, int accumulate, void* stream);
+/* The same times the activation derivative of the upsampled map (gate: its H x W LeakyReLU / ReLU output,
+ * row stride ldg): out = sum * (gate > 0 ? 1 : slope) -- the conv_up1 / conv_up2 lrelu backward
+ * (rrdbnet_arch.py:116-117) fused into the 2x2 sum; gate null = sr_nearest_up_backward. */
+int sr_nearest_up_backward_gate(int dtype, const void* d, int ldd, int N, int H, int W, int C, int s,
+                                const void* gate, int ldg, float slope, void* out, int ldo, int accumulate,
+                                void* stream);
 /* Strided channel-slice copy (RRDB dense-block buffers). */
 int sr_copy_channels(int dtype, const void* src, int lds, int scoff, void* dst, int ldd, int dcoff, int64_t P,
                      int C, void* stream);
