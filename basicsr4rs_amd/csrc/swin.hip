@@ -924,12 +924,43 @@ __global__ __launch_bounds__(1024) void wattn_dbias_slots(const float* __restric
     *(f32x4*)(slots + ((int64_t)q * nH + h) * ATT_SLOTS + sl) = t;
   }
 }
+// bin b's candidate slots (d, r, gh, g1) in the fold order, as a compile-time CSR table: every one of
+// the 1792 slots of a row feeds exactly one of the 225 bins (1 .. 16 each).  (The fold used to test
+// all 112 candidates per bin at run time, integer divisions included: 23 us per call in the step.)
+struct alignas(16) DbiasTab {
+  short idx[ATT_SLOTS];  // first: 16-B aligned for the staging loads
+  short start[226];
+};
+constexpr DbiasTab make_dbias_tab() {
+  DbiasTab t{};
+  int n = 0;
+  for (int b = 0; b < 225; ++b) {
+    t.start[b] = (short)n;
+    for (int e = 0; e < 112; ++e) {
+      const int d = e >> 4, r = (e >> 2) & 3, gh = (e >> 1) & 1, g1 = e & 1;
+      const int qq = b - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
+      if (qq < 0 || qq >= 225) continue;
+      const int dyp = qq / 15, dxp = qq - 15 * dyp;  // (g >> 1) - (c >> 3) + 7, 4 (g & 1) - (c & 7) + 7
+      const int chh = gh - (dyp - 7), c7 = 4 * g1 - (dxp - 7);
+      if (dyp < 6 || dyp > 8 || dxp > 11 || chh < 0 || chh > 1 || c7 < 0 || c7 > 7) continue;
+      t.idx[n++] = (short)(((2 * gh + g1) * 16 + 8 * chh + c7) * ATT_SLOTS_LANE + 4 * d + r);
+    }
+  }
+  t.start[225] = (short)n;
+  return t;
+}
+constexpr DbiasTab kDbiasTabHost = make_dbias_tab();
+static_assert(kDbiasTabHost.start[225] == ATT_SLOTS, "every slot feeds one bin");
+__constant__ DbiasTab kDbiasTab = make_dbias_tab();
+
 __global__ __launch_bounds__(256) void wattn_dbias_fold(const float* __restrict__ slots, int nH,
                                                         float* __restrict__ dbias, int acc) {
   // one block per head: the head's 4 quarter rows summed into an LDS slot row with coalesced 16-B
   // loads (scattered 4-B global reads of other XCDs' freshly written lines were the cost: 27 us in
-  // the step), then thread b folds bin b's candidate slots from LDS in a fixed order
+  // the step), the bin table staged beside it; then thread b sums bin b's slots in a fixed order
   __shared__ f32x4 sl4[ATT_SLOTS / 4];
+  __shared__ __attribute__((aligned(16))) short sidx[ATT_SLOTS];
+  __shared__ short sst[226];
   const int h = blockIdx.x, t = threadIdx.x;
   for (int i = t; i < ATT_SLOTS / 4; i += 256) {
     f32x4 v = ((const f32x4*)(slots + (int64_t)h * ATT_SLOTS))[i];
@@ -937,21 +968,14 @@ __global__ __launch_bounds__(256) void wattn_dbias_fold(const float* __restrict_
     for (int q = 1; q < DB_Q; ++q) v += ((const f32x4*)(slots + ((int64_t)q * nH + h) * ATT_SLOTS))[i];
     sl4[i] = v;
   }
+  for (int i = t; i < ATT_SLOTS / 8; i += 256) ((u32x4*)sidx)[i] = ((const u32x4*)kDbiasTab.idx)[i];
+  if (t < 226) sst[t] = kDbiasTab.start[t];
   __syncthreads();
   const float* sl = (const float*)sl4;
   const int b = t;
   if (b >= 225) return;
   float s = 0.f;
-#pragma unroll
-  for (int e = 0; e < 112; ++e) {  // candidate (d, r, gh, g1)
-    const int d = e >> 4, r = (e >> 2) & 3, gh = (e >> 1) & 1, g1 = e & 1;
-    const int qq = b - 30 * (d - 3) - r;  // bin_base_qk of the contributing lanes
-    const int dyp = qq / 15, dxp = qq - 15 * dyp;  // (g >> 1) - (c >> 3) + 7, 4 (g & 1) - (c & 7) + 7
-    const int chh = gh - (dyp - 7), c7 = 4 * g1 - (dxp - 7);
-    const bool v = qq >= 0 && qq < 225 && dyp >= 6 && dyp <= 8 && dxp <= 11 && chh >= 0 && chh <= 1 && c7 >= 0 && c7 <= 7;
-    const int idx = ((2 * gh + g1) * 16 + 8 * chh + c7) * ATT_SLOTS_LANE + 4 * d + r;
-    s += v ? sl[v ? idx : 0] : 0.f;
-  }
+  for (int i = sst[b], e = sst[b + 1]; i < e; ++i) s += sl[sidx[i]];
   dbias[b * nH + h] = (acc ? dbias[b * nH + h] : 0.f) + s;
 }
 
