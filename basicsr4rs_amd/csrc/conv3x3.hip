@@ -3830,7 +3830,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_narrow_kernel(const float* w
 // with 4 independent loads in flight, then a fixed-order LDS combine -- deterministic.  The host
 // sizes P to ~8 slabs per thread and GPW so that the grid covers the chip (RCAN: S 256 over 9216
 // groups = 288 blocks of 32 groups x 32 phases instead of 144 of 64 x 16).
-template <int GPW, bool TR>
+// CIG (TR false with a ci_map, the SwinIR proj / dense linears over padded head channels): groups run
+// over the GEMM columns (16-B loads, no gather) and each sum is stored at its parameter column, through
+// the GEMM -> parameter inverse of ci_map built in LDS (-1: a padding column, dropped).  (The gathered
+// wgrad_reduce4_kernel it replaces read 36 MB in 60 us in the SwinIR step.)
+template <int GPW, bool TR, bool CIG = false>
 __global__ __launch_bounds__(1024) void wgrad_reduce_g_kernel(const float* ws, const float* wsb, float* dw, float* db,
                                                               int S, int Cout, int Cin, int Cout_real, int Cin_real,
                                                               int out_ps, int taps, const int* co_map,
@@ -3861,7 +3865,16 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_g_kernel(const float* ws, c
   const int P = nw * (64 / GPW);
   const int ph = wv * (64 / GPW) + lane / GPW, gl = lane % GPW;
   const int64_t i = (int64_t)blockIdx.x * GPW + gl;
-  const int c4n = TR ? (Cout_real + 3) >> 2 : Cin_real >> 2;
+  const int c4n = TR ? (Cout_real + 3) >> 2 : (CIG ? Cin >> 2 : Cin_real >> 2);
+  [[maybe_unused]] int* inv = nullptr;
+  if constexpr (CIG) {
+    __shared__ int inv_s[1024];  // GEMM column -> parameter column (Cin <= 1024, checked on the host)
+    inv = inv_s;
+    for (int k = threadIdx.x; k < Cin; k += blockDim.x) inv_s[k] = -1;
+    __syncthreads();
+    for (int c = threadIdx.x; c < Cin_real; c += blockDim.x) inv_s[ci_map[c]] = c;
+    __syncthreads();
+  }
   const int rows = TR ? Cin_real : Cout_real;
   const int64_t total = (int64_t)taps * rows * c4n;
   int q4 = 0, rw = 0, tap = 0;
@@ -3897,6 +3910,15 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_g_kernel(const float* ws, c
         const int co = q4 * 4 + e;
         if (co < Cout_real) {
           float* d = dw + ((size_t)co * Cin_real + rw) * taps + tap;
+          *d = sm[e] * scale + (accumulate ? *d : 0.f);
+        }
+      }
+    } else if constexpr (CIG) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int pc = inv[q4 * 4 + e];
+        if (pc >= 0) {
+          float* d = dw + ((size_t)rw * Cin_real + pc) * taps + tap;
           *d = sm[e] * scale + (accumulate ? *d : 0.f);
         }
       }
@@ -4610,10 +4632,12 @@ bool wg_use_lin(const sr_conv3x3_wgrad_desc* d) {
   return !off && g_variant != 63 && g_variant != 1 && d->dtype == SR_BF16 && d->ksize == 1 && d->in_up <= 1 &&
          d->out_ps == 0 && d->Cout >= 64 && d->Cin >= 64;
 }
-// Block target of its split plan: 256 (one 144-KB block per CU), or knob SR_LWG_T (A/B)
+// Block target of its split plan: 128 (half the chip: it runs on the weight-gradient side stream beside
+// the main stream, and half the splits halve its slab; SwinIR 35.74 -> 34.71 ms against 256, 160 / 96 / 64
+// slower, round 5), or knob SR_LWG_T (A/B)
 int lin_wg_target() {
   const int x = sr_knob(K_LWG_T);
-  return x >= 16 && x <= 4096 ? x : 256;
+  return x >= 16 && x <= 4096 ? x : 128;
 }
 // Row-streaming wgrad (conv3x3_wgrad_ring_kernel): bf16 3x3, Cout <= 64, W % 64 == 0, nearest upsample
 // <= 2 (or over 64-channel output tiles, wg_ring_wide).
@@ -4940,9 +4964,11 @@ int wgrad_reduce_launch(const sr_conv3x3_wgrad_desc* d, int S, int taps, const f
   const int64_t work = total > Cout_real ? total : Cout_real;
   const bool tr = wg_use_halo(d);
   // (the row-streaming slab keeps wgrad_reduce_tr_kernel: 32-group blocks measured slower on RCAN / RRDB)
-  if (g_variant != 40 && !tr && Cin_real % 4 == 0 && !ci_map) {
+  const bool cig = !tr && ci_map && d->Cin % 4 == 0 && d->Cin <= 1024;  // ci gather on the output side
+  if (g_variant != 40 && !tr && ((Cin_real % 4 == 0 && !ci_map) || cig)) {
     // split phases P ~ S / 8 (pow2 <= 32), group width GPW so that the grid covers the chip
-    const int64_t groups = tr ? (int64_t)taps * Cin_real * ((Cout_real + 3) / 4) : (int64_t)taps * Cout_real * (Cin_real / 4);
+    const int64_t groups = tr ? (int64_t)taps * Cin_real * ((Cout_real + 3) / 4)
+                              : (int64_t)taps * Cout_real * ((cig ? d->Cin : Cin_real) / 4);
     int P = 1;
     while (P * 8 < S && P < 32) P <<= 1;
     int gpw = 64;
@@ -4952,11 +4978,12 @@ int wgrad_reduce_launch(const sr_conv3x3_wgrad_desc* d, int S, int taps, const f
     const int wblocks = (int)((groups + gpw - 1) / gpw);
     const int bblocks = db ? (Cout_real + 63) / 64 : 0;
     const dim3 grid((unsigned)(wblocks + bblocks)), blk((unsigned)(nw * 64));
-#define SR_RG(G, T)                                                                                             \
-  hipLaunchKernelGGL((wgrad_reduce_g_kernel<G, T>), grid, blk, (size_t)nw * 64 * 16, s, (const float*)ws, (const float*)wsb, dw, db, \
+#define SR_RG(G, T, ...)                                                                                        \
+  hipLaunchKernelGGL((wgrad_reduce_g_kernel<G, T, ##__VA_ARGS__>), grid, blk, (size_t)nw * 64 * 16, s, (const float*)ws, (const float*)wsb, dw, db, \
                      S, d->Cout, d->Cin, Cout_real, Cin_real, d->out_ps, taps, co_map, ci_map, d->scale, wblocks,  \
                      acc1)
     if (tr) { if (gpw == 64) SR_RG(64, true); else if (gpw == 32) SR_RG(32, true); else SR_RG(16, true); }
+    else if (cig) { if (gpw == 64) SR_RG(64, false, true); else if (gpw == 32) SR_RG(32, false, true); else SR_RG(16, false, true); }
     else { if (gpw == 64) SR_RG(64, false); else if (gpw == 32) SR_RG(32, false); else SR_RG(16, false); }
 #undef SR_RG
   } else if (tr) {
