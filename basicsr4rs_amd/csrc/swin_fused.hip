@@ -124,20 +124,24 @@ struct SabArgs {
   int nwx, nwin, nwin_total;
 };
 
-// LDS layout of a block of NW windows (TOK = 64 NW tokens, 256 NW threads).  O_h overlays Q_h: a
-// wave reads the Q rows of its own queries (step B) before it writes their O rows, and no other wave
-// reads them.  The bias table is staged one head column at a time (the next head's column is loaded
-// at the head's top, with its weights, and written after S2).
+// LDS layout of a block of NW windows (TOK = 64 NW tokens, 256 NW threads).  O_h has its own image
+// and the bias table is staged one head column at a time in two slots (head h in slot h & 1; the
+// next head's column is loaded at the head's top, with its weights, and written after S1), so a head
+// needs two barriers: S1 (Q, K, V of the head in LDS; the weight image and the other table slot free)
+// and S2 (O_h in LDS; the next head's weights and table column visible).  Step C of head h and step A
+// of head h + 1 then run back to back: A writes Q / K / V, which nobody reads after S2, and C reads O,
+// which the next head writes only after its S1.  (Round 4 / early round 5: O_h overlaid Q_h and a
+// third barrier per head closed step C.)
 template <int NW> struct SabL {
   static constexpr int TOK = 64 * NW, NT = 256 * NW;
   static constexpr int X = 0;                      // [3 cg][TOK rows][128 B]
   static constexpr int W = X + 3 * TOK * 128;      // [3 cg][96 rows][128 B]
-  static constexpr int Q = W + 3 * 96 * 128;       // [TOK][64 B]; O_h overlays it
+  static constexpr int Q = W + 3 * 96 * 128;       // [TOK][64 B]
   static constexpr int K = Q + TOK * 64;
   static constexpr int V = K + TOK * 64;           // [NW windows][64][64 B], sx_byte layout (tr reads)
-  static constexpr int O = Q;
-  static constexpr int TB = V + TOK * 64;          // float [256]: this head's bias-table column
-  static constexpr int GB = TB + 256 * 4;          // float [2][192]: LayerNorm gamma, beta
+  static constexpr int O = V + TOK * 64;           // [TOK][64 B]
+  static constexpr int TB = O + TOK * 64;          // float [2][256]: bias-table column of head h in slot h & 1
+  static constexpr int GB = TB + 2 * 256 * 4;      // float [2][192]: LayerNorm gamma, beta
   static constexpr int BQ = GB + 2 * 192 * 4;      // float [3 nH 32 <= 576]: qkv bias
   static constexpr int BP = BQ + 576 * 4;          // float [192]: proj bias
   static constexpr int LDS = BP + 192 * 4;
@@ -349,13 +353,13 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
     __builtin_amdgcn_sched_barrier(0);  // keep these loads here, ahead of the head's stores
     // step B's 16 bias-table values of this lane (+ the shift mask), read now: their LDS latency hides
     // under step A instead of 8 dependent ds_read round trips in the softmax (the column was staged
-    // before the previous head's S3 barrier)
+    // after the previous head's S1 barrier)
     float tbv[16];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        tbv[4 * i + r] = (sTB + tbase - 93)[93 - 30 * i - r];
+        tbv[4 * i + r] = (sTB + (h & 1) * 256 + tbase - 93)[93 - 30 * i - r];
         if constexpr (SH) tbv[4 * i + r] += mk[4 * i + r];
       }
 
@@ -402,7 +406,11 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
         *(uint2*)(smem + la) = u;
       }
     }
-    __syncthreads();  // S1: Q, K, V of head h in LDS
+    __syncthreads();  // S1: Q, K, V of head h in LDS; every wave is past step A (sW) and the top (table slot)
+    if (h + 1 < a.nH) {
+      if constexpr ((DBG & 16) == 0) w_store();
+      if (tid < 256) sTB[((h + 1) & 1) * 256 + tid] = tbn * LOG2E;  // (scaled here: a multiply next to the load would wait for it)
+    }
 
     // ---- B: window attention, wave = (window wi, queries 16 jq ..)
     {
@@ -457,11 +465,7 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
         *(uint2*)(smem + L::O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
       }
     }
-    __syncthreads();  // S2: O_h in LDS; every wave is past step A (sW) and step B (sTB)
-    if (h + 1 < a.nH) {
-      if constexpr ((DBG & 16) == 0) w_store();
-      if (tid < 256) sTB[tid] = tbn * LOG2E;  // (scaled here: a multiply next to the load would wait for it)
-    }
+    __syncthreads();  // S2: O_h in LDS (Q, K, V free); the next head's weights and table column visible
 
     // ---- C: x2acc += Wp[:, head h] . O_h^T
 #pragma unroll
@@ -473,7 +477,6 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
         else xacc[i][j][0] += __builtin_bit_cast(float, (int)(wpf[i][0] ^ (unsigned)of[1]));
       }
     }
-    __syncthreads();  // S3: sO read; the next head's sW written
   }
 
   // ---- epilogue: x2 = x + s1[n] * (proj + bias); all loads before the first store (see above)
