@@ -189,25 +189,28 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
 #pragma unroll
       for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
     }
-    if (a.aux) {  // pre-activation side output (GELU backward needs it)
+    if (a.aux) {  // activation side output (act_aux_n: GELU' for GELU, which the backward's gate reads)
+      float ax[8];
+      act_aux_n(v, ax, a.act, a.slope);
       const size_t da = (size_t)m * a.ldy + a.ycoff + n;
       if constexpr (SZ == 2) {
         u32x4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(ax[2 * j], ax[2 * j + 1]);
         *(u32x4*)((bf16_t*)a.aux + da) = o;
       } else {
-        *(f32x4*)((float*)a.aux + da) = f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)((float*)a.aux + da + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        *(f32x4*)((float*)a.aux + da) = f32x4{ax[0], ax[1], ax[2], ax[3]};
+        *(f32x4*)((float*)a.aux + da + 4) = f32x4{ax[4], ax[5], ax[6], ax[7]};
       }
+    } else {
+      act_apply_n(v, a.act, a.slope);
     }
-    act_apply_n(v, a.act, a.slope);
     if (a.gate && a.gate_mode != 2) {
       float g[8];
       unpack(gv[it], g);
-      if (a.gate_mode == 1) {
+      if (a.gate_mode == 1) {  // the stored GELU' (the forward's aux)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(g[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= g[j];
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= (g[j] > 0.f ? 1.f : a.gate_slope);
@@ -1321,13 +1324,14 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
         v[r] = acc[2 * P][j][r] + bv[P][r];
         v[4 + r] = acc[2 * P + 1][j][r] + bv[P][4 + r];
       }
-      if constexpr (AUX) {  // the pre-activation value (GELU backward)
+      if constexpr (AUX) {  // activation side output (act_aux_n: GELU' for GELU)
+        float ax[8];
+        act_aux_n(v, ax, ACT, a.slope);
         u32x4 o;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
+        for (int q = 0; q < 4; ++q) o[q] = pack_bf16x2(ax[2 * q], ax[2 * q + 1]);
         __builtin_amdgcn_raw_buffer_store_b128(o, ar, (n < a.Cout && m < a.M) ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB, 0, 0);
-      }
-      if constexpr (ACT == 1) {
+      } else if constexpr (ACT == 1) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = v[q] > 0.f ? v[q] : 0.f;
       } else if constexpr (ACT == 2) {
@@ -1347,9 +1351,9 @@ __global__ __launch_bounds__(256, 2) void linear_wk_kernel(FwdArgs a) {
         if constexpr (GATE == 1) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) v[q] *= gf[q] > 0.f ? 1.f : a.gate_slope;
-        } else {
+        } else {  // the stored GELU' (the forward's aux)
 #pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] *= gelu_grad(gf[q]);
+          for (int q = 0; q < 8; ++q) v[q] *= gf[q];
         }
       }
 #pragma unroll
@@ -1593,14 +1597,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
-        if constexpr (AUX) {
+        if constexpr (AUX) {  // activation side output (act_aux_n: GELU' for GELU)
+          float ax[8];
+          act_aux_n(v, ax, ACT, a.slope);
           u32x4 o;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+          for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(ax[2 * j], ax[2 * j + 1]);
           __builtin_amdgcn_raw_buffer_store_b128(o, ar,
                                                  ok ? (uint32_t)(((size_t)m * a.ldy + a.ycoff + n) * 2) : SR_OOB, 0, 0);
-        }
-        if constexpr (ACT == 1) {
+        } else if constexpr (ACT == 1) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : 0.f;
         } else if constexpr (ACT == 2) {
@@ -1621,9 +1626,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
         if constexpr (GATE == 1) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
-        } else if constexpr (GATE == 2) {
+        } else if constexpr (GATE == 2) {  // the stored GELU' (the forward's aux)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
+          for (int j = 0; j < 8; ++j) v[j] *= gf[j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= alpha_blk;
@@ -1669,20 +1674,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
-      if (a.aux) {
+      if (a.aux) {  // activation side output (act_aux_n: GELU' for GELU)
+        float ax[8];
+        act_aux_n(v, ax, a.act, a.slope);
         u32x4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(ax[2 * j], ax[2 * j + 1]);
         *(u32x4*)((bf16_t*)a.aux + (size_t)m * a.ldy + a.ycoff + n) = o;
+      } else {
+        act_apply_n(v, a.act, a.slope);
       }
-      act_apply_n(v, a.act, a.slope);
       if (a.gate && a.gate_mode != 2) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const float g0 = bf16_to_f32(gv1[j] & 0xffff), g1 = bf16_to_f32(gv1[j] >> 16);
-          if (a.gate_mode == 1) {
-            v[2 * j] *= gelu_grad(g0);
-            v[2 * j + 1] *= gelu_grad(g1);
+          if (a.gate_mode == 1) {  // the stored GELU'
+            v[2 * j] *= g0;
+            v[2 * j + 1] *= g1;
           } else {
             v[2 * j] *= g0 > 0.f ? 1.f : a.gate_slope;
             v[2 * j + 1] *= g1 > 0.f ? 1.f : a.gate_slope;
@@ -1896,18 +1904,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
-      if (a.aux) {
+      if (a.aux) {  // activation side output (act_aux_n: GELU' for GELU)
+        float ax[8];
+        act_aux_n(v, ax, a.act, a.slope);
         u32x4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
+        for (int j = 0; j < 4; ++j) o[j] = pack_bf16x2(ax[2 * j], ax[2 * j + 1]);
         *(u32x4*)((bf16_t*)a.aux + (size_t)m * a.ldy + a.ycoff + nn) = o;
+      } else {
+        act_apply_n(v, a.act, a.slope);
       }
-      act_apply_n(v, a.act, a.slope);
       float gf[8];
       if (a.gate) unpack8(gv, gf);
-      if (a.gate && a.gate_mode == 1) {
+      if (a.gate && a.gate_mode == 1) {  // the stored GELU'
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= gf[j];
       } else if (a.gate && a.gate_mode == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
@@ -2280,11 +2291,12 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) { v[r] = acc[i][0][r] + bv[r]; v[4 + r] = acc[i][1][r] + bv[4 + r]; }
-      if constexpr (AUX) {
+      if constexpr (AUX) {  // activation side output (act_aux_n: GELU' for GELU)
+        float ax[8];
+        act_aux_n(v, ax, ACT, a.slope);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) avx[i][j] = pack_bf16x2(v[2 * j], v[2 * j + 1]);
-      }
-      if constexpr (ACT == 1) {
+        for (int j = 0; j < 4; ++j) avx[i][j] = pack_bf16x2(ax[2 * j], ax[2 * j + 1]);
+      } else if constexpr (ACT == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : 0.f;
       } else if constexpr (ACT == 2) {
@@ -2299,9 +2311,9 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
       if constexpr (GATE == 1) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= gf[j] > 0.f ? 1.f : a.gate_slope;
-      } else if constexpr (GATE == 2) {
+      } else if constexpr (GATE == 2) {  // the stored GELU'
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= gelu_grad(gf[j]);
+        for (int j = 0; j < 8; ++j) v[j] *= gf[j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= rs;

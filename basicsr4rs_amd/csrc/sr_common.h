@@ -138,6 +138,42 @@ SR_DEV float gelu_grad(float z) {
   return fmaf(0.5f, erf, 0.5f) + z * 0.39894228040143268f * e;
 }
 
+// GELU and GELU' from one erf_fast evaluation: returns gelu(z), dg = gelu'(z) (2 FMAs more than gelu_exact)
+SR_DEV float gelu_pair(float z, float& dg) {
+  const float x = z * 0.70710678118654752f, ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * ax);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
+  const float phi2 = fmaf(0.5f, copysignf(1.f - p * e, x), 0.5f);  // Phi(z)
+  dg = fmaf(z * 0.39894228040143268f, e, phi2);
+  return z * phi2;
+}
+
+// The aux side output of an activation epilogue (sr_conv3x3_desc.aux): GELU' of the pre-activation for
+// GELU -- what the backward's gate (gate_mode 1) multiplies by, so the backward evaluates no erf -- and
+// the pre-activation value for the other activations; v becomes act(v).
+template <int N>
+SR_DEV void act_aux_n(float (&v)[N], float (&aux)[N], int act, float slope) {
+  if (act == 3) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = gelu_pair(v[j], aux[j]);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) aux[j] = v[j];
+  if (act == 1) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = v[j] > 0.f ? v[j] : 0.f;
+  } else if (act == 2) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = v[j] > 0.f ? v[j] : v[j] * slope;
+  }
+}
+
 SR_DEV float act_apply(float v, int act, float slope) {
   // act: 0 none, 1 relu, 2 leaky relu(slope), 3 GELU (exact erf form, nn.GELU default)
   if (act == 1) return v > 0.f ? v : 0.f;

@@ -527,7 +527,7 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
 // bf16, Cp <= 192, hidden Hp <= 384 (mlp_ratio 2: 360).  A 512-thread block owns 128 consecutive
 // token rows: LN2 into an LDS tile (and, training, ln_out / mean / rstd), fc1 with W1 fragments from
 // L2 into registers (wave w: hidden tiles w, w + 8, w + 16 over all 128 tokens), bias + exact GELU
-// in the epilogue (training: z and h stored, as the lin kernel's aux / output), h into an LDS tile
+// in the epilogue (training: GELU'(z) and h stored, as the lin kernel's aux / output), h into an LDS tile
 // that overlays the dead LN tile, then fc2 (wave: 48 output channels x 64 tokens) + bias, DropPath
 // row scale and the residual.  HBM (training): x2 read twice, ln_out / z / h / out written once =
 // 376 MB per SwinIR-M layer at B 32 against 470 MB for the lin kernel + linear_wk_kernel pair; h is
@@ -689,12 +689,9 @@ __global__ __launch_bounds__(512, 1) void swin_mlp_block_fwd_kernel(SmbArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int t = 16 * j + c16, m = m0 + t;
-      float zv[4], hv[4];
+      float zv[4], hv[4];  // zv: GELU' of the pre-activation (the aux the fc2 dgrad's gate multiplies by)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        zv[r] = hr + r < a.Hp ? acc[i][j][r] + bias[r] : 0.f;
-        hv[r] = gelu_exact(zv[r]);
-      }
+      for (int r = 0; r < 4; ++r) hv[r] = gelu_pair(hr + r < a.Hp ? acc[i][j][r] + bias[r] : 0.f, zv[r]);
       uint2 uz, uh;
       uz.x = pack_bf16x2(zv[0], zv[1]);
       uz.y = pack_bf16x2(zv[2], zv[3]);

@@ -456,7 +456,7 @@ class _STB(torch.autograd.Function):
         s1, s2 = ctx.dp if ctx.dp is not None else (None, None)
         g2 = row_scale(dout, s2, H * W) if s2 is not None else dout  # fc2-branch gradient
         _, f2wd, _ = prepared_linear(f2w, f2b, fc2s, dtype)
-        dz = linear_dgrad(g2, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)
+        dz = linear_dgrad(g2, f2wd, fc2s, N, H, W, gate=z, gate_mode=1)  # z: GELU' of fc1's output (its aux)
         df2w, df2b = linear_wgrad(g2, h, fc2s, N, H, W, params=(f2w, f2b))
         _, f1wd, _ = prepared_linear(f1w, f1b, fc1s, dtype)
         df1w, df1b = linear_wgrad(dz, ln2, fc1s, N, H, W, params=(f1w, f1b))

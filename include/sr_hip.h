@@ -82,7 +82,8 @@ typedef struct sr_conv3x3_desc {
   int rcols;  /* residuals apply to output columns n < rcols (0 = all) */
   int in_up;  /* x is the [N, H/u, W/u] map read through nearest-neighbour upsampling (0/1 = none) */
   int ksize;  /* 3 (default, 0 = 3) or 1: a 1x1 conv = nn.Linear over the NHWC tokens */
-  int gate_mode; /* 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= GELU'(gate) (gate = pre-activation);
+  int gate_mode; /* 0: v *= (gate > 0 ? 1 : gate_slope); 1: v *= gate (gate = the GELU' map a GELU
+                  forward stored as its aux: the backward evaluates no erf);
                   2: after the residuals, v *= (gate > 0 ? 1 : gate_slope) on output columns
                   gcol0 <= n < gcol1 only (activation backward of a dense-block slice whose
                   gradient this call completes) */
@@ -103,15 +104,16 @@ typedef struct sr_conv3x3_desc {
  * eps), the normalised rows also written to ln_out [M][Cin] (padded columns zero) with the per-row
  * mean / rstd, as sr_layernorm_fwd would (they feed the weight gradient and the LayerNorm
  * backward).  The linear is sr_conv3x3_fwd's ksize-1 path with a plain (act 0) or GELU +
- * pre-activation aux epilogue and Cin <= 192, Cout <= 640. */
+ * GELU' aux epilogue and Cin <= 192, Cout <= 640. */
 int sr_linear_ln_fwd(const sr_conv3x3_desc* d, const void* x, const float* ln_gamma, const float* ln_beta, int ln_C,
                      float eps, void* ln_out, float* ln_mean, float* ln_rstd, const void* w, const float* bias, void* y,
                      void* aux, void* stream);
 
 
 /* y = beta*res + beta2*res2 + alpha * gate_factor * act(conv(x, w) + bias); res/res2/gate may be NULL.
- * act: SR_ACT_* or 3 = GELU (exact erf).  aux (may be NULL): also store the pre-activation
- * value conv(x, w) + bias in y's layout (GELU backward).  colsum (may be NULL): fp32
+ * act: SR_ACT_* or 3 = GELU (exact erf).  aux (may be NULL): also store, in y's layout, GELU'(z) for
+ * act 3 (z = conv(x, w) + bias; the fc2 dgrad's gate_mode-1 factor, computed with the GELU from one
+ * erf) and z itself for the other activations.  colsum (may be NULL): fp32
  * [N * P][Cout] partial channel sums of y as stored, P = sr_conv3x3_fwd_colsum_parts(d) rows per
  * image, sum_p colsum[n*P + p][c] = sum over image n's pixels of y[n, pixel, c] -- RCAN's
  * AdaptiveAvgPool2d(1) (rcan_arch.py:19) fused into the conv that produces its input. */

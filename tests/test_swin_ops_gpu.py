@@ -131,8 +131,8 @@ def test_window_attention_bwd_reduce_paths_bitwise(cuda, shift, geom):
 @pytest.mark.parametrize('shape', [(2, 16, 16, 180, 6), (1, 8, 24, 60, 6), (3, 5, 13, 96, 3)])
 def test_linear_ln_fused_vs_separate(cuda, which, shape):
     """sr_linear_ln_fwd (LayerNorm in the lin kernel's prologue) against the standalone LayerNorm
-    kernel followed by the linear: the normalised rows, mean / rstd, the GELU pre-activation and
-    the output; ragged last token tile (M % 128 != 0) included."""
+    kernel followed by the linear: the normalised rows, mean / rstd, the GELU' side output (against
+    float64 GELU' of the pre-activation) and the output; ragged last token tile (M % 128 != 0) included."""
     from basicsr4rs_amd.ops import swin as S
     N, H, W, C_, nH = shape
     torch.manual_seed(3)
@@ -165,6 +165,11 @@ def test_linear_ln_fused_vs_separate(cuda, which, shape):
     assert (y.float() - y_r.float()).abs().max().item() <= 2e-2 * max(1.0, y_r.float().abs().max().item())
     if aux is not None:
         assert (aux.float() - aux_r.float()).abs().max().item() <= 2e-2 * max(1.0, aux_r.float().abs().max().item())
+        # the aux of a GELU linear is GELU' of the pre-activation (the fc2 dgrad's gate multiplies by it)
+        pre = ln_r[..., :C_].double() @ lin.weight.detach().to(dt).double().t() + lin.bias.detach().double()
+        dref = 0.5 * (1 + torch.erf(pre / 2**0.5)) + pre * torch.exp(-pre * pre / 2) / (2 * torch.pi) ** 0.5
+        got = aux[..., :2 * C_].double()
+        assert (got - dref).abs().max().item() <= 2e-2, (got - dref).abs().max().item()
 
 
 @pytest.mark.parametrize('K,Cout', [(360, 184), (576, 184), (200, 96), (256, 304), (384, 40), (184, 184), (184, 360)])
@@ -194,7 +199,7 @@ def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
     if rs is not None:
         kw.update(row_scale=rs)
     if gate is not None:
-        kw.update(gate=gate, gate_mode=1)  # GELU'(g) (the fc2 dgrad gate)
+        kw.update(gate=gate, gate_mode=1)  # times the stored GELU' map g (the fc2 dgrad gate)
 
     def run():
         y = torch.empty(N, H, W, Cout, device=cuda, dtype=dt)
@@ -208,7 +213,7 @@ def test_linear_wide_k_vs_fp64(cuda, K, Cout, epi):
     ref = x.double() @ w.to(dt).double().t() + bias.double()
     if gate is not None:
         gd = gate.double()
-        ref = ref * (0.5 * (1 + torch.erf(gd / 2**0.5)) + gd * torch.exp(-gd * gd / 2) / (2 * torch.pi) ** 0.5)
+        ref = ref * gd
     if rs is not None:
         ref = ref * rs.double().view(N, 1, 1, 1)
     if res is not None:
