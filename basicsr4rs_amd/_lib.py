@@ -10,7 +10,9 @@ import os
 
 import torch
 
-LIB_PATH = os.environ.get('SR_HIP_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib',
+from ._switches import switch
+
+LIB_PATH = switch('SR_HIP_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib',
                                                          'libsr_hip.so')
 
 SR_F32, SR_BF16 = 0, 1
@@ -159,7 +161,7 @@ def load():
         _LIB = lib
         # SR_CONV_VARIANT=<n>: a kernel-selection variant for the whole process (A/B runs,
         # tools/ab_val.sh); 0 / unset = automatic
-        v = int(os.environ.get('SR_CONV_VARIANT', '0') or 0)
+        v = int(switch('SR_CONV_VARIANT') or 0)
         if v:
             check(lib.sr_conv3x3_set_variant(v))
     return _LIB

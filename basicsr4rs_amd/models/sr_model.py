@@ -18,7 +18,6 @@ import torch
 from ..archs import build_network
 from ..losses import build_loss
 from ..metrics import calculate_metric
-import os
 
 from ..ops.conv import async_wgrad, bump_param_epoch, take_captured_tables
 from ..utils.flat import FlatParams
@@ -27,6 +26,7 @@ from ..utils.logger import get_root_logger
 from ..utils.registry import MODEL_REGISTRY
 from ..utils.step_graph import SegmentedStepGraph
 from .base_model import BaseModel, SRDistributed
+from .._switches import switch
 
 
 @MODEL_REGISTRY.register()
@@ -67,7 +67,7 @@ class SRModel(BaseModel):
         self.use_graph = bool(train_opt.get('cuda_graph', False))
         # weight gradients on a side stream during backward (train.async_wgrad, ops.conv.async_wgrad);
         # the environment variable SR_ASYNC_WGRAD=0/1 overrides the option (A/B)
-        env = os.environ.get('SR_ASYNC_WGRAD')
+        env = switch('SR_ASYNC_WGRAD')
         mode = train_opt.get('async_wgrad', False)
         self.async_wgrad = {'0': False, '1': True, 'reduce': 'reduce'}.get(env, mode if mode == 'reduce' else bool(mode))
         if self.async_wgrad and self.opt.get('dist', False) and env != '1':
@@ -81,7 +81,7 @@ class SRModel(BaseModel):
                 self.async_wgrad = False
         # blocks whose side-stream launches share one fork (train.async_wgrad_blocks, ops.conv.side_batch;
         # SR_SIDE_BATCH overrides); applied only inside this model's backward (async_wgrad(blocks=))
-        self.async_blocks = int(os.environ.get('SR_SIDE_BATCH', train_opt.get('async_wgrad_blocks', 1)))
+        self.async_blocks = int(switch('SR_SIDE_BATCH') or train_opt.get('async_wgrad_blocks', 1))
         self.ema_decay = train_opt.get('ema_decay', 0)
         if self.ema_decay > 0:
             self.net_g_ema = build_network(self.opt['network_g']).to(self.device)

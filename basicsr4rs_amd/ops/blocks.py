@@ -10,16 +10,16 @@ launches (implicit-GEMM convs with fused epilogues + the HBM kernels of csrc/blo
   no torch.cat copies); the two residual scalings of the last RDB fuse into its conv5 epilogue.
 * ``bilinear_up_add`` — MSRResNet ``out += F.interpolate(x, bilinear)`` (srresnet_arch.py:64-65).
 """
-import os
 
 import torch
 
 from .. import _lib
 from . import conv as C
+from .._switches import switch
 
 
 # SR_CA_UNFUSED=1: the round-2 channel-attention launches (A/B of the fused kernels, tools/ab_env.sh)
-_CA_UNFUSED = os.environ.get('SR_CA_UNFUSED', '0') == '1'
+_CA_UNFUSED = switch('SR_CA_UNFUSED') == '1'
 
 
 def _ws(nbytes, device):
@@ -60,7 +60,7 @@ def _colsum_ok(N, H, W, spec, dtype):
 # instead of their own pass (sr_channel_partials).  Measured slower on RCAN x4 (40.3 vs 37.7 ms, three
 # A/B rounds in one GPU call): the band kernel's 128 partial rows per image (vs the pass's few) make
 # ca_bwd_apply, which stages every partial row of its image per block, the slower kernel.
-_CA_DOT_FUSED = os.environ.get('SR_CA_DOT', '0') == '1'
+_CA_DOT_FUSED = switch('SR_CA_DOT') == '1'
 
 
 def _dot_parts_put(dx, parts, u):

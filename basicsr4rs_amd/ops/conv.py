@@ -16,12 +16,12 @@ import ctypes
 import weakref
 import math
 
-import os
 
 import torch
 
 from .. import _lib
 from ..utils import ktrace
+from .._switches import switch
 
 _PARAM_EPOCH = [0]  # bumped by optimizers that update parameters behind autograd's back
 
@@ -114,7 +114,7 @@ class async_wgrad:
 # k > 1 (async_wgrad(blocks=k), SR_SIDE_BATCH=k) forks once per k blocks (the queue is flushed at
 # the latest by the join).
 _SIDE_BATCH = []
-_SIDE = {'items': [], 'blocks': 0, 'k': max(0, int(os.environ.get('SR_SIDE_BATCH', '1')))}
+_SIDE = {'items': [], 'blocks': 0, 'k': max(0, int(switch('SR_SIDE_BATCH') or 1))}
 
 
 class side_batch:

@@ -23,7 +23,6 @@ Under ``torch.autocast('cuda')`` samples, columns and GEMMs run in bf16 (fp32 ac
 offsets, masks and all their gradients stay fp32.
 """
 import math
-import os
 
 import torch
 from torch import nn
@@ -35,6 +34,7 @@ from torch.nn.modules.utils import _pair, _single
 from .. import _lib
 from . import conv as C
 from .swin import LinearSpec
+from .._switches import switch
 
 __all__ = ['DeformConvFunction', 'ModulatedDeformConvFunction', 'deform_conv', 'modulated_deform_conv', 'DeformConv',
            'DeformConvPack', 'ModulatedDeformConv', 'ModulatedDeformConvPack', 'offset_conv', 'split_offset_mask']
@@ -162,7 +162,7 @@ def _dcn_forward(x, offset, mask, weight, bias, g, dtype, need_cols=True):
     return C.nhwc_to_nchw(y, g.cout), (xh, off, msk, cols)
 
 
-BWD_FUSED = os.environ.get('SR_DCN_BWD_FUSED') != '0'
+BWD_FUSED = switch('SR_DCN_BWD_FUSED') != '0'
 
 
 def bwd_fused_ok(g, dtype):

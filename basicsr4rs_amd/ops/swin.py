@@ -24,22 +24,21 @@ s = floor(keep + U[0,1)) / keep drawn per forward (archs/swinir_arch.py).  The f
 the proj / fc2 GEMM epilogues (sr_conv3x3_desc.row_scale); the backward scales the branch
 gradients once (sr_row_scale) and feeds them to both the dgrad and the wgrad.
 """
-import os
-
 import torch
 
 from .. import _lib
 from ..utils import ktrace
 from . import conv as C
+from .._switches import switch
 
 GELU = 3
 # SR_PARAM_REDUCE_MAIN=1 keeps the LayerNorm / attention-table gradient reduces on the main stream
 # under async_wgrad (A/B)
-_PARAM_REDUCE_SIDE = os.environ.get('SR_PARAM_REDUCE_MAIN') != '1'
+_PARAM_REDUCE_SIDE = switch('SR_PARAM_REDUCE_MAIN') != '1'
 # SR_ROWSCALE_UNFUSED=1: the proj-branch stochastic-depth gradient by a separate row-scale pass (A/B)
-_ROWSCALE_FUSED = os.environ.get('SR_ROWSCALE_UNFUSED') != '1'
+_ROWSCALE_FUSED = switch('SR_ROWSCALE_UNFUSED') != '1'
 # SR_SWIN_FUSED=0: the attention half of a block as three launches (LN+qkv, attention, proj) (A/B)
-_SWIN_FUSED = os.environ.get('SR_SWIN_FUSED') != '0'
+_SWIN_FUSED = switch('SR_SWIN_FUSED') != '0'
 
 
 class LinearSpec:
@@ -157,7 +156,7 @@ def linear_ln_fwd(x, weight, bias, Creal, wf, bg, spec, N, H, W, act=0, aux=None
     Cp = x.shape[-1]
     if x.dtype != torch.bfloat16 or Cp != spec.cin_p or spec.cin_p > 192 or spec.cout_p > 640:
         return None
-    unf = os.environ.get('SR_LN_UNFUSED')  # A/B: the standalone LayerNorm kernel + linear ('1': both
+    unf = switch('SR_LN_UNFUSED')  # A/B: the standalone LayerNorm kernel + linear ('1': both
     if unf == '1' or (unf == 'fc1' and aux is not None) or (unf == 'qkv' and aux is None):  # or one of them)
         return None
     M = N * H * W
@@ -390,7 +389,7 @@ def swin_mlp_fused(x, n2w, n2b, Creal, f1wf, f1bg, fc1s, f2wf, f2bg, s2, train):
     return out, ln2, m2, r2, z, h
 
 
-_STB_SIDE_BATCH = os.environ.get('SR_STB_SIDE_BATCH', '1') != '0'
+_STB_SIDE_BATCH = switch('SR_STB_SIDE_BATCH') != '0'
 
 
 class _STB(torch.autograd.Function):

@@ -31,13 +31,13 @@ order, which is what sharing one pool requires.  Every segment starts with one t
 two cuts with nothing launched between them (a conv's weight and bias in two buckets) never make an
 empty graph.
 """
-import os
 
 import torch
 
 from ..ops.conv import _ASYNC
+from .._switches import switch
 
-_TRACE = os.environ.get('SR_STEP_TRACE') or None
+_TRACE = switch('SR_STEP_TRACE') or None
 
 
 class _BeginBackward(torch.autograd.Function):
