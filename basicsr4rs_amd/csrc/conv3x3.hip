@@ -1745,8 +1745,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
 // row-permuted (tile c row r -> channel 8(r/4) + 4c + r%4), so each lane ends with 8
 // consecutive channels of one pixel and the fused epilogue stores 16 B from registers -- no
 // LDS staging round trip (which cost ~1/3 of the kernel at nf 64).
-template <int CO_T, int DBG = 0, bool W256 = false, bool DIRECT = false>
-__global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
+template <int CO_T, int DBG = 0, bool W256 = false, bool DIRECT = false, int HALF = 0>
+__global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   static_assert(!DIRECT || CO_T == 4, "direct epilogue: two co tiles per wave");
   constexpr int BN = CO_T * 16;
   constexpr int CSTR = BN + 4;
@@ -1756,7 +1756,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   constexpr int PT = 16 / WP;                    // 16-pixel tiles per wave
   // >= (R+2)*(W+2) rounded up to 8: 400 (W 64), 520 (W 128), 776 (W 256: HR-resolution conv_last)
   constexpr int HROWS = W256 ? 776 : 528;
-  constexpr int SMEM_H = HROWS * 128;
+  constexpr int SMEM_H = HROWS * (HALF ? 64 : 128);
   constexpr int SMEM_E = 128 * CSTR * 4;
   constexpr int SMEM = SMEM_H > SMEM_E ? SMEM_H : SMEM_E;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -1789,14 +1789,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
 #pragma unroll
     for (int c = 0; c < CW; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int lc = (lane & 7) ^ (lane >> 3);  // logical 16-B chunk of this lane's DMA slot
-  const int nch = (a.Cin + 63) >> 6;
-  const int ninstr = (HR + 7) >> 3;
+  const int lc8 = (lane & 7) ^ (lane >> 3);  // logical 16-B chunk of this lane's DMA slot
+  constexpr int CCH = HALF ? 32 : 64;        // channels per chunk
+  const int nch = (a.Cin + CCH - 1) / CCH;
+  const int ninstr = HALF ? (HR + 15) >> 4 : (HR + 7) >> 3;
   const int rps = a.in_ps > 0 ? a.in_ps : 1;
   for (int ch = 0; ch < nch; ++ch) {
-    const int ci0 = ch * 64;
+    const int ci0 = ch * CCH;
     if (ch) __syncthreads();  // every wave is done with the previous chunk's halo
-    const bool cv = ci0 + lc * 8 < a.Cin;
     // in_ps = r (pixel-shuffled input: the upsample convs' dgrads): LR channel sl * C' + c of LR pixel
     // (y, x) is channel c of HR pixel (y r + si, x r + sj); a 64-channel chunk lies in one slot
     int si = 0, sj = 0, cch0 = ci0;
@@ -1808,9 +1808,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
     }
     // the chunk's upper 32 channels exist (not for Cin 32: RRDB dense dgrads).  A runtime flag
     // even for Cin 64: measured 2-3 % faster on RCAN / RRDB than the constant-folded form
-    const bool khi = ci0 + 32 < a.Cin;
+    const bool khi = !HALF && ci0 + 32 < a.Cin;
     for (int k = w; k < ninstr; k += 4) {
-      const int hr = 8 * k + (lane >> 3);
+      // HALF: 64-B rows, 4 lanes per row, chunk swizzled by (row >> 2) & 3
+      const int hr = HALF ? 16 * k + (lane >> 2) : 8 * k + (lane >> 3);
+      const int lc = HALF ? (lane & 3) ^ ((hr >> 2) & 3) : lc8;
+      const bool cv = ci0 + lc * 8 < a.Cin;
       const int hy = hr / WPAD, hx = hr - hy * WPAD;
       const int yy = y0 - 1 + hy, xx = hx - 1;
       const bool v = cv && hr < HR && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
@@ -1855,7 +1858,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
           if (kk == 1 && !khi) continue;
 #pragma unroll
           for (int i = 0; i < PT; ++i) {
-            const u32x4 fa = *(const u32x4*)(smem + swz128(hb[i] + z + toff, kk * 4 + g));
+            const uint32_t hrow = hb[i] + z + toff;
+            const u32x4 fa = *(const u32x4*)(smem + (HALF ? hrow * 64u + ((g ^ ((hrow >> 2) & 3u)) << 4)
+                                                          : swz128(hrow, kk * 4 + g)));
 #pragma unroll
             for (int c = 0; c < CW; ++c) {
               if constexpr (DIRECT)
@@ -4277,6 +4282,8 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   const dim3 grid(a.tiles, a.tiles_n);
   if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
   else if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
+  else if (ct == 2 && a.in_ps == 0)
+    hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<2, 0, false, false, 3>), grid, dim3(256), 0, s, a);
   else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, grid, dim3(256), 0, s, a);
   else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);
   else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), grid, dim3(256), 0, s, a);

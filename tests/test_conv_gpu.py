@@ -616,6 +616,17 @@ def test_wgrad_rgb_head_reduce_vs_fp64(cuda, shape, variant):
     assert (db.cpu().double() - b.grad).abs().max().item() <= 1e-3 * b.grad.abs().max().item() + 1e-3
 
 
+def _same_or_ulp(a, b, exact):
+    """Bitwise equal, or (a different fp32 summation order before the bf16 store) within one bf16
+    rounding step of the larger magnitude plus 1e-3 of the tensor's range for cancelled values."""
+    if exact:
+        assert torch.equal(a, b)
+        return
+    a, b = a.float(), b.float()
+    tol = torch.maximum(a.abs(), b.abs()) * 2.0 ** -7 + 1e-3 * a.abs().max().item()
+    assert bool(((a - b).abs() <= tol).all()), (a - b).abs().max().item()
+
+
 @pytest.mark.parametrize('shape', [(16, 64, 64, 64, 64), (5, 13, 64, 64, 64), (1, 1, 64, 64, 64), (3, 2, 64, 32, 32),
                                    (2, 24, 128, 64, 32), (2, 9, 128, 32, 64), (4, 7, 64, 32, 64), (2, 9, 128, 32, 96),
                                    (3, 5, 128, 64, 192), (2, 6, 64, 32, 160)])
@@ -625,7 +636,8 @@ def test_wgrad_rgb_head_reduce_vs_fp64(cuda, shape, variant):
 def test_fwd_band_bitwise_equals_halo(cuda, shape, epi, grid):
     """Row-streaming narrow conv (conv3x3_fwd_band_kernel: persistent bands of image rows, 4-slot
     LDS row ring, epilogue operands staged by LDS-DMA) against the tile kernel it replaces
-    (variant 34) -- same K order, so bitwise equal -- on every epilogue the nets use, with bands
+    (variant 34) -- same K order, so bitwise equal (Cout <= 32: see _same_or_ulp) -- on every
+    epilogue the nets use, with bands
     of one row (variant 36: 256 blocks, one row each on small shapes) and long bands crossing image
     boundaries (variant 35: 64 blocks); colsum partial rows sum to the stored output's channel
     sums."""
@@ -683,9 +695,11 @@ def test_fwd_band_bitwise_equals_halo(cuda, shape, epi, grid):
         _lib.check(lib.sr_conv3x3_set_variant(0))
     torch.cuda.synchronize()
     (y0, e0), (y1, e1) = outs
-    assert torch.equal(y0, y1)
+    # the halo kernel's Cout <= 32 form sums K in 32-channel chunks (three blocks per CU), the band
+    # kernel in 64-channel ones: bitwise equal up to Cin 32, within one bf16 rounding step beyond
+    _same_or_ulp(y0, y1, exact=cout > 32 or cin <= 32)
     if epi == 'gelu_gate_aux':
-        assert torch.equal(e0, e1)
+        _same_or_ulp(e0, e1, exact=cout > 32 or cin <= 32)
     if epi == 'colsum':
         ref = y0.double().sum((1, 2))
         for parts in (e0, e1):
