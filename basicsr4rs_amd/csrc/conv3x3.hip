@@ -2046,8 +2046,13 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
   constexpr int WBYTES = CO * WROW;
   constexpr int RING = (S + 1) * SLOT + 4 * EPI;
   // ring + one all-zero slot (the rows above / below an image read it, so the MFMA sequence has
-  // no branches) + staging; the weight image is staged in the same space before the ring starts
-  __shared__ __attribute__((aligned(16))) char smem[RING > WBYTES ? RING : WBYTES];
+  // no branches) + staging; the weight image after them where both fit (WSEP: the ring prologue
+  // is issued before the weights are waited for; only forms built for one block per CU: the extra
+  // LDS would cost the W 64 forms their second block and RCAN 2.7 ms), else in the same space
+  // before the ring starts
+  constexpr bool WSEP = band_occ(W, E) == 1 && RING + WBYTES <= 160 * 1024;
+  __shared__ __attribute__((aligned(16))) char smem[WSEP ? RING + WBYTES : (RING > WBYTES ? RING : WBYTES)];
+  char* const wimg = smem + (WSEP ? RING : 0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = w % WC, wp = w / WC;
@@ -2074,7 +2079,7 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
   for (int p = w; p < WBYTES / 1024; p += 4) {
     const int e = p * 1024 + lane * 16;
     const int co = e / WROW, off = e - co * WROW;
-    glds16(wr, smem + p * 1024, (uint32_t)(co * a.ldw * 2 + off));
+    glds16(wr, wimg + p * 1024, (uint32_t)(co * a.ldw * 2 + off));
   }
   const int nn = wc * 32 + 8 * g;  // this lane's 8 output channels
   float bv[8];
@@ -2090,39 +2095,48 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
     const int ni = s0 / H + lane;
     rsv = ni < a.N ? a.alpha * a.row_scale[ni] : 0.f;
   }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
-  asm volatile("" ::"v"(rsv));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   u32x4 bw[9][2][2];
+  auto read_weights = [&]() {
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int co = wc * 32 + 8 * (c16 >> 2) + 4 * c + (c16 & 3);
-        bw[tap][kk][c] = kk < KH ? *(const u32x4*)(smem + co * WROW + (tap * CIN + kk * 32 + 8 * g) * 2)
-                                 : u32x4{0u, 0u, 0u, 0u};
-      }
-  // every fragment in registers (and the compiler knows it) before the ring overwrites the image
+        for (int c = 0; c < 2; ++c) {
+          const int co = wc * 32 + 8 * (c16 >> 2) + 4 * c + (c16 & 3);
+          bw[tap][kk][c] = kk < KH ? *(const u32x4*)(wimg + co * WROW + (tap * CIN + kk * 32 + 8 * g) * 2)
+                                   : u32x4{0u, 0u, 0u, 0u};
+        }
+    // every fragment in registers (and the compiler knows it) before the ring overwrites the image
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
+    for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int c = 0; c < 2; ++c) asm volatile("" ::"v"(bw[tap][kk][c]));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  // zero border columns (pixel rows 0 and W + 1) of every slot, and the zero slot S
-  for (int i = tid; i < S * 2 * 8; i += 256) {
-    const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
-    *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
+        for (int c = 0; c < 2; ++c) asm volatile("" ::"v"(bw[tap][kk][c]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto zero_borders = [&]() {  // pixel rows 0 and W + 1 of every slot, and the zero slot S
+    for (int i = tid; i < S * 2 * 8; i += 256) {
+      const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
+      *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
+    }
+    for (int i = tid; i < SLOT / 16; i += 256) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
+  };
+  if constexpr (!WSEP) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
+    asm volatile("" ::"v"(rsv));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    read_weights();
+    __syncthreads();
+    zero_borders();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    zero_borders();  // disjoint from the weight image and from the pixel rows the prologue DMAs
   }
-  for (int i = tid; i < SLOT / 16; i += 256) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
 #ifdef SR_BAND_STAMPS
   const unsigned long long t_loaded = __builtin_readcyclecounter();
 #endif
@@ -2171,6 +2185,17 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
   if (s0 < s1) {
     for (int q = s0 - 1; q < s0 + LA; ++q) issue_row(q);
     issue_staging(s0);
+  }
+  if constexpr (WSEP) {
+    // this wave's weight pieces landed (older than the (LA + 1) * PPW + NG prologue ops just
+    // issued), then every wave's; the zeros visible to every wave
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
+    asm volatile("" ::"v"(rsv));
+    vm_wait_dyn(s0 < s1 ? (LA + 1) * PPW + NG : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    read_weights();
   }
   const int n0 = s0 / H;
 
