@@ -2023,20 +2023,25 @@ SR_DEV void vm_wait_dyn(int n) { vm_wait_bs<0, 63>(n < 0 ? 0 : (n > 63 ? 63 : n)
 constexpr int band_occ(int W, int E) {
   return W == 64 && (E == 0 || E == 1 || E == 2 || E == 4 || E == 16 || E == 128) ? 2 : 1;
 }
-template <int CO, int W, int LA, int KH, int E>
-__global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(FwdArgs a) {
+// NWV: waves per block, 4 (one per SIMD) or 8 (two per SIMD, each with half the row's pixel
+// tiles, so one wave's epilogue and LDS waits overlap the other's MFMAs; the ring and the weight
+// image shared).  8 at W 128: RRDB 63.8 -> 61.0 ms; at W 64 (one pixel tile per wave) RCAN
+// 33.8 -> 37.0 ms, so 4 there.
+template <int CO, int W, int LA, int KH, int E, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3x3_fwd_band_kernel(FwdArgs a) {
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
   constexpr bool RES = (E & 16) != 0, RES2 = (E & 32) != 0, AUX = (E & 64) != 0, CS = (E & 128) != 0,
                  RSC = (E & 256) != 0, DOT = (E & 512) != 0;
   static_assert(!DOT || CS, "band: dot partials need colsum");
   constexpr int IR = GATE ? 1 : 0, IR2 = IR + (RES ? 1 : 0), ID = IR2 + (RES2 ? 1 : 0), NSTG = ID + (DOT ? 1 : 0);
+  static_assert(NWV == 4 || (NWV == 8 && W / 16 / (8 / (CO / 32)) >= 1), "band: a pixel tile per wave");
   constexpr int WC = CO / 32;       // waves along output channels (32 each = 2 co tiles)
-  constexpr int WP = 4 / WC;        // waves along the row's pixels
+  constexpr int WP = NWV / WC;      // waves along the row's pixels
   constexpr int PT = W / 16 / WP;   // 16-pixel tiles per wave
   constexpr int WPAD = W + 2;
   constexpr int SLOT = WPAD * 128;
   constexpr int S = LA + 2;         // ring slots: rows s-1 .. s+1 read, s+2 .. s+LA in flight
-  constexpr int PPW = W / 8 / 4;    // 1-KB DMA pieces per wave per row
+  constexpr int PPW = W / 8 / NWV;  // 1-KB DMA pieces per wave per row
   constexpr int NG = NSTG * PT;     // staging pieces per wave per row (gate / res / res2)
   constexpr int NC = (CS ? 2 : 0) + (AUX ? PT : 0);  // stores after the PT output stores
   constexpr int KROW = NG + PPW + PT + NC;            // vector memory ops per wave per row
@@ -2044,7 +2049,7 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
   constexpr int CIN = 32 * KH;
   constexpr int WROW = 9 * CIN * 2;  // bytes of one output channel's weights [tap][ci]
   constexpr int WBYTES = CO * WROW;
-  constexpr int RING = (S + 1) * SLOT + 4 * EPI;
+  constexpr int RING = (S + 1) * SLOT + NWV * EPI;
   // ring + one all-zero slot (the rows above / below an image read it, so the MFMA sequence has
   // no branches) + staging; the weight image after them where both fit (WSEP: the ring prologue
   // is issued before the weights are waited for; only forms built for one block per CU: the extra
@@ -2076,7 +2081,7 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
   // weights: one coalesced LDS-DMA image [co][tap][ci] (1 KB contiguous per wave instruction),
   // then each wave reads its MFMA fragments from it: co = wc*32 + 8*(c16>>2) + 4*c + (c16&3)
   // (DIRECT row permutation), K chunk kk*32 + 8*g of every tap
-  for (int p = w; p < WBYTES / 1024; p += 4) {
+  for (int p = w; p < WBYTES / 1024; p += NWV) {
     const int e = p * 1024 + lane * 16;
     const int co = e / WROW, off = e - co * WROW;
     glds16(wr, wimg + p * 1024, (uint32_t)(co * a.ldw * 2 + off));
@@ -2117,11 +2122,11 @@ __global__ __launch_bounds__(256, band_occ(W, E)) void conv3x3_fwd_band_kernel(F
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   auto zero_borders = [&]() {  // pixel rows 0 and W + 1 of every slot, and the zero slot S
-    for (int i = tid; i < S * 2 * 8; i += 256) {
+    for (int i = tid; i < S * 2 * 8; i += NWV * 64) {
       const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
       *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
     }
-    for (int i = tid; i < SLOT / 16; i += 256) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < SLOT / 16; i += NWV * 64) *(u32x4*)(smem + S * SLOT + i * 16) = u32x4{0u, 0u, 0u, 0u};
   };
   if constexpr (!WSEP) {
 #pragma unroll
@@ -4423,7 +4428,44 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
   *nt = k == FK_BIG ? 512 : 256;
 }
 
+// waves per band block: 8 at W 128, 4 at W 64 (variant 14: 4 everywhere, A/B).  With channel sums
+// at Cout 32, 4: the partial rows per image (H x pixel waves) then match the tile and halo
+// epilogues' (H W / 128 x 4), so the count does not depend on which of them a call lands on.
+int band_nwv(const FwdArgs& a) {
+  return a.W == 128 && g_variant != 14 && !(a.Cout == 32 && (a.colsum || a.dot)) ? 8 : 4;
+}
+hipError_t launch_band8(const FwdArgs& a, hipStream_t s) {
+  const int rows = a.N * a.H;
+  FwdArgs ab = a;
+  ab.stamps = g_stamps;
+  const int gmax = g_variant == 35 ? 64 : 256;
+  const dim3 grid(rows < gmax ? rows : gmax);
+  const int e = band_epi(a, grid.x);
+#define SR_BAND_E(CO_, W_, LA_, KH_, E_) \
+  case E_: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<CO_, W_, LA_, KH_, E_, 8>), grid, dim3(512), 0, s, ab); break;
+#define SR_BAND(CO_, W_, LA_, KH_) \
+  if (a.Cout == CO_ && a.W == W_ && a.Cin == 32 * KH_) { \
+switch (e) { \
+  SR_BAND_E(CO_, W_, LA_, KH_, 0) SR_BAND_E(CO_, W_, LA_, KH_, 1) SR_BAND_E(CO_, W_, LA_, KH_, 2) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 4) SR_BAND_E(CO_, W_, LA_, KH_, 16) SR_BAND_E(CO_, W_, LA_, KH_, 20) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 28) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 48) SR_BAND_E(CO_, W_, LA_, KH_, 72) SR_BAND_E(CO_, W_, LA_, KH_, 128) \
+  SR_BAND_E(CO_, W_, LA_, KH_, 304) \
+  default: return hipErrorInvalidValue; \
+} \
+return hipGetLastError(); \
+  }
+  if (e == 656) {  // instantiated for the RCAN shapes only
+    hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 2, 656, 8>), grid, dim3(512), 0, s, ab);
+    return hipGetLastError();
+  }
+  SR_BAND(64, 128, 3, 2) SR_BAND(64, 128, 3, 1) SR_BAND(32, 128, 4, 2) SR_BAND(32, 128, 4, 1)
+#undef SR_BAND
+#undef SR_BAND_E
+  return hipErrorInvalidValue;
+}
 hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
+  if (band_nwv(a) == 8) return launch_band8(a, s);
   // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64 blocks
   // (long bands: ring wrap-around and image crossings inside a band, for tests).  (Two bands per CU
   // for the band_occ forms measured faster alone but slower in the RCAN step beside the side-stream
@@ -4819,9 +4861,12 @@ FwdArgs fwd_shape(const sr_conv3x3_desc* d) {
 }
 
 // Partial rows per image of the colsum output, or 0 when the call cannot produce it.
-int colsum_parts(const sr_conv3x3_desc* d, const FwdArgs& a) {
+int colsum_parts(const sr_conv3x3_desc* d, const FwdArgs& a0) {
+  static float one;
+  FwdArgs a = a0;
+  a.colsum = &one;  // the kernel choice of a call that asks for the sums
   if (d->out_ps || d->out_nchw || fwd_kind(a, d->dtype == SR_BF16) == FK_LIN) return 0;
-  if (fwd_kind(a, d->dtype == SR_BF16) == FK_BAND) return d->H * (4 / (d->Cout / 32));  // rows x pixel waves
+  if (fwd_kind(a, d->dtype == SR_BF16) == FK_BAND) return d->H * (band_nwv(a) / (d->Cout / 32));  // rows x pixel waves
   int rows, nt;
   fwd_epi_geom(fwd_kind(a, d->dtype == SR_BF16), &rows, &nt);
   const int HW = d->H * d->W;
@@ -4972,7 +5017,7 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 // Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 13 && variant < 21) || variant > 75)
+  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 14 && variant < 21) || variant > 75)
     return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
   g_variant = variant;
   return SR_OK;
