@@ -133,8 +133,16 @@ class SRModel(BaseModel):
         if before_backward is not None:
             l_total = before_backward(l_total)
         # weight gradients on a side stream, joined here
-        with async_wgrad(self.async_wgrad, blocks=getattr(self, 'async_blocks', None)):
-            l_total.backward()
+        try:
+            with async_wgrad(self.async_wgrad, blocks=getattr(self, 'async_blocks', None)):
+                l_total.backward()
+        except BaseException:
+            # a failed backward leaves the DDP reducer mid-step (buckets issued, counts short):
+            # join and reset it so a caller that skips the batch can keep training
+            red = getattr(self.net_g, 'reducer', None)
+            if red is not None:
+                red.abandon_step()
+            raise
         # drop the autograd graph now: a graph kept alive by self.output would pin this step's
         # AccumulateGrad nodes (and their stream) into the next step / a HIP-graph capture
         self.output = self.output.detach()

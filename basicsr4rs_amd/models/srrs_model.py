@@ -52,8 +52,16 @@ class SRRSModel(SRModel):
             # drop this batch and its graph like the reference (srrs_model.py:68-77)
             del self.lq, self.gt, self.output
             return
-        with async_wgrad(self.async_wgrad, blocks=getattr(self, 'async_blocks', None)):
-            l_total.backward()
+        try:
+            with async_wgrad(self.async_wgrad, blocks=getattr(self, 'async_blocks', None)):
+                l_total.backward()
+        except BaseException:
+            # a failed backward leaves the DDP reducer mid-step (buckets issued, counts short):
+            # join and reset it so a caller that skips the batch can keep training
+            red = getattr(self.net_g, 'reducer', None)
+            if red is not None:
+                red.abandon_step()
+            raise
         self.sync_gradients()
         if hasattr(self.optimizer_g, 'fp') and self.ema_decay > 0 and self.flat_ema is not None:
             self.optimizer_g.step(ema=self.flat_ema, ema_decay=self.ema_decay)

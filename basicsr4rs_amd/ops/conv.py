@@ -94,7 +94,8 @@ class async_wgrad:
         if self.enabled:
             if exc_type is None:
                 side_flush_pending()  # launches still queued by side_batch fork before the join
-            else:  # backward failed: its queued gradient launches and callbacks are dropped
+            else:  # backward failed: its queued gradient launches and callbacks are dropped; a DDP
+                # reducer is then mid-step -- the models call GradBucketReducer.abandon_step()
                 _SIDE['items'], _SIDE['blocks'] = [], 0
             if self._prev_k is not None:
                 _SIDE['k'], self._prev_k = self._prev_k, None
@@ -733,10 +734,12 @@ class _ConvChain(torch.autograd.Function):
                 if up:
                     dx = nearest_up_backward(dx, spec.in_up, gate=xi if gated else None, slope=pslope)
                 d = dx
-            grads[2 * i], grads[2 * i + 1] = conv_wgrad_raw(dY, xi, N, H, W, spec.cin_p, spec.cin, spec.cout_p,
-                                                            spec.cout, scale=alpha, out_ps=spec.out_ps,
-                                                            need_bias=params[2 * i + 1] is not None,
-                                                            in_up=spec.in_up, params=(w, b))
+            # needs_input_grad: (x, specs, w0, b0, w1, b1, ...); a frozen conv pays no weight gradient
+            has_b = params[2 * i + 1] is not None
+            if ctx.needs_input_grad[2 + 2 * i] or (has_b and ctx.needs_input_grad[3 + 2 * i]):
+                grads[2 * i], grads[2 * i + 1] = conv_wgrad_raw(dY, xi, N, H, W, spec.cin_p, spec.cin, spec.cout_p,
+                                                                spec.cout, scale=alpha, out_ps=spec.out_ps,
+                                                                need_bias=has_b, in_up=spec.in_up, params=(w, b))
         return (d if ctx.needs_input_grad[0] else None, None, *grads)
 
 

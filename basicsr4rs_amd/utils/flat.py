@@ -233,6 +233,20 @@ class GradBucketReducer:
             self.pending = [sum(1 for i in idx if self.expected[i] > 0) for (_, _, idx) in self.buckets]
         self.handles = []
 
+    def abandon_step(self):
+        """Recover after a backward that raised: join the bucket reductions this step already
+        issued and reset the per-step contribution counts, so the next step starts clean (without
+        it the next step's counts run past the learned ones and raise, or a bucket never completes).
+        ``ops.conv.async_wgrad`` drops the failed backward's queued side-stream launches and their
+        gradient-ready callbacks, so the counts of such a step are short.  The failed step's
+        gradients are partial: zero them before the next step.  As with DDP, every rank must abandon
+        the same step (a step that fails on one rank only leaves the collectives unmatched).  The
+        models call this when their backward raises (SRModel._step_body)."""
+        for h in self.handles:
+            h.wait()
+        self.issue_log = []
+        self.reset()
+
     def all_reduce_bucket(self, b):
         """Launch the async all-reduce of bucket b on the current stream's order (or from the
         side stream while weight gradients run there)."""

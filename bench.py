@@ -10,8 +10,11 @@ Run: python bench.py --gpus N --steps K --warmup W.  N > 1 runs one rank per GPU
 torch.distributed.run as launched by the driver, or -- started plainly -- bench.py itself starts
 torch.distributed.run with N ranks as a child process before touching the GPU.  A WORLD_SIZE from a
 launcher that disagrees with --gpus is an error.
-`--workload` selects another BASELINE.json config in the same HR-pixels/s unit (rcan = C3,
-swinir = C4, rrdb = C5); the default (edsr = C2) is the north-star line.
+A plain N = 1 run (no --workload) is a suite: the EDSR_Lx4 headline (C2) plus one sub-record per
+other BASELINE config in the same HR-pixels/s unit (rcan = C3, swinir = C4, rrdb = C5), each
+measured in its own child process by `bench.py --workload X` (run_suite; the parent never touches
+the GPU).  `--workload X` measures one workload in this process; `--lr-px 256` is the SURVEY §8
+secondary sweep (LR 256 -> HR 1024).
 Prints ONE JSON line on rank 0 with the roofline of the dominant kernel (HIP events on an
 untimed warm-up step; bound chosen from its arithmetic intensity against the 312 FLOP/B
 ridge), the CPU baseline (oracle restatement of the same workload's train step on the host
@@ -48,16 +51,29 @@ SWINIR_M = dict(type='SwinIR', upscale=4, in_chans=3, img_size=64, window_size=8
 RRDB_X4 = dict(type='RRDBNet', num_in_ch=3, num_out_ch=3, num_feat=64, num_block=23, num_grow_ch=32, scale=4)
 
 # workload -> (network, model_type, lr, per-GPU batch, LR tile, train FLOPs per HR pixel, label)
+# (the FLOPs per HR pixel do not depend on the tile: convs and linears are per pixel, window attention
+# per token with a fixed window)
 WORKLOADS = {
     'edsr': (EDSR_L, 'SRModel', 1e-4, 32, 64, 18.85e6,
-             'EDSR_Lx4 train step (32 RB, nf 256, res_scale 0.1), LR 64x64 -> HR 256x256'),
+             'EDSR_Lx4 train step (32 RB, nf 256, res_scale 0.1)'),
     'rcan': (RCAN_X4, 'SRModel', 1e-4, 32, 64, 5.97e6,
-             'RCAN x4 train step (10 groups x 20 RCAB, nf 64, squeeze 16), LR 64x64 -> HR 256x256'),
+             'RCAN x4 train step (10 groups x 20 RCAB, nf 64, squeeze 16)'),
     'swinir': (SWINIR_M, 'SwinIRModel', 2e-4, 32, 64, 4.90e6,
-               'SwinIR-M x4 classical-SR train step (embed 180, 6x6 STB, 6 heads, window 8), LR 64x64 -> HR 256x256'),
+               'SwinIR-M x4 classical-SR train step (embed 180, 6x6 STB, 6 heads, window 8)'),
     'rrdb': (RRDB_X4, 'SRModel', 1e-4, 16, 128, 6.72e6,
-             'RRDBNet x4 train step (nf 64, gc 32, 23 RRDB), LR 128x128 -> HR 512x512 (remote-sensing tile)'),
+             'RRDBNet x4 train step (nf 64, gc 32, 23 RRDB)'),
 }
+# BASELINE.json config each workload line is quoted on
+BASELINE_CONFIG = {'edsr': 'configs[1]', 'rcan': 'configs[2]', 'swinir': 'configs[3]', 'rrdb': 'configs[4]'}
+# the workloads a plain `python bench.py` (N = 1) reports beside the EDSR headline, one child process each
+SUB_WORKLOADS = ('rcan', 'swinir', 'rrdb')
+
+
+def workload_label(workload, lr_px):
+    tile = f'LR {lr_px}x{lr_px} -> HR {4 * lr_px}x{4 * lr_px}'
+    if workload == 'rrdb' and lr_px == 128:
+        tile += ' (remote-sensing tile)'
+    return f'{WORKLOADS[workload][6]}, {tile}'
 
 
 # train.async_wgrad per workload (weight gradients on a side stream, ops.conv.async_wgrad), from A/B
@@ -151,7 +167,7 @@ def _cpu_threads():
     return usable, f'all {usable} usable CPUs (affinity mask; {os.cpu_count()} logical)'
 
 
-def cpu_baseline(workload, seconds=20.0):
+def cpu_baseline(workload, seconds=20.0, lr_px=None):
     """The oracle train step of ``workload`` (fwd + L1 + bwd + torch Adam) in torch-CPU fp32 at
     batch 1 on the host's cores: ONE image of the benchmarked tile, timed as the median of as
     many steps as fit in ~``seconds`` (at least 1 after a warm-up).  SwinIR runs eval-mode
@@ -162,7 +178,8 @@ def cpu_baseline(workload, seconds=20.0):
     nthr, why = _cpu_threads()
     prev_thr = torch.get_num_threads()
     torch.set_num_threads(nthr)
-    net_cfg, _, lr, _, lr_px = WORKLOADS[workload][:5]
+    net_cfg, _, lr, _, lr_def = WORKLOADS[workload][:5]
+    lr_px = lr_px or lr_def
     torch.manual_seed(42)
     net = build_network(dict(net_cfg))
     params = {k: v.detach().clone().requires_grad_(v.is_floating_point()) for k, v in net.state_dict().items()}
@@ -383,9 +400,10 @@ def spawn_ranks(n, argv):
     return subprocess.call(cmd, env=env)
 
 
-def _config(workload, B, world, use_graph, async_wgrad):
+def _config(workload, B, world, use_graph, async_wgrad, lr_px):
     wl = WORKLOADS[workload]
-    return {'workload': wl[6], 'global_batch': B * world, 'per_gpu_batch': B, 'seq_len': None,
+    return {'workload': workload_label(workload, lr_px), 'baseline_config': BASELINE_CONFIG[workload],
+            'global_batch': B * world, 'per_gpu_batch': B, 'lr_tile': lr_px, 'seq_len': None,
             'parallelism': f'dp{world}', 'model': wl[0]['type'], 'hip_graph': use_graph,
             'async_wgrad': bool(async_wgrad)}
 
@@ -412,12 +430,92 @@ def dry_run(args, world, rank):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(json.dumps({'metric': BASELINE_METRIC, 'value': None, 'unit': 'HR-pixels/s', 'n_gpus': world,
-                          'steps': args.steps, 'warmup': args.warmup, 'dry_run': True, 'ranks_seen': world,
-                          'max_rank_s': t.item(), 'config': _config(args.workload, B, world, use_graph,
-                                                                     opt['train']['async_wgrad'])}))
+                          'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': None, 'dry_run': True,
+                          'ranks_seen': world, 'max_rank_s': t.item(),
+                          'config': _config(args.workload, B, world, use_graph, opt['train']['async_wgrad'],
+                                            args.lr_px or WORKLOADS[args.workload][4]),
+                          'roofline': None, 'cpu_baseline': None, 'parity': None}))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _compact(line):
+    """The per-workload summary a suite line carries (kept short: the driver's record keeps the
+    last 2000 characters of stdout, so the four summaries sit at the end of the one line)."""
+    if line is None:
+        return None
+    roof, cpu, par, sw = line.get('roofline'), line.get('cpu_baseline'), line.get('parity'), \
+        line.get('swin_fused_attention')
+    out = {'config': (line.get('config') or {}).get('baseline_config'), 'B': (line.get('config') or {}).get('per_gpu_batch'),
+           'lr': (line.get('config') or {}).get('lr_tile'), 'ms_per_step': line.get('ms_per_step'),
+           'value': line.get('value'), 'model_tflops': line.get('model_tflops')}
+    if roof:
+        out['roofline'] = {k: roof.get(k) for k in ('kernel', 'bound', 'achieved', 'peak', 'unit', 'frac', 'traffic')}
+    else:
+        out['roofline'] = None
+    out['cpu_baseline'] = {k: cpu.get(k) for k in ('value', 'cores', 'kind')} if cpu else None
+    out['parity'] = {'max_abs_fp32': par.get('max_abs_fp32'), 'psnr_bf16_db': par.get('psnr_bf16_db')} if par else None
+    if sw:
+        out['swin_attn_frac'] = {k: sw[k]['frac_mfma_peak'] for k in ('attention_train', 'attention_inference', 'mlp_train')
+                                 if k in sw}
+    return out
+
+
+def run_suite(args):
+    """A plain ``python bench.py`` at N = 1: the EDSR headline and one sub-record per other BASELINE
+    workload (SUB_WORKLOADS), each measured by ``bench.py --workload X`` in a CHILD process with the
+    same --steps / --warmup.  This process never touches the GPU (it only starts the children, one
+    after another, and merges their JSON lines), so every child starts on an idle, freshly
+    initialised device.  The printed line is the headline child's line unchanged (value, timing,
+    roofline, cpu_baseline of EDSR_Lx4 B 32), plus ``workloads``: a compact summary of all four
+    (ms/step, HR-px/s, the dominant kernel's roofline, cpu_baseline, parity; SwinIR's fused-attention
+    MFMA fractions) and ``sub_records``: each child's full line.  Exit status: the headline child's;
+    a failed sub-workload is recorded in its entry (``rc``) and on stderr."""
+    import subprocess
+    base = [sys.executable, os.path.abspath(__file__), '--gpus', '1', '--steps', str(args.steps),
+            '--warmup', str(args.warmup), '--graph', str(args.graph)]
+    for flag in ('no_cpu_baseline', 'no_trace', 'no_parity', 'ddp', 'dry_run'):
+        if getattr(args, flag):
+            base.append('--' + flag.replace('_', '-'))
+    if args.batch:
+        base += ['--batch', str(args.batch)]
+    if args.lr_px:
+        base += ['--lr-px', str(args.lr_px)]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    lines, rcs, walls = {}, {}, {}
+    for wl in ('edsr',) + tuple(w for w in args.sub_workloads.split(',') if w):
+        cmd = base + ['--workload', wl, '--cpu-seconds', str(args.cpu_seconds if wl == 'edsr' else args.sub_cpu_seconds)]
+        t0 = time.time()
+        try:
+            p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True, timeout=args.child_timeout)
+            rc, out = p.returncode, p.stdout
+        except subprocess.TimeoutExpired as e:
+            rc, out = 124, (e.stdout.decode() if isinstance(e.stdout, bytes) else (e.stdout or ''))
+        walls[wl] = round(time.time() - t0, 1)
+        js = [ln for ln in out.splitlines() if ln.startswith('{')]
+        for ln in out.splitlines():  # the child's other stdout (none expected) stays visible
+            if not ln.startswith('{'):
+                print(ln, file=sys.stderr)
+        lines[wl] = json.loads(js[-1]) if js else None
+        rcs[wl] = rc
+        if rc != 0:
+            print(f'bench: workload {wl} exited {rc}', file=sys.stderr)
+        print(f'bench: {wl} done in {walls[wl]} s (rc {rc})', file=sys.stderr, flush=True)
+        if wl == 'edsr' and lines[wl] is None:
+            return rc or 1
+    line = dict(lines['edsr'])
+    line['suite'] = {'parent_touches_gpu': False, 'child_wall_s': walls,
+                     'note': 'each workload measured by `bench.py --workload X` in its own child process'}
+    line['sub_records'] = {wl: lines[wl] for wl in lines if wl != 'edsr'}
+    line['workloads'] = {}
+    for wl in lines:
+        c = _compact(lines[wl]) or {'error': 'no JSON line'}
+        c['rc'] = rcs[wl]
+        line['workloads'][wl] = c
+    print(json.dumps(line), flush=True)
+    return rcs['edsr']
 
 
 def main():
@@ -426,7 +524,16 @@ def main():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=0, help='per-GPU batch (0: the workload default)')
-    ap.add_argument('--workload', default='edsr', choices=sorted(WORKLOADS))
+    ap.add_argument('--workload', default=None, choices=sorted(WORKLOADS),
+                    help='measure one workload in this process (default: the EDSR headline, plus the '
+                         '--sub-workloads as sub-records at N = 1, each in a child process)')
+    ap.add_argument('--sub-workloads', default=','.join(SUB_WORKLOADS),
+                    help='comma list reported beside the headline when --workload is not given at N = 1 ("" none)')
+    ap.add_argument('--lr-px', type=int, default=0,
+                    help='LR tile side (0: the workload default, 64; RRDB 128); HR = 4x (SURVEY §8 sweep: 256)')
+    ap.add_argument('--cpu-seconds', type=float, default=20.0, help='CPU-baseline sample budget (s)')
+    ap.add_argument('--sub-cpu-seconds', type=float, default=12.0, help='the same for each sub-workload (s)')
+    ap.add_argument('--child-timeout', type=float, default=900.0, help='per-workload child time limit (s)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-trace', action='store_true')
     ap.add_argument('--no-parity', action='store_true')
@@ -451,6 +558,10 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.workload is None:
+        if env_world is None and args.sub_workloads:
+            sys.exit(run_suite(args))  # N = 1, plain start: headline + sub-records in child processes
+        args.workload = 'edsr'
     if args.dry_run:
         return dry_run(args, world, rank)
     ddp = world > 1 or args.ddp
@@ -476,7 +587,7 @@ def main():
     torch.manual_seed(42)
     wl = WORKLOADS[args.workload]
     B = args.batch or wl[3]
-    lr_px = wl[4]
+    lr_px = args.lr_px or wl[4]
     hr_px_tile = (4 * lr_px) ** 2
     # the step as HIP-graph replay (one graph; under DDP a chain of graphs cut at the gradient
     # buckets, utils/step_graph.py), except single-process SwinIR whose eager step is faster
@@ -552,14 +663,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_parity:
         parity = parity_check(args.workload, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.workload)
+        cpu = cpu_baseline(args.workload, args.cpu_seconds, lr_px)
     if rank == 0:
         line = {
             'metric': BASELINE_METRIC, 'value': round(value, 1), 'unit': 'HR-pixels/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16',
             'data': 'synthetic U[0,1) LR/GT tiles resident in HBM, random-init weights',
-            'config': _config(args.workload, B, world, use_graph, opt['train']['async_wgrad']),
+            'config': _config(args.workload, B, world, use_graph, opt['train']['async_wgrad'], lr_px),
             'train_flops_per_hr_px': wl[5], 'model_tflops': round(wl[5] * value / 1e12, 1),
             'last_loss': loss, 'cuda_graph': use_graph, 'roofline': roof, 'cpu_baseline': cpu, 'parity': parity,
             'swin_fused_attention': swin_att,

@@ -37,7 +37,7 @@ def test_bench_gpus2_spawns_two_ranks():
 
 
 def test_bench_gpus1_single_process():
-    p = _run(['--dry-run', '--steps', '2'])
+    p = _run(['--dry-run', '--steps', '2', '--workload', 'edsr'])
     assert p.returncode == 0, p.stderr[-3000:]
     d = _line(p)
     assert d['n_gpus'] == 1 and d['config']['parallelism'] == 'dp1'
@@ -60,3 +60,32 @@ def test_pmc_traffic_record_per_dominant_kernel():
         rec = bench._pmc_traffic(wl, kernel)
         assert rec is not None and rec['bench_kernel'] == kernel and rec['hbm_bytes_per_launch'] > 0, (wl, kernel)
     assert bench._pmc_traffic('edsr', 'linear_wk_kernel') is None  # another workload's record never answers
+
+
+def test_bench_suite_sub_records_per_workload():
+    """A plain N = 1 run measures the EDSR headline and RCAN / SwinIR / RRDB each in a child
+    process (the parent never touches the GPU) and prints ONE line: the headline's fields, then
+    ``workloads`` as the last key (the driver keeps the tail of stdout) with one compact record per
+    BASELINE config."""
+    p = _run(['--dry-run', '--steps', '2'])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p)
+    assert d['config']['model'] == 'EDSR' and d['config']['baseline_config'] == 'configs[1]'
+    assert d['suite']['parent_touches_gpu'] is False
+    assert list(d)[-1] == 'workloads'
+    assert list(d['workloads']) == ['edsr', 'rcan', 'swinir', 'rrdb']
+    cfg = {wl: r['config'] for wl, r in d['workloads'].items()}
+    assert cfg == {'edsr': 'configs[1]', 'rcan': 'configs[2]', 'swinir': 'configs[3]', 'rrdb': 'configs[4]'}
+    for wl, r in d['workloads'].items():
+        assert r['rc'] == 0 and 'roofline' in r and 'cpu_baseline' in r and 'parity' in r, (wl, r)
+    assert set(d['sub_records']) == {'rcan', 'swinir', 'rrdb'}
+    assert d['sub_records']['rrdb']['config']['per_gpu_batch'] == 16
+
+
+def test_bench_lr_px_sweep_label():
+    """--lr-px (SURVEY §8 secondary sweep, LR 256 -> HR 1024) changes the tile in the label."""
+    p = _run(['--dry-run', '--steps', '1', '--workload', 'swinir', '--lr-px', '256', '--batch', '2'])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p)
+    assert d['config']['lr_tile'] == 256 and 'LR 256x256 -> HR 1024x1024' in d['config']['workload']
+    assert d['config']['per_gpu_batch'] == 2

@@ -711,6 +711,41 @@ def test_fwd_band_bitwise_equals_halo(cuda, shape, epi, grid):
         assert y0[..., :16].abs().max().item() == 0 and y0[..., 16 + cout:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize('cin', [64, 96, 128, 160, 192])
+@pytest.mark.parametrize('act', [0, 1])
+def test_fwd_halo_cout32_vs_fp64(cuda, cin, act):
+    """The halo kernel's Cout-32 form (32-channel K chunks in 64-B halo rows, three blocks per CU;
+    the RRDB dense convs 2-5 -> 32) against float64 on the same bf16 operands: relative L2 within
+    bf16 output rounding (<= 4e-3) and every element within two bf16 steps plus 1e-3 of the range --
+    a dropped chunk or a wrong chunk swizzle moves whole channels by O(1)."""
+    N, H, W, cout = 3, 20, 128, 32
+    torch.manual_seed(12)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    wf, _, bg = C.prepared(conv.weight, conv.bias, C.ConvSpec(cin, cout), dt)
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    kw = dict(act=_lib.ACT_LRELU, slope=0.2) if act else {}
+    try:
+        _lib.check(lib.sr_conv3x3_set_variant(34))
+        name = lib.sr_conv3x3_fwd_kernel_name(C._desc(dt, N, H, W, cin, cin, cout, cout, cout)).decode()
+        assert name == 'conv3x3_fwd_halo_kernel', name
+        y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+        C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, **kw)
+        torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double().cpu(), bf(conv.weight.detach().cpu()).double(),
+                   conv.bias.detach().cpu().double(), padding=1)
+    if act:
+        ref = F.leaky_relu(ref, 0.2)
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel <= 4e-3, rel
+    tol = ref.abs() * 2.0 ** -7 + 1e-3 * ref.abs().max().item()
+    assert bool(((got - ref).abs() <= tol).all()), (got - ref).abs().max().item()
+
+
 @pytest.mark.parametrize('shape', [(2, 4, 64, 1024, 256, 2), (1, 2, 128, 1024, 256, 2), (1, 4, 64, 2304, 256, 3)])
 def test_fwd_pph_pixel_shuffled_input(cuda, shape):
     """The halo-row kernel reading a pixel-shuffled input (in_ps: the upsample convs' dgrads read

@@ -237,3 +237,66 @@ def test_reducer_relearns_after_unfreeze():
         red.remove()
     finally:
         dist.destroy_process_group()
+
+
+class _FailOnce(torch.autograd.Function):
+    """Identity whose backward raises while ``armed`` (a backward that fails mid-way)."""
+    armed = [False]
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if _FailOnce.armed[0]:
+            raise RuntimeError('injected backward failure')
+        return g
+
+
+def test_reducer_abandon_step_after_failed_backward():
+    """A backward that raises after some buckets went out (the last conv's gradient is complete
+    before the failure) leaves the reducer mid-step; ``abandon_step`` joins and resets it, and the
+    next step reduces every bucket during backward to the right gradient.  Without it the next
+    step's counts run past the learned ones and raise.  World 1 over gloo (one process)."""
+    port = _free_port()
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        c1, c2 = torch.nn.Conv2d(3, 8, 3, padding=1), torch.nn.Conv2d(8, 3, 3, padding=1)
+        net = torch.nn.ModuleList([c1, c2])
+        flat = FlatParams(net)
+        red = GradBucketReducer(flat, bucket_mb=0.0005)
+        x = torch.randn(2, 3, 8, 8)
+
+        def loss():
+            return c2(_FailOnce.apply(torch.relu(c1(x)))).square().mean()
+
+        def step(fail=False):
+            flat.zero_grad()
+            _FailOnce.armed[0] = fail
+            try:
+                loss().backward()
+            finally:
+                _FailOnce.armed[0] = False
+
+        step()
+        red.wait()  # learning step
+        ref = flat.grad.clone()
+        with pytest.raises(RuntimeError, match='injected'):
+            step(fail=True)
+        assert any(when == 'backward' for _, when in red.issue_log)  # c2's bucket already went out
+        red.abandon_step()
+        step()
+        red.wait()
+        assert all(when == 'backward' for _, when in red.last_issue_log), red.last_issue_log
+        assert torch.equal(flat.grad, ref)
+        # without abandon_step the step after a failure over-counts c2's contributions
+        with pytest.raises(RuntimeError, match='injected'):
+            step(fail=True)
+        with pytest.raises(RuntimeError, match='more than'):
+            step()
+    finally:
+        dist.destroy_process_group()

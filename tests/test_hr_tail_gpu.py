@@ -114,6 +114,54 @@ def test_hr_tail_chain_vs_fp64_512(cuda):
     assert exact['y'] <= 5e-3 and max(exact.values()) <= 8e-2, exact
 
 
+def test_hr_tail_chain_fp32_vs_fp64(cuda):
+    """The chain in the fp32 parity path (no autocast: exact-f32 MFMA convs, fp32 maps): the fp32
+    branches of the gated nearest-upsample backward and of the gated dgrad epilogue against the
+    exact float64 reference, output and every gradient within 1e-4 relative L2."""
+    convs = _tail(5)
+    torch.manual_seed(6)
+    feat = torch.randn(2, 24, 40, NF, device='cuda')
+    g = torch.randn(2, 3, 96, 160, device='cuda')
+    y, dx, grads = _run(convs, feat, g, chain=True)
+    assert dx.dtype == torch.float32
+    errs = _errs(y, dx, grads, _reference(convs, feat, g, False))
+    print('fp32 chain rel L2 vs fp64:', {k: f'{v:.2e}' for k, v in errs.items()})
+    assert max(errs.values()) <= 1e-4, errs
+
+
+def test_hr_tail_chain_frozen_convs_skip_wgrad(cuda):
+    """A frozen conv in the chain (requires_grad False) gets no weight-gradient launch: its .grad
+    stays None while the trainable convs' gradients equal the all-trainable run."""
+    from basicsr4rs_amd.utils import ktrace
+    convs = _tail(7)
+    torch.manual_seed(8)
+    feat = torch.randn(1, 16, 16, NF, device='cuda').to(torch.bfloat16)
+    g = torch.randn(1, 3, 64, 64, device='cuda')
+    _, dx_all, g_all = _run(convs, feat, g, chain=True)
+    for c in convs[:2]:
+        c.weight.requires_grad_(False)
+        c.bias.requires_grad_(False)
+    try:
+        for c in convs:
+            c.weight.grad = c.bias.grad = None
+        x = feat.clone().requires_grad_(True)
+        y = C.conv_chain(x, tuple(convs), KWS)
+        ktrace.start()
+        y.backward(g)
+        stats = ktrace.stop()
+        torch.cuda.synchronize()
+    finally:
+        for c in convs[:2]:
+            c.weight.requires_grad_(True)
+            c.bias.requires_grad_(True)
+    assert convs[0].weight.grad is None and convs[1].bias.grad is None
+    wg = sum(v['count'] for k, v in stats.items() if 'wgrad' in k)
+    assert wg == 2, stats  # the two trainable convs' weight gradients only
+    assert torch.equal(x.grad, dx_all)
+    for i in (2, 3):
+        assert torch.equal(convs[i].weight.grad, g_all[i][0]) and torch.equal(convs[i].bias.grad, g_all[i][1])
+
+
 def test_hr_tail_chain_matches_per_conv_path(cuda):
     convs = _tail(2)
     torch.manual_seed(3)

@@ -182,7 +182,7 @@ _NETS = {
 }
 
 
-@pytest.mark.parametrize('net', ['rcan', 'swinir', 'edsr'])
+@pytest.mark.parametrize('net', ['rcan', 'swinir', 'edsr', 'rrdb'])
 def test_async_wgrad_delayed_side_stream_bitwise(cuda, net):
     """The side stream held back by a spin kernel queued ahead of each backward: the main stream then
     runs the whole dgrad chain, including autograd's accumulation of a residual's two gradient
