@@ -444,20 +444,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 // ------------------------------------------------------------------------------------
 constexpr int BIG_STAGE = 65536;
 
-// One buffer_load_dwordx4 ... lds per call, exactly (inline asm: hipcc cannot split it into
-// exec-divergent copies, which would break the hand-counted vmcnt).  M0 is written and
-// restored inside the statement (cdna_hip_programming.md §5.7).  `lds` must be wave-uniform.
-SR_DEV void glds16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
-  const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(off), "s"(__builtin_amdgcn_readfirstlane(dst)), "s"(r)
-      : "memory");
-}
-
 __global__ __launch_bounds__(512) void conv3x3_fwd_big_kernel(FwdArgs a) {
   constexpr int MI = 8, NI = 4;
   constexpr int CSTR = 256 + 4;
