@@ -24,7 +24,6 @@ namespace {
 // set by sr_conv3x3_set_variant (tests / A-B timing): 0 auto (phase-interleaved 256x256),
 // 1 never a 256x256 kernel, 2 the two-barrier 256x256 kernel (previous schedule)
 int g_variant = 0;
-unsigned long long* g_stamps = nullptr;
 #define g_disable_big (g_variant == 1)
 
 struct FwdArgs {
@@ -4423,7 +4422,7 @@ int band_nwv(const FwdArgs& a) {
 hipError_t launch_band8(const FwdArgs& a, hipStream_t s) {
   const int rows = a.N * a.H;
   FwdArgs ab = a;
-  ab.stamps = g_stamps;
+  ab.stamps = g_sr_stamps;
   const int gmax = g_variant == 35 ? 64 : 256;
   const dim3 grid(rows < gmax ? rows : gmax);
   const int e = band_epi(a, grid.x);
@@ -4459,7 +4458,7 @@ hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
   const int rows = a.N * a.H;
   const int gmax = g_variant == 35 ? 64 : 256;
   FwdArgs ab = a;
-  ab.stamps = g_stamps;
+  ab.stamps = g_sr_stamps;
   const dim3 grid(rows < gmax ? rows : gmax);
   const int e = band_epi(a, grid.x);
   if (e == 656) {  // instantiated for the RCAN shapes only
@@ -5015,7 +5014,7 @@ int sr_conv3x3_get_variant(void) { return g_variant; }
 // end, rows, cycles summed over rows in the row wait / barrier / MFMA / epilogue phases, then
 // LDS zeroed, weight loads issued) into buf while it is set; null turns it off.
 int sr_conv3x3_set_stamps(void* buf) {
-  g_stamps = (unsigned long long*)buf;
+  g_sr_stamps = (unsigned long long*)buf;
   return SR_OK;
 }
 
@@ -5128,7 +5127,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
   a.fd_cps = make_fastdiv(cps);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  a.stamps = g_stamps;
+  a.stamps = g_sr_stamps;
   if (wg_use_halo(d)) {
     a.tiles_co = ring_tiles_co(d);
     a.tiles_ci = (a.Cin + 63) / 64;

@@ -7,6 +7,7 @@
 #include "sr_internal.h"
 
 static thread_local char g_err[512] = "";
+unsigned long long* g_sr_stamps = nullptr;
 
 int sr_fail(int code, const char* msg) {
   snprintf(g_err, sizeof(g_err), "%s", msg);

@@ -27,3 +27,5 @@ enum SrKnob {
   K_COUNT
 };
 int sr_knob(SrKnob k);
+// diagnostics buffer of per-block clock stamps (sr_conv3x3_set_stamps; null = off)
+extern unsigned long long* g_sr_stamps;

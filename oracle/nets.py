@@ -25,24 +25,83 @@ import torch.nn.functional as F
 # HIP bf16 path stores between kernels (a conv's activated output, a fused residual result) is
 # rounded to bf16 and widened again, so the oracle shows the error budget of bf16 activations
 # alone.  Off by default: the oracle is the exact restatement.
+# ``bf16_storage(grads=True)`` also rounds the gradient of every stored tensor (the HIP backward's
+# bf16 gradient maps), plus the two rounding points of the attention MFMAs: the probabilities P
+# (forward only: the engine packs them to bf16 for the AV product; dP stays fp32) and the score
+# gradient dS (backward only); and the MLP's pre-activation gradient dz (the fc2 dgrad's gated
+# output) while h = GELU(z) is rounded forward only.
 _STORE_DTYPE = [None]
+_STORE_GRADS = [False]
 
 
 class bf16_storage:
+    def __init__(self, grads=False):
+        self.grads = grads
+
     def __enter__(self):
-        self._prev = _STORE_DTYPE[0]
+        self._prev = (_STORE_DTYPE[0], _STORE_GRADS[0])
         _STORE_DTYPE[0] = torch.bfloat16
+        _STORE_GRADS[0] = self.grads
         return self
 
     def __exit__(self, *exc):
-        _STORE_DTYPE[0] = self._prev
+        _STORE_DTYPE[0], _STORE_GRADS[0] = self._prev
         return False
+
+
+def _round(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _RoundFB(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t):
+        return _round(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _round(g)
+
+
+class _RoundB(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t):
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _round(g)
+
+
+class _RoundF(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, t):
+        return _round(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
 
 
 def store(t):
     """A tensor written to HBM between kernels: identity unless bf16_storage() is active."""
-    dt = _STORE_DTYPE[0]
-    return t if dt is None else t.to(dt).to(t.dtype)
+    if _STORE_DTYPE[0] is None:
+        return t
+    if _STORE_GRADS[0] and t.requires_grad:
+        return _RoundFB.apply(t)
+    return _round(t)
+
+
+def store_fwd(t):
+    """Rounded forward only (a bf16 MFMA operand whose gradient stays fp32)."""
+    if _STORE_DTYPE[0] is None:
+        return t
+    return _RoundF.apply(t) if (_STORE_GRADS[0] and t.requires_grad) else _round(t)
+
+
+def store_grad(t):
+    """Identity forward, bf16-rounded gradient (a gradient map the backward stores)."""
+    return _RoundB.apply(t) if (_STORE_DTYPE[0] is not None and _STORE_GRADS[0] and t.requires_grad) else t
 
 
 def conv(x, sd, name, act=None, slope=0.0, stored=True):
@@ -241,7 +300,7 @@ def window_attention(xw, sd, p, nH, ws, mask):
     """WindowAttention.forward (swinir_arch.py:144-175)."""
     b_, n, c = xw.shape
     hd = c // nH
-    qkv = _linear(xw, sd, f'{p}.qkv').reshape(b_, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
+    qkv = store(_linear(xw, sd, f'{p}.qkv')).reshape(b_, n, 3, nH, hd).permute(2, 0, 3, 1, 4)
     q, k, v = qkv[0] * hd**-0.5, qkv[1], qkv[2]
     attn = q @ k.transpose(-2, -1)
     table = sd[f'{p}.relative_position_bias_table']
@@ -251,8 +310,8 @@ def window_attention(xw, sd, p, nH, ws, mask):
         nw = mask.shape[0]
         attn = attn.view(b_ // nw, nw, nH, n, n) + mask.unsqueeze(1).unsqueeze(0)
         attn = attn.view(-1, nH, n, n)
-    attn = attn.softmax(-1)
-    out = (attn @ v).transpose(1, 2).reshape(b_, n, c)
+    attn = store_fwd(store_grad(attn).softmax(-1))
+    out = store((attn @ v).transpose(1, 2).reshape(b_, n, c))
     return _linear(out, sd, f'{p}.proj')
 
 
@@ -306,7 +365,7 @@ def swin_block(x, sd, p, hw, nH, ws, shift, res=None, dp=None):
     if min(res) <= ws:
         shift, ws = 0, min(res)
     sc = x
-    t = _ln(x, sd, f'{p}.norm1').view(b, h, w, c)
+    t = store(_ln(x, sd, f'{p}.norm1')).view(b, h, w, c)
     if shift > 0:
         t = torch.roll(t, shifts=(-shift, -shift), dims=(1, 2))
     tw = window_partition(t, ws).view(-1, ws * ws, c)
@@ -315,12 +374,13 @@ def swin_block(x, sd, p, hw, nH, ws, shift, res=None, dp=None):
     if shift > 0:
         t = torch.roll(t, shifts=(shift, shift), dims=(1, 2))
     t = t.reshape(b, h * w, c)
-    m_fn = lambda v: _linear(F.gelu(_linear(_ln(v, sd, f'{p}.norm2'), sd, f'{p}.mlp.fc1')), sd, f'{p}.mlp.fc2')  # noqa: E731
+    m_fn = lambda v: _linear(store_fwd(F.gelu(store_grad(_linear(store(_ln(v, sd, f'{p}.norm2')), sd, f'{p}.mlp.fc1')))),  # noqa: E731
+                             sd, f'{p}.mlp.fc2')
     if dp is not None:
-        x = sc + drop_path(t, dp[0], dp[1][0])
-        return x + drop_path(m_fn(x), dp[0], dp[1][1])
-    x = sc + t
-    return x + m_fn(x)
+        x = store(sc + drop_path(t, dp[0], dp[1][0]))
+        return store(x + drop_path(m_fn(x), dp[0], dp[1][1]))
+    x = store(sc + t)
+    return store(x + m_fn(x))
 
 
 def swinir(sd, x, cfg, dp_rand=None):
@@ -344,7 +404,7 @@ def swinir(sd, x, cfg, dp_rand=None):
     def features(f):
         t = f.flatten(2).transpose(1, 2)
         if cfg.get('patch_norm', True):
-            t = _ln(t, sd, 'patch_embed.norm')
+            t = store(_ln(t, sd, 'patch_embed.norm'))
         if cfg.get('ape', False):  # swinir_arch.py:879-880
             t = t + sd['absolute_pos_embed']
         k = 0
@@ -356,8 +416,8 @@ def swinir(sd, x, cfg, dp_rand=None):
                                0 if j % 2 == 0 else ws // 2, res=res, dp=dp)
                 k += 1
             g = g.transpose(1, 2).reshape(b, -1, h, w)
-            t = conv(g, sd, f'layers.{i}.conv').flatten(2).transpose(1, 2) + t
-        t = _ln(t, sd, 'norm')
+            t = store(conv(g, sd, f'layers.{i}.conv', stored=False).flatten(2).transpose(1, 2) + t)
+        t = store(_ln(t, sd, 'norm'))
         return t.transpose(1, 2).reshape(b, -1, h, w)
 
     if ups == 'pixelshuffle':

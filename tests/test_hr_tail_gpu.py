@@ -114,18 +114,56 @@ def test_hr_tail_chain_vs_fp64_512(cuda):
     assert exact['y'] <= 5e-3 and max(exact.values()) <= 8e-2, exact
 
 
+class _LReluMasked(torch.autograd.Function):
+    """leaky_relu(z, 0.2) whose derivative takes its sign pattern from ``pos`` (the engine's stored
+    activation > 0) instead of z: fp32 and fp64 disagree on the sign of a pre-activation within
+    rounding of zero, and one such element moves a 30k-pixel gradient by ~6e-4 relative L2."""
+
+    @staticmethod
+    def forward(ctx, z, pos):
+        ctx.save_for_backward(pos)
+        return F.leaky_relu(z, 0.2)
+
+    @staticmethod
+    def backward(ctx, g):
+        (pos, ) = ctx.saved_tensors
+        return g * torch.where(pos, 1.0, 0.2).to(g.dtype), None
+
+
 def test_hr_tail_chain_fp32_vs_fp64(cuda):
     """The chain in the fp32 parity path (no autocast: exact-f32 MFMA convs, fp32 maps): the fp32
-    branches of the gated nearest-upsample backward and of the gated dgrad epilogue against the
-    exact float64 reference, output and every gradient within 1e-4 relative L2."""
+    branches of the gated nearest-upsample backward and of the gated dgrad epilogue against float64,
+    output and every gradient within 1e-4 relative L2.  The float64 LeakyReLU derivatives use the
+    engine's activation signs (_LReluMask; the engine's activations come from the per-conv forward,
+    the same kernels); the count of elements whose sign differs from float64's is printed."""
     convs = _tail(5)
     torch.manual_seed(6)
     feat = torch.randn(2, 24, 40, NF, device='cuda')
     g = torch.randn(2, 3, 96, 160, device='cuda')
     y, dx, grads = _run(convs, feat, g, chain=True)
     assert dx.dtype == torch.float32
-    errs = _errs(y, dx, grads, _reference(convs, feat, g, False))
-    print('fp32 chain rel L2 vs fp64:', {k: f'{v:.2e}' for k, v in errs.items()})
+    acts, h = [], feat
+    with torch.no_grad():
+        for c, kw in zip(convs[:3], KWS[:3]):
+            h = C.conv3x3(h, c, **kw)
+            acts.append(h.permute(0, 3, 1, 2).double().cpu() > 0)
+    x = feat.detach().permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
+    ws = [(c.weight.detach().double().cpu().requires_grad_(True), c.bias.detach().double().cpu().requires_grad_(True))
+          for c in convs]
+    z1 = F.conv2d(F.interpolate(x, scale_factor=2, mode='nearest'), *ws[0], padding=1)
+    h1 = _LReluMasked.apply(z1, acts[0])
+    z2 = F.conv2d(F.interpolate(h1, scale_factor=2, mode='nearest'), *ws[1], padding=1)
+    h2 = _LReluMasked.apply(z2, acts[1])
+    z3 = F.conv2d(h2, *ws[2], padding=1)
+    h3 = _LReluMasked.apply(z3, acts[2])
+    yr = F.conv2d(h3, *ws[3], padding=1)
+    yr.backward(g.double().cpu())
+    flips = sum(int(((z > 0) != a).sum()) for z, a in zip((z1, z2, z3), acts))
+    ref = (yr.detach(), x.grad.permute(0, 2, 3, 1), [(w.grad, b.grad) for w, b in ws])
+    errs = _errs(y.cpu(), dx.cpu(), [(a.cpu(), b.cpu()) for a, b in grads], ref)
+    print(f'fp32 chain rel L2 vs fp64 ({flips} activation sign(s) differ from fp64):',
+          {k: f'{v:.2e}' for k, v in errs.items()})
+    assert flips <= 16
     assert max(errs.values()) <= 1e-4, errs
 
 

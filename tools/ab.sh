@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for w in ${WORKLOADS:-edsr}; do
   for r in $(seq ${ROUNDS:-2}); do
     for v in A B; do
-      SR_HIP_LIB=tools/ab/lib$v.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-trace --workload $w \
+      SR_HIP_LIB=${ABDIR:-tools/ab}/lib$v.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-trace --workload $w \
         --steps ${STEPS:-10} --warmup 3 > gpurun_out/ab_${w}_$v.log 2>&1 || exit 1
       python3 -c "import json; d=json.loads(open('gpurun_out/ab_${w}_$v.log').read().strip().splitlines()[-1]); print('$w $v', d['ms_per_step'])"
     done
