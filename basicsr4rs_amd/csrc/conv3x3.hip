@@ -3072,9 +3072,6 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
 // halves and issues all four half-tiles of step t+1 (their buffer was last read at R2 of step t-1
 // by both groups), two quadrants per MFMA interval, R2 reads A half 1; the leading group retires
 // step t+1's DMAs after issuing its second MFMA interval, the lagging group at the end of its R2.
-#ifndef WG_EXP
-#define WG_EXP 0
-#endif
 template <bool P2 = false>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   constexpr int STAGE = 65536;
@@ -3085,9 +3082,6 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;
-#if WG_EXP == 3  // (experiment) static priority for the second wave group
-  if (wr) __builtin_amdgcn_s_setprio(1);
-#endif
   const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
   const int ntile = a.taps * a.tiles_co * a.tiles_ci;
   int split, rem;
@@ -3225,14 +3219,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   auto mma = [&](int h, int g) {
-#if WG_EXP == 2  // (experiment) no MFMA, fragment reads kept
-    acc[h][g][0][0][0] += __builtin_bit_cast(float, (int)(fa[0][0][0] ^ fa[0][1][1] ^ fa[0][2][2] ^ fa[0][3][3] ^ fa[1][0][4] ^
-        fa[1][1][5] ^ fa[1][2][6] ^ fa[1][3][7] ^ fb[g][0][0][0] ^ fb[g][0][1][1] ^ fb[g][1][0][2] ^ fb[g][1][1][3]));
-    return;
-#endif
-#if WG_EXP != 3 && WG_EXP != 4
     __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -3249,9 +3236,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
         else accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk][3], ones, accb[h], 0, 0, 0);
       }
     }
-#if WG_EXP != 3 && WG_EXP != 4
     __builtin_amdgcn_s_setprio(0);
-#endif
   };
 
   const int nk = (p_end - p_begin + 63) / 64;  // >= 1 (every split owns >= 1 pixel)
@@ -3272,7 +3257,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
       read_a(buf, 0);
       read_b(buf, 0);
       read_b(buf, 1);
-      if (more && WG_EXP != 1) {
+      if (more) {
         k_eval(t + 1);
         issue_a(t + 1, 0);
         issue_b(t + 1, 0);

@@ -23,7 +23,6 @@ enum SrKnob {
   K_DCN_COORD_WIN,  // SR_DCN_COORD_WIN=0: global-memory coordinate gradients (A/B)
   K_DCN_GX_FX,      // SR_DCN_GX_FX: 32 / 64-bit fixed-point scatter image
   K_SWIN_ATTN_DBG,  // SR_SWIN_ATTN_DBG: fused attention timing ablations (wrong results)
-  K_SWIN_ATTN_V,    // SR_SWIN_ATTN_V: fused attention schedule flags (A/B; see swin_fused.hip)
   K_COUNT
 };
 int sr_knob(SrKnob k);

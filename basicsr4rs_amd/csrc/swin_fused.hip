@@ -136,12 +136,11 @@ struct SabArgs {
 // of head h + 1 then run back to back: A writes Q / K / V, which nobody reads after S2, and C reads O,
 // which the next head writes only after its S1.  (Round 4 / early round 5: O_h overlaid Q_h and a
 // third barrier per head closed step C.)
-template <int NW, bool DB = false> struct SabL {
+template <int NW> struct SabL {
   static constexpr int TOK = 64 * NW, NT = 256 * NW;
-  static constexpr int WIMG = 3 * 96 * 128;        // one head's q / k / v weight rows, [3 cg][96 rows][128 B]
   static constexpr int X = 0;                      // [3 cg][TOK rows][128 B]
-  static constexpr int W = X + 3 * TOK * 128;      // DB: two images, head h in image h & 1
-  static constexpr int Q = W + (DB ? 2 : 1) * WIMG;  // [TOK][64 B]
+  static constexpr int W = X + 3 * TOK * 128;      // [3 cg][96 rows][128 B]
+  static constexpr int Q = W + 3 * 96 * 128;       // [TOK][64 B]
   static constexpr int K = Q + TOK * 64;
   static constexpr int V = K + TOK * 64;           // [NW windows][64][64 B], sx_byte layout (tr reads)
   static constexpr int O = V + TOK * 64;           // [TOK][64 B]
@@ -151,13 +150,8 @@ template <int NW, bool DB = false> struct SabL {
   static constexpr int BP = BQ + 576 * 4;          // float [192]: proj bias
   static constexpr int LDS = BP + 192 * 4;
   static constexpr int WREG = (96 * 24 + NT - 1) / NT;  // 16-B pieces of W_h (K <= 192) per thread
-  static_assert(LDS <= 163840, "fused attention LDS");
 };
 constexpr int SAB_WPIECES = 96 * 24;
-// DB: the W image of a head is 36 LDS-DMA pieces of 1 KB (8 rows of one 128-B channel group); wave w
-// issues pieces w, w + 8, .. (waves 4-7 repeat their last piece for a fifth: the same bytes to the
-// same place), so every wave issues exactly SAB_WDMA per head and the vmcnt bookkeeping is constant.
-constexpr int SAB_WDMA = 5;
 
 // 16-B chunk ch of row r of a [cg][rows][128 B] image (chunk XOR row & 7 within its 128-B group)
 SR_DEV uint32_t tile_off(int rows, int r, int ch) {
@@ -168,32 +162,31 @@ SR_DEV uint32_t tile_off(int rows, int r, int ch) {
 SR_DEV uint32_t qk_off16(int t, int c) { return (uint32_t)(t * 64 + ((c ^ ((t >> 2) & 3)) << 4)); }
 SR_DEV uint32_t qk_off(int t, int d) { return qk_off16(t, d >> 3) + (uint32_t)((d & 7) * 2); }
 
-// NW windows per block: 2 (8 waves, one block per CU).  (One-window blocks, two per CU at 77.5 KB,
-// measured the same in round 4 and were removed in round 5.)
+// NW windows per block: 2 (8 waves, one block per CU: 122 KB of LDS).  (One-window blocks, two per
+// CU at 77.5 KB, measured the same in round 4 and were removed in round 5.)
 // SH: the shifted-window block (the mask arithmetic is compiled only there).
 // DBG (timing ablations, wrong results; knob SR_SWIN_ATTN_DBG): 1 no step-A MFMAs, 2 no softmax
-// VALU, 4 no step-C MFMAs, 8 no LayerNorm arithmetic, 16 no per-head weight staging.
+// VALU, 4 no step-C MFMAs, 8 no LayerNorm arithmetic, 16 no per-head weight staging; 32: phase stamps
+// (s_memtime; results unchanged): per block, waves 0 and 4, the LayerNorm prologue, steps A / B / C
+// and the two barrier waits summed over the heads (tools/swin_attn_stamps.py).
 // Round 5 (VALU per wave was the bound: ablations put 30-36 us of a 148 us inference launch each in
 // the softmax, the LayerNorm and the per-head weight staging): head-invariant addresses hoisted out
 // of the head loop (weight pieces: one offset per piece + the head as the buffer soffset; the step-A /
 // B store offsets), the softmax in base 2 (table column and scale pre-multiplied by log2 e: one fma
 // per score, v_exp_f32 directly), the mask only in shifted blocks.
-// VF (round 6, knob SR_SWIN_ATTN_V): schedule flags.
-//   1 (DB): the per-head weight images double-buffered in LDS and filled by LDS-DMA (no VGPR staging,
-//     no ds_write; 162 KB of LDS): head h + 1's image is issued at head h's top, into the image head
-//     h - 1 read, and waited for (counted vmcnt) before head h's S2 instead of at S1.
-//   2 (PRIO): static s_setprio 1 for waves 4-7 (the second-dispatched half, the arbitration loser:
-//     MI355X_MICROARCH.md "two waves per SIMD" item 4).
-//   4 (EARLYX): the last head is peeled and the epilogue's residual x rows are loaded at its top, so
-//     their HBM latency hides under the last head instead of sitting between the loop and the stores.
-template <int NW, int DBG = 0, bool SH = true, int VF = 0>
+// Round 6: the prologue's operands in one round trip (s_memtime phase stamps, DBG 32, put the
+// LayerNorm prologue at 22 % of the kernel).  Measured and removed (profiles/r06/ab/swin_attn/): the
+// per-head weight images double-buffered in LDS and filled by LDS-DMA (no VGPR staging; train
+// 142 -> 152..158 us with the wait at S1, 151 -> 150 us waited before S2), static s_setprio 1 for
+// waves 4-7 (+-2 us), the last head peeled with the residual loads at its top (inference +4 us),
+// and a role-split form (waves 0-3 the qkv projection with W in registers, waves 4-7 softmax / AV /
+// proj, a 3-stage pipeline with one barrier per stage: train 144 -> 172 us, inference 115 -> 129 us).
+template <int NW, int DBG = 0, bool SH = true>
 __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(SabArgs a) {
-  constexpr bool DB = (VF & 1) != 0, PRIO = (VF & 2) != 0, EARLYX = (VF & 4) != 0;
-  constexpr bool ST = (DBG & 32) != 0;  // phase stamps (s_memtime), no other change
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tst = 0;
+  constexpr bool ST = (DBG & 32) != 0;
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tst = 0, t0 = 0, t1 = 0;
   if constexpr (ST) tst = __builtin_readcyclecounter();
-  static_assert(!DB || NW == 2, "DB: 8 waves");
-  using L = SabL<NW, DB>;
+  using L = SabL<NW>;
   constexpr int TOK = L::TOK, NT = L::NT;
   __shared__ __attribute__((aligned(16))) char smem[L::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -241,64 +234,35 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
   const auto wqr = make_rsrc(a.wq, (uint32_t)((size_t)3 * a.nH * 32 * a.Cp * 2));
   const auto wpr = make_rsrc(a.wp, (uint32_t)((size_t)a.Cp * a.ldo * 2));
   const auto tbr = make_rsrc(a.table, (uint32_t)(225 * a.nH * 4));
-  constexpr int NWR = DB ? 1 : L::WREG;
-  u32x4 wreg[NWR];
+  u32x4 wreg[L::WREG];
   // piece p = (row rr of the head's 96, 16-B chunk ch): its global offset at head 0 (the head adds
   // 64 Cp bytes, passed as the buffer soffset) and its LDS offset, computed once
-  uint32_t wgo[NWR], wlo[NWR];
-  // DB: this lane's source offset (head 0) of each of the wave's DMA pieces and their LDS offsets
-  uint32_t wdo[SAB_WDMA];
-  int wdk[SAB_WDMA];
-  if constexpr (DB) {
+  uint32_t wgo[L::WREG], wlo[L::WREG];
 #pragma unroll
-    for (int j = 0; j < SAB_WDMA; ++j) {
-      int k = w + 8 * j;
-      if (k >= 36) k -= 8;
-      wdk[j] = k;
-      const int cg = k / 12, rr = (k - cg * 12) * 8 + (lane >> 3);
-      const int ch = cg * 8 + ((lane & 7) ^ (rr & 7));
-      const int grow = (rr >> 5) * a.nH * 32 + (rr & 31);
-      wdo[j] = ch < a.KC ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < NWR; ++k) {
-      const int p = tid + NT * k;
-      const int rr = p / 24, ch = p - rr * 24;
-      const int grow = (rr >> 5) * a.nH * 32 + (rr & 31);
-      wgo[k] = (p < SAB_WPIECES && ch < a.KC) ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB;
-      wlo[k] = L::W + tile_off(96, rr, ch);
-    }
+  for (int k = 0; k < L::WREG; ++k) {
+    const int p = tid + NT * k;
+    const int rr = p / 24, ch = p - rr * 24;
+    const int grow = (rr >> 5) * a.nH * 32 + (rr & 31);
+    wgo[k] = (p < SAB_WPIECES && ch < a.KC) ? (uint32_t)(grow * a.Cp + ch * 8) * 2u : SR_OOB;
+    wlo[k] = L::W + tile_off(96, rr, ch);
   }
   auto w_load = [&](int h) {
     const uint32_t so = (uint32_t)(h * 64 * a.Cp);
 #pragma unroll
-    for (int k = 0; k < NWR; ++k)
+    for (int k = 0; k < L::WREG; ++k)
       wreg[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wqr, wgo[k], so, 0));
   };
   auto w_store = [&]() {
 #pragma unroll
-    for (int k = 0; k < NWR; ++k)
+    for (int k = 0; k < L::WREG; ++k)
       if (tid + NT * k < SAB_WPIECES) *(u32x4*)(smem + wlo[k]) = wreg[k];
   };
-  // DB: head h's image into LDS image `buf` by LDS-DMA (h >= nH: zero fill of a dead image)
-  auto w_dma = [&](int h, int buf) {
-    const uint32_t ho = (uint32_t)(h * 64 * a.Cp);
-    const bool hv = h < a.nH;
-#pragma unroll
-    for (int j = 0; j < SAB_WDMA; ++j)
-      glds16(wqr, smem + L::W + buf * L::WIMG + wdk[j] * 1024, (hv && wdo[j] != SR_OOB) ? wdo[j] + ho : SR_OOB);
-  };
-  if constexpr (DB) {
-    w_dma(0, 0);
-  } else {
-    w_load(0);
-  }
+  w_load(0);
   // every small operand (bias table column, qkv / proj biases, LayerNorm gamma / beta) and the token rows
   // are issued together, as unconditional buffer loads (out of range -> 0), before the first global
   // store (on gfx9 vmcnt counts stores too, so a load issued after stores makes its wait drain them):
   // one HBM round trip for the whole prologue.  (Round 5: loads inside `if (tid < ..)` branches made
-  // each its own load-wait-write round trip -- the prologue was 22 % of the kernel, s_memtime stamps.)
+  // each its own load-wait-write round trip -- the prologue was 22 % of the kernel, DBG 32 stamps.)
   constexpr float LOG2E = 1.4426950408889634f;
   const auto tbl0 = make_rsrc(a.table, (uint32_t)(225 * a.nH * 4));
   const auto bqr = make_rsrc(a.bq, (uint32_t)(3 * a.nH * 32 * 4));
@@ -352,14 +316,9 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
     buf_store4f(mur, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, mu);
     buf_store4f(rsr, (vr && part == 0) ? (uint32_t)pr * 4u : SR_OOB, rs);
   }
-  if constexpr (DB)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // head 0's image landed (the 8 LN stores issued after it)
-  else
-    w_store();
+  w_store();
   __syncthreads();
   if constexpr (ST) ph[0] = __builtin_readcyclecounter() - tst;  // LayerNorm prologue
-  if constexpr (PRIO)
-    if (w >= 4) __builtin_amdgcn_s_setprio(1);
 
   // per-wave constants
   const int og = w & 1, tg = w >> 1;   // step A: 48 q/k/v rows x 32 tokens
@@ -412,57 +371,19 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
 #pragma unroll
     for (int j = 0; j < 4; ++j) xacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // epilogue operands: x2 = x + s1[n] * (proj + bias); loaded before the epilogue's stores (EARLYX: at
-  // the last head's top, before its stores)
-  f32x4 biasp[3];
-  uint2 xres[3][4];
-  float scj[4];
-  int64_t pixj[4];
-  bool vj[4];
-  const auto xr = make_rsrc(a.x, (uint32_t)((size_t)a.N * a.H * a.W * a.Cp * 2));
-  auto epi_load = [&]() {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int n;
-      vj[j] = tok_pix(ptg * 64 + 16 * j + c16, pixj[j], n);
-      scj[j] = (a.rsc && vj[j]) ? a.rsc[n] : 1.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int oc = pog * 48 + 16 * i + 4 * g;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        xres[i][j] = buf_load8(xr, (oc < a.Cp && vj[j]) ? (uint32_t)(pixj[j] * a.Cp + oc) * 2u : SR_OOB);
-    }
-  };
-
-  auto head = [&](int h, auto last_) {
-    constexpr bool LAST = decltype(last_)::value;
-    unsigned long long t0 = 0, t1 = 0;
+  for (int h = 0; h < a.nH; ++h) {
     if constexpr (ST) t0 = __builtin_readcyclecounter();
     // The head's global loads (projection columns, the next head's weights) are issued here, before
     // its qkv / ao / lse stores; the biases and the table come from LDS (a bias loaded from global
     // after the stores drained all of them, three times per head, in the first version).
     // this head's projection columns (A operand of step C) and the next head's weights, in flight
     u32x4 wpf[3];
-    auto wp_load = [&]() {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int row = pog * 48 + 16 * i + c16;
-        wpf[i] = buf_load16(wpr, row < a.Cp ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
-      }
-    };
-    if constexpr (EARLYX && LAST) epi_load();
-    if constexpr (DB) {
-      // head h + 1's image into the one head h - 1 read (every wave is past that head's S2): first of
-      // the head's vector-memory operations, so the compiler's own counted waits (it does not see the
-      // DMAs) stay exact for everything issued after them
-      if constexpr ((DBG & 16) == 0 && !LAST) w_dma(h + 1, (h + 1) & 1);
-      wp_load();
-    } else {
-      wp_load();
-      if (h + 1 < a.nH && (DBG & 16) == 0) w_load(h + 1);
+    for (int i = 0; i < 3; ++i) {
+      const int row = pog * 48 + 16 * i + c16;
+      wpf[i] = buf_load16(wpr, row < a.Cp ? (uint32_t)(row * a.ldo + h * 32 + 8 * g) * 2u : SR_OOB);
     }
+    if (h + 1 < a.nH && (DBG & 16) == 0) w_load(h + 1);
     const float tbn = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
         tbr, (h + 1 < a.nH && tid < 225) ? (uint32_t)(tid * a.nH + h + 1) * 4u : SR_OOB, 0, 0));  // next column
     __builtin_amdgcn_sched_barrier(0);  // keep these loads here, ahead of the head's stores
@@ -479,7 +400,6 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
       }
 
     // ---- A: q / k / v of head h
-    const char* sW = smem + L::W + (DB ? (h & 1) * L::WIMG : 0);
     f32x4 acc[3][2];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -490,7 +410,7 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
       const int ch = 4 * kk + g;
       s16x8 af[3], bf[2];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) af[i] = *(const s16x8*)(sW + tile_off(96, og * 48 + 16 * i + c16, ch));
+      for (int i = 0; i < 3; ++i) af[i] = *(const s16x8*)(smem + L::W + tile_off(96, og * 48 + 16 * i + c16, ch));
 #pragma unroll
       for (int j = 0; j < 2; ++j) bf[j] = *(const s16x8*)(smem + L::X + tile_off(TOK, tg * 32 + 16 * j + c16, ch));
 #pragma unroll
@@ -526,7 +446,7 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
     __syncthreads();  // S1: Q, K, V of head h in LDS; every wave is past step A (sW) and the top (table slot)
     if constexpr (ST) { t0 = __builtin_readcyclecounter(); ph[2] += t0 - t1; }
     if (h + 1 < a.nH) {
-      if constexpr (!DB && (DBG & 16) == 0) w_store();
+      if constexpr ((DBG & 16) == 0) w_store();
       if (tid < 256) sTB[((h + 1) & 1) * 256 + tid] = tbn * LOG2E;  // (scaled here: a multiply next to the load would wait for it)
     }
 
@@ -583,11 +503,7 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
         *(uint2*)(smem + L::O + qk_off(wi * 64 + qq, 16 * d + 4 * g)) = u;
       }
     }
-    // DB: head h + 1's image (issued at this head's top) has landed: 13 of this wave's vector-memory
-    // operations were issued after its last DMA (1 table load, 3 projection-column loads, 6 qkv stores,
-    // 1 lse + 2 ao stores)
     if constexpr (ST) { t1 = __builtin_readcyclecounter(); ph[3] += t1 - t0; }
-    if constexpr (DB && !LAST) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
     __syncthreads();  // S2: O_h in LDS (Q, K, V free); the next head's weights and table column visible
     if constexpr (ST) { t0 = __builtin_readcyclecounter(); ph[4] += t0 - t1; }
 
@@ -602,20 +518,28 @@ __global__ __launch_bounds__(256 * NW, 3 - NW) void swin_attn_block_fwd_kernel(S
       }
     }
     if constexpr (ST) ph[5] += __builtin_readcyclecounter() - t0;
-  };
-  if constexpr (EARLYX) {
-    for (int h = 0; h + 1 < a.nH; ++h) head(h, std::false_type{});
-    head(a.nH - 1, std::true_type{});
-  } else {
-    for (int h = 0; h < a.nH; ++h) head(h, std::false_type{});
-    epi_load();
   }
 
   // ---- epilogue: x2 = x + s1[n] * (proj + bias); all loads before the first store (see above)
+  f32x4 biasp[3];
+  uint2 xres[3][4];
+  float scj[4];
+  int64_t pixj[4];
+  bool vj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int n;
+    vj[j] = tok_pix(ptg * 64 + 16 * j + c16, pixj[j], n);
+    scj[j] = (a.rsc && vj[j]) ? a.rsc[n] : 1.f;
+  }
+  const auto xr = make_rsrc(a.x, (uint32_t)((size_t)a.N * a.H * a.W * a.Cp * 2));
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int oc = pog * 48 + 16 * i + 4 * g;
     biasp[i] = oc < a.Cp ? *(const f32x4*)(sBP + oc) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      xres[i][j] = buf_load8(xr, (oc < a.Cp && vj[j]) ? (uint32_t)(pixj[j] * a.Cp + oc) * 2u : SR_OOB);
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -938,25 +862,12 @@ int sr_swin_attn_fused_fwd(const void* x, const float* ln_g, const float* ln_b, 
   const dim3 g2((a.nwin_total + 1) / 2);
   hipStream_t s = (hipStream_t)stream;
   const int dbg = sr_knob(K_SWIN_ATTN_DBG);
-  if (dbg <= 0) {  // the kernel, specialised for unshifted / shifted blocks and the schedule flags (A/B)
-    const int vf = sr_knob(K_SWIN_ATTN_V) < 0 ? 0 : sr_knob(K_SWIN_ATTN_V);
-#define SAB_LAUNCH(VF)                                                                                 \
-  if (shift) hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 0, true, VF>), g2, dim3(512), 0, s, a); \
-  else hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 0, false, VF>), g2, dim3(512), 0, s, a);
-    switch (vf) {
-      case 0: SAB_LAUNCH(0) break;
-      case 1: SAB_LAUNCH(1) break;
-      case 2: SAB_LAUNCH(2) break;
-      case 3: SAB_LAUNCH(3) break;
-      case 4: SAB_LAUNCH(4) break;
-      case 5: SAB_LAUNCH(5) break;
-      case 7: SAB_LAUNCH(7) break;
-      default: return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: unknown SR_SWIN_ATTN_V");
-    }
-#undef SAB_LAUNCH
+  if (dbg <= 0) {  // the kernel, specialised for unshifted / shifted blocks
+    if (shift) hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 0, true>), g2, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 0, false>), g2, dim3(512), 0, s, a);
     return sr_check(hipGetLastError(), "swin_attn_fused_fwd launch");
   }
-  if (dbg == 32) {  // phase stamps (sr_conv3x3_set_stamps buffer: 2 x 8 per block), the V = 0 schedule
+  if (dbg == 32) {  // phase stamps (sr_conv3x3_set_stamps buffer: 2 x 8 per block)
     a.stamps = g_sr_stamps;
     if (!a.stamps) return sr_fail(SR_EINVAL, "swin_attn_fused_fwd: SR_SWIN_ATTN_DBG=32 needs sr_conv3x3_set_stamps");
     if (shift) hipLaunchKernelGGL((swin_attn_block_fwd_kernel<2, 32, true>), g2, dim3(512), 0, s, a);
