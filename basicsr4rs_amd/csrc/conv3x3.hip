@@ -19,10 +19,6 @@
 #include "sr_common.h"
 #include "sr_internal.h"
 
-#ifndef WG_PP_FORM
-#define WG_PP_FORM 1  // conv3x3_wgrad_pp_kernel schedule: 1 two 64-KB stages, 2 five 32-KB slots
-#endif
-
 namespace {
 
 // set by sr_conv3x3_set_variant (tests / A-B timing): 0 auto (phase-interleaved 256x256),
@@ -3076,21 +3072,12 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_big_kernel(WgArgs a) {
 // halves and issues all four half-tiles of step t+1 (their buffer was last read at R2 of step t-1
 // by both groups), two quadrants per MFMA interval, R2 reads A half 1; the leading group retires
 // step t+1's DMAs after issuing its second MFMA interval, the lagging group at the end of its R2.
-// P2 == 2 (round 6): the operands in 32-pixel sub-steps through a ring of FIVE 32-KB slots (A0 A1
-// B0 B1 of one sub-step each; the whole 160 KB), MFMA intervals by sub-step -- R1 reads every
-// fragment of sub-step 2t, the first interval runs all four quadrants' kk = 0 MFMAs, R2 reads
-// sub-step 2t + 1, the second interval kk = 1 -- and each slot refilled in the interval after its
-// last read: sub-step u + 4 is issued at R(u) into the slot sub-step u - 1 held.  A sub-step's DMA
-// is then issued two 64-pixel steps ahead of its read instead of one (the two-stage form waits for
-// the whole next step at the end of each step: no-DMA and no-MFMA ablations 145 / 131 us against
-// 185 us with both, note 30).  Every accumulator still sums its pixels in order (sub-step u
-// covers pixels 32u ..): bitwise equal to P2 == 1.
-template <int P2 = 0>
+template <bool P2 = false>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   constexpr int STAGE = 65536;
   constexpr int CSTR = 256 + 4;
-  constexpr int SMEM = P2 == 2 ? 5 * 32768 : 128 * CSTR * 4;
-  static_assert(SMEM >= 2 * STAGE && SMEM >= 128 * CSTR * 4, "LDS too small");
+  constexpr int SMEM = 128 * CSTR * 4;
+  static_assert(SMEM >= 2 * STAGE, "LDS too small");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -3134,166 +3121,6 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const int rps = a.out_ps > 0 ? a.out_ps : 1;
 
-  if constexpr (P2 == 2) {
-    constexpr uint32_t SLOT = 32768, SA0 = 0, SA1 = 8192, SB0 = 16384, SB1 = 24576;
-    // DMA row of this lane in a 32-row half-tile image: R = 4 w + (lane >> 4), 16-B slot lane & 15
-    // holding the logical chunk lc of the swizzled 256-B row (the two-stage form's mapping per 32 rows)
-    const int R = 4 * w + (lane >> 4);
-    uint32_t la, lb;
-    {
-      const int f = (R & 3) | (((R >> 3) & 1) << 2);
-      const int sl = lane & 15;
-      const int lc = (((sl >> 1) ^ f) << 1) | (sl & 1);
-      la = (uint32_t)(R * rps * a.ldy) * 2u + (uint32_t)lc * 16u;
-      lb = (uint32_t)(R * a.ldx) * 2u + (uint32_t)lc * 16u;
-    }
-    const int nsub = (p_end - p_begin + 31) / 32;  // >= 1
-    // sub-step u's four half-tiles (one 1-KB DMA each per wave) into slot u % 5; past the range the
-    // pieces are out of bounds (zero fill of a dead slot), so every wave issues exactly 4 per call
-    auto issue = [&](int u) {
-      const int p0s = p_begin + u * 32;
-      const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
-      const int x0 = p0s - q * a.W;
-      const int n = (int)fdiv((uint32_t)q, a.fd_H);
-      const int y = q - n * a.H;
-      int ua[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int cu = co0 + h * 128;
-        if (a.out_ps == 0) {
-          ua[h] = (p0s * a.ldy + a.ycoff + cu) * 2;
-        } else {
-          const int r = a.out_ps;
-          const int sl = (int)fdiv((uint32_t)cu, a.fd_cps);
-          const int cch = cu - sl * a.fd_cps.d;
-          const int si = sl / r, sj = sl - si * r;
-          ua[h] = (((q * r + si) * (a.W * r) + x0 * r + sj) * a.ldy + a.ycoff + cch) * 2;
-        }
-      }
-      const int ua0 = __builtin_amdgcn_readfirstlane(ua[0]);
-      const int ua1 = __builtin_amdgcn_readfirstlane(ua[1]);
-      const int ub = __builtin_amdgcn_readfirstlane((((q + dy_) * a.W + x0 + dx_) * a.ldx + a.xcoff + ci0) * 2);
-      const int sx0 = __builtin_amdgcn_readfirstlane(x0 + dx_);
-      const int left = __builtin_amdgcn_readfirstlane(p_end - p0s);
-      const int yv = __builtin_amdgcn_readfirstlane((unsigned)(y + dy_) < (unsigned)a.H ? 1 : 0);
-      char* base = smem + (u % 5) * SLOT + w * 1024;
-      glds16(dyr, base + SA0, R < left ? (uint32_t)ua0 + la : SR_OOB);
-      glds16(dyr, base + SA1, R < left ? (uint32_t)ua1 + la : SR_OOB);
-      const bool v = yv && R < left && (unsigned)(sx0 + R) < (unsigned)a.W;
-      glds16(xr, base + SB0, v ? (uint32_t)ub + lb : SR_OOB);
-      glds16(xr, base + SB1, v ? (uint32_t)ub + 256u + lb : SR_OOB);
-    };
-    const int tg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
-    auto tr8 = [&](const char* base, int r0, int col) -> s16x8 {
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0, col * 2, 256)));
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s16x4*)(base + swz_tr(r0 + 4, col * 2, 256)));
-      return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    };
-    s16x8 fa[2][4], fb[2][2];  // one sub-step's fragments: fa[h][i], fb[g][j]
-    auto read = [&](int u) {
-      const char* S = smem + (u % 5) * SLOT;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[h][i] = tr8(S + (h ? SA1 : SA0), 8 * tg + tq, wr * 64 + i * 16 + 4 * tp);
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb[g][j] = tr8(S + (g ? SB1 : SB0), 8 * tg + tq, wc * 32 + j * 16 + 4 * tp);
-    };
-    f32x4 acc[2][2][4][2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[h][g][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool bias_here = a.bias_fused && a.wsb && tap == a.taps / 2 && ci0 == 0;
-    const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
-    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    auto mma = [&]() {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[h][g][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[g][j], acc[h][g][i][j], 0, 0, 0);
-      if (bias_here) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          if (wc == 0) accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][0], ones, accb[h], 0, 0, 0);
-          else if (wc == 1) accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][1], ones, accb[h], 0, 0, 0);
-          else if (wc == 2) accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][2], ones, accb[h], 0, 0, 0);
-          else accb[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][3], ones, accb[h], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
-    };
-    // Schedule (the two wave groups one barrier apart, as in P2 == 1): per sub-step u a read interval
-    // R(u) -- its fragments, then sub-step u + 4 into the slot of u - 1 -- and an MFMA interval M(u).
-    // Global barrier 2u + 2 ends the leading group's M(u) and the lagging group's R(u); before it every
-    // wave has sub-step u + 1 complete: 12 of its DMAs (u + 2 .. u + 4) are younger.
-    issue(0);
-    issue(1);
-    issue(2);
-    issue(3);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    pp_barrier();
-    if (wr) pp_barrier();
-    for (int u = 0; u < nsub; ++u) {
-      read(u);
-      issue(u + 4);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot is re-filled one interval later
-      if (wr) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      pp_barrier();
-      mma();
-      if (!wr) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      pp_barrier();
-    }
-    if (!wr) pp_barrier();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-fill pieces land before LDS reuse
-
-    if (bias_here && (lane & 15) == 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = co0 + h * 128 + wr * 64 + wc * 16 + (lane >> 4) * 4 + r;
-          if (co < a.Cout) a.wsb[(size_t)split * a.Cout + co] = accb[h][r];
-        }
-    }
-    float* ws = a.ws + ((size_t)split * a.taps + tap) * a.Cout * a.Cin;
-    float* Cs = (float*)smem;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      __syncthreads();
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              Cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CSTR + g * 128 + wc * 32 + j * 16 + (lane & 15)] =
-                  acc[h][g][i][j][r];
-      __syncthreads();
-      for (int idx = tid; idx < 128 * 64; idx += 512) {
-        const int row = idx >> 6, c4 = (idx & 63) * 4;
-        const int co = co0 + h * 128 + row, ci = ci0 + c4;
-        if (co < a.Cout && ci < a.Cin) *(f32x4*)(ws + (size_t)co * a.Cin + ci) = *(const f32x4*)(Cs + row * CSTR + c4);
-      }
-    }
-    return;
-  } else {
   // DMA rows of this lane: R_j = 8w + 4j + (lane >> 4), 16-B slot lane & 15 holding the
   // logical chunk lc_j of the swizzled 256-B row.
   int Rj[2];
@@ -3521,7 +3348,6 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_pp_kernel(WgArgs a) {
       if (co < a.Cout && ci < a.Cin)
         *(f32x4*)(ws + (size_t)co * a.Cin + ci) = *(const f32x4*)(Cs + row * CSTR + c4);
     }
-  }
   }
 }
 
@@ -5339,17 +5165,17 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     if (a.bias_fused) {
       a.bias_group = 0;
       if (g_variant != 59)
-        hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<WG_PP_FORM>), dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<true>), dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
       else
-        hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+        hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<false>, dim3(S * taps * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
     } else if (a.bias_group > 0) {
       const int nb = S * taps * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
-      if (g_variant != 59) hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<WG_PP_FORM>), dim3(nb), dim3(512), 0, s, a);
-      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(nb), dim3(512), 0, s, a);
+      if (g_variant != 59) hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<true>), dim3(nb), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<false>, dim3(nb), dim3(512), 0, s, a);
     } else if (wg_use_pp(d) && g_variant != 59)
-      hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<WG_PP_FORM>), dim3(S * per_split), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv3x3_wgrad_pp_kernel<true>), dim3(S * per_split), dim3(512), 0, s, a);
     else if (wg_use_pp(d))
-      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<0>, dim3(S * per_split), dim3(512), 0, s, a);
+      hipLaunchKernelGGL(conv3x3_wgrad_pp_kernel<false>, dim3(S * per_split), dim3(512), 0, s, a);
     else
       hipLaunchKernelGGL(conv3x3_wgrad_big_kernel, dim3(S * per_split), dim3(512), 0, s, a);
     e = hipGetLastError();
