@@ -161,20 +161,10 @@ def test_round3_kernel_selection():
         _lib.check(lib.sr_conv3x3_set_variant(0))
 
 
-def test_dot_parts_handoff_and_async_hold():
-    """The RCAB dot-partials hand-off takes the partials only for the same u and an unmodified dy, once;
-    the side-stream dy references are dropped when the outermost async_wgrad context exits."""
-    from basicsr4rs_amd.ops import blocks as B
+def test_async_hold_released_at_outermost_exit():
+    """The side-stream dy references are dropped when the outermost async_wgrad context exits."""
     from basicsr4rs_amd.ops import conv as C
-    u, dy, parts = torch.zeros(2, 3), torch.zeros(2, 3), torch.ones(1)
-    B._dot_parts_put(dy, parts, u)
-    assert B._dot_parts_take(dy, torch.zeros(2, 3)) is None  # another u
-    B._dot_parts_put(dy, parts, u)
-    dy.add_(1.0)  # an in-place accumulation after the hand-off
-    assert B._dot_parts_take(dy, u) is None
-    B._dot_parts_put(dy, parts, u)
-    assert B._dot_parts_take(dy, u) is parts
-    assert B._dot_parts_take(dy, u) is None  # consumed
+    dy = torch.zeros(2, 3)
     with C.async_wgrad(True):
         with C.async_wgrad(True):
             C._ASYNC['hold'].append(dy)
