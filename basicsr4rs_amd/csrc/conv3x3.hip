@@ -2010,8 +2010,9 @@ template <int CO, int W, int LA, int KH, int E, int NWV = 4>
 __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3x3_fwd_band_kernel(FwdArgs a) {
   constexpr int ACT = E & 3, GATE = (E >> 2) & 3;
   constexpr bool RES = (E & 16) != 0, RES2 = (E & 32) != 0, AUX = (E & 64) != 0, CS = (E & 128) != 0,
-                 RSC = (E & 256) != 0, DOT = (E & 512) != 0;
+                 RSC = (E & 256) != 0, DOT = (E & 512) != 0, STRIP = (E & 1024) != 0;
   static_assert(!DOT || CS, "band: dot partials need colsum");
+  static_assert(!STRIP || (!CS && !RSC), "band: column strips carry no per-image epilogue");
   constexpr int IR = GATE ? 1 : 0, IR2 = IR + (RES ? 1 : 0), ID = IR2 + (RES2 ? 1 : 0), NSTG = ID + (DOT ? 1 : 0);
   static_assert(NWV == 4 || (NWV == 8 && W / 16 / (8 / (CO / 32)) >= 1), "band: a pixel tile per wave");
   constexpr int WC = CO / 32;       // waves along output channels (32 each = 2 co tiles)
@@ -2023,7 +2024,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
   constexpr int PPW = W / 8 / NWV;  // 1-KB DMA pieces per wave per row
   constexpr int NG = NSTG * PT;     // staging pieces per wave per row (gate / res / res2)
   constexpr int NC = (CS ? 2 : 0) + (AUX ? PT : 0);  // stores after the PT output stores
-  constexpr int KROW = NG + PPW + PT + NC;            // vector memory ops per wave per row
+  constexpr int PPWX = PPW + (STRIP ? 1 : 0);  // + the strip's border piece (or a dummy) per wave
+  constexpr int KROW = NG + PPWX + PT + NC;           // vector memory ops per wave per row
   constexpr int EPI = (NSTG ? NSTG : 1) * PT * 1024;  // per-wave staging
   constexpr int CIN = 32 * KH;
   constexpr int WROW = 9 * CIN * 2;  // bytes of one output channel's weights [tap][ci]
@@ -2042,7 +2044,29 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
   const int wc = w % WC, wp = w / WC;
   const int g = lane >> 4, c16 = lane & 15;
   const int H = a.H;
-  const int T = a.N * H;  // output rows
+  // STRIP (E bit 10): the image is a.W = strips x W pixels wide and each band row is one W-px column
+  // strip of an image row, strip rows ordered (image, strip, y) so a band streams down a strip; the
+  // strip's two border columns are real pixels of its neighbours (one extra 1-KB piece per row from
+  // waves 0 / 1, a zero dummy from the others), and with in_up = 2 the pieces gather the nearest
+  // upsample of a half-size input
+  const int strips = STRIP ? a.W / W : 1;
+  const int HS = H * strips;
+  const int T = a.N * HS;  // output rows (strip rows)
+  struct RowG { size_t base; int y, irow, x0; };  // first pixel, y, image row n*H + y, strip x origin
+  auto row_geom = [&](int q) -> RowG {
+    if constexpr (!STRIP) {
+      return RowG{(size_t)q * W, q % H, q, 0};
+    } else {
+      const int nq = q / HS, rem = q - nq * HS, j = rem / H, y = rem - j * H;
+      return RowG{(size_t)(nq * H + y) * a.W + j * W, y, nq * H + y, j * W};
+    }
+  };
+  const int upsh = STRIP && a.in_up == 2 ? 1 : 0;
+  // input offset (bytes, chunk lc) of pixel sx of image row irow (STRIP)
+  auto src_off = [&](int irow, int sx, int lc) -> uint32_t {
+    const size_t px = (size_t)(irow >> upsh) * (a.W >> upsh) + (sx >> upsh);
+    return (uint32_t)((px * a.ldx + a.xcoff + lc * 8) * 2);
+  };
 #ifdef SR_BAND_STAMPS
   const unsigned long long t_start = __builtin_readcyclecounter();
   unsigned long long ph[4] = {0ull, 0ull, 0ull, 0ull};  // row wait / barrier / MFMA / epilogue
@@ -2063,7 +2087,12 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
   for (int p = w; p < WBYTES / 1024; p += NWV) {
     const int e = p * 1024 + lane * 16;
     const int co = e / WROW, off = e - co * WROW;
-    glds16(wr, wimg + p * 1024, (uint32_t)(co * a.ldw * 2 + off));
+    if constexpr (STRIP) {  // Cin may be 8 / 16 / 24 below CIN (the RRDBNet conv_last dgrad): zero-padded per tap
+      const int tap = off / (CIN * 2), cib = off - tap * (CIN * 2);
+      glds16(wr, wimg + p * 1024, cib < a.Cin * 2 ? (uint32_t)(co * a.ldw * 2 + tap * a.Cin * 2 + cib) : SR_OOB);
+    } else {
+      glds16(wr, wimg + p * 1024, (uint32_t)(co * a.ldw * 2 + off));
+    }
   }
   const int nn = wc * 32 + 8 * g;  // this lane's 8 output channels
   float bv[8];
@@ -2100,8 +2129,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
         for (int c = 0; c < 2; ++c) asm volatile("" ::"v"(bw[tap][kk][c]));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
-  auto zero_borders = [&]() {  // pixel rows 0 and W + 1 of every slot, and the zero slot S
-    for (int i = tid; i < S * 2 * 8; i += NWV * 64) {
+  auto zero_borders = [&]() {  // pixel rows 0 and W + 1 of every slot (STRIP: DMA'd per row), and the zero slot S
+    for (int i = tid; i < (STRIP ? 0 : S * 2 * 8); i += NWV * 64) {
       const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
       *(u32x4*)(smem + sl * SLOT + (side ? (W + 1) * 128 : 0) + ch * 16) = u32x4{0u, 0u, 0u, 0u};
     }
@@ -2129,14 +2158,34 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
   const int lc_lane = lane & 7;
   auto issue_row = [&](int q) {
     char* slot = smem + (q % S) * SLOT;
+    const bool qv = q >= 0 && q < T;
+    RowG rg{};
+    if constexpr (STRIP) rg = row_geom(q);
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       const int k = w * PPW + j;            // piece: pixel rows 1 + 8k .. 8 + 8k
       const int px = 1 + 8 * k + (lane >> 3);
       const int lc = lc_lane ^ (px & 7);    // logical 16-B chunk landing in physical slot lane & 7
-      const bool v = q >= 0 && q < T && lc * 8 < a.Cin;
-      const uint32_t off = (uint32_t)((((size_t)q * W + (px - 1)) * a.ldx + a.xcoff + lc * 8) * 2);
+      const bool v = qv && lc * 8 < a.Cin;
+      uint32_t off;
+      if constexpr (STRIP) off = src_off(rg.irow, rg.x0 + px - 1, lc);
+      else off = (uint32_t)((((size_t)q * W + (px - 1)) * a.ldx + a.xcoff + lc * 8) * 2);
       glds16(xr, slot + (1 + 8 * k) * 128, v ? off : SR_OOB);
+    }
+    if constexpr (STRIP) {
+      // wave 0: slot pixels 0..7 (the left border, 1..7 again as piece 0 has them), wave 1: W-6..W+1
+      // (W+1 the right border): a rewrite of the same bytes is harmless.  The image's outer columns
+      // load as zeros (OOB).  Other waves: one zero dummy into the zero slot (uniform vmcnt counts).
+      if (w < 2) {
+        const int pb = w == 0 ? 0 : W - 6;
+        const int px = pb + (lane >> 3);
+        const int lc = lc_lane ^ (px & 7);
+        const int sx = rg.x0 + px - 1;
+        const bool v = qv && (unsigned)sx < (unsigned)a.W && lc * 8 < a.Cin;
+        glds16(xr, slot + pb * 128, v ? src_off(rg.irow, sx, lc) : SR_OOB);
+      } else {
+        glds16(xr, smem + S * SLOT, SR_OOB);
+      }
     }
   };
   const bool gok = GATE != 3 || (nn >= a.gcol0 && nn < a.gcol1);
@@ -2152,9 +2201,10 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
   // gate / res / res2 of this wave's pixels of output row q into its staging buffer (NG ops)
   auto issue_staging = [&](int q) {
     const bool qv = q < T;
+    const size_t mb = row_geom(q).base;
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      const size_t m = (size_t)q * W + wp * PT * 16 + i * 16 + c16;
+      const size_t m = mb + wp * PT * 16 + i * 16 + c16;
       if constexpr (GATE != 0)
         glds16(gr, epi + i * 1024, qv && gok ? (uint32_t)((m * a.ldg + a.gcoff + nn) * 2) : SR_OOB);
       if constexpr (RES)
@@ -2176,7 +2226,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(bv[j]));
     asm volatile("" ::"v"(rsv));
-    vm_wait_dyn(s0 < s1 ? (LA + 1) * PPW + NG : 0);
+    vm_wait_dyn(s0 < s1 ? (LA + 1) * PPWX + NG : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     read_weights();
@@ -2198,7 +2248,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
       static_assert(STEADY <= 63, "band: too many vector memory ops in flight for vmcnt");
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEADY) : "memory");
     } else {
-      vm_wait_dyn((s0 + LA - 2 - s) * PPW + NG + (s - s0) * KROW);
+      vm_wait_dyn((s0 + LA - 2 - s) * PPWX + NG + (s - s0) * KROW);
     }
 #ifdef SR_BAND_STAMPS
     const unsigned long long t1 = __builtin_readcyclecounter();
@@ -2209,7 +2259,8 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
 #ifdef SR_BAND_STAMPS
     const unsigned long long t2 = __builtin_readcyclecounter();
 #endif
-    const int n_img = s / H, y = s - n_img * H;
+    const RowG rgs = row_geom(s);
+    const int n_img = STRIP ? 0 : s / H, y = rgs.y;
 
     f32x4 acc[PT][2];
 #pragma unroll
@@ -2292,7 +2343,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
     // this row's staging landed (issued before row s + LA - 1's pieces and row s - 1's stores)
     if constexpr (NG > 0) {
       if (s == s0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW + PT + NC) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPWX + PT + NC) : "memory");
     }
     float rs = a.alpha;
     if constexpr (RSC) rs = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, rsv), n_img - n0));
@@ -2376,13 +2427,13 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
     issue_row(s + LA);
 #pragma unroll
     for (int i = 0; i < PT; ++i) {
-      const size_t m = (size_t)s * W + wp * PT * 16 + i * 16 + c16;
+      const size_t m = rgs.base + wp * PT * 16 + i * 16 + c16;
       *(u32x4*)((bf16_t*)a.y + m * a.ldy + a.ycoff + nn) = ov[i];
     }
     if constexpr (AUX) {
 #pragma unroll
       for (int i = 0; i < PT; ++i) {
-        const size_t m = (size_t)s * W + wp * PT * 16 + i * 16 + c16;
+        const size_t m = rgs.base + wp * PT * 16 + i * 16 + c16;
         *(u32x4*)((bf16_t*)a.aux + m * a.ldy + a.ycoff + nn) = avx[i];
       }
     }
@@ -4350,6 +4401,20 @@ bool fwd_use_band(const FwdArgs& a, bool bf) {
   const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
   return band_epi(a, rows < gmax ? rows : gmax) >= 0;
 }
+// 64-channel-output convs on images wider than 128 px (W 256 / 512: the RRDBNet HR convs conv_up1 /
+// conv_up2 / conv_hr, their dgrads and conv_last's dgrad from its 8 padded output channels), and W 128
+// with the nearest x2 upsample folded in, as band launches over 128-px column strips (STRIP: E bit
+// 10): Cin 64 with a plain, ReLU, LeakyReLU or lrelu-gate epilogue, Cin 8..32 plain or gated.
+// Variant 76: the generic tile kernel for them (A/B, tests).
+bool fwd_use_band_strip(const FwdArgs& a, bool bf) {
+  if (!(bf && a.tap0 == 0 && (a.in_up == 1 || a.in_up == 2) && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
+        a.W % 128 == 0 && (a.W > 128 || a.in_up == 2) && (a.Cin == 64 || (a.Cin <= 32 && a.Cin % 8 == 0)) &&
+        a.Cout == 64 && a.Cout_real == a.Cout && !a.colsum && !a.dot && !a.row_scale && !a.res2 && !a.aux &&
+        g_variant != 1 && g_variant != 34 && g_variant != 76))
+    return false;
+  const int e = band_epi(a, 256);
+  return a.Cin == 64 ? (e == 0 || e == 1 || e == 2 || e == 4) : (e == 0 || e == 4);
+}
 // wider outputs (RRDB dense-block dgrads: Cout 96..192 from a 32- or 64-channel input) as
 // band launches over 64-channel output column slices: the narrow input is re-read per slice
 bool fwd_use_band_sliced(const FwdArgs& a, bool bf) {
@@ -4403,7 +4468,7 @@ bool fwd_use_tail(const FwdArgs& a, bool bf) {
 FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_tail(a, bf)) return FK_TAIL;
   if (fwd_use_lin(a, bf)) return FK_LIN;
-  if (fwd_use_band(a, bf)) return FK_BAND;
+  if (fwd_use_band(a, bf) || fwd_use_band_strip(a, bf)) return FK_BAND;
   if (fwd_use_band_sliced(a, bf)) return FK_BANDS;
   if (fwd_use_halo(a, bf)) return FK_HALO;
   // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
@@ -4458,7 +4523,31 @@ return hipGetLastError(); \
 #undef SR_BAND_E
   return hipErrorInvalidValue;
 }
+hipError_t launch_band_strip(const FwdArgs& a, hipStream_t s) {
+  const int rows = a.N * a.H * (a.W / 128);
+  FwdArgs ab = a;
+  ab.stamps = g_sr_stamps;
+  const int gmax = g_variant == 35 ? 64 : 256;  // 35: long bands crossing strips and images (tests)
+  const dim3 grid(rows < gmax ? rows : gmax);
+  if (a.Cin <= 32) {
+    switch (band_epi(a, grid.x)) {
+      case 0: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 1, 1024, 8>), grid, dim3(512), 0, s, ab); break;
+      case 4: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 1, 1028, 8>), grid, dim3(512), 0, s, ab); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  switch (band_epi(a, grid.x)) {
+    case 0: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 2, 1024, 8>), grid, dim3(512), 0, s, ab); break;
+    case 1: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 2, 1025, 8>), grid, dim3(512), 0, s, ab); break;
+    case 2: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 2, 1026, 8>), grid, dim3(512), 0, s, ab); break;
+    case 4: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 2, 1028, 8>), grid, dim3(512), 0, s, ab); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
+  if (a.W > 128 || a.in_up != 1) return launch_band_strip(a, s);
   if (band_nwv(a) == 8) return launch_band8(a, s);
   // one block per CU (one wave per SIMD: the weights live in registers); variant 35 forces 64 blocks
   // (long bands: ring wrap-around and image crossings inside a band, for tests).  (Two bands per CU
@@ -5010,10 +5099,10 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 
 // Kernel-variant switch for the parity tests' cross-checks: 0 = automatic, 1 = never a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels; the others each route one family to the kernel it replaced
-// (24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68: see their sites above).  The
+// (24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76: see their sites above).  The
 // measured-slower paths and the timing ablations were removed in round 6 (git history).
 int sr_conv3x3_set_variant(int variant) {
-  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68};
+  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76};
   bool ok = false;
   for (int v : kValid) ok = ok || v == variant;
   if (!ok) return sr_fail(SR_EINVAL, "conv3x3_set_variant: not a parity cross-check variant");

@@ -170,3 +170,31 @@ def test_async_hold_released_at_outermost_exit():
             C._ASYNC['hold'].append(dy)
         assert C._ASYNC['hold'] == [dy]  # inner exit: still inside the outer backward
     assert C._ASYNC['hold'] == []
+
+
+def test_strip_band_selection():
+    """Host-side choice of the column-strip band kernel (no GPU launch): the RRDBNet HR tail's 64-channel
+    convs at W 256 / 512 (with the nearest x2 upsample folded in for conv_up1 / conv_up2), conv_last's
+    8-channel dgrad, W 128 with the upsample; widths that are not whole 128-px strips and variant 76 stay
+    on the generic tile kernel."""
+    from basicsr4rs_amd.ops import conv as C
+    lib = _lib.load()
+    bf = torch.bfloat16
+
+    def name(N, H, W, cin, cout=64, **kw):
+        return lib.sr_conv3x3_fwd_kernel_name(C._desc(bf, N, H, W, cin, cin, cout, cout, cout, **kw))
+
+    band = b'conv3x3_fwd_band_kernel'
+    try:
+        assert name(16, 512, 512, 64) == band                 # conv_hr and the conv_hr / conv_up2 dgrads
+        assert name(16, 512, 512, 64, in_up=2) == band        # conv_up2
+        assert name(16, 256, 256, 64, in_up=2) == band        # conv_up1
+        assert name(16, 512, 512, 8) == band                  # conv_last dgrad (8 padded channels)
+        assert name(2, 64, 128, 64, in_up=2) == band          # one strip with the upsample
+        assert name(2, 96, 96, 64) != band                    # not whole strips
+        assert name(2, 64, 256, 64, cout=32) != band          # 64 output channels only
+        assert name(2, 64, 256, 40) != band                   # Cin 8..32 or 64
+        _lib.check(lib.sr_conv3x3_set_variant(76))
+        assert name(16, 512, 512, 64) != band
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
