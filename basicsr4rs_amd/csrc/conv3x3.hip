@@ -4415,6 +4415,14 @@ bool fwd_use_band_strip(const FwdArgs& a, bool bf) {
   const int e = band_epi(a, 256);
   return a.Cin == 64 ? (e == 0 || e == 1 || e == 2 || e == 4) : (e == 0 || e == 4);
 }
+// the same from a narrow input (Cin 8..32) into 128 / 192 / 256 output channels (EDSR's conv_last dgrad:
+// 8 padded channels -> 256 at HR): 64-channel output-column slices, the narrow input re-read per slice
+bool fwd_use_band_strip_sliced(const FwdArgs& a, bool bf) {
+  if (!(a.Cout > 64 && a.Cout <= 256 && a.Cout % 64 == 0 && a.Cin <= 32)) return false;
+  FwdArgs b = a;
+  b.Cout = b.Cout_real = 64;
+  return fwd_use_band_strip(b, bf);
+}
 // wider outputs (RRDB dense-block dgrads: Cout 96..192 from a 32- or 64-channel input) as
 // band launches over 64-channel output column slices: the narrow input is re-read per slice
 bool fwd_use_band_sliced(const FwdArgs& a, bool bf) {
@@ -4469,7 +4477,7 @@ FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_tail(a, bf)) return FK_TAIL;
   if (fwd_use_lin(a, bf)) return FK_LIN;
   if (fwd_use_band(a, bf) || fwd_use_band_strip(a, bf)) return FK_BAND;
-  if (fwd_use_band_sliced(a, bf)) return FK_BANDS;
+  if (fwd_use_band_sliced(a, bf) || fwd_use_band_strip_sliced(a, bf)) return FK_BANDS;
   if (fwd_use_halo(a, bf)) return FK_HALO;
   // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
   // kernel with a partial N tile: x read once (vs twice by 128x128 tiles); 68 -> 57 us and 82 -> 65 us

@@ -190,6 +190,9 @@ def test_strip_band_selection():
         assert name(16, 512, 512, 64, in_up=2) == band        # conv_up2
         assert name(16, 256, 256, 64, in_up=2) == band        # conv_up1
         assert name(16, 512, 512, 8) == band                  # conv_last dgrad (8 padded channels)
+        assert name(32, 256, 256, 8, cout=256) == band        # EDSR conv_last dgrad: 4 output slices
+        assert lib.sr_conv3x3_fwd_launches(C._desc(bf, 32, 256, 256, 8, 8, 256, 256, 256)) == 4
+        assert name(32, 256, 256, 64, cout=256) != band       # wide input: stays on the 256-wide kernels
         assert name(2, 64, 128, 64, in_up=2) == band          # one strip with the upsample
         assert name(2, 96, 96, 64) != band                    # not whole strips
         assert name(2, 64, 256, 64, cout=32) != band          # 64 output channels only

@@ -746,29 +746,32 @@ def test_fwd_halo_cout32_vs_fp64(cuda, cin, act):
     assert bool(((got - ref).abs() <= tol).all()), (got - ref).abs().max().item()
 
 
-@pytest.mark.parametrize('shape', [(2, 6, 256, 1, 64), (1, 5, 512, 1, 64), (3, 7, 384, 1, 64), (2, 4, 256, 2, 64),
-                                   (1, 6, 128, 2, 64), (2, 8, 512, 2, 64), (2, 5, 512, 1, 8), (1, 6, 256, 1, 32)])
+@pytest.mark.parametrize('shape', [(2, 6, 256, 1, 64, 64), (1, 5, 512, 1, 64, 64), (3, 7, 384, 1, 64, 64),
+                                   (2, 4, 256, 2, 64, 64), (1, 6, 128, 2, 64, 64), (2, 8, 512, 2, 64, 64),
+                                   (2, 5, 512, 1, 8, 64), (1, 6, 256, 1, 32, 64), (2, 5, 256, 1, 8, 256),
+                                   (1, 3, 384, 1, 16, 192)])
 @pytest.mark.parametrize('epi', ['plain', 'lrelu', 'gate'])
 @pytest.mark.parametrize('grid', [0, 35])
 def test_fwd_band_strips_vs_fp64(cuda, shape, epi, grid):
     """64-channel-output convs on images wider than 128 px, and W 128 with the nearest x2 upsample
     folded in: the band kernel over 128-px column strips (the RRDBNet HR convs conv_up1 / conv_up2 /
-    conv_hr, their dgrads and conv_last's 8-channel dgrad) -- each strip's border columns loaded from
+    conv_hr, their dgrads and conv_last's 8-channel dgrads; into 128-256 channels as 64-channel output
+    slices: EDSR's conv_last dgrad) -- each strip's border columns loaded from
     its neighbours, zeros at the image edges; strip rows crossing strips and images inside a band with
     variant 35 (64 blocks) -- against float64 on the same bf16 operands (relative L2 <= 4e-3 and every
     element within two bf16 steps plus 1e-3 of the range: a wrong border column or strip origin moves
     a whole pixel column by O(1)) and against the generic tile kernel it replaces (variant 76) within
     one bf16 rounding step."""
-    N, H, W, up, cin = shape
+    N, H, W, up, cin, cout = shape
     if cin < 64 and epi == 'lrelu':
         pytest.skip('narrow-input strips: plain and gated (dgrad) epilogues only')
     torch.manual_seed(31)
     dt = torch.bfloat16
     lib = _lib.load()
-    conv = nn.Conv2d(cin, 64, 3, 1, 1).to(cuda)
-    wf, _, bg = C.prepared(conv.weight, conv.bias, C.ConvSpec(cin, 64), dt)
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    wf, _, bg = C.prepared(conv.weight, conv.bias, C.ConvSpec(cin, cout), dt)
     x = torch.randn(N, H // up, W // up, cin, device=cuda).to(dt)
-    gate = torch.randn(N, H, W, 64, device=cuda).to(dt)
+    gate = torch.randn(N, H, W, cout, device=cuda).to(dt)
     kw = {'plain': {}, 'lrelu': dict(act=_lib.ACT_LRELU, slope=0.2),
           'gate': dict(gate=gate, gate_slope=0.2, alpha=0.5)}[epi]
     if up > 1:
@@ -777,11 +780,12 @@ def test_fwd_band_strips_vs_fp64(cuda, shape, epi, grid):
     try:
         for variant in (grid, 76):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
-            d = C._desc(dt, N, H, W, cin, cin, 64, 64, 64, in_up=up if up > 1 else 0)
+            d = C._desc(dt, N, H, W, cin, cin, cout, cout, cout, in_up=up if up > 1 else 0)
             name = lib.sr_conv3x3_fwd_kernel_name(d).decode()
             assert (name == 'conv3x3_fwd_band_kernel') == (variant != 76), (variant, name)
-            y = torch.empty(N, H, W, 64, device=cuda, dtype=dt)
-            C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, 64, 64, **kw)
+            assert lib.sr_conv3x3_fwd_launches(d) == (cout // 64 if variant != 76 else 1)
+            y = torch.empty(N, H, W, cout, device=cuda, dtype=dt)
+            C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, **kw)
             outs.append(y)
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
