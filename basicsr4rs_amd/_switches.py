@@ -14,6 +14,7 @@ SR_ROWSCALE_UNFUSED   1: the proj-branch DropPath gradient by a separate row-sca
 SR_SWIN_FUSED         0: a SwinIR block's attention half as three launches
 SR_LN_UNFUSED         1 / qkv / fc1: the standalone LayerNorm kernel + linear instead of the LN-prologue linear
 SR_CA_UNFUSED         1: the round-2 channel-attention launches
+SR_CA_DOT             1: channel-attention dots from the next block's dgrad epilogue (measured slower, A/B)
 SR_DCN_BWD_FUSED      0: the DCN backward through the dcols matrix
 SR_STEP_TRACE         host time stamps of the segmented DDP graph step (a file path)
 """
@@ -30,6 +31,7 @@ _DEFAULTS = {
     'SR_SWIN_FUSED': '1',
     'SR_LN_UNFUSED': None,
     'SR_CA_UNFUSED': '0',
+    'SR_CA_DOT': '0',
     'SR_DCN_BWD_FUSED': '1',
     'SR_STEP_TRACE': None,
 }

@@ -73,6 +73,7 @@ struct FwdArgs {
   const void* dot;  // band kernel, with colsum: partial sums of y * dot (sr_conv3x3_desc.dot)
   uint32_t d_bytes;
   int ldd, dcoff;
+  int cs_band;  // band kernel: colsum / dot partial rows summed over the band's rows (band_cs_rows), 0: per row
 };
 
 // alpha of output row m: a.alpha, times the per-image row_scale when given
@@ -1998,9 +1999,13 @@ SR_DEV void vm_wait_dyn(int n) { vm_wait_bs<0, 63>(n < 0 ? 0 : (n > 63 ? 63 : n)
 // channels gcol0..gcol1), 4 res, 5 res2, 6 aux, 7 colsum, 8 row_scale, 9 dot (with 7: the partial
 // sums are of y * dot, the dot operand staged like the residuals).
 // blocks per CU the band kernel is built for: two for the W 64 forms whose ring + staging fit
-// 80 KB of LDS and 256 registers (no second staging operand, no dot), one otherwise
+// 80 KB of LDS and 256 registers (no second staging operand), one otherwise.  And (round 6) the RCAB
+// conv1 dgrad with the dot epilogue (656: residual + dot staging, 82 KB): not for a second band block
+// but so that it shares a CU with a side-stream ring wgrad block (78 KB) as the plain residual form
+// does -- at one block per CU (the weight image beside the ring, 154 KB) it held whole CUs against the
+// side stream and RCAN ran 35.6 vs 33.6 ms
 constexpr int band_occ(int W, int E) {
-  return W == 64 && (E == 0 || E == 1 || E == 2 || E == 4 || E == 16 || E == 128) ? 2 : 1;
+  return W == 64 && (E == 0 || E == 1 || E == 2 || E == 4 || E == 16 || E == 128 || E == 656) ? 2 : 1;
 }
 // NWV: waves per block, 4 (one per SIMD) or 8 (two per SIMD, each with half the row's pixel
 // tiles, so one wave's epilogue and LDS waits overlap the other's MFMAs; the ring and the weight
@@ -2232,6 +2237,9 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
     read_weights();
   }
   const int n0 = s0 / H;
+  float cst[8];  // band-reduced channel sums (a.cs_band)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cst[j] = 0.f;
 
   // Per row, in issue order: [MFMAs] [epilogue] [staging of row s + 1: NG] [pieces of row
   // s + LA: PPW] [stores: PT + NC].  Vector memory ops complete in issue order, so a wait for
@@ -2439,12 +2447,19 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
     }
     if constexpr (CS) {
       // the 16 lanes of a g group hold the same 8 channels: fixed-order butterfly, then lane
-      // c16 == 0 writes partial row s * WP + wp (P = H * WP rows per image)
+      // c16 == 0 writes partial row s * WP + wp (P = H * WP rows per image) -- or, band-reduced
+      // (a.cs_band: every band is a.cs_band rows of one image), the running sum over the band's rows
+      // so far to partial row bb * WP + wp, so the last row's store leaves the band's sum
+      // (P = H / cs_band * WP rows per image; same-address stores of one wave land in order)
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1)
 #pragma unroll
         for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
-      float* dstp = a.colsum + ((size_t)s * WP + wp) * a.Cout + nn;
+      if (a.cs_band) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { cst[j] += cs[j]; cs[j] = cst[j]; }
+      }
+      float* dstp = a.colsum + ((size_t)(a.cs_band ? bb : s) * WP + wp) * a.Cout + nn;
       // exactly two vector store instructions per wave (lanes masked): counted in NC
       if (c16 == 0) *(f32x4*)dstp = f32x4{cs[0], cs[1], cs[2], cs[3]};
       if (c16 == 0) *(f32x4*)(dstp + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
@@ -4498,6 +4513,20 @@ void fwd_epi_geom(FwdKind k, int* rows, int* nt) {
 // waves per band block: 8 at W 128, 4 at W 64.  With channel sums
 // at Cout 32, 4: the partial rows per image (H x pixel waves) then match the tile and halo
 // epilogues' (H W / 128 x 4), so the count does not depend on which of them a call lands on.
+// Band-reduced channel sums: when the band grid splits the rows evenly and a band never crosses an
+// image (rows per band divides H), each band leaves one partial row per pixel wave instead of one per
+// row -- RCAN B 32: 16 instead of 128 partial rows per image, the count the standalone partials pass
+// (sr_channel_partials) gives, so the channel-attention kernels that sum them stage 8x less.  Returns
+// the rows per band, 0 when the sums stay per row.  Variant 37: per-row sums (tests).
+int band_grid(const FwdArgs& a) {
+  const int rows = a.N * a.H, gmax = g_variant == 35 ? 64 : 256;
+  return rows < gmax ? rows : gmax;
+}
+int band_cs_rows(const FwdArgs& a) {
+  const int T = a.N * a.H, G = band_grid(a);
+  if (g_variant == 37 || T % G || a.H % (T / G) || T / G < 2) return 0;
+  return T / G;
+}
 int band_nwv(const FwdArgs& a) {
   return a.W == 128 && !(a.Cout == 32 && (a.colsum || a.dot)) ? 8 : 4;
 }
@@ -4505,6 +4534,7 @@ hipError_t launch_band8(const FwdArgs& a, hipStream_t s) {
   const int rows = a.N * a.H;
   FwdArgs ab = a;
   ab.stamps = g_sr_stamps;
+  ab.cs_band = a.colsum ? band_cs_rows(a) : 0;
   const int gmax = g_variant == 35 ? 64 : 256;
   const dim3 grid(rows < gmax ? rows : gmax);
   const int e = band_epi(a, grid.x);
@@ -4565,6 +4595,7 @@ hipError_t launch_band(const FwdArgs& a, hipStream_t s) {
   const int gmax = g_variant == 35 ? 64 : 256;
   FwdArgs ab = a;
   ab.stamps = g_sr_stamps;
+  ab.cs_band = a.colsum ? band_cs_rows(a) : 0;
   const dim3 grid(rows < gmax ? rows : gmax);
   const int e = band_epi(a, grid.x);
   if (e == 656) {  // instantiated for the RCAN shapes only
@@ -4957,7 +4988,10 @@ int colsum_parts(const sr_conv3x3_desc* d, const FwdArgs& a0) {
   FwdArgs a = a0;
   a.colsum = &one;  // the kernel choice of a call that asks for the sums
   if (d->out_ps || d->out_nchw || fwd_kind(a, d->dtype == SR_BF16) == FK_LIN) return 0;
-  if (fwd_kind(a, d->dtype == SR_BF16) == FK_BAND) return d->H * (band_nwv(a) / (d->Cout / 32));  // rows x pixel waves
+  if (fwd_kind(a, d->dtype == SR_BF16) == FK_BAND) {  // (rows or bands) x pixel waves
+    const int rpb = band_cs_rows(a);
+    return (rpb ? d->H / rpb : d->H) * (band_nwv(a) / (d->Cout / 32));
+  }
   int rows, nt;
   fwd_epi_geom(fwd_kind(a, d->dtype == SR_BF16), &rows, &nt);
   const int HW = d->H * d->W;
@@ -5107,10 +5141,10 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 
 // Kernel-variant switch for the parity tests' cross-checks: 0 = automatic, 1 = never a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels; the others each route one family to the kernel it replaced
-// (24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76: see their sites above).  The
+// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76: see their sites above).  The
 // measured-slower paths and the timing ablations were removed in round 6 (git history).
 int sr_conv3x3_set_variant(int variant) {
-  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76};
+  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76};
   bool ok = false;
   for (int v : kValid) ok = ok || v == variant;
   if (!ok) return sr_fail(SR_EINVAL, "conv3x3_set_variant: not a parity cross-check variant");

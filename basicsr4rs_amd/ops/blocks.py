@@ -56,12 +56,44 @@ def _colsum_ok(N, H, W, spec, dtype):
     return _lib.load().sr_conv3x3_fwd_colsum_parts(d) > 0
 
 
+# SR_CA_DOT=1 (opt-in): the channel-attention dot partials dy * u from the next block's conv1 dgrad
+# epilogue (the band kernel's dot epilogue) instead of their own pass (sr_channel_partials).  Measured
+# slower every round: rounds 3-5 blamed the band kernel's 128 partial rows per image, which ca_bwd_apply
+# stages per block; round 6 sums them per band (16 rows per image at B 32, the pass's own count) and it
+# is still slower (RCAN x4 35.15 / 35.15 vs 33.49 / 33.35 ms, profiles/r06/ab/cadot/): the dot form of
+# the dgrad runs 30.2 vs 20.1 us (residual only), more than the 8.9 us pass it replaces.
+_CA_DOT_FUSED = switch('SR_CA_DOT') == '1'
+
+
+def _dot_parts_put(dx, parts, u):
+    """Attach the partial dots of dx * u (the previous RCAB's conv2 output) to dx, with dx's version
+    counter: autograd hands dx to that block's backward as its dy."""
+    dx._sr_ca_dot = (parts, u.data_ptr(), dx._version)
+
+
+def _dot_parts_take(dy, u):
+    """The fused partial dots of dy * u if dy carries them for this u and was not modified since (an
+    in-place gradient accumulation bumps the version); else None."""
+    e = getattr(dy, '_sr_ca_dot', None)
+    if e is None:
+        return None
+    dy._sr_ca_dot = None
+    parts, uptr, ver = e
+    return parts if (uptr == u.data_ptr() and dy._version == ver) else None
+
+
 class _RCAB(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, aw1, ab1, aw2, ab2, spec1, spec2, rs):
         dtype = x.dtype
         N, H, W, Cp = x.shape
+        # x is the previous RCAB's output: its conv2 output u rides on it (_sr_ca_u), and this block's
+        # conv1 dgrad -- which produces that block's dy -- also emits the partial dots dy * u its
+        # channel-attention backward needs (the band kernel's dot epilogue, _dot_parts_put / _take)
+        u_prev = getattr(x, '_sr_ca_u', None) if _CA_DOT_FUSED else None
+        ctx.u_prev = u_prev if (u_prev is not None and u_prev.shape == x.shape and u_prev.dtype == dtype and
+                                C.dot_partials_ok(dtype, N, H, W, spec1.cout_p, spec1.cin_p)) else None
         wf1, _, bg1 = C.prepared(w1, b1, spec1, dtype)
         wf2, _, bg2 = C.prepared(w2, b2, spec2, dtype)
         t = torch.empty(N, H, W, spec1.cout_p, device=x.device, dtype=dtype)
@@ -98,6 +130,7 @@ class _RCAB(torch.autograd.Function):
             ctx.specs = (spec1, spec2)
             ctx.rs = rs
             ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2)
+            y._sr_ca_u = u
             return y
         y = torch.empty_like(u)
         # squeeze MLP + y = x + rs * u * s in one launch (csrc/blocks.hip ca_fwd_apply_kernel)
@@ -110,6 +143,7 @@ class _RCAB(torch.autograd.Function):
         ctx.specs = (spec1, spec2)
         ctx.rs = rs
         ctx.save_for_backward(x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2)
+        y._sr_ca_u = u
         return y
 
     @staticmethod
@@ -129,16 +163,14 @@ class _RCAB(torch.autograd.Function):
         Cr = aw1.shape[0]
         a1 = aw1.detach().reshape(Cr, -1)
         a2 = aw2.detach().reshape(-1, Cr)
+        parts = _dot_parts_take(dy, u)  # emitted by the next block's conv1 dgrad, which produced dy
         dy = dy.to(dtype).contiguous()
         lib = _lib.load()
-        # dL/ds[n,c] = rs * sum_p dy*u: per-chunk dot partials, summed in the MLP backward kernel.  (The
-        # band kernel can emit them from the next block's conv1 dgrad epilogue -- the C ABI's `dot`
-        # epilogue, test_band_dot_partials -- measured slower on RCAN (40.3 vs 37.7 ms): its 128 partial
-        # rows per image make ca_bwd_apply, which stages every partial row of its image, the slower
-        # kernel; the SR_CA_DOT opt-in was removed in round 6.)
-        parts = torch.empty(N, lib.sr_channel_partials_count(H * W), Cp, device=x.device, dtype=torch.float32)
-        _lib.check(lib.sr_channel_partials(_lib.dtype_code(dtype), _lib.ptr(dy), Cp, 0, _lib.ptr(u), Cp, 0, N,
-                                           H * W, Cp, _lib.ptr(parts), _lib.stream()))
+        if parts is None:
+            # dL/ds[n,c] = rs * sum_p dy*u: per-chunk dot partials, summed in the MLP backward kernel
+            parts = torch.empty(N, lib.sr_channel_partials_count(H * W), Cp, device=x.device, dtype=torch.float32)
+            _lib.check(lib.sr_channel_partials(_lib.dtype_code(dtype), _lib.ptr(dy), Cp, 0, _lib.ptr(u), Cp, 0, N,
+                                               H * W, Cp, _lib.ptr(parts), _lib.stream()))
         if not ctx.ca_fused or parts.shape[1] * Cp > 8192:
             return _RCAB._backward_unfused(ctx, dy, parts, x, t, u, pool, h, s, w1, b1, w2, b2, aw1, aw2, ab1, ab2,
                                            spec1, spec2, rs, a1, a2, Cr, N, H, W, Cp, dtype)
@@ -179,7 +211,12 @@ class _RCAB(torch.autograd.Function):
         C.conv_fwd_raw(du, wd2, None, dz1, N, H, W, spec2.cout_p, spec2.cin_p, spec2.cin_p, gate=t, gate_slope=0.0)
         dw2, db2 = C.conv_wgrad_raw(du, t, N, H, W, spec2.cin_p, spec2.cin, spec2.cout_p, spec2.cout, params=(w2, b2))
         dx = torch.empty_like(x)
-        C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
+        if ctx.u_prev is not None:  # dx is the previous block's dy: its CA dot partials in the same pass
+            _, dparts = C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy,
+                                       beta=1.0, colsum=True, dot=ctx.u_prev)
+            _dot_parts_put(dx, dparts, ctx.u_prev)
+        else:
+            C.conv_fwd_raw(dz1, wd1, None, dx, N, H, W, spec1.cout_p, spec1.cin_p, spec1.cin_p, res=dy, beta=1.0)
         dw1, db1 = C.conv_wgrad_raw(dz1, x, N, H, W, spec1.cin_p, spec1.cin, spec1.cout_p, spec1.cout, params=(w1, b1))
         if direct:
             return dx, dw1, db1, dw2, db2, None, None, None, None, None, None, None

@@ -74,8 +74,17 @@ def test_colsum_geometry():
     from basicsr4rs_amd.ops import conv as C
     lib = _lib.load()
     bf = torch.bfloat16
-    # RCAN body conv: narrow halo kernel, 128-row epilogue chunks x 4 waves
-    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 32, 64, 64, 64, 64, 64, 64, 64)) == 4096 // 128 * 4
+    # RCAN body conv: band kernel, 8 rows per band (2048 rows over 256 bands) x 2 pixel waves, summed per
+    # band (round 6; per row: 64 x 2); variant 37 keeps the per-row sums, and so do one-row bands (B 3: 192
+    # rows) and bands that do not divide the image height (B 12: 3 rows per band)
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 32, 64, 64, 64, 64, 64, 64, 64)) == 64 // 8 * 2
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 3, 64, 64, 64, 64, 64, 64, 64)) == 64 * 2
+    assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 12, 64, 64, 64, 64, 64, 64, 64)) == 64 * 2
+    try:
+        _lib.check(lib.sr_conv3x3_set_variant(37))
+        assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 32, 64, 64, 64, 64, 64, 64, 64)) == 64 * 2
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
     # EDSR-L body conv: 256x256 phase-interleaved kernel, 8 waves per 128-row chunk
     assert lib.sr_conv3x3_fwd_colsum_parts(C._desc(bf, 32, 64, 64, 256, 256, 256, 256, 256)) == 4096 // 128 * 8
     # Cout 16: 256-row chunks of 4 waves
@@ -201,3 +210,17 @@ def test_strip_band_selection():
         assert name(16, 512, 512, 64) != band
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
+
+
+def test_dot_parts_handoff():
+    """The RCAB dot-partials hand-off takes the partials only for the same u and an unmodified dy, once."""
+    from basicsr4rs_amd.ops import blocks as B
+    u, dy, parts = torch.zeros(2, 3), torch.zeros(2, 3), torch.ones(1)
+    B._dot_parts_put(dy, parts, u)
+    assert B._dot_parts_take(dy, torch.zeros(2, 3)) is None  # another u
+    B._dot_parts_put(dy, parts, u)
+    dy.add_(1.0)  # an in-place accumulation after the hand-off
+    assert B._dot_parts_take(dy, u) is None
+    B._dot_parts_put(dy, parts, u)
+    assert B._dot_parts_take(dy, u) is parts
+    assert B._dot_parts_take(dy, u) is None  # consumed

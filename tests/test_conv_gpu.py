@@ -916,12 +916,20 @@ def test_two_interval_schedule_bitwise(cuda, shape):
             assert torch.equal(a, b), (v, name, (a.float() - b.float()).abs().max().item())
 
 
-@pytest.mark.parametrize('shape', [(2, 64, 64), (3, 20, 128), (1, 5, 64)])
+@pytest.mark.parametrize('shape', [(2, 64, 64), (3, 20, 128), (1, 5, 64), (32, 64, 64), (8, 64, 64), (16, 32, 128)])
 def test_band_dot_partials(cuda, shape):
     """Band kernel residual + dot epilogue (RCAB conv1 dgrad with the previous block's channel-attention
     dot fused, rcan_arch.py:19-27): y equals the plain residual call bitwise, and the partial rows sum
-    per image to sum_p y[n, p, c] * dot[n, p, c] over the stored bf16 y (fp64 reference, fp32 sums)."""
+    per image to sum_p y[n, p, c] * dot[n, p, c] over the stored bf16 y (fp64 reference, fp32 sums) --
+    per-row partials and (round 6) partials summed over each band (RCAN B 32: 8 rows per band, 16 partial
+    rows per image), whose count the host query reports."""
     N, H, W = shape
+    rows = N * H
+    rpb = rows // 256 if rows % 256 == 0 and rows >= 512 and H % (rows // 256) == 0 else 0
+    lib0 = _lib.load()
+    d = C._desc(torch.bfloat16, N, H, W, 64, 64, 64, 64, 64)
+    P = lib0.sr_conv3x3_fwd_colsum_parts(d)
+    assert P == (H // rpb if rpb else H) * (8 if W == 128 else 4) // 2, (P, rpb)
     cin = cout = 64
     dt = torch.bfloat16
     torch.manual_seed(21)
@@ -937,6 +945,7 @@ def test_band_dot_partials(cuda, shape):
     y1, parts = C.conv_fwd_raw(x, wf, None, y1, N, H, W, cin, cout, cout, res=res, beta=1.0, colsum=True, dot=dot)
     torch.cuda.synchronize()
     assert torch.equal(y0, y1)
+    assert parts.shape == (N, P, cout)
     ref = (y1.double() * dot.double()).sum((1, 2))
     got = parts.double().sum(1)
     scale = (y1.double() * dot.double()).abs().sum((1, 2)).max().item()
