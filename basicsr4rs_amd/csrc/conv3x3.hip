@@ -74,6 +74,7 @@ struct FwdArgs {
   uint32_t d_bytes;
   int ldd, dcoff;
   int cs_band;  // band kernel: colsum / dot partial rows summed over the band's rows (band_cs_rows), 0: per row
+  int strip64;  // pph kernel over 64-px column strips of a wider image: 256-row tiles are 4 rows x 64 px
 };
 
 // alpha of output row m: a.alpha, times the per-image row_scale when given
@@ -108,13 +109,26 @@ SR_DEV uint32_t swz128(uint32_t r, uint32_t c) { return r * 128u + ((c ^ (r & 7u
 template <typename T, int ROWS, int BN, int NT>
 SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, int n0, int tid) {
   constexpr int SZ = Elt<T>::SIZE;
+  // tile row -> NHWC pixel: m0 + row, or (a.strip64: the pph kernel's column strips, tiles ordered
+  // (image, strip, 4-row block)) row r of the 256-row tile is pixel (r / 64, r % 64) of its block
+  int sbase = 0;
+  if (a.strip64) {
+    const int tm = m0 >> 8, tps = a.H >> 2, ns = a.W >> 6;
+    const int img = tm / (tps * ns), rem = tm - img * tps * ns, j = rem / tps, yb = rem - j * tps;
+    sbase = (img * a.H + yb * 4) * a.W + j * 64;
+  }
+  auto mpix = [&](int row) -> int {
+    if (!a.strip64) return m0 + row;
+    const int rr = (m0 & 255) + row;
+    return sbase + (rr >> 6) * a.W + (rr & 63);
+  };
   if (a.out_nchw) {
     float* y = (float*)a.y;
     const int HW = a.H * a.W;
     for (int idx = tid; idx < ROWS * BN; idx += NT) {
       const int row = idx % ROWS, col = idx / ROWS;
-      const int m = m0 + row, n = n0 + col;
-      if (m >= a.M || n >= a.Cout_real) continue;
+      const int m = mpix(row), n = n0 + col;
+      if (m0 + row >= a.M || n >= a.Cout_real) continue;
       float v = Cs[row * CSTR + col] + (a.bias ? a.bias[n] : 0.f);
       v = act_apply(v, a.act, a.slope) * row_alpha(a, m);
       v = v * (a.aff_scale ? a.aff_scale[n] : 1.f) + (a.aff_shift ? a.aff_shift[n] : 0.f);
@@ -146,8 +160,8 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
     const int it = ib;
     const int idx = tid + (it0 + ib) * NT;
     const int row = idx / CG, cg = idx % CG;
-    const int m = m0 + row, n = n0 + cg * 8;
-    const bool ok = m < a.M && n < a.Cout;
+    const int m = mpix(row), n = n0 + cg * 8;
+    const bool ok = m0 + row < a.M && n < a.Cout;
     const bool okr = ok && n < a.rcols;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -176,8 +190,8 @@ SR_DEV void epilogue_tile(const FwdArgs& a, const float* Cs, int CSTR, int m0, i
   for (int it = 0; it < IB; ++it) {
     const int idx = tid + (it0 + it) * NT;
     const int row = idx / CG, cg = idx % CG;
-    const int m = m0 + row, n = n0 + cg * 8;
-    if (m >= a.M || n >= a.Cout) continue;
+    const int m = mpix(row), n = n0 + cg * 8;
+    if (m0 + row >= a.M || n >= a.Cout) continue;
     float v[8];
     const f32x4 c0 = *(const f32x4*)(Cs + row * CSTR + cg * 8);
     const f32x4 c1 = *(const f32x4*)(Cs + row * CSTR + cg * 8 + 4);
@@ -881,8 +895,15 @@ struct PphGeom {
 // the issue order is [B(t+2) 4 ops][halo(t) 1 op]; the retire point (as above) waits vmcnt(6),
 // which retires B(t+2)'s predecessor B(t+1) and every older halo piece (a halo piece issued at step
 // t is then visible from step t+3 on; the ring schedule's first uses are >= 4 steps after issue).
-template <int R, int P2 = 0>
+// STRIP (R 4, P2 2): images wider than 64 px (W 256 / 512: EDSR at LR 256) as 64-px column strips,
+// tiles ordered (image, strip, 4-row block); each halo row also DMAs its two border columns from the
+// neighbouring strips (waves 0 / 1: slot pixels 0..7 and 58..65, the overlap rewriting bytes the row's
+// own pieces hold; zeros at the image edges; the other waves a zero dummy, so every halo issue is two
+// ops per wave and the retire point counts 8 instead of 6), and the epilogue maps tile rows to pixels
+// (FwdArgs.strip64)
+template <int R, int P2 = 0, bool STRIP = false>
 __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
+  static_assert(!STRIP || (R == 4 && P2 == 2), "pph strips: the R 4 two-interval form");
   using G = PphGeom<R>;
   constexpr int W = G::W, RH = R + 2;
   constexpr int CSTR = 256 + 4;
@@ -895,9 +916,18 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   const uint32_t tile = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (int)(tile / a.tiles_n) * 256;
   const int n0 = (int)(tile % a.tiles_n) * 256;
-  const int HW = a.H * W;
-  const int img = m0 / HW;
-  const int y0 = (m0 - img * HW) / W;
+  int img, y0, sx0 = 0;  // image, first row, first column of the tile (sx0: STRIP)
+  if constexpr (STRIP) {
+    const int tm = m0 >> 8, tps = a.H >> 2, ns = a.W >> 6;
+    img = tm / (tps * ns);
+    const int rem = tm - img * tps * ns, j = rem / tps;
+    y0 = (rem - j * tps) * 4;
+    sx0 = j * 64;
+  } else {
+    const int HW = a.H * W;
+    img = m0 / HW;
+    y0 = (m0 - img * HW) / W;
+  }
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const __amdgpu_buffer_rsrc_t wr_ = make_rsrc(a.w, a.w_bytes);
 
@@ -916,8 +946,8 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   // (y r + si, x r + sj) (sl = si r + sj) channel cch: rows r HR rows apart, pixels r apart, and a
   // per-chunk (si, sj, cch) offset instead of cc * 128
   const int rps = a.in_ps > 0 ? a.in_ps : 1;
-  const uint32_t hlane = (uint32_t)((8 * w + (lane >> 3)) * rps * a.ldx + a.xcoff) * 2u + (uint32_t)ch_h * 16u;
-  const uint32_t rowb = (uint32_t)(W * rps * rps * a.ldx) * 2u;
+  const uint32_t hlane = (uint32_t)((sx0 + 8 * w + (lane >> 3)) * rps * a.ldx + a.xcoff) * 2u + (uint32_t)ch_h * 16u;
+  const uint32_t rowb = (uint32_t)((STRIP ? a.W : W) * rps * rps * a.ldx) * 2u;
   const uint32_t pieceb = (uint32_t)(64 * rps * a.ldx) * 2u;
   auto chunk_off = [&](int cc) -> uint32_t {
     if (a.in_ps == 0) return (uint32_t)cc * 128u;
@@ -928,7 +958,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
   };
 
   if (tid < 64) *(u32x4*)(smem + G::ZERO + tid * 16) = u32x4{0u, 0u, 0u, 0u};
-  if (tid < G::NSLOT * 16) {  // border columns (slot px index 0 and W + 1) of every slot
+  if (!STRIP && tid < G::NSLOT * 16) {  // border columns (slot px index 0 and W + 1) of every slot
     const int sl = tid >> 4, e = tid & 15;
     *(u32x4*)(smem + PPH_SLOT0 + sl * G::ROWB + (e < 8 ? 0 : (W + 1) * 128) + (e & 7) * 16) =
         u32x4{0u, 0u, 0u, 0u};
@@ -946,6 +976,7 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
 
   const int nchunk = a.Cin >> 6;
   const int nk = nchunk * 9;
+  auto issue_dummy = [&]() { glds16(xr, smem + G::ZERO, SR_OOB); };
   auto issue_row = [&](int cc, int rr, int p) {  // piece p of row rr of chunk cc into its slot
     const int y = y0 - 1 + rr;
     const int slot = (RH * cc + rr) % G::NSLOT;
@@ -953,16 +984,32 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
            (unsigned)y < (unsigned)a.H
                ? (uint32_t)(img * a.H + y) * rowb + (uint32_t)p * pieceb + hlane + chunk_off(cc)
                : SR_OOB);
+    if constexpr (STRIP) {  // the strip's border columns (see the kernel comment)
+      if (w < 2) {
+        const int q = (w == 0 ? 0 : W - 6) + (lane >> 3);  // slot px index
+        const int sx = sx0 + q - 1;
+        const int lcb = (lane & 7) ^ (q & 7);
+        const bool v = (unsigned)y < (unsigned)a.H && (unsigned)sx < (unsigned)a.W;
+        glds16(xr, smem + PPH_SLOT0 + slot * G::ROWB + (w == 0 ? 0 : (W - 6) * 128),
+               v ? (uint32_t)(((img * a.H + y) * a.W + sx) * a.ldx + a.xcoff) * 2u + (uint32_t)lcb * 16u + chunk_off(cc)
+                 : SR_OOB);
+      } else {
+        issue_dummy();
+      }
+    }
   };
-  auto issue_dummy = [&]() { glds16(xr, smem + G::ZERO, SR_OOB); };
+  auto issue_halo_dummy = [&]() {  // a halo issue's op count without a row
+    issue_dummy();
+    if constexpr (STRIP) issue_dummy();
+  };
   // the halo piece issued at tap j of chunk cc (ring schedule above)
   auto issue_halo = [&](int cc, int j) {
     if constexpr (R == 4) {
-      if (j < 6 && cc + 1 < nchunk) issue_row(cc + 1, j, 0); else issue_dummy();
+      if (j < 6 && cc + 1 < nchunk) issue_row(cc + 1, j, 0); else issue_halo_dummy();
     } else {
       if (j < 2) issue_row(cc, 3, j);
       else if (j < 8 && cc + 1 < nchunk) issue_row(cc + 1, (j - 2) >> 1, j & 1);
-      else issue_dummy();
+      else issue_halo_dummy();
     }
   };
   // B half g of K-step (chunk kc, tap kt): weight columns kt*Cin + kc*64
@@ -1072,11 +1119,19 @@ __global__ __launch_bounds__(512) void conv3x3_fwd_pph_kernel(FwdArgs a) {
       if (t + 2 < nk) { issue_b(buf, n2cc, n2tap, 0); issue_b(buf, n2cc, n2tap, 1); }
       else { issue_b_dummy(); issue_b_dummy(); }
       issue_halo(cc, tap);
-      if (wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (STRIP) {  // the halo issues are two ops: [halo(t-1) 2][B(t+2) 4][halo(t) 2]
+        if (wr) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        if (wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
       pp_barrier();
       mma(1, 1);
       mma(1, 0);
-      if (!wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if constexpr (STRIP) {
+        if (!wr) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        if (!wr) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      }
       pp_barrier();
       cc = ncc;
       tap = ntap;
@@ -4324,6 +4379,13 @@ hipError_t launch_fwd(const FwdArgs& a0, hipStream_t s) {
   return hipGetLastError();
 }
 
+// pph over 64-px column strips (STRIP): bf16, W a multiple of 64 above 128 (EDSR at LR 256: the body
+// convs and their dgrads), H a multiple of 4, no pixel-shuffled input, no channel sums.  Variant 77:
+// the pp kernel for them (A/B, tests).
+bool fwd_use_pph_strip(const FwdArgs& a) {
+  return g_variant != 2 && g_variant != 24 && g_variant != 77 && a.W > 128 && a.W % 64 == 0 && a.H % 4 == 0 &&
+         a.Cin % 64 == 0 && a.in_ps == 0 && a.in_up == 1 && a.tap0 == 0 && !a.colsum;
+}
 // Halo variant of the 256x256 kernel: whole-row tiles of W = 64 / 128 images, 64-channel chunks.
 bool fwd_use_pph(const FwdArgs& a) {
   return g_variant != 2 && g_variant != 24 &&
@@ -4338,7 +4400,10 @@ hipError_t launch_fwd_big(const FwdArgs& a0, hipStream_t s) {
   a.tiles = tm * a.tiles_n;
   if (g_variant == 2)
     hipLaunchKernelGGL(conv3x3_fwd_big_kernel, dim3(a.tiles), dim3(512), 0, s, a);
-  else if (fwd_use_pph(a) && a.W == 128 && g_variant != 59)
+  else if (fwd_use_pph_strip(a)) {
+    a.strip64 = 1;
+    hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<4, 2, true>), dim3(a.tiles), dim3(512), 0, s, a);
+  } else if (fwd_use_pph(a) && a.W == 128 && g_variant != 59)
     if (g_variant == 61) hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 1>), dim3(a.tiles), dim3(512), 0, s, a);
     else hipLaunchKernelGGL((conv3x3_fwd_pph_kernel<2, 2>), dim3(a.tiles), dim3(512), 0, s, a);
   else if (fwd_use_pph(a) && a.W == 128)
@@ -5116,7 +5181,7 @@ const char* sr_conv3x3_fwd_kernel_name(const sr_conv3x3_desc* d) {
     case FK_BANDS: return "conv3x3_fwd_band_kernel";
     case FK_BIG: {
       if (g_variant == 2) return "conv3x3_fwd_big_kernel";
-      return fwd_use_pph(fwd_shape(d)) ? "conv3x3_fwd_pph_kernel" : "conv3x3_fwd_pp_kernel";
+      return fwd_use_pph(fwd_shape(d)) || fwd_use_pph_strip(fwd_shape(d)) ? "conv3x3_fwd_pph_kernel" : "conv3x3_fwd_pp_kernel";
     }
     case FK_256_16: return bf ? "conv3x3_fwd_kernel<bf16,256,16>" : "conv3x3_fwd_kernel<f32,256,16>";
     case FK_256_32: return bf ? "conv3x3_fwd_kernel<bf16,256,32>" : "conv3x3_fwd_kernel<f32,256,32>";
@@ -5141,10 +5206,10 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 
 // Kernel-variant switch for the parity tests' cross-checks: 0 = automatic, 1 = never a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels; the others each route one family to the kernel it replaced
-// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76: see their sites above).  The
+// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77: see their sites above).  The
 // measured-slower paths and the timing ablations were removed in round 6 (git history).
 int sr_conv3x3_set_variant(int variant) {
-  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76};
+  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77};
   bool ok = false;
   for (int v : kValid) ok = ok || v == variant;
   if (!ok) return sr_fail(SR_EINVAL, "conv3x3_set_variant: not a parity cross-check variant");

@@ -202,12 +202,16 @@ def test_strip_band_selection():
         assert name(32, 256, 256, 8, cout=256) == band        # EDSR conv_last dgrad: 4 output slices
         assert lib.sr_conv3x3_fwd_launches(C._desc(bf, 32, 256, 256, 8, 8, 256, 256, 256)) == 4
         assert name(32, 256, 256, 64, cout=256) != band       # wide input: stays on the 256-wide kernels
+        assert name(2, 256, 256, 256, cout=256) == b'conv3x3_fwd_pph_kernel'  # EDSR body at LR 256: pph strips
+        assert name(2, 256, 256, 256, cout=1024, out_ps=2) == b'conv3x3_fwd_pph_kernel'
         assert name(2, 64, 128, 64, in_up=2) == band          # one strip with the upsample
         assert name(2, 96, 96, 64) != band                    # not whole strips
         assert name(2, 64, 256, 64, cout=32) != band          # 64 output channels only
         assert name(2, 64, 256, 40) != band                   # Cin 8..32 or 64
         _lib.check(lib.sr_conv3x3_set_variant(76))
         assert name(16, 512, 512, 64) != band
+        _lib.check(lib.sr_conv3x3_set_variant(77))
+        assert name(2, 256, 256, 256, cout=256) == b'conv3x3_fwd_pp_kernel'
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))
 

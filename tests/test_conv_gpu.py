@@ -878,6 +878,53 @@ def test_fwd_halo_pixel_shuffled_input(cuda, shape):
     assert (outs[0].float() - outs[1].float()).abs().max().item() <= tol
 
 
+@pytest.mark.parametrize('shape', [(2, 8, 256, 256, 256, 0), (1, 4, 512, 64, 256, 0), (1, 8, 192, 128, 256, 0),
+                                   (1, 4, 256, 256, 1024, 2), (3, 12, 320, 64, 320, 0)])
+@pytest.mark.parametrize('epi', ['plain', 'relu_res'])
+def test_fwd_pph_strips(cuda, shape, epi):
+    """The halo-row pph kernel over 64-px column strips of images wider than 128 px (EDSR at LR 256: the
+    body convs, their dgrads and the upsample convs' pixel-shuffled stores): tiles of 4 rows x 64 px, each
+    halo row's two border columns DMA'd from the neighbouring strips (zeros at the image edges), the
+    epilogue mapping tile rows to pixels -- against float64 on the same bf16 operands (every element within
+    two bf16 steps plus 1e-3 of the range) and against the per-tap pp kernel it replaces (variant 77)
+    within one bf16 step; 3 and 5 strips, a partial 256-channel tile, the pixel-shuffled store."""
+    N, H, W, cin, cout, ps = shape
+    torch.manual_seed(41)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    conv = nn.Conv2d(cin, cout, 3, 1, 1).to(cuda)
+    spec = C.ConvSpec(cin, cout, out_ps=ps)
+    wf, _, bg = C.prepared(conv.weight, conv.bias, spec, dt)
+    x = torch.randn(N, H, W, cin, device=cuda).to(dt)
+    yshape = C._out_shape(spec, N, H, W)
+    res = torch.randn(yshape, device=cuda).to(dt) if epi == 'relu_res' and ps == 0 else None
+    kw = dict(act=_lib.ACT_RELU) if epi == 'relu_res' else {}
+    outs = []
+    try:
+        for variant in (0, 77):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            name = lib.sr_conv3x3_fwd_kernel_name(C._desc(dt, N, H, W, cin, cin, cout, cout, cout, out_ps=ps))
+            assert (name == b'conv3x3_fwd_pph_kernel') == (variant == 0), (variant, name)
+            y = torch.empty(yshape, device=cuda, dtype=dt)
+            C.conv_fwd_raw(x, wf, bg, y, N, H, W, cin, cout, cout, out_ps=ps, res=res, **kw)
+            outs.append(y)
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double().cpu(), bf(conv.weight.detach().cpu()).double(),
+                   conv.bias.detach().cpu().double(), padding=1)
+    if ps:
+        ref = F.pixel_shuffle(ref, ps)
+    if epi == 'relu_res':
+        ref = F.relu(ref)
+        if res is not None:
+            ref = ref + res.permute(0, 3, 1, 2).double().cpu()
+    got = outs[0].permute(0, 3, 1, 2).double().cpu()
+    tol = ref.abs() * 2.0 ** -7 + 1e-3 * ref.abs().max().item()
+    assert bool(((got - ref).abs() <= tol).all()), (got - ref).abs().max().item()
+    _same_or_ulp(outs[0], outs[1], exact=False)
+
+
 @pytest.mark.parametrize('shape', [(2, 256, 256, 64, 0), (1, 256, 1024, 64, 2), (1, 256, 1024, 128, 2),
                                    (2, 128, 128, 128, 0)])
 def test_two_interval_schedule_bitwise(cuda, shape):
