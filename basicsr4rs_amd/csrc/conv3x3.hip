@@ -2086,7 +2086,9 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
   constexpr int NC = (CS ? 2 : 0) + (AUX ? PT : 0);  // stores after the PT output stores
   constexpr int PPWX = PPW + (STRIP ? 1 : 0);  // + the strip's border piece (or a dummy) per wave
   constexpr int KROW = NG + PPWX + PT + NC;           // vector memory ops per wave per row
-  constexpr int EPI = (NSTG ? NSTG : 1) * PT * 1024;  // per-wave staging
+  // per-wave staging (none for the wide strip forms without epilogue operands, CO > 64: their LDS is
+  // the weight image's)
+  constexpr int EPI = (NSTG ? NSTG : (CO > 64 ? 0 : 1)) * PT * 1024;
   constexpr int CIN = 32 * KH;
   constexpr int WROW = 9 * CIN * 2;  // bytes of one output channel's weights [tap][ci]
   constexpr int WBYTES = CO * WROW;
@@ -2340,7 +2342,7 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
     // before its use and exposes the full LDS latency per 2 MFMAs (one wave per SIMD has nothing
     // else to run).
     constexpr int NK = 9 * KH;
-    constexpr int FD = 5;
+    constexpr int FD = PT >= 8 ? 2 : 5;  // 8 pixel tiles (CO 256 over 8 waves): 2 K steps of fragments
     u32x4 fa[FD][PT];
     uint32_t rbase[3];
 #pragma unroll
@@ -2378,6 +2380,13 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
           case 6: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(f[0]), "+v"(f[1])); break;
           default: asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1])); break;
         }
+      } else if constexpr (PT == 8) {
+        if (ahead == 0)
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]),
+                       "+v"(f[6]), "+v"(f[7]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]),
+                       "+v"(f[6]), "+v"(f[7]));
       } else {
         switch (ahead) {
           case 0: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3])); break;
@@ -4489,16 +4498,20 @@ bool fwd_use_band(const FwdArgs& a, bool bf) {
 bool fwd_use_band_strip(const FwdArgs& a, bool bf) {
   if (!(bf && a.tap0 == 0 && (a.in_up == 1 || a.in_up == 2) && a.in_ps == 0 && !a.out_nchw && a.out_ps == 0 &&
         a.W % 128 == 0 && (a.W > 128 || a.in_up == 2) && (a.Cin == 64 || (a.Cin <= 32 && a.Cin % 8 == 0)) &&
-        a.Cout == 64 && a.Cout_real == a.Cout && !a.colsum && !a.dot && !a.row_scale && !a.res2 && !a.aux &&
-        g_variant != 1 && g_variant != 34 && g_variant != 76))
+        (a.Cout == 64 || (a.Cin <= 32 && (a.Cout == 128 || a.Cout == 256))) && a.Cout_real == a.Cout &&
+        !a.colsum && !a.dot && !a.row_scale && !a.res2 && !a.aux && g_variant != 1 && g_variant != 34 &&
+        g_variant != 76))
     return false;
   const int e = band_epi(a, 256);
+  if (a.Cout > 64) return e == 0;  // 8-channel input into 128 / 256 (EDSR's conv_last dgrad): one launch
   return a.Cin == 64 ? (e == 0 || e == 1 || e == 2 || e == 4) : (e == 0 || e == 4);
 }
-// the same from a narrow input (Cin 8..32) into 128 / 192 / 256 output channels (EDSR's conv_last dgrad:
-// 8 padded channels -> 256 at HR): 64-channel output-column slices, the narrow input re-read per slice
+// the same from a narrow input (Cin 8..32) into 192 output channels (or 128 / 256 with an epilogue
+// operand): 64-channel output-column slices, the narrow input re-read per slice.  (EDSR's conv_last
+// dgrad, 8 -> 256 at HR, ran as four slices at 99 us each -- 2.7 TB/s, bound by the per-row latency of
+// a band that stores 128 B per pixel -- and is now one CO 256 launch.)
 bool fwd_use_band_strip_sliced(const FwdArgs& a, bool bf) {
-  if (!(a.Cout > 64 && a.Cout <= 256 && a.Cout % 64 == 0 && a.Cin <= 32)) return false;
+  if (!(a.Cout > 64 && a.Cout <= 256 && a.Cout % 64 == 0 && a.Cin <= 32) || fwd_use_band_strip(a, bf)) return false;
   FwdArgs b = a;
   b.Cout = b.Cout_real = 64;
   return fwd_use_band_strip(b, bf);
@@ -4632,6 +4645,11 @@ hipError_t launch_band_strip(const FwdArgs& a, hipStream_t s) {
   ab.stamps = g_sr_stamps;
   const int gmax = g_variant == 35 ? 64 : 256;  // 35: long bands crossing strips and images (tests)
   const dim3 grid(rows < gmax ? rows : gmax);
+  if (a.Cin <= 32 && a.Cout > 64) {  // plain epilogue only (fwd_use_band_strip)
+    if (a.Cout == 256) hipLaunchKernelGGL((conv3x3_fwd_band_kernel<256, 128, 3, 1, 1024, 8>), grid, dim3(512), 0, s, ab);
+    else hipLaunchKernelGGL((conv3x3_fwd_band_kernel<128, 128, 3, 1, 1024, 8>), grid, dim3(512), 0, s, ab);
+    return hipGetLastError();
+  }
   if (a.Cin <= 32) {
     switch (band_epi(a, grid.x)) {
       case 0: hipLaunchKernelGGL((conv3x3_fwd_band_kernel<64, 128, 3, 1, 1024, 8>), grid, dim3(512), 0, s, ab); break;

@@ -199,8 +199,9 @@ def test_strip_band_selection():
         assert name(16, 512, 512, 64, in_up=2) == band        # conv_up2
         assert name(16, 256, 256, 64, in_up=2) == band        # conv_up1
         assert name(16, 512, 512, 8) == band                  # conv_last dgrad (8 padded channels)
-        assert name(32, 256, 256, 8, cout=256) == band        # EDSR conv_last dgrad: 4 output slices
-        assert lib.sr_conv3x3_fwd_launches(C._desc(bf, 32, 256, 256, 8, 8, 256, 256, 256)) == 4
+        assert name(32, 256, 256, 8, cout=256) == band        # EDSR conv_last dgrad: one CO 256 launch
+        assert lib.sr_conv3x3_fwd_launches(C._desc(bf, 32, 256, 256, 8, 8, 256, 256, 256)) == 1
+        assert lib.sr_conv3x3_fwd_launches(C._desc(bf, 32, 256, 256, 8, 8, 192, 192, 192)) == 3  # 64-ch slices
         assert name(32, 256, 256, 64, cout=256) != band       # wide input: stays on the 256-wide kernels
         assert name(2, 256, 256, 256, cout=256) == b'conv3x3_fwd_pph_kernel'  # EDSR body at LR 256: pph strips
         assert name(2, 256, 256, 256, cout=1024, out_ps=2) == b'conv3x3_fwd_pph_kernel'
