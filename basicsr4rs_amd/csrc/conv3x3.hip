@@ -4041,15 +4041,29 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_g_kernel(const float* ws, c
     else rp = co_map ? co_map[rw] : (out_ps > 0 ? (rw % r2) * cps + rw / r2 : rw);
     const size_t stride = (size_t)taps * Cout * Cin;
     const float* src = ws + ((size_t)tap * (TR ? Cin : Cout) + rp) * (TR ? Cout : Cin) + q4 * 4;
+    // 8 independent 16-B loads in flight, and the < 8 left over issued together too (clamped to a
+    // valid split, zeroed after the load: no branch, so no load waits for the one before it -- the
+    // round-5 form ran its remainder one dependent iteration at a time, e.g. 2-3 of the 6-7 loads per
+    // lane at the EDSR body wgrad's 26 splits)
     int k = ph;
-    for (; k + 3 * P < S; k += 4 * P) {
-      const f32x4 v0 = *(const f32x4*)(src + (size_t)k * stride);
-      const f32x4 v1 = *(const f32x4*)(src + (size_t)(k + P) * stride);
-      const f32x4 v2 = *(const f32x4*)(src + (size_t)(k + 2 * P) * stride);
-      const f32x4 v3 = *(const f32x4*)(src + (size_t)(k + 3 * P) * stride);
-      acc += v0; acc += v1; acc += v2; acc += v3;
+    for (; k + 7 * P < S; k += 8 * P) {
+      f32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *(const f32x4*)(src + (size_t)(k + j * P) * stride);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j];
     }
-    for (; k < S; k += P) acc += *(const f32x4*)(src + (size_t)k * stride);
+    if (k < S) {
+      f32x4 v[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const int kj = k + j * P < S ? k + j * P : S - 1;
+        v[j] = *(const f32x4*)(src + (size_t)kj * stride);
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+        if (k + j * P < S) acc += v[j];
+    }
   }
   red[ph * GPW + gl] = acc;
   __syncthreads();
