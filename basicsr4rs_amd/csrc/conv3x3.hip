@@ -2515,13 +2515,24 @@ __global__ __launch_bounds__(NWV * 64, NWV == 8 ? 2 : band_occ(W, E)) void conv3
       // (a.cs_band: every band is a.cs_band rows of one image), the running sum over the band's rows
       // so far to partial row bb * WP + wp, so the last row's store leaves the band's sum
       // (P = H / cs_band * WP rows per image; same-address stores of one wave land in order)
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
+      // Band-reduced: each lane keeps its own sums over the band's rows and the butterfly runs once, at
+      // the band's last row (it costs ~1300 cycles per row at one wave per SIMD: 32 cross-lane moves in
+      // 4 dependent rounds); the rows before store the lane's unreduced running sum to the same
+      // address, which the last row's store overwrites (the two stores per row keep the vmcnt counts)
       if (a.cs_band) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) { cst[j] += cs[j]; cs[j] = cst[j]; }
+        if (s + 1 == s1) {
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
+        }
+      } else {
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cs[j] += __shfl_xor(cs[j], off, 64);
       }
       float* dstp = a.colsum + ((size_t)(a.cs_band ? bb : s) * WP + wp) * a.Cout + nn;
       // exactly two vector store instructions per wave (lanes masked): counted in NC
