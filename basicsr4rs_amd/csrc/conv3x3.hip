@@ -16,6 +16,8 @@
 // bias, activation, ReLU-mask gate, scale, residual, pixel-shuffle / NCHW store with
 // 16-byte coalesced stores.
 #include <cstdlib>
+#include <utility>
+#include <type_traits>
 #include "sr_common.h"
 #include "sr_internal.h"
 
@@ -3893,6 +3895,314 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Weight gradient over one kernel ROW of taps (round 6): bf16 3x3, Cout % 256 == 0, Cin % 128 == 0,
+// W % 64 == 0, no pixel shuffle / upsample (the EDSR-L body convs).  A pp-kernel block is one tap of
+// a 256 x 256 (co x ci) tile: each K-step DMAs the dy tile AND a tap-shifted x tile (64 KB per 4.2 M
+// MACs) and its 8 waves of 128 x 64 read 192 KB of fragments.  Here a block owns the three taps
+// (ky, 0..2) of a 256 x 128 tile: a K-step (64 pixels of one image row) DMAs the dy tile (32 KB) and
+// ONE x halo row of 66 pixels (16.5 KB), and the three taps' B operands are that row read at row
+// offsets 0 / 1 / 2: 48.5 KB per 6.3 M MACs.  4 waves, one per SIMD; wave (wr, wc) = 128 co x 64 ci x
+// 3 taps, 384 accumulator registers (taps 0 / 1 pinned to AGPRs, tap 2 in VGPRs); an A fragment feeds
+// 12 MFMAs and a B fragment 8 (40 KB of fragment reads per wave and step for 1.6 M MACs).  Three LDS
+// stages; one barrier per step, placed before the step's last MFMA group, after which the next step's
+// first fragment reads run under that group.  Operand images as the ring kernel's: [16-channel tile]
+// [row][32 B] with rows permuted by hrow (conflict-free tr reads at any row offset); the halo row's 66
+// rows arrive as three 32-row pieces, the third (rows 34..65) rewriting 30 rows of the second with the
+// same bytes.  Image edges and rows outside the image read zeros (out-of-range buffer offsets).  Bias:
+// bias-role blocks after the tile blocks, each summing dy over bias_group splits.  Output: the pp
+// kernel's [S][9][Cout][Cin] slab (same reduce), staged through LDS for 16-B row stores.
+// ------------------------------------------------------------------------------------
+// Compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N - 1 (fully unrolled by construction;
+// a #pragma unroll loop this large exceeds the unroller's threshold and its arrays go to scratch).
+template <typename F, int... I>
+SR_DEV void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+SR_DEV void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+constexpr int row3_need(int gi) { return (gi / 12) * 20 + 8 + gi % 12; }  // last fragment read group gi uses
+
+// LA: fragment reads run LA MFMA groups ahead; SPREAD: a step's 14 LDS-DMAs are issued one per MFMA group
+// instead of in one burst at the barrier; DIRECT: the slab written from the accumulators (no LDS staging).
+template <int LA, bool SPREAD, bool DIRECT>
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
+  constexpr int DYT = 2048;      // one 16-co tile of dy: 64 rows x 32 B
+  constexpr int XT = 66 * 32;    // one 16-ci tile of the halo row: 66 rows x 32 B
+  constexpr int DYB = 16 * DYT;  // 256 co
+  constexpr int STG = DYB + 8 * XT;
+  constexpr int NOPS = 14;       // LDS-DMAs per wave and K-step: 8 dy + 6 x
+  constexpr int CSTR = 128 + 4;  // epilogue staging row (floats)
+  static_assert(3 * STG >= 256 * CSTR * 4, "epilogue staging exceeds the stages");
+  __shared__ __attribute__((aligned(16))) char smem[3 * STG];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const uint32_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = 3 * a.tiles_co * a.tiles_ci;
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy, a.dy_bytes);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+
+  // dy pieces of this wave: k = w + 4 i -> co tile k >> 1, physical rows 32 (k & 1) + (lane >> 1)
+  uint32_t dyl[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int k = w + 4 * i;
+    const int pr = hrow((k & 1) * 32 + (lane >> 1));
+    dyl[i] = (uint32_t)((pr * a.ldy + (k >> 1) * 16 + (lane & 1) * 8) * 2);
+  }
+  auto issue_dy = [&](char* st, int s_dyb) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = w + 4 * i;
+      glds16(dyr, st + (k >> 1) * DYT + (k & 1) * 1024, (uint32_t)s_dyb + dyl[i]);
+    }
+  };
+  auto tr2 = [&](const char* img, int r0_) -> s16x8 {  // rows r0 + tq (K 0..3), r0 + 4 + tq (K 4..7)
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0_ + tq) * 32 + tp * 8));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + hrow(r0_ + 4 + tq) * 32 + tp * 8));
+    return s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+
+  if ((int)b >= a.splits * ntile) {
+    // bias role: dy column sums of one 256-co tile over bias_group splits (dy images only, two stages)
+    const int bb = (int)b - a.splits * ntile;
+    const int grp = bb / a.tiles_co, co0 = (bb - grp * a.tiles_co) * 256;
+    const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+    const int s1 = min(a.splits, (grp + 1) * a.bias_group);
+    for (int sp = grp * a.bias_group; sp < s1; ++sp) {
+      const int p_begin = sp * a.kper, p_end = min(a.M, p_begin + a.kper);
+      const int nk = (p_end - p_begin) >> 6;
+      auto base = [&](int ks) { return __builtin_amdgcn_readfirstlane(((p_begin + ks * 64) * a.ldy + a.ycoff + co0) * 2); };
+      f32x4 accb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      __syncthreads();  // the previous split's stage reads are done
+      if (nk > 0) issue_dy(smem, base(0));
+      if (nk > 1) issue_dy(smem + STG, base(1));
+      for (int ks = 0; ks < nk; ++ks) {
+        if (ks + 1 < nk)
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* st = smem + (ks & 1) * STG;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr2(st + (w * 4 + i) * DYT, kk * 32 + 8 * g), ones, accb[i], 0, 0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (ks + 2 < nk) issue_dy(smem + (ks & 1) * STG, base(ks + 2));
+      }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int co = co0 + (w * 4 + i) * 16 + g * 4 + r;
+            if (co < a.Cout) a.wsb[(size_t)sp * a.Cout + co] = accb[i][r];
+          }
+      }
+    }
+    return;
+  }
+
+  const int split = (int)b / ntile;
+  int rem = (int)b - split * ntile;
+  const int ky = rem / (a.tiles_co * a.tiles_ci);
+  rem -= ky * a.tiles_co * a.tiles_ci;
+  const int co0 = (rem / a.tiles_ci) * 256;
+  const int ci0 = (rem % a.tiles_ci) * 128;
+  const int dy_ = ky - 1;
+  const int p_begin = split * a.kper;
+  const int p_end = min(a.M, p_begin + a.kper);
+  const int nk = (p_end - p_begin) >> 6;  // >= 1: whole 64-pixel steps (M, kper multiples of 64)
+
+  // x pieces of this wave: k = w + 4 i (i < 6) -> ci tile k / 3, piece k % 3 at physical row 0 / 32 / 34;
+  // lane: physical row base + (lane >> 1) = logical halo row (pixel x0 - 1 + row) hrow(.), channel half lane & 1
+  uint32_t xl[6];
+  int xlr[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int k = w + 4 * i, t = k / 3, pc = k - 3 * t;
+    const int lr = hrow((pc == 0 ? 0 : (pc == 1 ? 32 : 34)) + (lane >> 1));
+    xlr[i] = lr;
+    xl[i] = (uint32_t)((lr * a.ldx + t * 16 + (lane & 1) * 8) * 2);
+  }
+  // scalar state of a K-step's DMAs (k_eval), then its 14 pieces (piece < 8: dy, else x)
+  int s_dyb = 0, s_xb = 0, s_xm1 = 0, s_yv = 0;
+  auto k_eval = [&](int ks) {
+    const int p0s = p_begin + ks * 64;
+    const int q = (int)fdiv((uint32_t)p0s, a.fd_W);
+    const int x0 = p0s - q * a.W;
+    const int n = (int)fdiv((uint32_t)q, a.fd_H);
+    const int y = q - n * a.H;
+    s_dyb = __builtin_amdgcn_readfirstlane((p0s * a.ldy + a.ycoff + co0) * 2);
+    s_xb = __builtin_amdgcn_readfirstlane((((q + dy_) * a.W + x0 - 1) * a.ldx + a.xcoff + ci0) * 2);
+    s_xm1 = __builtin_amdgcn_readfirstlane(x0 - 1);
+    s_yv = __builtin_amdgcn_readfirstlane((unsigned)(y + dy_) < (unsigned)a.H ? 1 : 0);
+  };
+  auto piece = [&](char* st, int pi) {  // pi: compile-time after unrolling
+    if (pi < 8) {
+      const int k = w + 4 * pi;
+      glds16(dyr, st + (k >> 1) * DYT + (k & 1) * 1024, (uint32_t)s_dyb + dyl[pi]);
+    } else {
+      const int i = pi - 8, k = w + 4 * i, t = k / 3, pc = k - 3 * t;
+      const bool v = s_yv && (unsigned)(s_xm1 + xlr[i]) < (unsigned)a.W;
+      glds16(xr, st + DYB + t * XT + (pc == 0 ? 0 : (pc == 1 ? 32 : 34)) * 32, v ? (uint32_t)(s_xb + (int)xl[i]) : SR_OOB);
+    }
+  };
+  auto issue = [&](int ks, char* st) {
+    k_eval(ks);
+#pragma unroll
+    for (int pi = 0; pi < NOPS; ++pi) piece(st, pi);
+  };
+
+  f32x4 acc0[8][4], acc1[8][4], acc2[8][4];  // taps kx 0 / 1 (AGPRs), 2 (VGPRs); [co tile][ci tile]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  // a step's fragment reads: r = 20 kk + i, i < 8: A (dy) co tile wr * 8 + i; 8 <= i < 20: B, tap
+  // kx = (i - 8) >> 2, ci tile wc * 4 + ((i - 8) & 3) (the halo row at row offset kx)
+  s16x8 fa[2][8], fb[2][12];
+  auto rd = [&](const char* st, auto R) {
+    constexpr int r = R, kk = r / 20, i = r - kk * 20;
+    if constexpr (i < 8) {
+      fa[kk][i] = tr2(st + (wr * 8 + i) * DYT, kk * 32 + 8 * g);
+    } else {
+      constexpr int c = i - 8;
+      fb[kk][c] = tr2(st + DYB + (wc * 4 + (c & 3)) * XT, kk * 32 + 8 * g + (c >> 2));
+    }
+  };
+  // MFMA group gi (24 per step): kk = gi / 12, B fragment c = gi % 12 against the 8 A fragments
+  auto group = [&acc0, &acc1, &acc2, &fa, &fb](auto GI) {  // (explicit: if constexpr branches)
+    constexpr int gi = GI, kk = gi / 12, c = gi % 12, kx = c >> 2, j = c & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (kx == 0)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc0[i][j]) : "v"(fa[kk][i]), "v"(fb[kk][c]));
+      else if constexpr (kx == 1)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc1[i][j]) : "v"(fa[kk][i]), "v"(fb[kk][c]));
+      else
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc2[i][j]) : "v"(fa[kk][i]), "v"(fb[kk][c]));
+    }
+  };
+  // read stream position x (group x's last read): x < 24 this step, x >= 24 the next step's
+  constexpr auto rpos = [](int x) { return x < 24 ? row3_need(x) : 40 + row3_need(x - 24); };
+  constexpr int GB = 24 - LA;  // the group before which the barrier runs (its reads reach the next step)
+
+  issue(0, smem);
+  if (nk > 1) issue(1, smem + STG);
+  if (nk > 2) issue(2, smem + 2 * STG);
+  vm_wait_dyn(NOPS * (min(nk, 3) - 1));
+  __builtin_amdgcn_s_barrier();
+  static_for<rpos(LA - 1) + 1>([&](auto R) { rd(smem, R); });
+  int stc = 0;          // stage of step t
+  bool pending = false; // SPREAD: a step's DMAs (k_eval'd at the barrier) issued over groups 0..13
+  char* pst = smem;
+  for (int t = 0; t < nk; ++t) {
+    const int stn = stc == 2 ? 0 : stc + 1;
+    const char* cur = smem + stc * STG;
+    const char* nxt = smem + stn * STG;
+    const bool more = t + 1 < nk;
+    static_for<24>([&](auto GI) {
+      constexpr int gi = GI;
+      if constexpr (SPREAD && gi < NOPS) {
+        if (pending) piece(pst, gi);
+      }
+      // this step's reads up to group gi + LA's
+      static_for<40>([&](auto R) {
+        if constexpr (R > rpos(gi + LA - 1) && R <= rpos(gi + LA) && R < 40) rd(cur, R);
+      });
+      if constexpr (gi == GB) {
+        pending = false;
+        if (more) {
+          // every read of step t is issued: once they completed and step t + 1 landed (in every wave),
+          // step t's stage takes step t + 3's DMAs and step t + 1's first reads run under these groups
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (t + 2 < nk)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NOPS) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          if (t + 3 < nk) {
+            if constexpr (SPREAD) {
+              k_eval(t + 3);
+              pending = true;
+              pst = smem + stc * STG;
+            } else {
+              issue(t + 3, smem + stc * STG);
+            }
+          }
+        }
+      }
+      if constexpr (gi >= GB) {
+        if (more) {
+          static_for<40>([&](auto R) {
+            if constexpr (R + 40 > rpos(gi + LA - 1) && R + 40 <= rpos(gi + LA)) rd(nxt, R);
+          });
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      group(GI);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    stc = stn;
+  }
+
+  // the last MFMAs' results are read below (inline-asm MFMAs: the hazard wait is ours)
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (DIRECT) {  // 4-B stores straight from the accumulators (16 lanes: 64 contiguous bytes)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      float* ws = a.ws + ((size_t)split * 9 + ky * 3 + kx) * a.Cout * a.Cin;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 v = kx == 0 ? acc0[i][j] : (kx == 1 ? acc1[i][j] : acc2[i][j]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ws[(size_t)(co0 + wr * 128 + i * 16 + g * 4 + r) * a.Cin + ci0 + wc * 64 + j * 16 + (lane & 15)] = v[r];
+        }
+    }
+    return;
+  }
+  float* Cs = (float*)smem;
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    __syncthreads();  // the stages' (or the previous tap's) LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = kx == 0 ? acc0[i][j] : (kx == 1 ? acc1[i][j] : acc2[i][j]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cs[(wr * 128 + i * 16 + g * 4 + r) * CSTR + wc * 64 + j * 16 + (lane & 15)] = v[r];
+      }
+    __syncthreads();
+    float* ws = a.ws + ((size_t)split * 9 + ky * 3 + kx) * a.Cout * a.Cin;
+    for (int idx = tid; idx < 256 * 32; idx += 256) {
+      const int row = idx >> 5, c4 = (idx & 31) * 4;
+      *(f32x4*)(ws + (size_t)(co0 + row) * a.Cin + ci0 + c4) = *(const f32x4*)(Cs + row * CSTR + c4);
+    }
+  }
+}
+
 // dw[co][ci][ky][kx] = scale * sum_s ws[s][tap][co'][ci], co' = GEMM column of co (out_ps
 // permutation); one thread per (co, ci): slab reads coalesced along ci, 9 taps per thread.
 __global__ void wgrad_reduce_kernel(const float* ws, const float* wsb, float* dw, float* db, int S,
@@ -4941,6 +5251,20 @@ bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d) {
   if (g_variant == 62 || ring_wide_env() > 0) return true;
   return d->Cout % 128 != 0 || d->Cin % 128 != 0;
 }
+// Kernel-row wgrad (conv3x3_wgrad_row3_kernel): bf16 3x3, Cout % 256, Cin % 128, W % 64, no shuffle /
+// upsample (the EDSR-L body convs).  Knob SR_WG_ROW3=0 or variant 78: the pp kernel (A/B, parity
+// cross-check); SR_WG_ROW3=k > 0: bias-role blocks of k splits (default 2).
+int wg_row3_bg() {
+  const int k = sr_knob(K_WG_ROW3);
+  return k > 0 && k <= 64 ? k : 2;
+}
+bool wg_use_row3(const sr_conv3x3_wgrad_desc* d) {
+  if (sr_knob(K_WG_ROW3) == 0 || g_variant == 1 || g_variant == 2 || g_variant == 28 || g_variant == 62 ||
+      g_variant == 78)
+    return false;
+  return d->dtype == SR_BF16 && d->ksize != 1 && d->Cout % 256 == 0 && d->Cin % 128 == 0 && d->W % 64 == 0 &&
+         d->out_ps == 0 && d->in_up <= 1 && ring_wide_env() <= 0;
+}
 // 1x1 weight gradient on linear_wgrad_kernel (192x192 tiles): bf16 dense token rows, no pixel
 // shuffle / upsample.  Knob SR_LWG=0 or variant 63: off (the pp kernel, A/B and tests).
 bool wg_use_lin(const sr_conv3x3_wgrad_desc* d) {
@@ -4997,6 +5321,20 @@ void wgrad_plan(const sr_conv3x3_wgrad_desc* d, int* splits, int* kper) {
     const int tiles = ((d->Cout + 191) / 192) * ((d->Cin + 191) / 192);
     int S = lin_wg_target() / tiles;
     const int maxS = (M + 63) / 64;
+    if (S > maxS) S = maxS;
+    if (S < 1) S = 1;
+    int kp = (M + S - 1) / S;
+    kp = (kp + 63) / 64 * 64;
+    *splits = (M + kp - 1) / kp;
+    *kper = kp;
+    return;
+  }
+  if (wg_use_row3(d)) {  // one 256-block wave: S x 3 x tiles tile blocks + the bias-role blocks
+    const int bg = wg_row3_bg(), tco = d->Cout / 256;
+    const int ntile = 3 * tco * (d->Cin / 128);
+    int S = (int)(256.0 / (ntile + (double)tco / bg));
+    while (S > 1 && S * ntile + (S + bg - 1) / bg * tco > 256) --S;
+    const int maxS = M / 64;
     if (S > maxS) S = maxS;
     if (S < 1) S = 1;
     int kp = (M + S - 1) / S;
@@ -5242,6 +5580,7 @@ int sr_conv3x3_fwd_launches(const sr_conv3x3_desc* d) {
 const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
   if (wg_use_halo(d)) return "conv3x3_wgrad_ring_kernel";
   if (wg_use_lin(d)) return "linear_wgrad_kernel";
+  if (wg_use_row3(d)) return "conv3x3_wgrad_row3_kernel";
   if (wg_use_pp(d)) return "conv3x3_wgrad_pp_kernel";
   if (wg_use_big(d)) return "conv3x3_wgrad_big_kernel";
   return d->dtype == SR_BF16 ? "conv3x3_wgrad_kernel<bf16>" : "conv3x3_wgrad_kernel<f32>";
@@ -5249,10 +5588,10 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 
 // Kernel-variant switch for the parity tests' cross-checks: 0 = automatic, 1 = never a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels; the others each route one family to the kernel it replaced
-// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77: see their sites above).  The
+// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77, 78: see their sites above).  The
 // measured-slower paths and the timing ablations were removed in round 6 (git history).
 int sr_conv3x3_set_variant(int variant) {
-  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77};
+  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77, 78};
   bool ok = false;
   for (int v : kValid) ok = ok || v == variant;
   if (!ok) return sr_fail(SR_EINVAL, "conv3x3_set_variant: not a parity cross-check variant");
@@ -5394,6 +5733,19 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.tiles_co = (a.Cout + 191) / 192;
     a.tiles_ci = (a.Cin + 191) / 192;
     hipLaunchKernelGGL(linear_wgrad_kernel, dim3(S * a.tiles_co * a.tiles_ci), dim3(512), 0, s, a);
+    e = hipGetLastError();
+  } else if (wg_use_row3(d)) {
+    a.tiles_co = a.Cout / 256;
+    a.tiles_ci = a.Cin / 128;
+    a.bias_group = wg_row3_bg();
+    const int nb = S * 3 * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
+    const int v = sr_knob(K_WG_ROW3_V) < 0 ? 0 : sr_knob(K_WG_ROW3_V);  // A/B forms
+    if (v == 1) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<1, true, false>), dim3(nb), dim3(256), 0, s, a);
+    else if (v == 2) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<2, false, false>), dim3(nb), dim3(256), 0, s, a);
+    else if (v == 3) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<2, true, false>), dim3(nb), dim3(256), 0, s, a);
+    else if (v == 4) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<1, false, true>), dim3(nb), dim3(256), 0, s, a);
+    else if (v == 5) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<2, true, true>), dim3(nb), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<1, false, false>), dim3(nb), dim3(256), 0, s, a);
     e = hipGetLastError();
   } else if (wg_use_big(d)) {
     a.tiles_co = (a.Cout + 255) / 256;

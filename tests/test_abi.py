@@ -146,7 +146,9 @@ def test_round3_kernel_selection():
             assert wname(cin, cout, 1) == b'linear_wgrad_kernel'
         assert wname(184, 184, 3) == b'conv3x3_wgrad_ring_kernel'   # SwinIR RSTB conv
         assert wname(8, 256, 3) == b'conv3x3_wgrad_ring_kernel'     # EDSR conv_first
-        assert wname(256, 256, 3) == b'conv3x3_wgrad_pp_kernel'     # EDSR-L body stays on pp
+        assert wname(256, 256, 3) == b'conv3x3_wgrad_row3_kernel'   # EDSR-L body: kernel-row wgrad
+        assert wname(128, 512, 3, W=128) == b'conv3x3_wgrad_row3_kernel'
+        assert wname(256, 264, 3) != b'conv3x3_wgrad_row3_kernel'   # Cout not a multiple of 256
         for cin, cout in ((576, 184), (360, 184), (184, 360), (184, 184), (192, 184)):
             assert fname(cin, cout) == b'linear_wk_kernel'
         assert fname(184, 576) == b'linear_wk_kernel'                 # qkv unfused (SR_LN_UNFUSED): 3 tiles
@@ -154,6 +156,8 @@ def test_round3_kernel_selection():
         assert fname(384, 40) == b'conv3x3_lin_kernel'                # Cout <= 96: lin
         _lib.check(lib.sr_conv3x3_set_variant(63))
         assert wname(184, 576, 1) == b'conv3x3_wgrad_pp_kernel'
+        _lib.check(lib.sr_conv3x3_set_variant(78))
+        assert wname(256, 256, 3) == b'conv3x3_wgrad_pp_kernel'     # variant 78: the pp kernel
         _lib.check(lib.sr_conv3x3_set_variant(64))
         assert fname(576, 184) == b'conv3x3_lin_kernel'
         _lib.check(lib.sr_conv3x3_set_variant(62))

@@ -233,7 +233,7 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
     dy = torch.randn(N, H * max(ps, 1), W * max(ps, 1), cout // max(ps * ps, 1), device=cuda).to(dt)
     outs = []
     try:
-        for variant in (0, 2):
+        for variant in (78, 2):  # 78: the pp kernel where the kernel-row wgrad would run
             _lib.check(lib.sr_conv3x3_set_variant(variant))
             outs.append(C.conv_wgrad_raw(dy, x, N, H, W, cin, cin, cout, cout, scale=1.0, out_ps=ps))
     finally:
@@ -241,6 +241,45 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize('shape', [(1, 3, 64, 256, 256), (4, 8, 64, 256, 256), (2, 64, 64, 256, 256),
+                                   (8, 64, 64, 256, 256), (1, 6, 64, 128, 256), (2, 5, 128, 128, 512),
+                                   (1, 7, 192, 384, 256), (3, 1, 64, 256, 512)])
+def test_wgrad_row3_vs_fp64(cuda, shape):
+    """Kernel-row weight gradient (conv3x3_wgrad_row3_kernel: three taps of a 256 x 128 tile per
+    block from one x halo row per 64-pixel step; bias-role blocks) against an fp64 reference on the
+    same bf16 operands, and against the pp kernel (variant 78) within fp32 summation-order noise:
+    one-step splits, splits crossing images, image rows of one pixel row (H 1), W 64 / 128 / 192,
+    Cin 128 / 384, two co tiles, several bias-group sizes."""
+    N, H, W, cin, cout = shape
+    torch.manual_seed(21)
+    dt = torch.bfloat16
+    lib = _lib.load()
+    x = torch.randn(N, H, W, cin).to(dt)
+    dy = torch.randn(N, H, W, cout).to(dt)
+    w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    d = _lib.WgradDesc()
+    d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.ksize = cin, cin, cin, cout, cout, cout, 3
+    assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_row3_kernel'
+    outs = []
+    try:
+        for variant, bg in ((0, -1), (0, 1), (0, 5), (78, -1)):
+            _lib.check(lib.sr_conv3x3_set_variant(variant))
+            with _lib.knob('SR_WG_ROW3', bg):
+                outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0))
+                torch.cuda.synchronize()
+    finally:
+        _lib.check(lib.sr_conv3x3_set_variant(0))
+    scale = w.grad.abs().max().item()
+    for dw, db in outs[:3]:
+        assert (dw.cpu().double() - w.grad).abs().max().item() <= 2e-5 * scale + 1e-4
+        assert (db.cpu().double() - b.grad).abs().max().item() <= 2e-5 * b.grad.abs().max().item() + 1e-4
+    for dw, db in outs[1:]:  # bias-group sizes change the split plan (and the fp32 summation order) only
+        assert (outs[0][0] - dw).abs().max().item() <= 2e-5 * scale + 1e-4
 
 
 @pytest.mark.parametrize('shape', [(2, 64, 64, 184, 576), (1, 64, 64, 192, 184), (3, 8, 64, 184, 360),
