@@ -3925,17 +3925,13 @@ SR_DEV void static_for(F&& f) {
 }
 constexpr int row3_need(int gi) { return (gi / 12) * 20 + 8 + gi % 12; }  // last fragment read group gi uses
 
-// LA: fragment reads run LA MFMA groups ahead; SPREAD: a step's 14 LDS-DMAs are issued one per MFMA group
-// instead of in one burst at the barrier; DIRECT: the slab written from the accumulators (no LDS staging).
-template <int LA, bool SPREAD, bool DIRECT>
 __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
+  constexpr int LA = 1;  // fragment reads one MFMA group ahead (two: the same time, 4 more VGPRs)
   constexpr int DYT = 2048;      // one 16-co tile of dy: 64 rows x 32 B
   constexpr int XT = 66 * 32;    // one 16-ci tile of the halo row: 66 rows x 32 B
   constexpr int DYB = 16 * DYT;  // 256 co
   constexpr int STG = DYB + 8 * XT;
   constexpr int NOPS = 14;       // LDS-DMAs per wave and K-step: 8 dy + 6 x
-  constexpr int CSTR = 128 + 4;  // epilogue staging row (floats)
-  static_assert(3 * STG >= 256 * CSTR * 4, "epilogue staging exceeds the stages");
   __shared__ __attribute__((aligned(16))) char smem[3 * STG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -4089,6 +4085,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
   // MFMA group gi (24 per step): kk = gi / 12, B fragment c = gi % 12 against the 8 A fragments
   auto group = [&acc0, &acc1, &acc2, &fa, &fb](auto GI) {  // (explicit: if constexpr branches)
     constexpr int gi = GI, kk = gi / 12, c = gi % 12, kx = c >> 2, j = c & 3;
+    (void)acc0, (void)acc1, (void)acc2;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if constexpr (kx == 0)
@@ -4109,9 +4106,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
   vm_wait_dyn(NOPS * (min(nk, 3) - 1));
   __builtin_amdgcn_s_barrier();
   static_for<rpos(LA - 1) + 1>([&](auto R) { rd(smem, R); });
-  int stc = 0;          // stage of step t
-  bool pending = false; // SPREAD: a step's DMAs (k_eval'd at the barrier) issued over groups 0..13
-  char* pst = smem;
+  int stc = 0;  // stage of step t
   for (int t = 0; t < nk; ++t) {
     const int stn = stc == 2 ? 0 : stc + 1;
     const char* cur = smem + stc * STG;
@@ -4119,15 +4114,11 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
     const bool more = t + 1 < nk;
     static_for<24>([&](auto GI) {
       constexpr int gi = GI;
-      if constexpr (SPREAD && gi < NOPS) {
-        if (pending) piece(pst, gi);
-      }
       // this step's reads up to group gi + LA's
       static_for<40>([&](auto R) {
         if constexpr (R > rpos(gi + LA - 1) && R <= rpos(gi + LA) && R < 40) rd(cur, R);
       });
       if constexpr (gi == GB) {
-        pending = false;
         if (more) {
           // every read of step t is issued: once they completed and step t + 1 landed (in every wave),
           // step t's stage takes step t + 3's DMAs and step t + 1's first reads run under these groups
@@ -4137,15 +4128,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
-          if (t + 3 < nk) {
-            if constexpr (SPREAD) {
-              k_eval(t + 3);
-              pending = true;
-              pst = smem + stc * STG;
-            } else {
-              issue(t + 3, smem + stc * STG);
-            }
-          }
+          if (t + 3 < nk) issue(t + 3, smem + stc * STG);
         }
       }
       if constexpr (gi >= GB) {
@@ -4166,40 +4149,20 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (DIRECT) {  // 4-B stores straight from the accumulators (16 lanes: 64 contiguous bytes)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      float* ws = a.ws + ((size_t)split * 9 + ky * 3 + kx) * a.Cout * a.Cin;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 v = kx == 0 ? acc0[i][j] : (kx == 1 ? acc1[i][j] : acc2[i][j]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ws[(size_t)(co0 + wr * 128 + i * 16 + g * 4 + r) * a.Cin + ci0 + wc * 64 + j * 16 + (lane & 15)] = v[r];
-        }
-    }
-    return;
-  }
-  float* Cs = (float*)smem;
+  // slab: 4-B stores straight from the accumulators (16 lanes: 64 contiguous bytes).  (Staged through
+  // LDS for 16-B row stores, as the pp kernel does, it measured slower: 165-173 vs 163-170 us.)
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx) {
-    __syncthreads();  // the stages' (or the previous tap's) LDS reads are done
+    float* ws = a.ws + ((size_t)split * 9 + ky * 3 + kx) * a.Cout * a.Cin;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 v = kx == 0 ? acc0[i][j] : (kx == 1 ? acc1[i][j] : acc2[i][j]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Cs[(wr * 128 + i * 16 + g * 4 + r) * CSTR + wc * 64 + j * 16 + (lane & 15)] = v[r];
+        for (int r = 0; r < 4; ++r)
+          ws[(size_t)(co0 + wr * 128 + i * 16 + g * 4 + r) * a.Cin + ci0 + wc * 64 + j * 16 + (lane & 15)] = v[r];
       }
-    __syncthreads();
-    float* ws = a.ws + ((size_t)split * 9 + ky * 3 + kx) * a.Cout * a.Cin;
-    for (int idx = tid; idx < 256 * 32; idx += 256) {
-      const int row = idx >> 5, c4 = (idx & 31) * 4;
-      *(f32x4*)(ws + (size_t)(co0 + row) * a.Cin + ci0 + c4) = *(const f32x4*)(Cs + row * CSTR + c4);
-    }
   }
 }
 
@@ -5739,13 +5702,7 @@ int sr_conv3x3_wgrad(const sr_conv3x3_wgrad_desc* d, const void* dy, const void*
     a.tiles_ci = a.Cin / 128;
     a.bias_group = wg_row3_bg();
     const int nb = S * 3 * a.tiles_co * a.tiles_ci + (a.wsb ? (S + a.bias_group - 1) / a.bias_group * a.tiles_co : 0);
-    const int v = sr_knob(K_WG_ROW3_V) < 0 ? 0 : sr_knob(K_WG_ROW3_V);  // A/B forms
-    if (v == 1) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<1, true, false>), dim3(nb), dim3(256), 0, s, a);
-    else if (v == 2) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<2, false, false>), dim3(nb), dim3(256), 0, s, a);
-    else if (v == 3) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<2, true, false>), dim3(nb), dim3(256), 0, s, a);
-    else if (v == 4) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<1, false, true>), dim3(nb), dim3(256), 0, s, a);
-    else if (v == 5) hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<2, true, true>), dim3(nb), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((conv3x3_wgrad_row3_kernel<1, false, false>), dim3(nb), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(conv3x3_wgrad_row3_kernel, dim3(nb), dim3(256), 0, s, a);
     e = hipGetLastError();
   } else if (wg_use_big(d)) {
     a.tiles_co = (a.Cout + 255) / 256;

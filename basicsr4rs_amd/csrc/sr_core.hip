@@ -26,7 +26,7 @@ int sr_check(hipError_t e, const char* what) {
 static const char* const kKnobNames[K_COUNT] = {
     "SR_LWK", "SR_LWK_MINK", "SR_RING_WIDE", "SR_RING_PS", "SR_LWG", "SR_LWG_T", "SR_RING_SPLITS",
     "SR_DCN_CPP", "SR_DCN_DBG", "SR_DCN_R", "SR_DCN_FUSED", "SR_DCN_COORD_WIN",
-    "SR_DCN_GX_FX", "SR_SWIN_ATTN_DBG", "SR_WG_ROW3", "SR_WG_ROW3_V"};
+    "SR_DCN_GX_FX", "SR_SWIN_ATTN_DBG", "SR_WG_ROW3"};
 static std::atomic<int> g_knob[K_COUNT];
 static std::once_flag g_knob_once;
 

@@ -24,7 +24,6 @@ enum SrKnob {
   K_DCN_GX_FX,      // SR_DCN_GX_FX: 32 / 64-bit fixed-point scatter image
   K_SWIN_ATTN_DBG,  // SR_SWIN_ATTN_DBG: fused attention timing ablations (wrong results)
   K_WG_ROW3,        // SR_WG_ROW3: 0 = the kernel-row wgrad off (pp kernel), > 0 = its bias-role group size
-  K_WG_ROW3_V,      // SR_WG_ROW3_V: kernel-row wgrad schedule form (A/B)
   K_COUNT
 };
 int sr_knob(SrKnob k);
