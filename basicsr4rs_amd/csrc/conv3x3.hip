@@ -3897,7 +3897,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_ring_kernel(WgArgs a) {
 
 // ------------------------------------------------------------------------------------
 // Weight gradient over one kernel ROW of taps (round 6): bf16 3x3, Cout % 256 == 0, Cin % 128 == 0,
-// W % 64 == 0, no pixel shuffle / upsample (the EDSR-L body convs).  A pp-kernel block is one tap of
+// W % 64 == 0, no upsample; pixel-shuffled dy with C' % 256 == 0 (the EDSR-L body and upsample convs).  A pp-kernel block is one tap of
 // a 256 x 256 (co x ci) tile: each K-step DMAs the dy tile AND a tap-shifted x tile (64 KB per 4.2 M
 // MACs) and its 8 waves of 128 x 64 read 192 KB of fragments.  Here a block owns the three taps
 // (ky, 0..2) of a 256 x 128 tile: a K-step (64 pixels of one image row) DMAs the dy tile (32 KB) and
@@ -3942,13 +3942,23 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
 
+  // pixel-shuffled dy (out_ps r, the upsample convs): a 256-co tile lies in ONE shuffle slot sl
+  // (C' % 256 == 0, checked on the host), so GEMM column co0 + c of LR pixel (q, x) is channel
+  // co0 - sl C' + c of HR pixel (q r + sl / r, x r + sl % r): LR pixels r HR pixels apart
+  const int rps = a.out_ps > 0 ? a.out_ps : 1;
+  auto dy_base = [&](int p0s, int co0) -> int {  // byte offset of (first pixel of the K-step, co0)
+    if (a.out_ps == 0) return (p0s * a.ldy + a.ycoff + co0) * 2;
+    const int q = (int)fdiv((uint32_t)p0s, a.fd_W), x0 = p0s - q * a.W;
+    const int sl = (int)fdiv((uint32_t)co0, a.fd_cps), si = sl / rps, sj = sl - si * rps;
+    return (((q * rps + si) * (a.W * rps) + x0 * rps + sj) * a.ldy + a.ycoff + co0 - sl * (int)a.fd_cps.d) * 2;
+  };
   // dy pieces of this wave: k = w + 4 i -> co tile k >> 1, physical rows 32 (k & 1) + (lane >> 1)
   uint32_t dyl[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int k = w + 4 * i;
     const int pr = hrow((k & 1) * 32 + (lane >> 1));
-    dyl[i] = (uint32_t)((pr * a.ldy + (k >> 1) * 16 + (lane & 1) * 8) * 2);
+    dyl[i] = (uint32_t)((pr * rps * a.ldy + (k >> 1) * 16 + (lane & 1) * 8) * 2);
   }
   auto issue_dy = [&](char* st, int s_dyb) {
 #pragma unroll
@@ -3974,7 +3984,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
     for (int sp = grp * a.bias_group; sp < s1; ++sp) {
       const int p_begin = sp * a.kper, p_end = min(a.M, p_begin + a.kper);
       const int nk = (p_end - p_begin) >> 6;
-      auto base = [&](int ks) { return __builtin_amdgcn_readfirstlane(((p_begin + ks * 64) * a.ldy + a.ycoff + co0) * 2); };
+      auto base = [&](int ks) { return __builtin_amdgcn_readfirstlane(dy_base(p_begin + ks * 64, co0)); };
       f32x4 accb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -4040,7 +4050,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_row3_kernel(WgArgs a) {
     const int x0 = p0s - q * a.W;
     const int n = (int)fdiv((uint32_t)q, a.fd_H);
     const int y = q - n * a.H;
-    s_dyb = __builtin_amdgcn_readfirstlane((p0s * a.ldy + a.ycoff + co0) * 2);
+    s_dyb = __builtin_amdgcn_readfirstlane(dy_base(p0s, co0));
     s_xb = __builtin_amdgcn_readfirstlane((((q + dy_) * a.W + x0 - 1) * a.ldx + a.xcoff + ci0) * 2);
     s_xm1 = __builtin_amdgcn_readfirstlane(x0 - 1);
     s_yv = __builtin_amdgcn_readfirstlane((unsigned)(y + dy_) < (unsigned)a.H ? 1 : 0);
@@ -5214,8 +5224,8 @@ bool wg_ring_wide(const sr_conv3x3_wgrad_desc* d) {
   if (g_variant == 62 || ring_wide_env() > 0) return true;
   return d->Cout % 128 != 0 || d->Cin % 128 != 0;
 }
-// Kernel-row wgrad (conv3x3_wgrad_row3_kernel): bf16 3x3, Cout % 256, Cin % 128, W % 64, no shuffle /
-// upsample (the EDSR-L body convs).  Knob SR_WG_ROW3=0 or variant 78: the pp kernel (A/B, parity
+// Kernel-row wgrad (conv3x3_wgrad_row3_kernel): bf16 3x3, Cout % 256, Cin % 128, W % 64, no upsample,
+// pixel-shuffled dy when a 256-co tile lies in one shuffle slot (the EDSR-L body and upsample convs).  Knob SR_WG_ROW3=0 or variant 78: the pp kernel (A/B, parity
 // cross-check); SR_WG_ROW3=k > 0: bias-role blocks of k splits (default 2).
 int wg_row3_bg() {
   const int k = sr_knob(K_WG_ROW3);
@@ -5225,8 +5235,9 @@ bool wg_use_row3(const sr_conv3x3_wgrad_desc* d) {
   if (sr_knob(K_WG_ROW3) == 0 || g_variant == 1 || g_variant == 2 || g_variant == 28 || g_variant == 62 ||
       g_variant == 78)
     return false;
+  const bool ps_ok = d->out_ps == 0 || (d->Cout / (d->out_ps * d->out_ps)) % 256 == 0;  // a co tile in one slot
   return d->dtype == SR_BF16 && d->ksize != 1 && d->Cout % 256 == 0 && d->Cin % 128 == 0 && d->W % 64 == 0 &&
-         d->out_ps == 0 && d->in_up <= 1 && ring_wide_env() <= 0;
+         ps_ok && d->in_up <= 1 && ring_wide_env() <= 0;
 }
 // 1x1 weight gradient on linear_wgrad_kernel (192x192 tiles): bf16 dense token rows, no pixel
 // shuffle / upsample.  Knob SR_LWG=0 or variant 63: off (the pp kernel, A/B and tests).

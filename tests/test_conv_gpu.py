@@ -245,32 +245,42 @@ def test_wgrad_pp_bitwise_equals_big(cuda, shape):
 
 @pytest.mark.parametrize('shape', [(1, 3, 64, 256, 256), (4, 8, 64, 256, 256), (2, 64, 64, 256, 256),
                                    (8, 64, 64, 256, 256), (1, 6, 64, 128, 256), (2, 5, 128, 128, 512),
-                                   (1, 7, 192, 384, 256), (3, 1, 64, 256, 512)])
+                                   (1, 7, 192, 384, 256), (3, 1, 64, 256, 512), (1, 4, 64, 256, 1024, 2),
+                                   (2, 3, 128, 256, 1024, 2), (1, 2, 64, 128, 2304, 3)])
 def test_wgrad_row3_vs_fp64(cuda, shape):
     """Kernel-row weight gradient (conv3x3_wgrad_row3_kernel: three taps of a 256 x 128 tile per
     block from one x halo row per 64-pixel step; bias-role blocks) against an fp64 reference on the
     same bf16 operands, and against the pp kernel (variant 78) within fp32 summation-order noise:
     one-step splits, splits crossing images, image rows of one pixel row (H 1), W 64 / 128 / 192,
-    Cin 128 / 384, two co tiles, several bias-group sizes."""
-    N, H, W, cin, cout = shape
+    Cin 128 / 384, two co tiles, several bias-group sizes; pixel-shuffled dy (r 2 / 3: the EDSR upsample
+    convs' GEMM columns, one shuffle slot per 256-co tile)."""
+    N, H, W, cin, cout = shape[:5]
+    ps = shape[5] if len(shape) > 5 else 0
     torch.manual_seed(21)
     dt = torch.bfloat16
     lib = _lib.load()
     x = torch.randn(N, H, W, cin).to(dt)
-    dy = torch.randn(N, H, W, cout).to(dt)
+    if ps:
+        dy = torch.randn(N, H * ps, W * ps, cout // (ps * ps)).to(dt)
+        dy_gemm = O.pixel_unshuffle(dy.permute(0, 3, 1, 2).double(), ps)
+    else:
+        dy = torch.randn(N, H, W, cout).to(dt)
+        dy_gemm = dy.permute(0, 3, 1, 2).double()
     w = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
     b = torch.zeros(cout, dtype=torch.float64, requires_grad=True)
-    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy.permute(0, 3, 1, 2).double()).sum().backward()
+    F.conv2d(x.permute(0, 3, 1, 2).double(), w, b, padding=1).mul(dy_gemm).sum().backward()
     d = _lib.WgradDesc()
     d.dtype, d.N, d.H, d.W = _lib.dtype_code(dt), N, H, W
-    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.ksize = cin, cin, cin, cout, cout, cout, 3
+    d.Cin, d.Cin_real, d.ldx, d.Cout, d.Cout_real, d.ldy, d.ksize = cin, cin, cin, cout, cout, dy.shape[-1], 3
+    d.out_ps = ps
     assert lib.sr_conv3x3_wgrad_kernel_name(d) == b'conv3x3_wgrad_row3_kernel'
     outs = []
     try:
         for variant, bg in ((0, -1), (0, 1), (0, 5), (78, -1)):
             _lib.check(lib.sr_conv3x3_set_variant(variant))
             with _lib.knob('SR_WG_ROW3', bg):
-                outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0))
+                outs.append(C.conv_wgrad_raw(dy.to(cuda), x.to(cuda), N, H, W, cin, cin, cout, cout, scale=1.0,
+                                             out_ps=ps))
                 torch.cuda.synchronize()
     finally:
         _lib.check(lib.sr_conv3x3_set_variant(0))

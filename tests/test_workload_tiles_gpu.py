@@ -199,9 +199,9 @@ def test_rrdb_workload_tile_bf16(cuda):
 
 
 def test_edsr_l_workload_tile_bf16_fwd_bwd(cuda):
-    _run(cuda, EDSR_L4, 2, 64, ['conv3x3_fwd_pph_kernel', 'conv3x3_fwd_tail_kernel', 'conv3x3_wgrad_row3_kernel+reduce',
-                                'conv3x3_wgrad_pp_kernel+reduce'],
-         out_tol=5e-3, grad_tol=0.13, l2_tol=0.085)
+    # every 256-channel weight gradient (body and the pixel-shuffled upsample convs) on the kernel-row form
+    _run(cuda, EDSR_L4, 2, 64, ['conv3x3_fwd_pph_kernel', 'conv3x3_fwd_tail_kernel', 'conv3x3_wgrad_row3_kernel+reduce'],
+         out_tol=5e-3, grad_tol=0.13, l2_tol=0.085, absent=('conv3x3_wgrad_pp_kernel+reduce',))
 
 
 def test_swinir_m_workload_tile_bf16(cuda):
