@@ -16,6 +16,7 @@ SR_LN_UNFUSED         1 / qkv / fc1: the standalone LayerNorm kernel + linear in
 SR_CA_UNFUSED         1: the round-2 channel-attention launches
 SR_CA_DOT             1: channel-attention dots from the next block's dgrad epilogue (measured slower, A/B)
 SR_DCN_BWD_FUSED      0: the DCN backward through the dcols matrix
+SR_CONV_KPAD          0: no K-padded weight images for the 184-channel 3x3 convs (the 64-channel halo kernel)
 SR_STEP_TRACE         host time stamps of the segmented DDP graph step (a file path)
 """
 import os
@@ -33,6 +34,7 @@ _DEFAULTS = {
     'SR_CA_UNFUSED': '0',
     'SR_CA_DOT': '0',
     'SR_DCN_BWD_FUSED': '1',
+    'SR_CONV_KPAD': '1',
     'SR_STEP_TRACE': None,
 }
 

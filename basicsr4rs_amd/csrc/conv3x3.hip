@@ -4879,6 +4879,12 @@ FwdKind fwd_kind(const FwdArgs& a, bool bf) {
   if (fwd_use_lin(a, bf)) return FK_LIN;
   if (fwd_use_band(a, bf) || fwd_use_band_strip(a, bf)) return FK_BAND;
   if (fwd_use_band_sliced(a, bf) || fwd_use_band_strip_sliced(a, bf)) return FK_BANDS;
+  // 128 < Cout < 256 from Cin >= 128, K a multiple of 64 (SwinIR-M's 180 -> 180 convs with the GEMM K padded
+  // to 192 on the host, ops/conv.py _kpad): the halo-row 256x256 kernel with a partial output tile rather
+  // than the 64-channel halo kernel (variant 79: the halo kernel, A/B and tests)
+  if (bf && a.Cout > 128 && a.Cout < 256 && a.Cin >= 128 && !a.out_nchw && a.out_ps == 0 && !a.colsum &&
+      !a.dot && fwd_use_pph(a) && !g_disable_big && g_variant != 79)
+    return FK_BIG;
   if (fwd_use_halo(a, bf)) return FK_HALO;
   // 1x1 convs with K > 192 (SwinIR fc2 fwd, qkv / fc1 dgrads: K 368 / 576 -> 184) on the 256x256
   // kernel with a partial N tile: x read once (vs twice by 128x128 tiles); 68 -> 57 us and 82 -> 65 us
@@ -5562,10 +5568,10 @@ const char* sr_conv3x3_wgrad_kernel_name(const sr_conv3x3_wgrad_desc* d) {
 
 // Kernel-variant switch for the parity tests' cross-checks: 0 = automatic, 1 = never a 256x256 kernel,
 // 2 = the two-barrier 256x256 kernels; the others each route one family to the kernel it replaced
-// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77, 78: see their sites above).  The
+// (24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77, 78, 79: see their sites above).  The
 // measured-slower paths and the timing ablations were removed in round 6 (git history).
 int sr_conv3x3_set_variant(int variant) {
-  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77, 78};
+  static const int kValid[] = {0, 1, 2, 24, 28, 29, 33, 34, 35, 36, 37, 50, 55, 59, 61, 62, 63, 64, 67, 68, 76, 77, 78, 79};
   bool ok = false;
   for (int v : kValid) ok = ok || v == variant;
   if (!ok) return sr_fail(SR_EINVAL, "conv3x3_set_variant: not a parity cross-check variant");

@@ -602,6 +602,26 @@ def _out_shape(spec, N, H, W):
     return (N, H, W, spec.cout_p)
 
 
+def _kpad(spec, dtype, H, W):
+    """K-padded weight images (cout_k, cin_k) for a bf16 3x3 conv whose channel counts (as stored) are
+    not multiples of 64 but whose output is wide (SwinIR-M's 180 -> 180 convs, stored as 184): with the
+    GEMM K padded to 192 (zero weight columns; x rows keep their 184-channel stride, so the last chunk's
+    8 extra channels are the next pixel's, times zero) the forward runs on the halo-row 256 x 256 kernel
+    with a partial output tile instead of the 64-channel halo kernel.  None otherwise."""
+    if (switch('SR_CONV_KPAD') == '0' or dtype != torch.bfloat16 or spec.out_nchw or spec.out_ps
+            or (spec.in_up or 1) != 1 or not ((W == 64 and H % 4 == 0) or (W == 128 and H % 2 == 0))):
+        return None
+    if not (128 <= spec.cin_p and 128 < spec.cout_p < 256) or (spec.cin_p % 64 == 0 and spec.cout_p % 64 == 0):
+        return None
+    return (spec.cout_p + 63) // 64 * 64, (spec.cin_p + 63) // 64 * 64
+
+
+def _images(weight, bias, spec, dtype, kp):
+    if kp is None:
+        return prepared(weight, bias, spec, dtype)
+    return prepared_images(weight, bias, dtype, (spec.cout, spec.cin, kp[0], kp[1], spec.out_ps, 3))
+
+
 class _Conv3x3(torch.autograd.Function):
     """y = beta*res + alpha*act(conv3x3(x) + b), fused pixel-shuffle / NCHW-affine store."""
 
@@ -609,14 +629,18 @@ class _Conv3x3(torch.autograd.Function):
     def forward(ctx, x, res, weight, bias, spec):
         dtype = x.dtype
         N, H, W = _grid(spec, x)
-        wf, wd, bg = prepared(weight, bias, spec, dtype)
+        kp = _kpad(spec, dtype, H, W)
+        wf, wd, bg = _images(weight, bias, spec, dtype, kp)
         out_dtype = torch.float32 if spec.out_nchw else dtype
         y = torch.empty(_out_shape(spec, N, H, W), device=x.device, dtype=out_dtype)
-        conv_fwd_raw(x, wf, bg, y, N, H, W, spec.cin_p, spec.cout_p, spec.cout, res=res,
+        conv_fwd_raw(x, wf, bg, y, N, H, W, kp[1] if kp else spec.cin_p, spec.cout_p, spec.cout, res=res,
                      aff_scale=spec.aff_scale, aff_shift=spec.aff_shift, act=spec.act, slope=spec.slope,
                      alpha=spec.alpha, beta=spec.beta, out_ps=spec.out_ps, out_nchw=spec.out_nchw,
                      in_up=spec.in_up)
         ctx.spec = spec
+        # the dgrad stays on the unpadded images: the 158-KB kernel would wait for CUs the side-stream
+        # weight gradients hold during backward (DESIGN note 38); the forward has the GPU to itself
+        ctx.kp = None
         ctx.has_res = res is not None
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x, weight, bias, y if spec.act else None)
@@ -641,12 +665,12 @@ class _Conv3x3(torch.autograd.Function):
             if spec.act:
                 dY = act_backward(dY, y, spec.act, spec.slope, alpha)
                 alpha = 1.0
-        _, wd, _ = prepared(weight, bias, spec, dtype)
+        _, wd, _ = _images(weight, bias, spec, dtype, ctx.kp)
         dx = dres = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(N, H, W, spec.cin_p, device=x.device, dtype=dtype)
-            conv_fwd_raw(dY, wd, None, dx, N, H, W, spec.cout_p, spec.cin_p, spec.cin_p, alpha=alpha,
-                         in_ps=spec.out_ps, ldx=dY.shape[-1])
+            conv_fwd_raw(dY, wd, None, dx, N, H, W, ctx.kp[0] if ctx.kp else spec.cout_p, spec.cin_p, spec.cin_p,
+                         alpha=alpha, in_ps=spec.out_ps, ldx=dY.shape[-1])
             if spec.in_up and spec.in_up > 1:
                 dx = nearest_up_backward(dx, spec.in_up)
         if ctx.has_res and ctx.needs_input_grad[1]:

@@ -292,6 +292,55 @@ def test_wgrad_row3_vs_fp64(cuda, shape):
         assert (outs[0][0] - dw).abs().max().item() <= 2e-5 * scale + 1e-4
 
 
+@pytest.mark.parametrize('shape', [(2, 64, 64, 180, 180), (1, 8, 128, 180, 180), (2, 16, 64, 136, 180)])
+def test_conv_kpad_pph_vs_halo_and_fp64(cuda, shape, monkeypatch):
+    """SwinIR-M's 180 -> 180 3x3 conv (stored as 184 channels) with a residual: with K-padded weight
+    images (ops.conv._kpad: GEMM K 192, the x rows keeping their 184-channel stride) the forward runs
+    on the halo-row 256x256 kernel with a partial output tile (the dgrad stays on the halo kernel);
+    against the 64-channel halo kernel (SR_CONV_KPAD=0) and a float64 conv of the same bf16 operands:
+    y, dx, dW, db."""
+    from basicsr4rs_amd.utils import ktrace
+    N, H, W, cin, cout = shape
+    torch.manual_seed(7)
+    conv = nn.Conv2d(cin, cout, 3, 1, 1)
+    x = torch.zeros(N, H, W, C.pad8(cin))
+    x[..., :cin] = torch.randn(N, H, W, cin)
+    x = x.to(torch.bfloat16)
+    res = torch.zeros(N, H, W, C.pad8(cout))
+    res[..., :cout] = torch.randn(N, H, W, cout)
+    res = res.to(torch.bfloat16)
+    gy = torch.zeros(N, H, W, C.pad8(cout))
+    gy[..., :cout] = torch.randn(N, H, W, cout)
+    gy = gy.to(torch.bfloat16)
+    outs = {}
+    for kp in ('1', '0'):
+        monkeypatch.setenv('SR_CONV_KPAD', kp)
+        c = copy.deepcopy(conv).to(cuda)
+        xx = x.to(cuda).requires_grad_()
+        ktrace.start()
+        try:
+            y = C.conv3x3(xx, c, res=res.to(cuda))
+            y.backward(gy.to(cuda))
+            torch.cuda.synchronize()
+        finally:
+            ran = set(ktrace.stop())
+        assert ('conv3x3_fwd_pph_kernel' in ran) == (kp == '1'), ran
+        outs[kp] = (y.float().cpu()[..., :cout], xx.grad.float().cpu()[..., :cin], c.weight.grad.cpu(),
+                    c.bias.grad.cpu())
+    xd = x[..., :cin].permute(0, 3, 1, 2).double().requires_grad_()
+    wd = conv.weight.detach().to(torch.bfloat16).double().requires_grad_()
+    bd = conv.bias.detach().double().requires_grad_()
+    yd = F.conv2d(xd, wd, bd, padding=1) + res[..., :cout].permute(0, 3, 1, 2).double()
+    yd.backward(gy[..., :cout].permute(0, 3, 1, 2).double())
+    ref = (yd.detach().permute(0, 2, 3, 1), xd.grad.permute(0, 2, 3, 1), wd.grad, bd.grad)
+    for kp in ('1', '0'):
+        for got, want in zip(outs[kp], ref):
+            scale = want.abs().max().item()
+            assert (got.double() - want).abs().max().item() <= 1e-2 * scale, kp
+    for a, b in zip(outs['1'], outs['0']):  # the two kernels: within bf16 rounding of each other
+        assert (a - b).abs().max().item() <= 1e-2 * b.abs().max().item()
+
+
 @pytest.mark.parametrize('shape', [(2, 64, 64, 184, 576), (1, 64, 64, 192, 184), (3, 8, 64, 184, 360),
                                    (1, 8, 64, 360, 184), (1, 5, 13, 64, 64), (1, 3, 7, 200, 72),
                                    (4, 32, 32, 384, 384), (1, 1, 1, 64, 64)])

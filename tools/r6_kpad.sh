@@ -1,9 +1,17 @@
 #!/bin/bash
-# K-padded 184-channel convs on the halo-row 256x256 kernel: tests, then the SwinIR step with / without
+# K-padded 184-channel conv forwards (SR_CONV_KPAD): the SwinIR step with / without, traced (the default
+# bench line) and untraced, alternating
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-kpad}; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_conv_gpu.py tests/test_workload_tiles_gpu.py tests/test_swin_fused_gpu.py -m gpu -x -q \
-  --timeout 200 --timeout-method thread -p no:cacheprovider -k "kpad or swinir or swin" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
-tail -1 $OUT/tests.log
-VAR=SR_CONV_KPAD VALS="unset 0" WORKLOADS=swinir ROUNDS=${ROUNDS:-2} bash tools/ab_vals.sh ${1:-kpad}
+for r in $(seq ${ROUNDS:-2}); do
+  for v in unset 0; do
+    if [ $v = unset ]; then unset SR_CONV_KPAD; else export SR_CONV_KPAD=$v; fi
+    timeout -k 10 300 python -u bench.py --workload swinir --no-cpu-baseline > $OUT/full_${v}_$r.log 2>&1 || exit 1
+    timeout -k 10 300 python -u bench.py --workload swinir --no-cpu-baseline --no-trace --no-parity > $OUT/notrace_${v}_$r.log 2>&1 || exit 1
+    python3 -c "
+import json
+f = lambda p: json.loads([l for l in open(p) if l.startswith('{\"metric')][-1])['ms_per_step']
+print('round $r SR_CONV_KPAD=$v full', f('$OUT/full_${v}_$r.log'), 'notrace', f('$OUT/notrace_${v}_$r.log'))"
+  done
+done
